@@ -1,0 +1,198 @@
+"""Benchmark: simulated packets/sec of the network.Config enforcement path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): storm-style random all-to-all traffic over
+10,000 instances per GPU, heterogeneous LinkShape (latency/jitter/loss/dup/corrupt/reorder/
+bandwidth), Poisson(0.5) packets per instance per 1 µs tick.  One step = one pass of the hot path
+over one window of `--window` ticks of offered traffic that is already resident in HBM (generated
+on the device before the timed region): filter -> netem -> HTB (k_sim), routing by destination
+shard, RCCL all-to-all (N > 1), per-destination delivery sort.
+
+N = 1 runs directly; N > 1 is launched by torch.distributed.run, one rank per GPU, each rank owning
+10,000 instances (weak scaling), cross-shard deliveries exchanged with all_to_all_single (RCCL).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "simulated packets/sec (whole node) at 10k & 1M peers; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+# Algorithmic HBM bytes of k_sim: per offered packet 16 B record read + 1 B verdict
+# write; per scheduled record 24 B delivery write + 16 B queue item write + 16 B read + 8 B departure
+# ring write + 8 B read; per source 64 B params + 32 B state read + 32 B state write + 8 B offsets
+# + 4 B emit count.
+B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 72, 140
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--peers", type=int, default=10_000, help="instances per GPU")
+    p.add_argument("--lam", type=float, default=0.5)
+    p.add_argument("--window", type=int, default=2000, help="ticks (1 us) per step")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(peers_total, lam, window, seconds):
+    """The CPU oracle (a 'port' of the reference semantics) timed on this host, single thread, on a
+    bounded sample: sources 0..999 of the same storm workload."""
+    from testground_amd import abi, workloads
+    from testground_amd.build import build_oracle
+    from testground_amd.engine import CABIEngine
+
+    lib = ctypes.CDLL(str(build_oracle()))
+    abi.declare(lib, "tgo_")
+    sample_src = min(1000, peers_total)
+    e = CABIEngine(lib, "tgo_", peers_total, shard=(0, sample_src))
+    workloads.configure_storm(e, peers_total)
+    busy, pkts, steps = 0.0, 0, 0
+    while busy < seconds:
+        e.gen_storm(lam, window)
+        t0 = time.perf_counter()
+        e.step(window)
+        busy += time.perf_counter() - t0
+        steps += 1
+        e.drain()
+        pkts = e.stats()["offered"]
+    return {"value": pkts / busy, "unit": "packets/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/tgoracle.c, sources 0..{sample_src - 1} of the {peers_total}-instance storm, "
+                      f"lambda={lam}, {steps} windows of {window} ticks, {pkts} packets, {busy:.1f} s"}
+
+
+def load_pmc(kernel="k_sim"):
+    f = ROOT / "profiles" / "pmc_k_sim.json"
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text())
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    from testground_amd import abi, workloads
+    from testground_amd.engine import Engine
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    peers_total = a.peers * world
+    lo, hi = rank * a.peers, (rank + 1) * a.peers
+    eng = Engine(peers_total, shard=(lo, hi), device=local, flags=abi.OPT_DISCARD_DELIVERIES)
+    shapes = workloads.storm_shapes(peers_total)
+    from testground_amd.network import Config, RoutingPolicyType
+    for i, s in enumerate(shapes):
+        eng.configure(i, Config(Network="default", Enable=True, Default=s, RoutingPolicy=RoutingPolicyType.DenyAll))
+    for _ in range(a.warmup + a.steps):
+        eng.gen_storm(a.lam, a.window)  # inputs resident in HBM before the timed region
+    bounds = [r * a.peers for r in range(world)] + [peers_total]
+    out_buf = None
+
+    def one_step():
+        nonlocal out_buf
+        if world == 1:
+            eng.step(a.window)
+            return
+        cap = eng.sim_capacity()
+        if out_buf is None or out_buf.numel() < cap * 24:
+            out_buf = torch.empty(int(cap * 1.25) * 24, dtype=torch.uint8, device="cuda")
+        cnt = eng.step_sim(a.window, bounds, out_buf.data_ptr(), out_buf.numel() // 24)
+        send = torch.tensor(cnt.astype(np.int64), device="cuda")
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send)
+        rc = recv.cpu().numpy()
+        inbuf = torch.empty(int(rc.sum()) * 24 + 24, dtype=torch.uint8, device="cuda")
+        dist.all_to_all_single(inbuf[: int(rc.sum()) * 24], out_buf[: int(cnt.sum()) * 24],
+                               [int(x) * 24 for x in rc], [int(x) * 24 for x in cnt])
+        eng.deliver(inbuf.data_ptr(), int(rc.sum()))
+
+    for _ in range(a.warmup):
+        one_step()
+    eng.drain()
+    s0 = eng.stats()
+    eng.sim_kernel_ms(reset=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    s1 = eng.stats()
+    offered = s1["offered"] - s0["offered"]
+    scheduled = s1["scheduled"] - s0["scheduled"]
+    sim_ms, n_launch = eng.sim_kernel_ms()
+    if dist:
+        t = torch.tensor([el, float(offered)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        el = float(mx[0])
+        offered_all = float(t[1])
+    else:
+        offered_all = float(offered)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled) / max(1, a.steps) + B_SOURCE * a.peers
+    achieved = per_launch / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else None
+    pmc = load_pmc()
+    traffic = None
+    if pmc and pmc.get("window") == a.window and pmc.get("peers") == a.peers and pmc.get("lam") == a.lam:
+        traffic = pmc.get("hbm_bytes_per_launch")
+    res = {
+        "metric": METRIC,
+        "value": offered_all / el,
+        "unit": "packets/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": el * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32/u64 integer",
+        "data": "synthetic (device-generated storm traffic, Philox-keyed)",
+        "config": {"workload": "C3 storm: random all-to-all, heterogeneous LinkShape (BASELINE.json configs[2])",
+                   "peers_per_gpu": a.peers, "peers_total": peers_total, "lambda_per_tick": a.lam,
+                   "tick_ns": 1000, "window_ticks": a.window,
+                   "packets_per_step": offered_all / a.steps, "parallelism": f"peer-sharded x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                     "traffic": traffic, "algorithmic_bytes_per_launch": per_launch,
+                     "kernel_ms_avg": sim_ms, "launches": n_launch},
+        "cpu_baseline": None,
+    }
+    if world == 1 and not a.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(peers_total, a.lam, a.window, a.cpu_seconds)
+        res["cpu_baseline"]["gpu_over_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    print(json.dumps(res))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,209 @@
+/*
+ * tgsim.h — C ABI of the MI355X network-emulation engine (libtgsim.so).
+ *
+ * This is the drop-in boundary for testground's per-packet enforcement of the sidecar's
+ * network.Config.  In the reference the sidecar programs the Linux kernel (HTB + netem + FIB)
+ * through netlink; every call below replaces one of those netlink/kernel interactions:
+ *
+ *   tgsim_configure   <- sidecar.Network.ConfigureNetwork       pkg/sidecar/instance.go:37-42
+ *                        DockerNetwork.ConfigureNetwork         pkg/sidecar/docker_network.go:51-148
+ *                          (network-name check :52-55, routing policy :57 -> route.go:102-117,
+ *                           Enable=false disconnect :65-75, IP change :77-88,
+ *                           link.Shape :139 -> link.go:155-183, link.AddRules :143 -> link.go:187-217)
+ *   tgsim_submit/step <- the kernel data path the sidecar configured: FIB lookup of the
+ *                        blackhole/prohibit routes (link.go:189-211), HTB class 1:2 token bucket
+ *                        (link.go:118-128, :156-167), netem leaf 2:0 (link.go:131-141, :169-179)
+ *   tgsim_drain       <- veth -> docker bridge -> peer delivery (pkg/runner/local_docker.go:706-721)
+ *   tgsim_signal/
+ *   tgsim_barrier     <- sync-service SignalEntry / SignalAndWait used by the handler
+ *                        (pkg/sidecar/sidecar_handler.go:40-44, :75-80)
+ *
+ * A Go maintainer binds these with cgo.  Rules of the ABI:
+ *   - plain C structs, caller-owned buffers, no exceptions across the boundary;
+ *   - every int-returning call returns 0 (or a count) on success and a negative errno value on
+ *     failure; tgsim_last_error() then describes the failure;
+ *   - one engine handle owns its HIP stream and device memory and is NOT re-entrant: a host that
+ *     calls from several goroutines/threads funnels the calls through one owner (the reference
+ *     handler calls ConfigureNetwork sequentially per instance, concurrently across instances,
+ *     sidecar_handler.go:26,:71 and pkg/docker/manager.go:166-177).
+ *
+ * Per-packet semantics (units, decision order, Philox keying, tie-breaks) are specified in
+ * DESIGN.md §3 and restated independently by the CPU oracle in oracle/tgoracle.c.
+ */
+#ifndef TGSIM_H
+#define TGSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TGSIM_ABI_VERSION 1u
+
+/* Reserved destination id: traffic leaving the data network (the "external" routes that
+ * RoutingPolicy AllowAll/DenyAll adds or removes, route.go:68-117). */
+#define TGSIM_EXTERNAL 0xFFFFFFFFu
+
+/* network.FilterAction (sdk-go; used at link.go:194-209). */
+enum tgsim_filter { TGSIM_ACCEPT = 0, TGSIM_REJECT = 1, TGSIM_DROP = 2 };
+
+/* network.RoutingPolicyType (route.go:106-112).  UNSET behaves as DenyAll (default case :110). */
+enum tgsim_policy { TGSIM_POLICY_UNSET = 0, TGSIM_ALLOW_ALL = 1, TGSIM_DENY_ALL = 2 };
+
+/* Per-packet verdict codes (low nibble: the offered packet; high nibble: its netem clone). */
+enum tgsim_verdict {
+    TGSIM_V_SCHEDULED = 0,    /* passed netem+HTB, delivered at tgsim_delivery.t_ns          */
+    TGSIM_V_DISCONNECTED = 1, /* src or dst has Enable=false (docker_network.go:65-75)        */
+    TGSIM_V_NO_ROUTE = 2,     /* external dst while routing policy != AllowAll (route.go:110) */
+    TGSIM_V_BLACKHOLE = 3,    /* LinkRule Drop -> blackhole route, sender sees EINVAL         */
+    TGSIM_V_PROHIBIT = 4,     /* LinkRule Reject -> prohibit route, sender sees EACCES        */
+    TGSIM_V_LOSS = 5,         /* netem loss event                                             */
+    TGSIM_V_QUEUE_FULL = 6,   /* netem limit (1000 packets) reached                           */
+    TGSIM_V_EXTERNAL = 7,     /* external dst with AllowAll: leaves the data network unshaped */
+    TGSIM_V_NONE = 15         /* (high nibble) no clone was made                              */
+};
+
+/* Delivery flags. */
+#define TGSIM_FLAG_DUP 0x1u     /* this record is the netem clone of the offered packet */
+#define TGSIM_FLAG_CORRUPT 0x2u /* netem corrupt event fired                          */
+
+/* Engine flags (tgsim_opts.flags). */
+#define TGSIM_OPT_KEEP_DELIVERIES 0x1u /* keep delivered records for tgsim_drain (default on via 0) */
+#define TGSIM_OPT_DISCARD_DELIVERIES 0x2u /* bench: sort deliveries but do not accumulate them  */
+
+typedef struct {
+    uint32_t abi_version;  /* = TGSIM_ABI_VERSION                                          */
+    uint32_t n_peers;      /* simulated instances in the whole run (all shards)            */
+    uint32_t shard_begin;  /* sources owned by this engine: [shard_begin, shard_end)       */
+    uint32_t shard_end;    /* 0/0 -> [0, n_peers)                                          */
+    uint64_t seed;         /* Philox4x32-10 key                                            */
+    uint64_t tick_ns;      /* simulation tick; 0 -> 1000 ns                                */
+    uint32_t queue_limit;  /* netem limit; 0 -> 1000 (netlink default); max 1024          */
+    uint32_t flags;        /* TGSIM_OPT_*                                                  */
+    uint64_t lookahead_ns; /* HTB horizon beyond the step end (closed-loop drivers); 0 = none */
+    uint32_t subnet_base;  /* data-network base address, host order; 0 -> 16.0.0.0          */
+    int32_t device;        /* HIP device ordinal; -1 -> current device                       */
+} tgsim_opts;
+
+/* One LinkRule (network.LinkRule{LinkShape.Filter, Subnet}); only Filter is honoured, exactly as
+ * in the reference (link.go:185-186). */
+typedef struct {
+    uint32_t prefix; /* IPv4 network address, host byte order */
+    uint8_t len;     /* prefix length 0..32                    */
+    uint8_t action;  /* enum tgsim_filter                      */
+    uint16_t _pad;
+} tgsim_rule;
+
+/* network.LinkShape as the reference passes it to netlink (link.go:155-183). */
+typedef struct {
+    int64_t latency_ns;     /* time.Duration */
+    int64_t jitter_ns;      /* time.Duration */
+    uint64_t bandwidth_bps; /* bits/s; 0 = unlimited (link.go:156-159) */
+    float loss, corrupt, corrupt_corr, reorder, reorder_corr, duplicate, duplicate_corr; /* percent */
+    uint32_t _pad;
+} tgsim_shape;
+
+/* network.Config flattened (sdk-go; fields used at docker_network.go:52-143). */
+typedef struct {
+    const char* network;    /* must be "default" (else "unsupported network: %s") */
+    uint8_t enable;
+    uint8_t routing_policy; /* enum tgsim_policy */
+    uint8_t has_ipv4;
+    uint8_t _pad;
+    uint32_t ipv4;          /* host order; used when has_ipv4 */
+    tgsim_shape shape;      /* cfg.Default */
+    const tgsim_rule* rules;
+    uint32_t n_rules;
+    uint32_t _pad2;
+} tgsim_config;
+
+/* Offered packet, host -> engine (16 B). tick is relative to the engine's current time and must
+ * be < the n_ticks of the next tgsim_step.  seq is the per-source sequence number that keys the
+ * Philox stream together with (seed, src, dst). */
+typedef struct {
+    uint32_t src;
+    uint32_t dst; /* peer id or TGSIM_EXTERNAL */
+    uint32_t seq;
+    uint16_t len; /* bytes on the wire */
+    uint16_t tick;
+} tgsim_pkt;
+
+/* Delivered packet, engine -> host (24 B).  Drain order: (dst, t_ns, src, seq, clone first). */
+typedef struct {
+    uint64_t t_ns; /* delivery time (HTB departure) */
+    uint32_t src;
+    uint32_t dst;
+    uint32_t seq;
+    uint16_t len;
+    uint16_t flags; /* TGSIM_FLAG_* */
+} tgsim_delivery;
+
+typedef struct {
+    uint64_t offered;         /* offered packets processed (originals)            */
+    uint64_t scheduled;       /* records given a delivery time (clones included)  */
+    uint64_t cloned;          /* netem duplicates created                        */
+    uint64_t corrupted;       /* corrupt events on scheduled records             */
+    uint64_t by_verdict[8];   /* originals+clones per enum tgsim_verdict         */
+    uint64_t bytes_scheduled; /* sum of len over scheduled records               */
+    uint64_t now_tick;        /* engine time after the last step                 */
+} tgsim_stats_t;
+
+/* ---- lifecycle ---------------------------------------------------------------------------- */
+int tgsim_create(const tgsim_opts* opts, void** out_engine);
+void tgsim_destroy(void* engine);
+const char* tgsim_last_error(const void* engine);
+uint32_t tgsim_abi_version(void);
+
+/* ---- configuration (replaces netlink: Shape / AddRules / routing policy / connect) --------- */
+/* Applies cfg to instance `peer` at the engine's current time (effective for packets offered in
+ * the next step).  Follows DockerNetwork.ConfigureNetwork's order of operations.  Every shard of a
+ * multi-GPU run must receive every call (peer tables are replicated). */
+int tgsim_configure(void* engine, uint32_t peer, const tgsim_config* cfg);
+
+/* ---- data path ---------------------------------------------------------------------------- */
+int tgsim_submit(void* engine, const tgsim_pkt* pkts, size_t n);
+/* Storm-style synthetic traffic generated on the device for the next step:
+ * per source and tick Poisson(lambda) packets to a uniform destination != src, len U{64..1500}. */
+int tgsim_gen_storm(void* engine, double lambda, uint32_t n_ticks);
+/* Advances time by n_ticks: every offered packet of the window goes through filter -> netem ->
+ * HTB; deliveries are routed to their destination and sorted.  Single-shard convenience. */
+int tgsim_step(void* engine, uint32_t n_ticks);
+
+/* Multi-shard form of tgsim_step.  Phase 1 simulates the owned sources and writes the scheduled
+ * records into d_out (DEVICE memory, caller-owned, capacity out_cap records) grouped by the
+ * destination's shard; rank_bounds[0..n_ranks] are the peer boundaries of the shards and
+ * rank_counts[0..n_ranks-1] receives the per-shard record counts (host memory). */
+int tgsim_step_sim(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* rank_bounds,
+                   void* d_out, size_t out_cap, uint64_t* rank_counts);
+/* Phase 2: sorts the records addressed to this shard (DEVICE memory, n records) into the
+ * delivery order and appends them to the drain buffer. */
+int tgsim_deliver(void* engine, const void* d_in, size_t n);
+/* Upper bound of records phase 1 can emit for the next step (for sizing d_out). */
+int64_t tgsim_sim_capacity(void* engine);
+
+/* Copies up to cap delivered records (oldest step first) and removes them; returns the count. */
+int64_t tgsim_drain(void* engine, tgsim_delivery* out, size_t cap);
+int64_t tgsim_pending_deliveries(void* engine);
+/* Per-packet verdict bytes of the last step, in submit order (host packets) or generation order. */
+int64_t tgsim_verdicts(void* engine, uint8_t* out, size_t cap);
+int tgsim_stats(void* engine, tgsim_stats_t* out);
+
+/* ---- sync counters (sync-service SignalEntry / Barrier) ------------------------------------ */
+/* Increments state `state` (0..1023) by n and returns the new value (1-based sequence). */
+int64_t tgsim_signal(void* engine, uint32_t state, uint32_t n);
+/* Returns 1 when the state's count >= target, 0 otherwise. */
+int tgsim_barrier_poll(void* engine, uint32_t state, uint64_t target);
+
+/* ---- device timing (bench instrumentation) ------------------------------------------------ */
+/* Average device time (ms) of the simulate kernel over the steps since the last reset, measured
+ * with HIP events on the engine's stream. */
+double tgsim_sim_kernel_ms(void* engine, uint64_t* n_launches, int reset);
+void* tgsim_stream(void* engine);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TGSIM_H */

@@ -1,0 +1,677 @@
+/*
+ * tgoracle.c — CPU golden model (TEST INFRASTRUCTURE ONLY; see tgoracle.h for the contract).
+ *
+ * A deliberately plain, single-threaded restatement of the per-packet step, written from the
+ * reference's call sites and the published netlink/kernel algorithms, NOT from the HIP engine:
+ *
+ *   unit conversion      pkg/sidecar/link.go:143-151 (toMicroseconds); netlink v1.1.0
+ *                        time2Tick / Percentage2u32 / NewNetem / NewHtbClass / Xmittime [ext]
+ *   shape application    link.go:155-183 (HTB class rate, netem attrs; no LossCorr/DelayCorr)
+ *   rule semantics       link.go:187-217 (Accept deletes, Reject=prohibit, Drop=blackhole,
+ *                        cumulative across configs, rule LinkShape ignored)
+ *   routing policy       route.go:102-117 (AllowAll enables external routes, anything else denies)
+ *   order of operations  docker_network.go:51-148
+ *   per-packet enqueue   Linux sch_netem.c netem_enqueue (dup -> loss -> clone -> corrupt ->
+ *                        limit -> reorder/delay), tabledist uniform branch, get_crandom [ext]
+ *   token bucket         Linux sch_htb.c class tokens + psched_ratecfg_precompute/l2t_ns [ext]
+ *
+ * Every decision is keyed by Philox4x32-10(key = seed, ctr = (src, dst, seq, draw)), so results
+ * do not depend on evaluation order, sharding or step partitioning.
+ */
+#include "tgoracle.h"
+
+#include <errno.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* Philox4x32-10 (Salmon et al., SC'11; constants as Random123 / rocrand_philox4x32_10.h:62-65) */
+void tgo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Go float->uint32 conversion on amd64: truncate to int64, keep the low 32 bits; NaN/Inf/out of
+ * range yield the "integer indefinite" 0x8000000000000000, whose low 32 bits are 0. */
+static uint32_t go_f64_to_u32(double x) {
+    if (!(x > -9.2233720368547758e18 && x < 9.2233720368547758e18)) return 0;
+    return (uint32_t)(int64_t)x;
+}
+
+/* netlink Percentage2u32: float32 arithmetic on math.MaxUint32 (rounds to 2^32 as float32). */
+uint32_t tgo_percentage2u32(float pct) {
+    if (pct == 100.0f) return 0xFFFFFFFFu;
+    volatile float q = pct / 100.0f;
+    volatile float v = 4294967296.0f * q;
+    return go_f64_to_u32((double)v);
+}
+
+/* link.go:143-151: Duration.Microseconds() truncates toward zero, clamp at MaxUint32, uint32(). */
+uint32_t tgo_to_microseconds(int64_t ns) {
+    int64_t us = ns / 1000;
+    if (us > (int64_t)0xFFFFFFFFu) us = 0xFFFFFFFFu;
+    return (uint32_t)us;
+}
+
+/* netlink time2Tick with /proc/net/psched = 3e8 40 f4240 3b9aca00: tickInUsec = 1000/64. */
+uint32_t tgo_time2tick(uint32_t us) { return go_f64_to_u32((double)us * 15.625); }
+
+/* psched_ratecfg_precompute (net/sched/sch_generic.c). */
+static void ratecfg(uint64_t rate_bps_bytes, uint32_t* mult, uint32_t* shift) {
+    *mult = 1;
+    *shift = 0;
+    if (rate_bps_bytes > 0) {
+        uint64_t factor = 1000000000ull;
+        for (;;) {
+            *mult = (uint32_t)(factor / rate_bps_bytes);
+            if ((*mult & (1u << 31)) || (factor & (1ull << 63))) break;
+            factor <<= 1;
+            (*shift)++;
+        }
+    }
+}
+
+typedef struct {
+    uint64_t lat_ns;
+    int32_t sigma;
+    uint64_t rate_Bps;
+    uint32_t mult, shift;
+    uint64_t burst_ns;
+    uint32_t thr_loss, thr_dup, thr_cor, thr_reo;
+    uint32_t rho_dup, rho_cor, rho_reo;
+    int cor_set, dup_corr_set, reo_set;
+} cshape;
+
+static void compile_shape(const tgsim_shape* s, cshape* c) {
+    memset(c, 0, sizeof *c);
+    /* netem (link.go:169-179 -> netlink NewNetem) */
+    uint32_t lat_us = tgo_to_microseconds(s->latency_ns);
+    uint32_t jit_us = tgo_to_microseconds(s->jitter_ns);
+    uint32_t lat_t = tgo_time2tick(lat_us);
+    uint32_t jit_t = lat_t > 0 ? tgo_time2tick(jit_us) : jit_us; /* "Jitter is only valid if latency is > 0" */
+    c->lat_ns = (uint64_t)lat_t << 6;                             /* PSCHED_TICKS2NS */
+    uint64_t jit_ns = (uint64_t)jit_t << 6;
+    c->sigma = (int32_t)(uint32_t)jit_ns; /* tabledist(s64 mu, s32 sigma, ...) */
+    if ((uint32_t)c->sigma == 0x80000000u) c->sigma = 0x7FFFFFFF; /* 2*(u32)sigma would be 0 */
+    c->thr_loss = tgo_percentage2u32(s->loss);
+    c->thr_dup = tgo_percentage2u32(s->duplicate);
+    c->thr_reo = tgo_percentage2u32(s->reorder);
+    c->thr_cor = tgo_percentage2u32(s->corrupt);
+    c->rho_dup = c->thr_dup > 0 ? tgo_percentage2u32(s->duplicate_corr) : 0;
+    c->rho_reo = tgo_percentage2u32(s->reorder_corr);
+    c->rho_cor = tgo_percentage2u32(s->corrupt_corr);
+    c->cor_set = c->thr_cor > 0;     /* TCA_NETEM_CORRUPT only when Probability > 0 */
+    c->reo_set = c->thr_reo > 0;     /* TCA_NETEM_REORDER only when Probability > 0 (gap = 1) */
+    c->dup_corr_set = c->rho_dup > 0; /* TCA_NETEM_CORR only when a correlation > 0 */
+    /* HTB class (link.go:156-167 -> netlink NewHtbClass: rate/8, mtu 1600, hz 1e9) */
+    uint64_t rate = s->bandwidth_bps ? s->bandwidth_bps : UINT64_MAX;
+    uint64_t rate_B = rate / 8;
+    uint32_t buf_bytes = go_f64_to_u32((double)rate_B / 1e9 + 1600.0);
+    uint32_t buf_us = go_f64_to_u32(1000000.0 * ((double)buf_bytes / (double)rate_B));
+    c->burst_ns = (uint64_t)tgo_time2tick(buf_us) << 6;
+    c->rate_Bps = (uint32_t)rate_B; /* TcRateSpec.Rate is u32 in netlink v1.1.0 (no RATE64) */
+    ratecfg(c->rate_Bps, &c->mult, &c->shift);
+}
+
+void tgo_compile_shape(const tgsim_shape* s, uint64_t out[13]) {
+    cshape c;
+    compile_shape(s, &c);
+    out[0] = c.lat_ns; out[1] = (uint64_t)(int64_t)c.sigma; out[2] = c.rate_Bps; out[3] = c.mult;
+    out[4] = c.shift; out[5] = c.burst_ns; out[6] = c.thr_loss; out[7] = c.thr_dup;
+    out[8] = c.thr_cor; out[9] = c.thr_reo; out[10] = c.rho_dup; out[11] = c.rho_cor;
+    out[12] = c.rho_reo;
+}
+
+/* Poisson(lambda) CDF as u32 thresholds (storm generator). */
+void tgo_poisson_table(double lambda, uint32_t out[16]) {
+    double p = exp(-lambda), F = p;
+    for (int k = 0; k < 16; ++k) {
+        double t = F * 4294967296.0;
+        out[k] = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+        p = p * lambda / (double)(k + 1);
+        F = F + p;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    uint64_t e;
+    uint32_t seq, dst;
+    uint16_t len, flags;
+} item;
+
+typedef struct {
+    uint32_t net;
+    uint8_t len, action;
+} rule;
+
+typedef struct {
+    /* netem/HTB parameters currently installed (kernel-side state, incl. persisting quirks) */
+    uint64_t lat_ns, burst_ns;
+    int32_t sigma;
+    uint32_t mult, shift;
+    uint32_t thr_loss, thr_dup, thr_cor, thr_reo;
+    uint32_t rho_dup, rho_cor, rho_reo;
+    uint32_t last_dup, last_cor, last_reo;
+    uint32_t shape_epoch;
+    int allow_ext;
+    /* FIB rules of this instance */
+    rule* rules;
+    uint32_t n_rules, cap_rules;
+    /* queue state */
+    uint64_t tat;
+    item* heap;
+    uint32_t heap_n;
+    uint64_t* ring;
+    uint32_t ring_head, ring_n;
+} source;
+
+typedef struct {
+    tgsim_pkt p;
+    uint64_t idx;
+} offered;
+
+typedef struct {
+    tgsim_opts o;
+    char err[256];
+    uint32_t nsrc;
+    source* src;
+    uint8_t* enabled;
+    uint32_t* ip;
+    uint32_t key[2];
+    uint64_t now_tick;
+    offered* off;
+    size_t n_off, cap_off;
+    uint8_t* verdicts;
+    size_t n_verdicts;
+    tgsim_delivery* out; /* undrained deliveries */
+    size_t n_out, cap_out, out_head;
+    tgsim_delivery* step_out;
+    size_t n_step, cap_step;
+    tgsim_stats_t st;
+    uint64_t counters[1024];
+    uint32_t* gen_seq;
+} oracle;
+
+#define HCAP 1024u
+
+static int fail(oracle* o, int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(o->err, sizeof o->err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+static void* grow(void* p, size_t* cap, size_t need, size_t elem) {
+    if (need <= *cap) return p;
+    size_t nc = *cap ? *cap : 64;
+    while (nc < need) nc *= 2;
+    void* q = realloc(p, nc * elem);
+    if (!q) abort();
+    *cap = nc;
+    return q;
+}
+
+static void reset_netem(oracle* o, uint32_t s) {
+    source* S = &o->src[s];
+    S->lat_ns = 0; S->burst_ns = 0; S->sigma = 0;
+    S->thr_loss = S->thr_dup = S->thr_cor = S->thr_reo = 0;
+    S->rho_dup = S->rho_cor = S->rho_reo = 0;
+    S->last_dup = S->last_cor = S->last_reo = 0;
+    /* HTB class created with Rate MaxUint64 (link.go:98-105) */
+    tgsim_shape z;
+    memset(&z, 0, sizeof z);
+    cshape c;
+    compile_shape(&z, &c);
+    S->mult = c.mult; S->shift = c.shift; S->burst_ns = c.burst_ns;
+    S->tat = 0;
+}
+
+int tgo_create(const tgsim_opts* opts, void** out) {
+    if (!opts || !out) return -EINVAL;
+    if (opts->abi_version != TGSIM_ABI_VERSION) return -EPROTO;
+    if (opts->n_peers == 0) return -EINVAL;
+    oracle* o = (oracle*)calloc(1, sizeof *o);
+    o->o = *opts;
+    if (o->o.shard_begin == 0 && o->o.shard_end == 0) o->o.shard_end = o->o.n_peers;
+    if (o->o.shard_begin >= o->o.shard_end || o->o.shard_end > o->o.n_peers) {
+        free(o);
+        return -EINVAL;
+    }
+    if (!o->o.tick_ns) o->o.tick_ns = 1000;
+    if (!o->o.queue_limit) o->o.queue_limit = 1000;
+    if (o->o.queue_limit > HCAP) {
+        free(o);
+        return -EINVAL;
+    }
+    if (!o->o.subnet_base) o->o.subnet_base = 16u << 24;
+    o->key[0] = (uint32_t)o->o.seed;
+    o->key[1] = (uint32_t)(o->o.seed >> 32);
+    o->nsrc = o->o.shard_end - o->o.shard_begin;
+    o->src = (source*)calloc(o->nsrc, sizeof(source));
+    o->enabled = (uint8_t*)malloc(o->o.n_peers);
+    memset(o->enabled, 1, o->o.n_peers); /* containers start attached (local_docker.go:459) */
+    o->ip = (uint32_t*)malloc(sizeof(uint32_t) * o->o.n_peers);
+    for (uint32_t i = 0; i < o->o.n_peers; ++i) o->ip[i] = o->o.subnet_base + 2 + i;
+    o->gen_seq = (uint32_t*)calloc(o->nsrc, sizeof(uint32_t));
+    for (uint32_t s = 0; s < o->nsrc; ++s) {
+        o->src[s].heap = (item*)malloc(sizeof(item) * HCAP);
+        o->src[s].ring = (uint64_t*)malloc(sizeof(uint64_t) * HCAP);
+        reset_netem(o, s);
+    }
+    *out = o;
+    return 0;
+}
+
+void tgo_destroy(void* p) {
+    oracle* o = (oracle*)p;
+    if (!o) return;
+    for (uint32_t s = 0; s < o->nsrc; ++s) {
+        free(o->src[s].heap);
+        free(o->src[s].ring);
+        free(o->src[s].rules);
+    }
+    free(o->src); free(o->enabled); free(o->ip); free(o->off); free(o->verdicts);
+    free(o->out); free(o->step_out); free(o->gen_seq);
+    free(o);
+}
+
+const char* tgo_last_error(const void* p) { return p ? ((const oracle*)p)->err : "null engine"; }
+
+/* link.go:187-217 */
+static int add_rules(oracle* o, source* S, const tgsim_rule* rules, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const tgsim_rule* r = &rules[i];
+        int bad = r->len > 32;
+        uint32_t mask = (!bad && r->len) ? (0xFFFFFFFFu << (32 - r->len)) : 0;
+        bad = bad || (r->prefix & ~mask) != 0; /* fib_table_insert/delete reject host bits */
+        if (r->action == TGSIM_ACCEPT) {         /* RouteDel blackhole + prohibit, errors ignored */
+            if (bad) continue;
+            for (uint32_t j = 0; j < S->n_rules;) {
+                if (S->rules[j].net == r->prefix && S->rules[j].len == r->len) {
+                    S->rules[j] = S->rules[--S->n_rules];
+                } else {
+                    ++j;
+                }
+            }
+            continue;
+        }
+        if (r->action != TGSIM_REJECT && r->action != TGSIM_DROP)
+            return fail(o, -EINVAL, "invalid filter action %u", r->action);
+        if (bad) return fail(o, -EINVAL, "invalid argument");
+        uint32_t j;
+        for (j = 0; j < S->n_rules; ++j)
+            if (S->rules[j].net == r->prefix && S->rules[j].len == r->len) break;
+        if (j == S->n_rules) { /* RouteReplace creates */
+            size_t cap = S->cap_rules;
+            S->rules = (rule*)grow(S->rules, &cap, (size_t)S->n_rules + 1, sizeof(rule));
+            S->cap_rules = (uint32_t)cap;
+            S->rules[S->n_rules].net = r->prefix;
+            S->rules[S->n_rules].len = r->len;
+            S->n_rules++;
+        }
+        S->rules[j].action = r->action;
+    }
+    return 0;
+}
+
+int tgo_configure(void* p, uint32_t peer, const tgsim_config* cfg) {
+    oracle* o = (oracle*)p;
+    if (!o || !cfg) return -EINVAL;
+    if (peer >= o->o.n_peers) return fail(o, -EINVAL, "peer %u out of range", peer);
+    const char* net = cfg->network ? cfg->network : "";
+    if (strcmp(net, "default") != 0) return fail(o, -EINVAL, "unsupported network: %s", net);
+    int owned = peer >= o->o.shard_begin && peer < o->o.shard_end;
+    source* S = owned ? &o->src[peer - o->o.shard_begin] : NULL;
+    if (S) S->allow_ext = cfg->routing_policy == TGSIM_ALLOW_ALL; /* route.go:102-117 */
+    if (!cfg->enable) {                                         /* docker_network.go:65-75 */
+        o->enabled[peer] = 0;
+        return 0;
+    }
+    int reconnect = !o->enabled[peer] || (cfg->has_ipv4 && cfg->ipv4 != o->ip[peer]);
+    if (cfg->has_ipv4) o->ip[peer] = cfg->ipv4;
+    o->enabled[peer] = 1;
+    if (!S) return 0;
+    uint32_t s = peer - o->o.shard_begin;
+    if (reconnect) reset_netem(o, s); /* NewNetlinkLink: fresh HTB class + netem qdisc */
+    /* link.Shape (docker_network.go:139) */
+    cshape c;
+    compile_shape(&cfg->shape, &c);
+    S->shape_epoch++;
+    uint32_t ctr[4] = {peer, 0xFFFFFFFEu, S->shape_epoch, 3}, rnd[4]; /* init_crandom: last = random */
+    tgo_philox4x32_10(ctr, o->key, rnd);
+    S->lat_ns = c.lat_ns;
+    S->sigma = c.sigma;
+    S->thr_loss = c.thr_loss;
+    S->thr_dup = c.thr_dup;
+    if (c.dup_corr_set) { S->rho_dup = c.rho_dup; S->last_dup = rnd[0]; }
+    if (c.cor_set) { S->thr_cor = c.thr_cor; S->rho_cor = c.rho_cor; S->last_cor = rnd[1]; }
+    if (c.reo_set) { S->rho_reo = c.rho_reo; S->last_reo = rnd[2]; }
+    S->thr_reo = c.thr_reo; /* gap = 0 disables reordering whatever q->reorder holds */
+    S->mult = c.mult;
+    S->shift = c.shift;
+    S->burst_ns = c.burst_ns;
+    /* link.AddRules (docker_network.go:143) */
+    return add_rules(o, S, cfg->rules, cfg->n_rules);
+}
+
+int tgo_submit(void* p, const tgsim_pkt* pkts, size_t n) {
+    oracle* o = (oracle*)p;
+    if (!o || (!pkts && n)) return -EINVAL;
+    for (size_t i = 0; i < n; ++i) {
+        const tgsim_pkt* k = &pkts[i];
+        if (k->src < o->o.shard_begin || k->src >= o->o.shard_end)
+            return fail(o, -EINVAL, "packet %zu: src %u not owned by this shard", i, k->src);
+        if (k->dst != TGSIM_EXTERNAL && k->dst >= o->o.n_peers)
+            return fail(o, -EINVAL, "packet %zu: dst %u out of range", i, k->dst);
+    }
+    o->off = (offered*)grow(o->off, &o->cap_off, o->n_off + n, sizeof(offered));
+    for (size_t i = 0; i < n; ++i) {
+        o->off[o->n_off].p = pkts[i];
+        o->off[o->n_off].idx = o->n_off;
+        o->n_off++;
+    }
+    return 0;
+}
+
+/* Storm generator restatement: per (src, tick) Poisson count, uniform dst != src,
+ * len 64 + u mod 1437. */
+int tgo_gen_storm(void* p, double lambda, uint32_t n_ticks) {
+    oracle* o = (oracle*)p;
+    if (!o || !(lambda >= 0.0) || lambda > 4.0 || n_ticks > 65536) return -EINVAL;
+    uint32_t tab[16];
+    tgo_poisson_table(lambda, tab);
+    uint32_t gk[2] = {o->key[0] ^ 0x9E3779B9u, o->key[1] ^ 0x7F4A7C15u};
+    uint32_t N = o->o.n_peers;
+    if (N < 2) return 0;
+    for (uint32_t s = 0; s < o->nsrc; ++s) {
+        uint32_t src = o->o.shard_begin + s;
+        for (uint32_t t = 0; t < n_ticks; ++t) {
+            uint32_t abs_t = (uint32_t)(o->now_tick + t);
+            uint32_t ctr[4] = {src, abs_t, 0x53544F52u, 0}, r[4];
+            tgo_philox4x32_10(ctr, gk, r);
+            uint32_t cnt = 0;
+            while (cnt < 16 && r[0] >= tab[cnt]) cnt++;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                uint32_t c2[4] = {src, abs_t, 0x53544F52u, j + 1}, q[4];
+                tgo_philox4x32_10(c2, gk, q);
+                uint32_t d = q[0] % (N - 1);
+                if (d >= src) d++;
+                tgsim_pkt k;
+                k.src = src; k.dst = d; k.seq = o->gen_seq[s]++;
+                k.len = (uint16_t)(64 + q[1] % 1437u); k.tick = (uint16_t)t;
+                o->off = (offered*)grow(o->off, &o->cap_off, o->n_off + 1, sizeof(offered));
+                o->off[o->n_off].p = k;
+                o->off[o->n_off].idx = o->n_off;
+                o->n_off++;
+            }
+        }
+    }
+    return 0;
+}
+
+int64_t tgo_offered(void* p, tgsim_pkt* out, size_t cap) {
+    oracle* o = (oracle*)p;
+    size_t n = o->n_off < cap ? o->n_off : cap;
+    for (size_t i = 0; i < n; ++i) out[i] = o->off[i].p;
+    return (int64_t)o->n_off;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+static int item_lt(const item* a, const item* b) {
+    if (a->e != b->e) return a->e < b->e;
+    if (a->seq != b->seq) return a->seq < b->seq;
+    return (a->flags & TGSIM_FLAG_DUP) && !(b->flags & TGSIM_FLAG_DUP); /* clone enqueued first */
+}
+
+static void heap_push(source* S, item it) {
+    uint32_t i = S->heap_n++;
+    while (i > 0) {
+        uint32_t p = (i - 1) / 2;
+        if (!item_lt(&it, &S->heap[p])) break;
+        S->heap[i] = S->heap[p];
+        i = p;
+    }
+    S->heap[i] = it;
+}
+
+static item heap_pop(source* S) {
+    item top = S->heap[0];
+    item last = S->heap[--S->heap_n];
+    uint32_t i = 0, n = S->heap_n;
+    for (;;) {
+        uint32_t c = 2 * i + 1;
+        if (c >= n) break;
+        if (c + 1 < n && item_lt(&S->heap[c + 1], &S->heap[c])) c++;
+        if (!item_lt(&S->heap[c], &last)) break;
+        S->heap[i] = S->heap[c];
+        i = c;
+    }
+    if (n) S->heap[i] = last;
+    return top;
+}
+
+/* HTB class 1:2 serving the netem leaf in eligibility order (sch_htb.c tokens in ns). */
+static void htb_until(oracle* o, uint32_t s, uint64_t horizon) {
+    source* S = &o->src[s];
+    while (S->heap_n && S->heap[0].e < horizon) {
+        item it = heap_pop(S);
+        uint64_t d = it.e > S->tat ? it.e : S->tat;
+        uint64_t floor_ = it.e > S->burst_ns ? it.e - S->burst_ns : 0;
+        uint64_t base = S->tat > floor_ ? S->tat : floor_;
+        S->tat = base + (((uint64_t)it.len * S->mult) >> S->shift);
+        S->ring[(S->ring_head + S->ring_n) % HCAP] = d;
+        S->ring_n++;
+        o->step_out = (tgsim_delivery*)grow(o->step_out, &o->cap_step, o->n_step + 1, sizeof(tgsim_delivery));
+        tgsim_delivery* r = &o->step_out[o->n_step++];
+        r->t_ns = d;
+        r->src = o->o.shard_begin + s;
+        r->dst = it.dst;
+        r->seq = it.seq;
+        r->len = it.len;
+        r->flags = it.flags;
+        o->st.scheduled++;
+        o->st.bytes_scheduled += it.len;
+        if (it.flags & TGSIM_FLAG_CORRUPT) o->st.corrupted++;
+    }
+}
+
+static uint32_t crandom(uint32_t raw, uint32_t rho, uint32_t* last) { /* get_crandom */
+    if (rho == 0) return raw;
+    uint64_t r = (uint64_t)rho + 1;
+    uint32_t a = (uint32_t)(((uint64_t)raw * ((1ull << 32) - r) + (uint64_t)(*last) * r) >> 32);
+    *last = a;
+    return a;
+}
+
+/* netem_enqueue from the queue-limit check on (dup/loss/corrupt already decided). */
+static int enqueue(oracle* o, uint32_t s, uint64_t T, const tgsim_pkt* k, uint32_t reo_raw,
+                   const uint32_t ctr_delay[4], int delay_word, uint16_t flags) {
+    source* S = &o->src[s];
+    htb_until(o, s, T);
+    while (S->ring_n && S->ring[S->ring_head] < T) {
+        S->ring_head = (S->ring_head + 1) % HCAP;
+        S->ring_n--;
+    }
+    if (S->heap_n + S->ring_n >= o->o.queue_limit) return TGSIM_V_QUEUE_FULL;
+    uint64_t e;
+    int reordered = 0;
+    if (S->thr_reo) {
+        uint32_t v = crandom(reo_raw, S->rho_reo, &S->last_reo);
+        reordered = !(S->thr_reo < v);
+    }
+    if (reordered) {
+        e = T;
+    } else if (S->sigma == 0) {
+        e = T + S->lat_ns;
+    } else {
+        uint32_t r[4];
+        tgo_philox4x32_10(ctr_delay, o->key, r);
+        uint32_t m = 2u * (uint32_t)S->sigma;
+        int64_t delay = (int64_t)(r[delay_word] % m) + (int64_t)S->lat_ns - (int64_t)S->sigma;
+        e = delay > 0 ? T + (uint64_t)delay : T;
+    }
+    item it;
+    it.e = e; it.seq = k->seq; it.dst = k->dst; it.len = k->len; it.flags = flags;
+    heap_push(S, it);
+    (void)o;
+    return TGSIM_V_SCHEDULED;
+}
+
+static uint32_t lpm(const source* S, uint32_t ip) {
+    int best = -1;
+    uint32_t act = TGSIM_ACCEPT;
+    for (uint32_t i = 0; i < S->n_rules; ++i) {
+        const rule* r = &S->rules[i];
+        uint32_t mask = r->len ? 0xFFFFFFFFu << (32 - r->len) : 0;
+        if ((ip & mask) == r->net && (int)r->len > best) {
+            best = r->len;
+            act = r->action;
+        }
+    }
+    return act;
+}
+
+static uint8_t process(oracle* o, uint32_t s, uint64_t T, const tgsim_pkt* k) {
+    source* S = &o->src[s];
+    o->st.offered++;
+    if (!o->enabled[k->src] || (k->dst != TGSIM_EXTERNAL && !o->enabled[k->dst]))
+        return 0xF0 | TGSIM_V_DISCONNECTED;
+    if (k->dst == TGSIM_EXTERNAL) return 0xF0 | (S->allow_ext ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE);
+    if (S->n_rules) {
+        uint32_t a = lpm(S, o->ip[k->dst]);
+        if (a == TGSIM_DROP) return 0xF0 | TGSIM_V_BLACKHOLE;
+        if (a == TGSIM_REJECT) return 0xF0 | TGSIM_V_PROHIBIT;
+    }
+    uint32_t c0[4] = {k->src, k->dst, k->seq, 0}, r0[4];
+    tgo_philox4x32_10(c0, o->key, r0);
+    int count = 1;
+    if (S->thr_dup && S->thr_dup >= crandom(r0[0], S->rho_dup, &S->last_dup)) count++;
+    if (S->thr_loss && S->thr_loss >= r0[1]) count--;
+    if (count == 0) return 0xF0 | TGSIM_V_LOSS;
+    uint8_t cv = TGSIM_V_NONE;
+    if (count == 2) { /* clone re-enters the root qdisc with duplicate = 0 */
+        o->st.cloned++;
+        uint32_t c2[4] = {k->src, k->dst, k->seq, 2}, r2[4];
+        tgo_philox4x32_10(c2, o->key, r2);
+        if (S->thr_loss && S->thr_loss >= r2[0]) {
+            cv = TGSIM_V_LOSS;
+        } else {
+            uint16_t fl = TGSIM_FLAG_DUP;
+            if (S->thr_cor && S->thr_cor >= crandom(r2[1], S->rho_cor, &S->last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+            cv = (uint8_t)enqueue(o, s, T, k, r2[2], c2, 3, fl);
+        }
+    }
+    uint16_t fl = 0;
+    if (S->thr_cor && S->thr_cor >= crandom(r0[2], S->rho_cor, &S->last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+    uint32_t c1[4] = {k->src, k->dst, k->seq, 1};
+    uint8_t ov = (uint8_t)enqueue(o, s, T, k, r0[3], c1, 0, fl);
+    return (uint8_t)((cv << 4) | ov);
+}
+
+static int cmp_off(const void* a, const void* b) {
+    const offered* x = (const offered*)a;
+    const offered* y = (const offered*)b;
+    if (x->p.src != y->p.src) return x->p.src < y->p.src ? -1 : 1;
+    if (x->p.tick != y->p.tick) return x->p.tick < y->p.tick ? -1 : 1;
+    if (x->p.seq != y->p.seq) return x->p.seq < y->p.seq ? -1 : 1;
+    return x->idx < y->idx ? -1 : (x->idx > y->idx);
+}
+
+static int cmp_del(const void* a, const void* b) {
+    const tgsim_delivery* x = (const tgsim_delivery*)a;
+    const tgsim_delivery* y = (const tgsim_delivery*)b;
+    if (x->dst != y->dst) return x->dst < y->dst ? -1 : 1;
+    if (x->t_ns != y->t_ns) return x->t_ns < y->t_ns ? -1 : 1;
+    if (x->src != y->src) return x->src < y->src ? -1 : 1;
+    if (x->seq != y->seq) return x->seq < y->seq ? -1 : 1;
+    int xd = (x->flags & TGSIM_FLAG_DUP) != 0, yd = (y->flags & TGSIM_FLAG_DUP) != 0;
+    return yd - xd; /* clone first */
+}
+
+int tgo_step(void* p, uint32_t n_ticks) {
+    oracle* o = (oracle*)p;
+    if (!o || n_ticks == 0) return -EINVAL;
+    for (size_t i = 0; i < o->n_off; ++i)
+        if (o->off[i].p.tick >= n_ticks)
+            return fail(o, -EINVAL, "packet %zu: tick %u beyond step of %u ticks", i, o->off[i].p.tick, n_ticks);
+    qsort(o->off, o->n_off, sizeof(offered), cmp_off);
+    free(o->verdicts);
+    o->verdicts = (uint8_t*)malloc(o->n_off ? o->n_off : 1);
+    o->n_verdicts = o->n_off;
+    o->n_step = 0;
+    uint64_t T0 = o->now_tick * o->o.tick_ns;
+    for (size_t i = 0; i < o->n_off; ++i) {
+        const tgsim_pkt* k = &o->off[i].p;
+        uint32_t s = k->src - o->o.shard_begin;
+        uint64_t T = T0 + (uint64_t)k->tick * o->o.tick_ns;
+        uint8_t v = process(o, s, T, k);
+        o->verdicts[o->off[i].idx] = v;
+        o->st.by_verdict[v & 15]++;
+        if ((v >> 4) != TGSIM_V_NONE) o->st.by_verdict[v >> 4]++;
+    }
+    uint64_t T1 = (o->now_tick + n_ticks) * o->o.tick_ns;
+    for (uint32_t s = 0; s < o->nsrc; ++s) htb_until(o, s, T1 + o->o.lookahead_ns);
+    qsort(o->step_out, o->n_step, sizeof(tgsim_delivery), cmp_del);
+    o->out = (tgsim_delivery*)grow(o->out, &o->cap_out, o->n_out + o->n_step, sizeof(tgsim_delivery));
+    memcpy(o->out + o->n_out, o->step_out, o->n_step * sizeof(tgsim_delivery));
+    o->n_out += o->n_step;
+    o->n_off = 0;
+    o->now_tick += n_ticks;
+    o->st.now_tick = o->now_tick;
+    return 0;
+}
+
+int64_t tgo_drain(void* p, tgsim_delivery* out, size_t cap) {
+    oracle* o = (oracle*)p;
+    size_t avail = o->n_out - o->out_head;
+    size_t n = avail < cap ? avail : cap;
+    memcpy(out, o->out + o->out_head, n * sizeof(tgsim_delivery));
+    o->out_head += n;
+    if (o->out_head == o->n_out) o->out_head = o->n_out = 0;
+    return (int64_t)n;
+}
+
+int64_t tgo_verdicts(void* p, uint8_t* out, size_t cap) {
+    oracle* o = (oracle*)p;
+    size_t n = o->n_verdicts < cap ? o->n_verdicts : cap;
+    memcpy(out, o->verdicts, n);
+    return (int64_t)o->n_verdicts;
+}
+
+int tgo_stats(void* p, tgsim_stats_t* out) {
+    *out = ((oracle*)p)->st;
+    return 0;
+}
+
+int64_t tgo_signal(void* p, uint32_t state, uint32_t n) {
+    oracle* o = (oracle*)p;
+    if (state >= 1024) return -EINVAL;
+    o->counters[state] += n;
+    return (int64_t)o->counters[state];
+}
+
+int tgo_barrier_poll(void* p, uint32_t state, uint64_t target) {
+    oracle* o = (oracle*)p;
+    if (state >= 1024) return -EINVAL;
+    return o->counters[state] >= target;
+}

@@ -1,0 +1,132 @@
+"""ctypes mirror of include/tgsim.h (plain C structs; no torch types cross the boundary)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+ABI_VERSION = 1
+EXTERNAL = 0xFFFFFFFF
+
+# enum tgsim_verdict
+V_SCHEDULED, V_DISCONNECTED, V_NO_ROUTE, V_BLACKHOLE, V_PROHIBIT, V_LOSS, V_QUEUE_FULL, V_EXTERNAL = range(8)
+V_NONE = 15
+VERDICT_NAMES = ["scheduled", "disconnected", "no_route", "blackhole", "prohibit", "loss",
+                 "queue_full", "external"]
+
+FLAG_DUP = 0x1
+FLAG_CORRUPT = 0x2
+
+OPT_DISCARD_DELIVERIES = 0x2
+
+
+class Opts(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32),
+        ("n_peers", C.c_uint32),
+        ("shard_begin", C.c_uint32),
+        ("shard_end", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("tick_ns", C.c_uint64),
+        ("queue_limit", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("lookahead_ns", C.c_uint64),
+        ("subnet_base", C.c_uint32),
+        ("device", C.c_int32),
+    ]
+
+
+class Rule(C.Structure):
+    _fields_ = [("prefix", C.c_uint32), ("len", C.c_uint8), ("action", C.c_uint8), ("_pad", C.c_uint16)]
+
+
+class Shape(C.Structure):
+    _fields_ = [
+        ("latency_ns", C.c_int64),
+        ("jitter_ns", C.c_int64),
+        ("bandwidth_bps", C.c_uint64),
+        ("loss", C.c_float),
+        ("corrupt", C.c_float),
+        ("corrupt_corr", C.c_float),
+        ("reorder", C.c_float),
+        ("reorder_corr", C.c_float),
+        ("duplicate", C.c_float),
+        ("duplicate_corr", C.c_float),
+        ("_pad", C.c_uint32),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("network", C.c_char_p),
+        ("enable", C.c_uint8),
+        ("routing_policy", C.c_uint8),
+        ("has_ipv4", C.c_uint8),
+        ("_pad", C.c_uint8),
+        ("ipv4", C.c_uint32),
+        ("shape", Shape),
+        ("rules", C.POINTER(Rule)),
+        ("n_rules", C.c_uint32),
+        ("_pad2", C.c_uint32),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("offered", C.c_uint64),
+        ("scheduled", C.c_uint64),
+        ("cloned", C.c_uint64),
+        ("corrupted", C.c_uint64),
+        ("by_verdict", C.c_uint64 * 8),
+        ("bytes_scheduled", C.c_uint64),
+        ("now_tick", C.c_uint64),
+    ]
+
+
+PKT_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("len", "<u2"), ("tick", "<u2")])
+DELIVERY_DTYPE = np.dtype([("t_ns", "<u8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"),
+                           ("len", "<u2"), ("flags", "<u2")])
+assert PKT_DTYPE.itemsize == 16 and DELIVERY_DTYPE.itemsize == 24
+assert C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56 and C.sizeof(Config) == 88
+
+# Every symbol include/tgsim.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "tgsim_create", "tgsim_destroy", "tgsim_last_error", "tgsim_abi_version", "tgsim_configure",
+    "tgsim_submit", "tgsim_gen_storm", "tgsim_step", "tgsim_step_sim", "tgsim_deliver",
+    "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
+    "tgsim_signal", "tgsim_barrier_poll", "tgsim_sim_kernel_ms", "tgsim_stream",
+]
+
+
+def declare(lib: C.CDLL, prefix: str) -> None:
+    """Sets argtypes/restype for the engine-shaped API under `prefix` (tgsim_ or tgo_)."""
+    vp = C.c_void_p
+
+    def f(name, res, *args):
+        fn = getattr(lib, prefix + name, None)
+        if fn is None:
+            return
+        fn.restype = res
+        fn.argtypes = list(args)
+
+    f("create", C.c_int, C.POINTER(Opts), C.POINTER(vp))
+    f("destroy", None, vp)
+    f("last_error", C.c_char_p, vp)
+    f("configure", C.c_int, vp, C.c_uint32, C.POINTER(Config))
+    f("submit", C.c_int, vp, C.c_void_p, C.c_size_t)
+    f("gen_storm", C.c_int, vp, C.c_double, C.c_uint32)
+    f("step", C.c_int, vp, C.c_uint32)
+    f("step_sim", C.c_int, vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), vp, C.c_size_t,
+      C.POINTER(C.c_uint64))
+    f("deliver", C.c_int, vp, vp, C.c_size_t)
+    f("sim_capacity", C.c_int64, vp)
+    f("drain", C.c_int64, vp, C.c_void_p, C.c_size_t)
+    f("pending_deliveries", C.c_int64, vp)
+    f("verdicts", C.c_int64, vp, C.c_void_p, C.c_size_t)
+    f("stats", C.c_int, vp, C.POINTER(Stats))
+    f("signal", C.c_int64, vp, C.c_uint32, C.c_uint32)
+    f("barrier_poll", C.c_int, vp, C.c_uint32, C.c_uint64)
+    f("sim_kernel_ms", C.c_double, vp, C.POINTER(C.c_uint64), C.c_int)
+    f("stream", vp, vp)
+    f("abi_version", C.c_uint32)
+    f("offered", C.c_int64, vp, C.c_void_p, C.c_size_t)

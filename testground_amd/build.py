@@ -1,0 +1,64 @@
+"""Build helpers: compile libtgsim.so for gfx950 in-tree and the CPU oracle.
+
+The product library is built with ``hipcc --offload-arch=gfx950`` straight into
+``testground_amd/libtgsim.so`` so that it travels to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libtgsim.so"
+SOURCES = [CSRC / "tgsim_kernels.hip", CSRC / "tgsim_engine.cpp"]
+HEADERS = [CSRC / "tgsim_internal.h", CSRC / "tgsim_launch.h", ROOT / "include" / "tgsim.h"]
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "build" / "libtgoracle.so"
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> Path:
+    """Compiles the HIP engine (kernels + host runtime) into libtgsim.so."""
+    if not force and not _stale(LIB, SOURCES + HEADERS):
+        return LIB
+    objs = []
+    build_dir = PKG / "build"
+    build_dir.mkdir(exist_ok=True)
+    for src in SOURCES:
+        obj = build_dir / (src.stem + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+               "-Wno-unused-result", "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(str(obj))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> Path:
+    """Compiles the CPU golden model (test infrastructure)."""
+    if force or _stale(ORACLE_LIB, [ORACLE_DIR / "tgoracle.c", ORACLE_DIR / "tgoracle.h", ROOT / "include" / "tgsim.h"]):
+        subprocess.run(["make", "-C", str(ORACLE_DIR), "-B" if force else "all"], check=True,
+                       stdout=subprocess.DEVNULL)
+    return ORACLE_LIB
+
+
+if __name__ == "__main__":
+    build_engine(force=True, verbose=True)
+    build_oracle(force=True)

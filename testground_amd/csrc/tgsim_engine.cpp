@@ -1,0 +1,968 @@
+// tgsim_engine.cpp — host runtime of libtgsim.so: the C ABI of include/tgsim.h.
+//
+// Replaces the reference sidecar's netlink programming (pkg/sidecar/link.go, route.go,
+// docker_network.go) with compiled SoA state on the GPU, and the kernel data path with the HIP
+// kernels of tgsim_kernels.hip.  Configuration is compiled on the host exactly as netlink v1.1.0
+// + the kernel would install it, staged, and scattered into HBM by the
+// config-apply kernel at the next step.
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "tgsim_launch.h"
+
+using namespace tgsim;
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// netlink / kernel unit conversions (link.go:143-183 and netlink v1.1.0 NewNetem/NewHtbClass).
+
+uint32_t go_float_to_u32(double x) {  // Go on amd64: CVTTSD2SQ then low 32 bits
+  if (!(x > -9.2233720368547758e18 && x < 9.2233720368547758e18)) return 0;
+  return static_cast<uint32_t>(static_cast<int64_t>(x));
+}
+
+uint32_t pct_to_u32(float pct) {  // netlink Percentage2u32 (float32 arithmetic)
+  if (pct == 100.0f) return 0xFFFFFFFFu;
+  volatile float frac = pct / 100.0f;
+  volatile float scaled = 4294967296.0f * frac;
+  return go_float_to_u32(static_cast<double>(scaled));
+}
+
+uint32_t duration_us(int64_t ns) {  // link.go:143-151
+  int64_t us = ns / 1000;
+  if (us > static_cast<int64_t>(UINT32_MAX)) us = UINT32_MAX;
+  return static_cast<uint32_t>(us);
+}
+
+uint32_t us_to_ticks(uint32_t us) { return go_float_to_u32(static_cast<double>(us) * 15.625); }
+
+void psched_precompute(uint64_t rate, uint32_t* mult, uint32_t* shift) {
+  *mult = 1;
+  *shift = 0;
+  if (!rate) return;
+  uint64_t factor = 1000000000ull;
+  for (;;) {
+    *mult = static_cast<uint32_t>(factor / rate);
+    if ((*mult & 0x80000000u) || (factor & 0x8000000000000000ull)) return;
+    factor <<= 1;
+    ++*shift;
+  }
+}
+
+struct Compiled {
+  SrcParams p;     // rule_off/rule_n/allow_ext left for the caller
+  bool corrupt_attr, reorder_attr, corr_attr;
+  uint32_t rho_dup_new, rho_cor_new, rho_reo_new, thr_cor_new;
+};
+
+Compiled compile_shape(const tgsim_shape& s) {
+  Compiled c;
+  memset(&c, 0, sizeof c);
+  const uint32_t lat_us = duration_us(s.latency_ns), jit_us = duration_us(s.jitter_ns);
+  const uint32_t lat_ticks = us_to_ticks(lat_us);
+  const uint32_t jit_ticks = lat_ticks ? us_to_ticks(jit_us) : jit_us;
+  c.p.lat_ns = static_cast<uint64_t>(lat_ticks) << 6;
+  int32_t sigma = static_cast<int32_t>(static_cast<uint32_t>(static_cast<uint64_t>(jit_ticks) << 6));
+  if (static_cast<uint32_t>(sigma) == 0x80000000u) sigma = 0x7FFFFFFF;
+  c.p.sigma = sigma;
+  c.p.thr_loss = pct_to_u32(s.loss);
+  c.p.thr_dup = pct_to_u32(s.duplicate);
+  c.p.thr_reo = pct_to_u32(s.reorder);
+  c.thr_cor_new = pct_to_u32(s.corrupt);
+  c.rho_dup_new = c.p.thr_dup ? pct_to_u32(s.duplicate_corr) : 0;
+  c.rho_cor_new = pct_to_u32(s.corrupt_corr);
+  c.rho_reo_new = pct_to_u32(s.reorder_corr);
+  c.corrupt_attr = c.thr_cor_new != 0;
+  c.reorder_attr = c.p.thr_reo != 0;
+  c.corr_attr = c.rho_dup_new != 0;
+  const uint64_t rate_bytes = (s.bandwidth_bps ? s.bandwidth_bps : UINT64_MAX) / 8;
+  const uint32_t buffer = go_float_to_u32(static_cast<double>(rate_bytes) / 1e9 + 1600.0);
+  const uint32_t buffer_us = go_float_to_u32(1e6 * (static_cast<double>(buffer) / static_cast<double>(rate_bytes)));
+  c.p.burst_ns = static_cast<uint64_t>(us_to_ticks(buffer_us)) << 6;
+  uint32_t mult, shift;
+  psched_precompute(static_cast<uint32_t>(rate_bytes), &mult, &shift);  // TcRateSpec.Rate is u32
+  c.p.mult = mult;
+  c.p.shift_ext = shift;
+  return c;
+}
+
+// Philox on the host (initial correlation state of init_crandom()).
+void philox_host(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t r[4]) {
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c0;
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c2;
+    const uint32_t n0 = static_cast<uint32_t>(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = static_cast<uint32_t>(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0;
+    c1 = static_cast<uint32_t>(p1);
+    c2 = n2;
+    c3 = static_cast<uint32_t>(p0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  r[0] = c0; r[1] = c1; r[2] = c2; r[3] = c3;
+}
+
+// Longest-prefix-match rule set -> sorted disjoint intervals carrying the winning action.
+std::vector<Interval> compile_rules(const std::map<uint64_t, uint8_t>& rules) {
+  struct R { uint64_t lo, hi; uint32_t len, act; };
+  std::vector<R> rs;
+  for (const auto& kv : rules) {
+    const uint32_t net = static_cast<uint32_t>(kv.first >> 8), len = kv.first & 0xFF;
+    const uint64_t size = len == 0 ? (1ull << 32) : (1ull << (32 - len));
+    rs.push_back({net, static_cast<uint64_t>(net) + size - 1, len, kv.second});
+  }
+  std::sort(rs.begin(), rs.end(), [](const R& a, const R& b) { return a.lo != b.lo ? a.lo < b.lo : a.len < b.len; });
+  std::vector<Interval> out;
+  auto emit = [&](uint64_t lo, uint64_t hi, uint32_t act) {
+    if (lo > hi || act == TGSIM_ACCEPT) return;
+    if (!out.empty() && out.back().act == act && static_cast<uint64_t>(out.back().hi) + 1 == lo)
+      out.back().hi = static_cast<uint32_t>(hi);
+    else
+      out.push_back({static_cast<uint32_t>(lo), static_cast<uint32_t>(hi), act});
+  };
+  struct Frame { uint64_t hi; uint32_t act; };
+  std::vector<Frame> stk;
+  uint64_t cur = 0;
+  for (const R& r : rs) {
+    while (!stk.empty() && stk.back().hi < r.lo) {
+      emit(cur, stk.back().hi, stk.back().act);
+      cur = stk.back().hi + 1;
+      stk.pop_back();
+    }
+    if (r.lo > cur) emit(cur, r.lo - 1, stk.empty() ? TGSIM_ACCEPT : stk.back().act);
+    cur = r.lo;
+    stk.push_back({r.hi, r.act});
+  }
+  while (!stk.empty()) {
+    emit(cur, stk.back().hi, stk.back().act);
+    cur = stk.back().hi + 1;
+    stk.pop_back();
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t c = n < 64 ? 64 : n + n / 4;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
+    if (e == hipSuccess) cap = c;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostSrc {
+  SrcParams p;          // installed netem/HTB parameters (rule_off/rule_n filled at flush)
+  uint32_t shape_epoch = 0;
+  bool allow_ext = false;
+  std::map<uint64_t, uint8_t> rules;  // (net << 8 | len) -> Reject/Drop
+  uint32_t patch_mask = 0;            // pending state patch (CfgPatch.mask)
+  uint32_t last[3] = {0, 0, 0};
+  bool dirty = false;
+};
+
+struct StagedPkt {
+  tgsim_pkt p;
+  uint64_t idx;
+};
+
+}  // namespace
+
+struct tgsim_engine_s {
+  tgsim_opts o{};
+  std::string err;
+  int dev = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint32_t S = 0, N = 0;
+  uint64_t now_tick = 0;
+  uint32_t key0 = 0, key1 = 0;
+
+  std::vector<uint8_t> enabled;
+  std::vector<uint32_t> ip;
+  std::vector<HostSrc> src;
+  bool peers_dirty = true, rules_dirty = true, any_patch = false, params_dirty = true;
+  std::vector<uint32_t> counters = std::vector<uint32_t>(kStates, 0);
+  std::vector<uint64_t> counters64 = std::vector<uint64_t>(kStates, 0);
+
+  DevBuf<SrcParams> d_params;
+  DevBuf<SrcState> d_state;
+  DevBuf<uint8_t> d_enabled;
+  DevBuf<uint32_t> d_ip;
+  DevBuf<Interval> d_rules;
+  DevBuf<uint4> d_heap;
+  DevBuf<uint64_t> d_ring;
+  DevBuf<CfgPatch> d_patch;
+  DevBuf<uint32_t> d_gen_seq;
+
+  // step input
+  std::vector<StagedPkt> staged;
+  std::vector<uint64_t> perm;  // internal index -> submit index (empty: identity)
+  struct GenWindow {
+    DevBuf<uint64_t> off;
+    DevBuf<InRec> in;
+    uint64_t n = 0;
+    uint32_t ticks = 0;
+  };
+  std::vector<GenWindow> gen_q;   // device-generated traffic, one window per future step
+  std::vector<GenWindow> gen_free;
+  uint64_t gen_q_ticks = 0;
+  uint64_t n_in = 0;
+  DevBuf<uint64_t> d_off, d_cnt, d_blk, d_tot;
+  DevBuf<InRec> d_in;
+  DevBuf<uint8_t> d_verdict;
+  uint64_t n_verdict = 0;
+  std::vector<uint64_t> last_perm;
+
+  // step output
+  DevBuf<tgsim_delivery> d_emit;
+  DevBuf<uint32_t> d_emit_n;
+  DevBuf<unsigned long long> d_rank;  // [0..7] counts, [8..15] offsets
+  DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
+  DevBuf<uint64_t> d_dcnt, d_doff, d_dcur, d_dblk, d_dtot;
+  DevBuf<uint8_t> d_sortkeys;
+  DevBuf<tgsim_delivery> d_drain;
+  uint64_t drain_head = 0, drain_n = 0;
+  DevBuf<unsigned long long> d_stats;
+
+  double sim_ms = 0;
+  uint64_t sim_launches = 0;
+
+  int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+  int hip(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return fail(-EIO, "%s: %s", what, hipGetErrorString(e));
+  }
+};
+
+using Eng = tgsim_engine_s;
+
+#define HIPCHK(expr)                              \
+  do {                                            \
+    int _rc = E->hip((expr), #expr);              \
+    if (_rc) return _rc;                          \
+  } while (0)
+
+namespace {
+
+void reset_source(Eng* E, uint32_t s) {
+  HostSrc& h = E->src[s];
+  tgsim_shape zero;
+  memset(&zero, 0, sizeof zero);
+  Compiled c = compile_shape(zero);  // HTB class created with Rate MaxUint64 (link.go:98-105)
+  const uint32_t keep_off = h.p.rule_off, keep_n = h.p.rule_n;
+  h.p = c.p;
+  h.p.rule_off = keep_off;
+  h.p.rule_n = keep_n;
+  h.p.thr_cor = 0;
+  h.p.rho_dup = h.p.rho_cor = h.p.rho_reo = 0;
+  h.patch_mask |= 1u | 2u | 4u | 8u;
+  h.last[0] = h.last[1] = h.last[2] = 0;
+  h.dirty = true;
+  E->any_patch = true;
+}
+
+int flush_config(Eng* E) {
+  if (E->peers_dirty) {
+    HIPCHK(hipMemcpyAsync(E->d_enabled.p, E->enabled.data(), E->N, hipMemcpyHostToDevice, E->st));
+    HIPCHK(hipMemcpyAsync(E->d_ip.p, E->ip.data(), sizeof(uint32_t) * E->N, hipMemcpyHostToDevice, E->st));
+    E->peers_dirty = false;
+  }
+  if (E->rules_dirty) {
+    std::vector<Interval> all;
+    for (uint32_t s = 0; s < E->S; ++s) {
+      HostSrc& h = E->src[s];
+      std::vector<Interval> iv = compile_rules(h.rules);
+      h.p.rule_off = static_cast<uint32_t>(all.size());
+      h.p.rule_n = static_cast<uint32_t>(iv.size());
+      all.insert(all.end(), iv.begin(), iv.end());
+    }
+    if (all.empty()) all.push_back({0, 0, 0});
+    HIPCHK(E->d_rules.ensure(all.size()));
+    HIPCHK(hipMemcpyAsync(E->d_rules.p, all.data(), sizeof(Interval) * all.size(), hipMemcpyHostToDevice, E->st));
+    E->rules_dirty = false;
+    E->params_dirty = true;
+  }
+  if (E->params_dirty) {
+    std::vector<SrcParams> ps(E->S);
+    for (uint32_t s = 0; s < E->S; ++s) {
+      ps[s] = E->src[s].p;
+      ps[s].shift_ext = (ps[s].shift_ext & 0xFFu) | (E->src[s].allow_ext ? 0x100u : 0u);
+    }
+    HIPCHK(hipMemcpyAsync(E->d_params.p, ps.data(), sizeof(SrcParams) * E->S, hipMemcpyHostToDevice, E->st));
+    HIPCHK(hipStreamSynchronize(E->st));
+    E->params_dirty = false;
+  }
+  if (E->any_patch) {
+    std::vector<CfgPatch> patches;
+    for (uint32_t s = 0; s < E->S; ++s) {
+      HostSrc& h = E->src[s];
+      if (!h.dirty) continue;
+      CfgPatch c;
+      memset(&c, 0, sizeof c);
+      c.s = s;
+      c.mask = h.patch_mask;
+      c.last_dup = h.last[0];
+      c.last_cor = h.last[1];
+      c.last_reo = h.last[2];
+      c.p = h.p;
+      c.p.shift_ext = (c.p.shift_ext & 0xFFu) | (h.allow_ext ? 0x100u : 0u);
+      patches.push_back(c);
+      h.dirty = false;
+      h.patch_mask = 0;
+    }
+    if (!patches.empty()) {
+      HIPCHK(E->d_patch.ensure(patches.size()));
+      HIPCHK(hipMemcpyAsync(E->d_patch.p, patches.data(), sizeof(CfgPatch) * patches.size(),
+                            hipMemcpyHostToDevice, E->st));
+      launch_apply_cfg(E->d_patch.p, static_cast<uint32_t>(patches.size()), E->d_params.p, E->d_state.p, E->st);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(E->st));
+    }
+    E->any_patch = false;
+  }
+  return 0;
+}
+
+// Builds the CSR input of the step from the host-staged packets.
+int stage_host_input(Eng* E, uint32_t n_ticks) {
+  std::vector<StagedPkt>& v = E->staged;
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i].p.tick >= n_ticks)
+      return E->fail(-EINVAL, "packet %zu: tick %u beyond step of %u ticks", i, v[i].p.tick, n_ticks);
+  std::stable_sort(v.begin(), v.end(), [](const StagedPkt& a, const StagedPkt& b) {
+    if (a.p.src != b.p.src) return a.p.src < b.p.src;
+    if (a.p.tick != b.p.tick) return a.p.tick < b.p.tick;
+    return a.p.seq < b.p.seq;
+  });
+  std::vector<uint64_t> off(E->S + 1, 0);
+  std::vector<InRec> recs(v.size());
+  E->perm.assign(v.size(), 0);
+  for (size_t i = 0; i < v.size(); ++i) {
+    off[v[i].p.src - E->o.shard_begin + 1]++;
+    recs[i].dst = v[i].p.dst;
+    recs[i].seq = v[i].p.seq;
+    recs[i].tick = v[i].p.tick;
+    recs[i].len = v[i].p.len;
+    E->perm[i] = v[i].idx;
+  }
+  for (uint32_t s = 0; s < E->S; ++s) off[s + 1] += off[s];
+  E->n_in = v.size();
+  HIPCHK(E->d_off.ensure(E->S + 1));
+  HIPCHK(E->d_in.ensure(E->n_in ? E->n_in : 1));
+  HIPCHK(hipMemcpyAsync(E->d_off.p, off.data(), sizeof(uint64_t) * (E->S + 1), hipMemcpyHostToDevice, E->st));
+  if (E->n_in)
+    HIPCHK(hipMemcpyAsync(E->d_in.p, recs.data(), sizeof(InRec) * E->n_in, hipMemcpyHostToDevice, E->st));
+  HIPCHK(hipStreamSynchronize(E->st));
+  E->staged.clear();
+  return 0;
+}
+
+// Device exclusive scan of cnt[0..n) into off[0..n] (off[n] = total); returns total on host.
+int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uint64_t>& blk,
+                DevBuf<uint64_t>& tot, uint64_t n, uint64_t* total) {
+  HIPCHK(off.ensure(n + 1));
+  HIPCHK(blk.ensure((n + 1023) / 1024 + 1));
+  HIPCHK(tot.ensure(1));
+  launch_scan(cnt.p, off.p, n, blk.p, tot.p, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(off.p + n, tot.p, sizeof(uint64_t), hipMemcpyDeviceToDevice, E->st));
+  HIPCHK(hipMemcpyAsync(total, tot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
+  HIPCHK(hipStreamSynchronize(E->st));
+  return 0;
+}
+
+int run_sim(Eng* E, uint32_t n_ticks) {
+  if (!E->gen_q.empty()) {
+    if (!E->staged.empty()) return E->fail(-EBUSY, "host packets and generated traffic in one step");
+    Eng::GenWindow& w = E->gen_q.front();
+    if (n_ticks != w.ticks)
+      return E->fail(-EINVAL, "generated window spans %u ticks, step is %u", w.ticks, n_ticks);
+    std::swap(E->d_off, w.off);
+    std::swap(E->d_in, w.in);
+    E->n_in = w.n;
+    E->gen_q_ticks -= w.ticks;
+    E->gen_free.push_back(std::move(w));
+    E->gen_q.erase(E->gen_q.begin());
+    E->perm.clear();
+  } else {
+    int rc = stage_host_input(E, n_ticks);
+    if (rc) return rc;
+  }
+  int rc = flush_config(E);
+  if (rc) return rc;
+  const uint64_t emit_cap = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;
+  HIPCHK(E->d_verdict.ensure(E->n_in ? E->n_in : 1));
+  HIPCHK(E->d_emit.ensure(emit_cap));
+  HIPCHK(E->d_emit_n.ensure(E->S));
+  SimArgs a;
+  a.params = E->d_params.p;
+  a.state = E->d_state.p;
+  a.enabled = E->d_enabled.p;
+  a.ip = E->d_ip.p;
+  a.rules = E->d_rules.p;
+  a.off = E->d_off.p;
+  a.in = E->d_in.p;
+  a.verdict = E->d_verdict.p;
+  a.heap = E->d_heap.p;
+  a.ring = E->d_ring.p;
+  a.emit = E->d_emit.p;
+  a.emit_n = E->d_emit_n.p;
+  a.stats = E->d_stats.p;
+  a.key0 = E->key0;
+  a.key1 = E->key1;
+  a.n_src = E->S;
+  a.shard_begin = E->o.shard_begin;
+  a.n_peers = E->N;
+  a.queue_limit = E->o.queue_limit;
+  a.tick_ns = E->o.tick_ns;
+  a.t0_ns = E->now_tick * E->o.tick_ns;
+  a.horizon_ns = (E->now_tick + n_ticks) * E->o.tick_ns + E->o.lookahead_ns;
+  HIPCHK(hipEventRecord(E->ev0, E->st));
+  launch_sim(a, (E->S + kWave - 1) / kWave, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(E->ev1, E->st));
+  E->n_verdict = E->n_in;
+  E->last_perm.swap(E->perm);
+  E->perm.clear();
+  E->now_tick += n_ticks;
+  return 0;
+}
+
+int finish_sim_timing(Eng* E) {
+  HIPCHK(hipEventSynchronize(E->ev1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, E->ev0, E->ev1));
+  E->sim_ms += ms;
+  E->sim_launches++;
+  unsigned long long errw = 0;
+  HIPCHK(hipMemcpy(&errw, E->d_stats.p + kStErr, sizeof errw, hipMemcpyDeviceToHost));
+  if (errw & kErrTimeOverflow) return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
+  return 0;
+}
+
+int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap,
+          uint64_t* counts) {
+  RouteArgsHost h;
+  memset(&h, 0, sizeof h);
+  h.emit = E->d_emit.p;
+  h.emit_n = E->d_emit_n.p;
+  h.off = E->d_off.p;
+  h.n_src = E->S;
+  h.n_ranks = n_ranks;
+  for (uint32_t i = 0; i <= n_ranks && i < 9; ++i) h.bounds[i] = bounds[i];
+  HIPCHK(E->d_rank.ensure(16));
+  HIPCHK(hipMemsetAsync(E->d_rank.p, 0, 16 * sizeof(unsigned long long), E->st));
+  h.rank_cnt = E->d_rank.p;
+  h.rank_off = E->d_rank.p + 8;
+  h.out = out;
+  launch_route(h, 0, E->st);
+  HIPCHK(hipGetLastError());
+  unsigned long long cnt[8] = {0};
+  HIPCHK(hipMemcpyAsync(cnt, E->d_rank.p, sizeof cnt, hipMemcpyDeviceToHost, E->st));
+  HIPCHK(hipStreamSynchronize(E->st));
+  unsigned long long offs[8] = {0};
+  uint64_t total = 0;
+  for (uint32_t r = 0; r < n_ranks; ++r) {
+    offs[r] = total;
+    total += cnt[r];
+    counts[r] = cnt[r];
+  }
+  if (total > out_cap) return E->fail(-ENOSPC, "route: %llu records exceed capacity %zu",
+                                      static_cast<unsigned long long>(total), out_cap);
+  HIPCHK(hipMemcpyAsync(E->d_rank.p + 8, offs, sizeof offs, hipMemcpyHostToDevice, E->st));
+  HIPCHK(hipMemsetAsync(E->d_rank.p, 0, 8 * sizeof(unsigned long long), E->st));
+  launch_route(h, 1, E->st);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int deliver(Eng* E, const tgsim_delivery* in, uint64_t n) {
+  const uint32_t nd = E->S;  // destinations owned by this shard
+  HIPCHK(E->d_dcnt.ensure(nd));
+  HIPCHK(E->d_dcur.ensure(nd));
+  HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * nd, E->st));
+  HIPCHK(hipMemsetAsync(E->d_dcur.p, 0, sizeof(uint64_t) * nd, E->st));
+  launch_dst_hist(in, n, E->o.shard_begin, E->d_dcnt.p, E->st);
+  HIPCHK(hipGetLastError());
+  uint64_t total = 0;
+  int rc = scan_counts(E, E->d_dcnt, E->d_doff, E->d_dblk, E->d_dtot, nd, &total);
+  if (rc) return rc;
+  if (total != n) return E->fail(-EINVAL, "deliver: %llu of %llu records address other shards",
+                                 static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
+  HIPCHK(E->d_scatter.ensure(n ? n : 1));
+  HIPCHK(E->d_sortkeys.ensure((2 * n + 1) * sort_key_bytes()));
+  launch_dst_scatter(in, n, E->o.shard_begin, E->d_doff.p, E->d_dcur.p, E->d_scatter.p, E->st);
+  HIPCHK(hipGetLastError());
+  tgsim_delivery* dst;
+  if (E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) {
+    HIPCHK(E->d_sorted.ensure(n ? n : 1));
+    dst = E->d_sorted.p;
+  } else {
+    const uint64_t need = E->drain_head + E->drain_n + n;
+    if (need > E->d_drain.cap) {
+      // grow, compacting the undrained tail to the front
+      DevBuf<tgsim_delivery> nb;
+      HIPCHK(nb.ensure(E->drain_n + n));
+      if (E->drain_n)
+        HIPCHK(hipMemcpyAsync(nb.p, E->d_drain.p + E->drain_head, sizeof(tgsim_delivery) * E->drain_n,
+                              hipMemcpyDeviceToDevice, E->st));
+      HIPCHK(hipStreamSynchronize(E->st));
+      E->d_drain.release();
+      E->d_drain = nb;
+      E->drain_head = 0;
+    }
+    dst = E->d_drain.p + E->drain_head + E->drain_n;
+    E->drain_n += n;
+  }
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->d_sortkeys.p, E->st);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+Eng* as_eng(void* e) { return static_cast<Eng*>(e); }
+
+}  // namespace
+
+// ================================================================================================
+extern "C" {
+
+uint32_t tgsim_abi_version(void) { return TGSIM_ABI_VERSION; }
+
+int tgsim_create(const tgsim_opts* opts, void** out) {
+  if (!opts || !out) return -EINVAL;
+  *out = nullptr;
+  if (opts->abi_version != TGSIM_ABI_VERSION) return -EPROTO;
+  if (opts->n_peers == 0) return -EINVAL;
+  Eng* E = new Eng();
+  E->o = *opts;
+  if (E->o.shard_begin == 0 && E->o.shard_end == 0) E->o.shard_end = E->o.n_peers;
+  if (E->o.shard_begin >= E->o.shard_end || E->o.shard_end > E->o.n_peers) {
+    delete E;
+    return -EINVAL;
+  }
+  if (!E->o.tick_ns) E->o.tick_ns = 1000;
+  if (!E->o.queue_limit) E->o.queue_limit = 1000;
+  if (E->o.queue_limit > kHeapCap) {
+    delete E;
+    return -EINVAL;
+  }
+  if (!E->o.subnet_base) E->o.subnet_base = 16u << 24;
+  E->N = E->o.n_peers;
+  E->S = E->o.shard_end - E->o.shard_begin;
+  E->key0 = static_cast<uint32_t>(E->o.seed);
+  E->key1 = static_cast<uint32_t>(E->o.seed >> 32);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    delete E;
+    return -ENODEV;  // no GPU: the engine has no CPU fallback by design
+  }
+  E->dev = E->o.device >= 0 ? E->o.device : 0;
+  if (E->o.device < 0) (void)hipGetDevice(&E->dev);
+  int rc = 0;
+  auto bail = [&](int code) {
+    tgsim_destroy(E);
+    return code;
+  };
+  if ((rc = E->hip(hipSetDevice(E->dev), "hipSetDevice"))) return bail(rc);
+  if ((rc = E->hip(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking), "stream"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreate(&E->ev0), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreate(&E->ev1), "event"))) return bail(rc);
+  E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
+  E->ip.resize(E->N);
+  for (uint32_t i = 0; i < E->N; ++i) E->ip[i] = E->o.subnet_base + 2 + i;
+  E->src.resize(E->S);
+  for (uint32_t s = 0; s < E->S; ++s) {
+    reset_source(E, s);
+    E->src[s].patch_mask = 0;
+    E->src[s].dirty = false;
+  }
+  E->any_patch = false;
+  const size_t nwg = (E->S + kWave - 1) / kWave;
+  if ((rc = E->hip(E->d_params.ensure(E->S), "alloc params"))) return bail(rc);
+  if ((rc = E->hip(E->d_state.ensure(E->S), "alloc state"))) return bail(rc);
+  if ((rc = E->hip(E->d_enabled.ensure(E->N), "alloc enabled"))) return bail(rc);
+  if ((rc = E->hip(E->d_ip.ensure(E->N), "alloc ip"))) return bail(rc);
+  if ((rc = E->hip(E->d_heap.ensure(nwg * kHeapCap * kWave), "alloc heap"))) return bail(rc);
+  if ((rc = E->hip(E->d_ring.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc ring"))) return bail(rc);
+  if ((rc = E->hip(E->d_gen_seq.ensure(E->S), "alloc gen_seq"))) return bail(rc);
+  if ((rc = E->hip(E->d_stats.ensure(kStSlots), "alloc stats"))) return bail(rc);
+  if ((rc = E->hip(E->d_off.ensure(E->S + 1), "alloc off"))) return bail(rc);
+  if ((rc = E->hip(E->d_in.ensure(1), "alloc in"))) return bail(rc);
+  if ((rc = E->hip(hipMemset(E->d_state.p, 0, sizeof(SrcState) * E->S), "memset"))) return bail(rc);
+  if ((rc = E->hip(hipMemset(E->d_gen_seq.p, 0, sizeof(uint32_t) * E->S), "memset"))) return bail(rc);
+  if ((rc = E->hip(hipMemset(E->d_stats.p, 0, sizeof(unsigned long long) * kStSlots), "memset"))) return bail(rc);
+  E->peers_dirty = E->rules_dirty = E->params_dirty = true;
+  if ((rc = flush_config(E))) return bail(rc);
+  *out = E;
+  return 0;
+}
+
+void tgsim_destroy(void* e) {
+  Eng* E = as_eng(e);
+  if (!E) return;
+  (void)hipSetDevice(E->dev);
+  if (E->st) (void)hipStreamSynchronize(E->st);
+  DevBuf<int> dummy;
+  (void)dummy;
+  E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
+  E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
+  E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rank.release();
+  E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
+  E->d_doff.release(); E->d_dcur.release(); E->d_dblk.release(); E->d_dtot.release();
+  E->d_sortkeys.release(); E->d_drain.release(); E->d_stats.release();
+  for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
+  for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
+  if (E->ev0) (void)hipEventDestroy(E->ev0);
+  if (E->ev1) (void)hipEventDestroy(E->ev1);
+  if (E->st) (void)hipStreamDestroy(E->st);
+  delete E;
+}
+
+const char* tgsim_last_error(const void* e) {
+  return e ? static_cast<const Eng*>(e)->err.c_str() : "null engine";
+}
+
+// DockerNetwork.ConfigureNetwork (docker_network.go:51-148), netlink replaced by staged state.
+int tgsim_configure(void* e, uint32_t peer, const tgsim_config* cfg) {
+  Eng* E = as_eng(e);
+  if (!E || !cfg) return -EINVAL;
+  if (peer >= E->N) return E->fail(-EINVAL, "peer %u out of range", peer);
+  const char* net = cfg->network ? cfg->network : "";
+  if (strcmp(net, "default") != 0) return E->fail(-EINVAL, "unsupported network: %s", net);
+  const bool owned = peer >= E->o.shard_begin && peer < E->o.shard_end;
+  const uint32_t s = peer - E->o.shard_begin;
+  if (owned) {  // handleRoutingPolicy (route.go:102-117): AllowAll enables, anything else disables
+    const bool allow = cfg->routing_policy == TGSIM_ALLOW_ALL;
+    if (allow != E->src[s].allow_ext) {
+      E->src[s].allow_ext = allow;
+      E->src[s].dirty = true;
+      E->any_patch = true;
+    }
+  }
+  if (!cfg->enable) {  // NetworkDisconnect; shape and rules untouched
+    if (E->enabled[peer]) {
+      E->enabled[peer] = 0;
+      E->peers_dirty = true;
+    }
+    return 0;
+  }
+  const bool reconnect = !E->enabled[peer] || (cfg->has_ipv4 && cfg->ipv4 != E->ip[peer]);
+  if (cfg->has_ipv4 && cfg->ipv4 != E->ip[peer]) {
+    E->ip[peer] = cfg->ipv4;
+    E->peers_dirty = true;
+  }
+  if (!E->enabled[peer]) {
+    E->enabled[peer] = 1;
+    E->peers_dirty = true;
+  }
+  if (!owned) return 0;
+  HostSrc& h = E->src[s];
+  if (reconnect) reset_source(E, s);  // NewNetlinkLink: fresh HTB class and netem qdisc
+  // link.Shape (link.go:155-183): HTB ClassChange + netem QdiscChange (netem_change semantics)
+  const Compiled c = compile_shape(cfg->shape);
+  h.shape_epoch++;
+  uint32_t rnd[4];
+  philox_host(peer, 0xFFFFFFFEu, h.shape_epoch, 3, E->key0, E->key1, rnd);  // init_crandom()
+  h.p.lat_ns = c.p.lat_ns;
+  h.p.sigma = c.p.sigma;
+  h.p.thr_loss = c.p.thr_loss;
+  h.p.thr_dup = c.p.thr_dup;
+  h.p.thr_reo = c.p.thr_reo;
+  h.p.burst_ns = c.p.burst_ns;
+  h.p.mult = c.p.mult;
+  h.p.shift_ext = c.p.shift_ext;
+  if (c.corr_attr) {
+    h.p.rho_dup = c.rho_dup_new;
+    h.last[0] = rnd[0];
+    h.patch_mask |= 1u;
+  }
+  if (c.corrupt_attr) {  // absent attribute: q->corrupt and its correlation persist
+    h.p.thr_cor = c.thr_cor_new;
+    h.p.rho_cor = c.rho_cor_new;
+    h.last[1] = rnd[1];
+    h.patch_mask |= 2u;
+  }
+  if (c.reorder_attr) {
+    h.p.rho_reo = c.rho_reo_new;
+    h.last[2] = rnd[2];
+    h.patch_mask |= 4u;
+  }
+  h.dirty = true;
+  E->any_patch = true;
+  // link.AddRules (link.go:187-217): cumulative; Accept deletes; host bits -> EINVAL
+  for (uint32_t i = 0; i < cfg->n_rules; ++i) {
+    const tgsim_rule& r = cfg->rules[i];
+    const bool bad_len = r.len > 32;
+    const uint32_t mask = (!bad_len && r.len) ? (0xFFFFFFFFu << (32 - r.len)) : 0u;
+    const bool bad = bad_len || (r.prefix & ~mask) != 0;
+    const uint64_t key = (static_cast<uint64_t>(r.prefix) << 8) | r.len;
+    if (r.action == TGSIM_ACCEPT) {
+      if (!bad && h.rules.erase(key)) E->rules_dirty = true;
+      continue;
+    }
+    if (r.action != TGSIM_REJECT && r.action != TGSIM_DROP)
+      return E->fail(-EINVAL, "invalid filter action %u", r.action);
+    if (bad) return E->fail(-EINVAL, "invalid argument");
+    auto it = h.rules.find(key);
+    if (it == h.rules.end() || it->second != r.action) {
+      h.rules[key] = r.action;
+      E->rules_dirty = true;
+    }
+  }
+  return 0;
+}
+
+int tgsim_submit(void* e, const tgsim_pkt* pkts, size_t n) {
+  Eng* E = as_eng(e);
+  if (!E || (!pkts && n)) return -EINVAL;
+  if (!E->gen_q.empty()) return E->fail(-EBUSY, "generated traffic already pending for the next step");
+  for (size_t i = 0; i < n; ++i) {
+    if (pkts[i].src < E->o.shard_begin || pkts[i].src >= E->o.shard_end)
+      return E->fail(-EINVAL, "packet %zu: src %u not owned by this shard", i, pkts[i].src);
+    if (pkts[i].dst != TGSIM_EXTERNAL && pkts[i].dst >= E->N)
+      return E->fail(-EINVAL, "packet %zu: dst %u out of range", i, pkts[i].dst);
+  }
+  const uint64_t base = E->staged.size();
+  for (size_t i = 0; i < n; ++i) E->staged.push_back({pkts[i], base + i});
+  return 0;
+}
+
+int tgsim_gen_storm(void* e, double lambda, uint32_t n_ticks) {
+  Eng* E = as_eng(e);
+  if (!E || !(lambda >= 0.0) || lambda > 4.0 || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
+  if (!E->staged.empty()) return E->fail(-EBUSY, "host packets already pending for the next step");
+  HIPCHK(hipSetDevice(E->dev));
+  GenArgsHost g;
+  double p = std::exp(-lambda), F = p;
+  for (int k = 0; k < 16; ++k) {
+    const double t = F * 4294967296.0;
+    g.tab[k] = t >= 4294967295.0 ? 0xFFFFFFFFu : static_cast<uint32_t>(t);
+    p = p * lambda / static_cast<double>(k + 1);
+    F = F + p;
+  }
+  g.k0 = E->key0 ^ 0x9E3779B9u;
+  g.k1 = E->key1 ^ 0x7F4A7C15u;
+  g.n_src = E->S;
+  g.shard_begin = E->o.shard_begin;
+  g.n_peers = E->N;
+  g.n_ticks = n_ticks;
+  g.now_tick = E->now_tick + E->gen_q_ticks;  // windows queue up back to back
+  Eng::GenWindow w;
+  if (!E->gen_free.empty()) {
+    w = std::move(E->gen_free.back());
+    E->gen_free.pop_back();
+  }
+  HIPCHK(E->d_cnt.ensure(E->S));
+  launch_gen(g, E->d_cnt.p, nullptr, nullptr, nullptr, 0, E->st);
+  HIPCHK(hipGetLastError());
+  uint64_t total = 0;
+  int rc = scan_counts(E, E->d_cnt, w.off, E->d_blk, E->d_tot, E->S, &total);
+  if (rc) return rc;
+  HIPCHK(w.in.ensure(total ? total : 1));
+  launch_gen(g, nullptr, w.off.p, E->d_gen_seq.p, w.in.p, 1, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(E->st));
+  w.n = total;
+  w.ticks = n_ticks;
+  E->gen_q_ticks += n_ticks;
+  E->gen_q.push_back(std::move(w));
+  return 0;
+}
+
+int64_t tgsim_sim_capacity(void* e) {
+  Eng* E = as_eng(e);
+  if (!E) return -EINVAL;
+  const uint64_t n = !E->gen_q.empty() ? E->gen_q.front().n : E->staged.size();
+  return static_cast<int64_t>(2 * n + static_cast<uint64_t>(kHeapCap) * E->S);
+}
+
+int tgsim_step_sim(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* d_out,
+                   size_t out_cap, uint64_t* counts) {
+  Eng* E = as_eng(e);
+  if (!E || n_ticks == 0 || n_ranks == 0 || n_ranks > 8 || !bounds || !counts || (!d_out && out_cap))
+    return -EINVAL;
+  if (bounds[0] != 0 || bounds[n_ranks] != E->N) return E->fail(-EINVAL, "rank bounds must cover [0, n_peers)");
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = run_sim(E, n_ticks);
+  if (rc) return rc;
+  rc = route(E, n_ranks, bounds, static_cast<tgsim_delivery*>(d_out), out_cap, counts);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(E->st));
+  return finish_sim_timing(E);
+}
+
+int tgsim_deliver(void* e, const void* d_in, size_t n) {
+  Eng* E = as_eng(e);
+  if (!E || (!d_in && n)) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = deliver(E, static_cast<const tgsim_delivery*>(d_in), n);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(E->st));
+  return 0;
+}
+
+int tgsim_step(void* e, uint32_t n_ticks) {
+  Eng* E = as_eng(e);
+  if (!E || n_ticks == 0) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = run_sim(E, n_ticks);
+  if (rc) return rc;
+  const uint64_t cap = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;
+  HIPCHK(E->d_bucket.ensure(cap));
+  const uint32_t bounds[2] = {0, E->N};
+  uint64_t count = 0;
+  rc = route(E, 1, bounds, E->d_bucket.p, E->d_bucket.cap, &count);
+  if (rc) return rc;
+  rc = deliver(E, E->d_bucket.p, count);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(E->st));
+  return finish_sim_timing(E);
+}
+
+int64_t tgsim_drain(void* e, tgsim_delivery* out, size_t cap) {
+  Eng* E = as_eng(e);
+  if (!E || (!out && cap)) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  const uint64_t n = std::min<uint64_t>(cap, E->drain_n);
+  if (n) {
+    HIPCHK(hipMemcpy(out, E->d_drain.p + E->drain_head, sizeof(tgsim_delivery) * n, hipMemcpyDeviceToHost));
+  }
+  E->drain_head += n;
+  E->drain_n -= n;
+  if (!E->drain_n) E->drain_head = 0;
+  return static_cast<int64_t>(n);
+}
+
+int64_t tgsim_pending_deliveries(void* e) {
+  Eng* E = as_eng(e);
+  return E ? static_cast<int64_t>(E->drain_n) : -EINVAL;
+}
+
+int64_t tgsim_verdicts(void* e, uint8_t* out, size_t cap) {
+  Eng* E = as_eng(e);
+  if (!E || (!out && cap)) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  if (cap >= E->n_verdict && E->n_verdict) {
+    std::vector<uint8_t> tmp(E->n_verdict);
+    HIPCHK(hipMemcpy(tmp.data(), E->d_verdict.p, E->n_verdict, hipMemcpyDeviceToHost));
+    if (E->last_perm.empty()) {
+      memcpy(out, tmp.data(), E->n_verdict);
+    } else {
+      for (uint64_t i = 0; i < E->n_verdict; ++i) out[E->last_perm[i]] = tmp[i];
+    }
+  }
+  return static_cast<int64_t>(E->n_verdict);
+}
+
+int tgsim_stats(void* e, tgsim_stats_t* out) {
+  Eng* E = as_eng(e);
+  if (!E || !out) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  unsigned long long s[kStSlots];
+  HIPCHK(hipMemcpy(s, E->d_stats.p, sizeof s, hipMemcpyDeviceToHost));
+  memset(out, 0, sizeof *out);
+  out->offered = s[kStOffered];
+  out->scheduled = s[kStScheduled];
+  out->cloned = s[kStCloned];
+  out->corrupted = s[kStCorrupted];
+  for (int i = 0; i < 8; ++i) out->by_verdict[i] = s[kStVerdict0 + i];
+  out->bytes_scheduled = s[kStBytes];
+  out->now_tick = E->now_tick;
+  return 0;
+}
+
+int64_t tgsim_signal(void* e, uint32_t state, uint32_t n) {
+  Eng* E = as_eng(e);
+  if (!E || state >= kStates) return -EINVAL;
+  E->counters64[state] += n;
+  return static_cast<int64_t>(E->counters64[state]);
+}
+
+int tgsim_barrier_poll(void* e, uint32_t state, uint64_t target) {
+  Eng* E = as_eng(e);
+  if (!E || state >= kStates) return -EINVAL;
+  return E->counters64[state] >= target ? 1 : 0;
+}
+
+double tgsim_sim_kernel_ms(void* e, uint64_t* n, int reset) {
+  Eng* E = as_eng(e);
+  if (!E) return -1;
+  const double avg = E->sim_launches ? E->sim_ms / static_cast<double>(E->sim_launches) : 0.0;
+  if (n) *n = E->sim_launches;
+  if (reset) {
+    E->sim_ms = 0;
+    E->sim_launches = 0;
+  }
+  return avg;
+}
+
+void* tgsim_stream(void* e) {
+  Eng* E = as_eng(e);
+  return E ? static_cast<void*>(E->st) : nullptr;
+}
+
+// Host-only building blocks (no device needed): used by the CPU test-suite to check the
+// configuration compiler against the oracle.
+int tgsim_host_compile_shape(const tgsim_shape* s, uint64_t out[13]) {
+  if (!s || !out) return -EINVAL;
+  const Compiled c = compile_shape(*s);
+  out[0] = c.p.lat_ns; out[1] = static_cast<uint64_t>(static_cast<int64_t>(c.p.sigma));
+  out[2] = static_cast<uint32_t>((s->bandwidth_bps ? s->bandwidth_bps : UINT64_MAX) / 8);
+  out[3] = c.p.mult; out[4] = c.p.shift_ext & 0xFF; out[5] = c.p.burst_ns;
+  out[6] = c.p.thr_loss; out[7] = c.p.thr_dup; out[8] = c.thr_cor_new; out[9] = c.p.thr_reo;
+  out[10] = c.rho_dup_new; out[11] = c.rho_cor_new; out[12] = c.rho_reo_new;
+  return 0;
+}
+
+// rules: (prefix, len, action) triples already applied in order; writes up to cap intervals
+// (lo, hi, act) and returns the count.
+int64_t tgsim_host_compile_rules(const tgsim_rule* rules, size_t n, uint32_t* out, size_t cap) {
+  std::map<uint64_t, uint8_t> m;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t key = (static_cast<uint64_t>(rules[i].prefix) << 8) | rules[i].len;
+    if (rules[i].action == TGSIM_ACCEPT) m.erase(key);
+    else m[key] = rules[i].action;
+  }
+  const std::vector<Interval> iv = compile_rules(m);
+  for (size_t i = 0; i < iv.size() && i < cap; ++i) {
+    out[3 * i] = iv[i].lo;
+    out[3 * i + 1] = iv[i].hi;
+    out[3 * i + 2] = iv[i].act;
+  }
+  return static_cast<int64_t>(iv.size());
+}
+
+}  // extern "C"

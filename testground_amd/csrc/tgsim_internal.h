@@ -1,0 +1,88 @@
+// tgsim_internal.h — device data layout of the engine (shared by host code and HIP kernels).
+//
+// HBM layout.  All per-source arrays are indexed by the shard-local source index
+// s = src - shard_begin; per-peer tables are global (replicated on every shard).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tgsim.h"
+
+namespace tgsim {
+
+constexpr uint32_t kHeapCap = 1024;   // >= queue_limit (netem limit, max 1024)
+constexpr uint32_t kWave = 64;        // sources per simulate workgroup (lane = source)
+constexpr uint64_t kEMask = (1ull << 46) - 1;  // eligibility time field of a queued item
+constexpr uint32_t kStates = 1024;    // sync states
+
+// Compiled netem + HTB parameters of one source (64 B, read once per step).
+struct alignas(16) SrcParams {
+  uint64_t lat_ns;     // netem latency (PSCHED ticks << 6)
+  uint64_t burst_ns;   // HTB buffer (ticks << 6)
+  int32_t sigma;       // tabledist sigma (s32)
+  uint32_t mult;       // psched_ratecfg mult
+  uint32_t shift_ext;  // bits 0..7 shift, bit 8 external traffic allowed
+  uint32_t thr_loss, thr_dup, thr_cor, thr_reo;
+  uint32_t rho_dup, rho_cor, rho_reo;
+  uint32_t rule_off;   // first interval of this source's compiled FIB rules
+  uint32_t rule_n;     // number of intervals
+};
+static_assert(sizeof(SrcParams) == 64, "SrcParams must stay 64 B");
+
+// Mutable per-source state carried across steps (32 B).
+struct alignas(16) SrcState {
+  uint64_t tat;        // HTB theoretical arrival time (tokens >= 0 once now >= tat)
+  uint32_t heap_n;     // queued, not yet eligible items
+  uint32_t ring_head;  // departure ring of items given a departure time
+  uint32_t ring_n;
+  uint32_t last_dup, last_cor, last_reo;  // get_crandom() correlation state
+};
+static_assert(sizeof(SrcState) == 32, "SrcState must stay 32 B");
+
+// Offered packet as staged on the device (16 B, CSR by source, ordered by (tick, seq)).
+struct alignas(16) InRec {
+  uint32_t dst;
+  uint32_t seq;
+  uint32_t tick;      // relative to the step start
+  uint32_t len;       // bytes (low 16 bits)
+};
+
+// Compiled FIB rule interval: every address in [lo, hi] resolves to `act` (Reject or Drop).
+struct Interval {
+  uint32_t lo, hi, act;
+};
+
+// Configuration delta scattered by the config-apply kernel (K9).
+struct CfgPatch {
+  uint32_t s;          // shard-local source
+  uint32_t mask;       // bit0 last_dup, bit1 last_cor, bit2 last_reo, bit3 reset tat
+  uint32_t last_dup, last_cor, last_reo, _pad;
+  SrcParams p;
+};
+
+enum StatSlot {
+  kStOffered = 0, kStScheduled, kStCloned, kStCorrupted, kStVerdict0,  // 4..11 verdicts
+  kStBytes = 12, kStErr = 13, kStSlots = 16
+};
+constexpr uint32_t kErrTimeOverflow = 1u;
+
+struct SimArgs {
+  const SrcParams* params;
+  SrcState* state;
+  const uint8_t* enabled;   // per global peer
+  const uint32_t* ip;       // per global peer
+  const Interval* rules;
+  const uint64_t* off;      // CSR offsets of the step's offered packets (S+1)
+  const InRec* in;
+  uint8_t* verdict;         // one byte per offered packet
+  uint4* heap;              // [wg][slot][lane] interleaved, 16 B items
+  uint64_t* ring;           // [s][kHeapCap] departure times
+  tgsim_delivery* emit;     // per-source regions, base 2*off[s] + kHeapCap*s
+  uint32_t* emit_n;         // records emitted per source this step
+  unsigned long long* stats;
+  uint32_t key0, key1;
+  uint32_t n_src, shard_begin, n_peers, queue_limit;
+  uint64_t t0_ns, tick_ns, horizon_ns;
+};
+
+}  // namespace tgsim

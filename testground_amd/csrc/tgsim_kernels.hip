@@ -1,0 +1,634 @@
+// tgsim_kernels.hip — gfx950 kernels of the per-packet network.Config enforcement path.
+//
+//   k_sim          K1+K2+K3+K4 of SURVEY §2.1: FIB filter, netem enqueue decisions (Philox
+//                  keyed by (seed, src, dst, seq)), netem queue limit, eligibility queue and HTB
+//                  token bucket.  One lane owns one source for the whole step (the state is a
+//                  sequential recurrence per source); a step spans many ticks so one launch
+//                  carries millions of packets.
+//   k_apply_cfg    K9: scatters compiled LinkShape deltas into the SoA parameter/state arrays.
+//   k_gen_*        synthetic storm traffic written straight into the CSR input.
+//   k_route_*      groups scheduled records by the destination's shard (input of the RCCL
+//                  all-to-all; plain compaction on one GPU).
+//   k_dst_*        K5: counting sort of deliveries by destination, then a per-destination sort
+//                  by (t, src, seq, clone-first).
+#include "tgsim_launch.h"
+
+namespace tgsim {
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 (Random123 constants).
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                       uint32_t k0, uint32_t k1, uint32_t r[4]) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t h0 = __umulhi(0xD2511F53u, c0), l0 = 0xD2511F53u * c0;
+    const uint32_t h1 = __umulhi(0xCD9E8D57u, c2), l1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+    c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  r[0] = c0; r[1] = c1; r[2] = c2; r[3] = c3;
+}
+
+// get_crandom(): correlated uniform, state updated only when rho != 0.
+__device__ __forceinline__ uint32_t crand(uint32_t raw, uint32_t rho, uint32_t& last) {
+  if (rho == 0) return raw;
+  const uint64_t r = (uint64_t)rho + 1;
+  const uint32_t a = (uint32_t)(((uint64_t)raw * ((1ull << 32) - r) + (uint64_t)last * r) >> 32);
+  last = a;
+  return a;
+}
+
+// Queued item (16 B): w0 = e | len << 46 | flags << 62, seq, dst.
+__device__ __forceinline__ uint64_t w0_of(const uint4& a) {
+  return ((uint64_t)a.y << 32) | a.x;
+}
+__device__ __forceinline__ bool item_lt(const uint4& a, const uint4& b) {
+  const uint64_t ea = w0_of(a) & kEMask, eb = w0_of(b) & kEMask;
+  if (ea != eb) return ea < eb;
+  if (a.z != b.z) return a.z < b.z;
+  return (a.y >> 30 & 1u) > (b.y >> 30 & 1u);  // DUP flag (bit 62) set sorts first
+}
+
+struct Lane {
+  // heap in the workgroup's interleaved block: slot k at hb[k * 64]
+  uint4* hb;
+  uint64_t* ring;
+  tgsim_delivery* emit;
+  uint32_t n_emit;
+  SrcState st;
+  SrcParams p;
+  uint32_t src;
+  // statistics
+  uint32_t scheduled, cloned, corrupted, offered;
+  uint32_t verdicts[8];
+  uint64_t bytes;
+  uint32_t err;
+};
+
+__device__ __forceinline__ void heap_push(Lane& L, uint4 it) {
+  uint32_t i = L.st.heap_n++;
+  while (i > 0) {
+    const uint32_t par = (i - 1) >> 1;
+    const uint4 pv = L.hb[(size_t)par * kWave];
+    if (!item_lt(it, pv)) break;
+    L.hb[(size_t)i * kWave] = pv;
+    i = par;
+  }
+  L.hb[(size_t)i * kWave] = it;
+}
+
+__device__ __forceinline__ uint4 heap_pop(Lane& L) {
+  const uint4 top = L.hb[0];
+  const uint32_t n = --L.st.heap_n;
+  const uint4 last = L.hb[(size_t)n * kWave];
+  uint32_t i = 0;
+  for (;;) {
+    uint32_t c = 2 * i + 1;
+    if (c >= n) break;
+    uint4 cv = L.hb[(size_t)c * kWave];
+    if (c + 1 < n) {
+      const uint4 rv = L.hb[(size_t)(c + 1) * kWave];
+      if (item_lt(rv, cv)) {
+        cv = rv;
+        ++c;
+      }
+    }
+    if (!item_lt(cv, last)) break;
+    L.hb[(size_t)i * kWave] = cv;
+    i = c;
+  }
+  if (n) L.hb[(size_t)i * kWave] = last;
+  return top;
+}
+
+// HTB class serving the netem queue in eligibility order: d = max(e, TAT),
+// TAT' = max(TAT, e - B) + len * mult >> shift.
+__device__ __forceinline__ void htb_until(Lane& L, uint64_t horizon) {
+  while (L.st.heap_n) {
+    const uint4 top = L.hb[0];
+    const uint64_t e = w0_of(top) & kEMask;
+    if (e >= horizon) break;
+    heap_pop(L);
+    const uint64_t w0 = w0_of(top);
+    const uint32_t len = (uint32_t)(w0 >> 46) & 0xFFFFu;
+    const uint32_t flags = (uint32_t)(w0 >> 62);
+    const uint64_t d = e > L.st.tat ? e : L.st.tat;
+    const uint64_t fl = e > L.p.burst_ns ? e - L.p.burst_ns : 0;
+    const uint64_t base = L.st.tat > fl ? L.st.tat : fl;
+    L.st.tat = base + (((uint64_t)len * L.p.mult) >> (L.p.shift_ext & 0xFFu));
+    L.ring[(L.st.ring_head + L.st.ring_n) & (kHeapCap - 1)] = d;
+    L.st.ring_n++;
+    tgsim_delivery* r = L.emit + L.n_emit++;
+    uint64_t* rw = reinterpret_cast<uint64_t*>(r);
+    rw[0] = d;
+    rw[1] = ((uint64_t)top.w << 32) | L.src;
+    rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | top.z;
+    L.scheduled++;
+    L.bytes += len;
+    L.corrupted += (flags >> 1) & 1u;
+  }
+}
+
+// netem_enqueue from the queue-limit check on.
+__device__ __forceinline__ uint32_t enqueue(Lane& L, const SimArgs& a, uint64_t T, uint32_t dst,
+                                            uint32_t seq, uint32_t len, uint32_t reo_raw,
+                                            uint32_t draw, int delay_word, uint32_t flags) {
+  htb_until(L, T);
+  while (L.st.ring_n && L.ring[L.st.ring_head] < T) {
+    L.st.ring_head = (L.st.ring_head + 1) & (kHeapCap - 1);
+    L.st.ring_n--;
+  }
+  if (L.st.heap_n + L.st.ring_n >= a.queue_limit) return TGSIM_V_QUEUE_FULL;
+  bool reordered = false;
+  if (L.p.thr_reo) reordered = !(L.p.thr_reo < crand(reo_raw, L.p.rho_reo, L.st.last_reo));
+  uint64_t e;
+  if (reordered) {
+    e = T;
+  } else if (L.p.sigma == 0) {
+    e = T + L.p.lat_ns;
+  } else {
+    uint32_t r[4];
+    philox(L.src, dst, seq, draw, a.key0, a.key1, r);
+    const uint32_t m = 2u * (uint32_t)L.p.sigma;
+    const int64_t delay = (int64_t)(r[delay_word] % m) + (int64_t)L.p.lat_ns - (int64_t)L.p.sigma;
+    e = delay > 0 ? T + (uint64_t)delay : T;
+  }
+  if (e > kEMask) {
+    L.err |= kErrTimeOverflow;
+    e = kEMask;
+  }
+  uint4 it;
+  const uint64_t w0 = e | ((uint64_t)(len & 0xFFFFu) << 46) | ((uint64_t)flags << 62);
+  it.x = (uint32_t)w0;
+  it.y = (uint32_t)(w0 >> 32);
+  it.z = seq;
+  it.w = dst;
+  heap_push(L, it);
+  return TGSIM_V_SCHEDULED;
+}
+
+__device__ __forceinline__ uint32_t fib_lookup(const SimArgs& a, const SrcParams& p, uint32_t ip) {
+  // binary search over sorted disjoint intervals
+  uint32_t lo = 0, hi = p.rule_n;
+  const Interval* iv = a.rules + p.rule_off;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (iv[mid].hi < ip) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < p.rule_n && iv[lo].lo <= ip) return iv[lo].act;
+  return TGSIM_ACCEPT;
+}
+
+__device__ __forceinline__ uint32_t process(Lane& L, const SimArgs& a, uint64_t T, const InRec& k) {
+  L.offered++;
+  const uint32_t dst = k.dst;
+  const bool ext = dst == TGSIM_EXTERNAL;
+  if (!a.enabled[L.src] || (!ext && !a.enabled[dst])) return 0xF0u | TGSIM_V_DISCONNECTED;
+  if (ext) return 0xF0u | ((L.p.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE);
+  if (L.p.rule_n) {
+    const uint32_t act = fib_lookup(a, L.p, a.ip[dst]);
+    if (act == TGSIM_DROP) return 0xF0u | TGSIM_V_BLACKHOLE;
+    if (act == TGSIM_REJECT) return 0xF0u | TGSIM_V_PROHIBIT;
+  }
+  uint32_t r0[4];
+  philox(L.src, dst, k.seq, 0, a.key0, a.key1, r0);
+  int count = 1;
+  if (L.p.thr_dup && L.p.thr_dup >= crand(r0[0], L.p.rho_dup, L.st.last_dup)) ++count;
+  if (L.p.thr_loss && L.p.thr_loss >= r0[1]) --count;
+  if (count == 0) return 0xF0u | TGSIM_V_LOSS;
+  uint32_t cv = TGSIM_V_NONE;
+  const uint32_t len = k.len & 0xFFFFu;
+  if (count == 2) {
+    L.cloned++;
+    uint32_t r2[4];
+    philox(L.src, dst, k.seq, 2, a.key0, a.key1, r2);
+    if (L.p.thr_loss && L.p.thr_loss >= r2[0]) {
+      cv = TGSIM_V_LOSS;
+    } else {
+      uint32_t fl = TGSIM_FLAG_DUP;
+      if (L.p.thr_cor && L.p.thr_cor >= crand(r2[1], L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+      cv = enqueue(L, a, T, dst, k.seq, len, r2[2], 2, 3, fl);
+    }
+  }
+  uint32_t fl = 0;
+  if (L.p.thr_cor && L.p.thr_cor >= crand(r0[2], L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+  const uint32_t ov = enqueue(L, a, T, dst, k.seq, len, r0[3], 1, 0, fl);
+  return (cv << 4) | ov;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, o, 64);
+    const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+    v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t s = blockIdx.x * kWave + lane;
+  const bool active = s < a.n_src;
+  Lane L;
+  L.offered = L.scheduled = L.cloned = L.corrupted = 0;
+  L.bytes = 0;
+  L.err = 0;
+  L.n_emit = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) L.verdicts[i] = 0;
+  if (active) {
+    L.p = a.params[s];
+    L.st = a.state[s];
+    L.src = a.shard_begin + s;
+    L.hb = a.heap + (size_t)blockIdx.x * kHeapCap * kWave + lane;
+    L.ring = a.ring + (size_t)s * kHeapCap;
+    const uint64_t b = a.off[s], e = a.off[s + 1];
+    L.emit = a.emit + 2 * b + (uint64_t)kHeapCap * s;
+    for (uint64_t i = b; i < e; ++i) {
+      const InRec k = a.in[i];
+      const uint64_t T = a.t0_ns + (uint64_t)k.tick * a.tick_ns;
+      const uint32_t v = process(L, a, T, k);
+      a.verdict[i] = (uint8_t)v;
+      L.verdicts[v & 15u]++;
+      if ((v >> 4) != TGSIM_V_NONE) L.verdicts[v >> 4]++;
+    }
+    htb_until(L, a.horizon_ns);
+    a.state[s] = L.st;
+    a.emit_n[s] = L.n_emit;
+  }
+  uint64_t sums[kStSlots];
+  sums[kStOffered] = wave_sum(L.offered);
+  sums[kStScheduled] = wave_sum(L.scheduled);
+  sums[kStCloned] = wave_sum(L.cloned);
+  sums[kStCorrupted] = wave_sum(L.corrupted);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sums[kStVerdict0 + i] = wave_sum(L.verdicts[i]);
+  sums[kStBytes] = wave_sum(L.bytes);
+  const uint32_t err = (uint32_t)wave_sum(L.err ? 1u : 0u);
+  if (lane == 0) {
+    for (int i = 0; i < kStBytes + 1; ++i)
+      if (sums[i]) atomicAdd(&a.stats[i], (unsigned long long)sums[i]);
+    if (err) atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K9: configuration apply.
+__global__ void k_apply_cfg(const CfgPatch* __restrict__ patches, uint32_t n, SrcParams* params,
+                            SrcState* state) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const CfgPatch c = patches[i];
+  params[c.s] = c.p;
+  SrcState st = state[c.s];
+  if (c.mask & 1u) st.last_dup = c.last_dup;
+  if (c.mask & 2u) st.last_cor = c.last_cor;
+  if (c.mask & 4u) st.last_reo = c.last_reo;
+  if (c.mask & 8u) st.tat = 0;
+  state[c.s] = st;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Storm traffic generator.
+struct GenArgs {
+  uint32_t tab[16];
+  uint32_t k0, k1, n_src, shard_begin, n_peers, n_ticks;
+  uint64_t now_tick;
+};
+
+__device__ __forceinline__ uint32_t poisson_count(const GenArgs& g, uint32_t u) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) c += (u >= g.tab[k]) && (c == (uint32_t)k);
+  return c;
+}
+
+__global__ void k_gen_count(GenArgs g, uint64_t* counts) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.n_src) return;
+  const uint32_t src = g.shard_begin + s;
+  uint64_t total = 0;
+  if (g.n_peers >= 2) {
+    for (uint32_t t = 0; t < g.n_ticks; ++t) {
+      uint32_t r[4];
+      philox(src, (uint32_t)(g.now_tick + t), 0x53544F52u, 0, g.k0, g.k1, r);
+      total += poisson_count(g, r[0]);
+    }
+  }
+  counts[s] = total;
+}
+
+__global__ void k_gen_write(GenArgs g, const uint64_t* off, uint32_t* gen_seq, InRec* out) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.n_src || g.n_peers < 2) return;
+  const uint32_t src = g.shard_begin + s;
+  uint64_t o = off[s];
+  uint32_t seq = gen_seq[s];
+  for (uint32_t t = 0; t < g.n_ticks; ++t) {
+    const uint32_t at = (uint32_t)(g.now_tick + t);
+    uint32_t r[4];
+    philox(src, at, 0x53544F52u, 0, g.k0, g.k1, r);
+    const uint32_t cnt = poisson_count(g, r[0]);
+    for (uint32_t j = 0; j < cnt; ++j) {
+      uint32_t q[4];
+      philox(src, at, 0x53544F52u, j + 1, g.k0, g.k1, q);
+      uint32_t d = q[0] % (g.n_peers - 1);
+      d += d >= src;
+      InRec rec;
+      rec.dst = d;
+      rec.seq = seq++;
+      rec.tick = t;
+      rec.len = 64u + q[1] % 1437u;
+      out[o++] = rec;
+    }
+  }
+  gen_seq[s] = seq;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Exclusive scan (u64), three phases, 1024 elements per block.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, uint64_t& total) {
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t lo = __shfl_up((uint32_t)x, o, 64), hi = __shfl_up((uint32_t)(x >> 32), o, 64);
+    if (lane >= (uint32_t)o) x += ((uint64_t)hi << 32) | lo;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < blockDim.x / 64; ++i) {
+      const uint64_t s = sh[i];
+      sh[i] = acc;
+      acc += s;
+    }
+    sh[15] = acc;
+  }
+  __syncthreads();
+  total = sh[15];
+  const uint64_t r = x - v + sh[w];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_scan_local(const uint64_t* in, uint64_t* out, uint64_t n,
+                                                    uint64_t* block_sums) {
+  __shared__ uint64_t sh[16];
+  const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x * 4;
+  uint64_t v[4], s = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = base + i < n ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t pre = block_excl_scan(s, sh, total);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (base + i < n) out[base + i] = pre;
+    pre += v[i];
+  }
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_sums(uint64_t* sums, uint64_t nb, uint64_t* total_out) {
+  __shared__ uint64_t sh[16];
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < nb; base += 256) {
+    const uint64_t i = base + threadIdx.x;
+    const uint64_t v = i < nb ? sums[i] : 0;
+    uint64_t total;
+    const uint64_t pre = block_excl_scan(v, sh, total);
+    if (i < nb) sums[i] = carry + pre;
+    carry += total;
+  }
+  if (threadIdx.x == 0) *total_out = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(uint64_t* out, uint64_t n, const uint64_t* sums) {
+  const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x * 4;
+  const uint64_t add = sums[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (base + i < n) out[base + i] += add;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Route: group the emitted records by the destination shard (wave-aggregated atomics).
+struct RouteArgs {
+  const tgsim_delivery* emit;
+  const uint32_t* emit_n;
+  const uint64_t* off;           // CSR offsets of the step input: region base 2*off[s] + kHeapCap*s
+  uint32_t n_src;
+  uint32_t n_ranks;
+  uint32_t bounds[9];
+  unsigned long long* rank_cnt;  // [n_ranks] counts (phase 0) / cursors (phase 1)
+  const unsigned long long* rank_off;
+  tgsim_delivery* out;
+};
+
+__device__ __forceinline__ uint32_t rank_of(const RouteArgs& a, uint32_t dst) {
+  uint32_t r = 0;
+  for (uint32_t i = 1; i < a.n_ranks; ++i) r += dst >= a.bounds[i];
+  return r;
+}
+
+template <int PHASE>
+__global__ __launch_bounds__(256) void k_route(RouteArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t s = wave; s < a.n_src; s += nw) {
+    const uint32_t n = a.emit_n[s];
+    const tgsim_delivery* base = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
+    for (uint32_t i = lane; i < ((n + 63u) & ~63u); i += 64) {
+      const bool valid = i < n;
+      tgsim_delivery r;
+      uint32_t rk = 0xFFFFFFFFu;
+      if (valid) {
+        r = base[i];
+        rk = rank_of(a, r.dst);
+      }
+      for (uint32_t q = 0; q < a.n_ranks; ++q) {
+        const uint64_t m = __ballot(rk == q);
+        if (!m) continue;
+        const uint32_t leader = __ffsll((long long)m) - 1;
+        unsigned long long bpos = 0;
+        if (lane == leader) bpos = atomicAdd(&a.rank_cnt[q], (unsigned long long)__popcll(m));
+        if (PHASE == 1) {
+          const uint32_t lo = __shfl((uint32_t)bpos, leader, 64);
+          const uint32_t hi = __shfl((uint32_t)(bpos >> 32), leader, 64);
+          const uint64_t pos = ((uint64_t)hi << 32 | lo) + __popcll(m & ((1ull << lane) - 1));
+          if (rk == q) a.out[a.rank_off[q] + pos] = r;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Delivery: counting sort by destination, then per-destination ordering.
+__global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[in[i].dst - dst_begin]), 1ull);
+}
+
+__global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin,
+                              const uint64_t* off, uint64_t* cursor, tgsim_delivery* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const tgsim_delivery r = in[i];
+  const uint32_t d = r.dst - dst_begin;
+  const uint64_t p = atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[d]), 1ull);
+  out[off[d] + p] = r;
+}
+
+struct SortKey {
+  uint64_t t;
+  uint64_t sq;   // src << 32 | seq
+  uint32_t idx;  // (clone ? 0 : 1) << 31 | position in the segment
+};
+
+__device__ __forceinline__ bool key_lt(const SortKey& a, const SortKey& b) {
+  if (a.t != b.t) return a.t < b.t;
+  if (a.sq != b.sq) return a.sq < b.sq;
+  return a.idx < b.idx;
+}
+
+__device__ __forceinline__ SortKey make_key(const tgsim_delivery& r, uint32_t i) {
+  SortKey k;
+  k.t = r.t_ns;
+  k.sq = ((uint64_t)r.src << 32) | r.seq;
+  k.idx = ((r.flags & TGSIM_FLAG_DUP) ? 0u : 0x80000000u) | i;
+  return k;
+}
+
+constexpr uint32_t kSegLds = 2048;
+
+// One workgroup per destination segment: bitonic sort of (t, src, seq, clone-first) keys in LDS
+// (global scratch for segments longer than kSegLds), then a gather into delivery order.
+__global__ __launch_bounds__(256) void k_dst_sort(const tgsim_delivery* in, const uint64_t* off,
+                                                  const uint64_t* cnt, tgsim_delivery* out,
+                                                  SortKey* scratch) {
+  __shared__ SortKey sk[kSegLds];
+  const uint32_t d = blockIdx.x;
+  const uint64_t b = off[d];
+  const uint32_t n = (uint32_t)cnt[d];
+  if (n == 0) return;
+  if (n == 1) {
+    if (threadIdx.x == 0) out[b] = in[b];
+    return;
+  }
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  SortKey* k = P <= kSegLds ? sk : scratch + 2 * b;  // P < 2n: disjoint per segment
+  for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+    if (i < n) {
+      k[i] = make_key(in[b + i], i);
+    } else {
+      k[i].t = ~0ull;
+      k[i].sq = ~0ull;
+      k[i].idx = 0xFFFFFFFFu;
+    }
+  }
+  __syncthreads();
+  for (uint32_t size = 2; size <= P; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+        const uint32_t j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const SortKey x = k[i], y = k[j];
+          if (key_lt(y, x) == up) {
+            k[i] = y;
+            k[j] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[b + i] = in[b + (k[i].idx & 0x7FFFFFFFu)];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host-side launchers.
+void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
+  hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);
+}
+
+void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_apply_cfg, dim3((n + 255) / 256), dim3(256), 0, st, p, n, params, state);
+}
+
+void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uint32_t* gen_seq,
+                InRec* out, int phase, hipStream_t st) {
+  GenArgs g;
+  for (int i = 0; i < 16; ++i) g.tab[i] = h.tab[i];
+  g.k0 = h.k0; g.k1 = h.k1; g.n_src = h.n_src; g.shard_begin = h.shard_begin;
+  g.n_peers = h.n_peers; g.n_ticks = h.n_ticks; g.now_tick = h.now_tick;
+  const dim3 grid((h.n_src + 63) / 64), blk(64);
+  if (phase == 0) hipLaunchKernelGGL(k_gen_count, grid, blk, 0, st, g, counts);
+  else hipLaunchKernelGGL(k_gen_write, grid, blk, 0, st, g, off, gen_seq, out);
+}
+
+void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums,
+                 uint64_t* total, hipStream_t st) {
+  const uint64_t nb = (n + 1023) / 1024;
+  if (nb == 0) {
+    (void)hipMemsetAsync(total, 0, sizeof(uint64_t), st);
+    return;
+  }
+  hipLaunchKernelGGL(k_scan_local, dim3((uint32_t)nb), dim3(256), 0, st, in, out, n, block_sums);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, block_sums, nb, total);
+  hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)nb), dim3(256), 0, st, out, n, block_sums);
+}
+
+void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
+  RouteArgs a;
+  a.emit = h.emit;
+  a.emit_n = h.emit_n;
+  a.off = h.off;
+  a.n_src = h.n_src;
+  a.n_ranks = h.n_ranks;
+  for (int i = 0; i < 9; ++i) a.bounds[i] = h.bounds[i];
+  a.rank_cnt = h.rank_cnt;
+  a.rank_off = h.rank_off;
+  a.out = h.out;
+  uint32_t grid = (h.n_src + 3) / 4;
+  if (grid > 2048) grid = 2048;
+  if (grid == 0) grid = 1;
+  if (phase == 0) hipLaunchKernelGGL(k_route<0>, dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(k_route<1>, dim3(grid), dim3(256), 0, st, a);
+}
+
+void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, cnt);
+}
+
+void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, const uint64_t* off,
+                        uint64_t* cursor, tgsim_delivery* out, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n,
+                     dst_begin, off, cursor, out);
+}
+
+void launch_dst_sort(const tgsim_delivery* in, const uint64_t* off, const uint64_t* cnt, uint32_t n_dst,
+                     tgsim_delivery* out, void* scratch, hipStream_t st) {
+  if (!n_dst) return;
+  hipLaunchKernelGGL(k_dst_sort, dim3(n_dst), dim3(256), 0, st, in, off, cnt, out,
+                     reinterpret_cast<SortKey*>(scratch));
+}
+
+size_t sort_key_bytes() { return sizeof(SortKey); }
+
+}  // namespace tgsim

@@ -1,0 +1,39 @@
+// tgsim_launch.h — host-callable launchers of the gfx950 kernels (tgsim_kernels.hip).
+#pragma once
+#include "tgsim_internal.h"
+
+namespace tgsim {
+
+struct GenArgsHost {
+  uint32_t tab[16];
+  uint32_t k0, k1, n_src, shard_begin, n_peers, n_ticks;
+  uint64_t now_tick;
+};
+
+struct RouteArgsHost {
+  const tgsim_delivery* emit;
+  const uint32_t* emit_n;
+  const uint64_t* off;
+  uint32_t n_src;
+  uint32_t n_ranks;
+  uint32_t bounds[9];
+  unsigned long long* rank_cnt;
+  const unsigned long long* rank_off;
+  tgsim_delivery* out;
+};
+
+void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
+void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st);
+void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uint32_t* gen_seq,
+                InRec* out, int phase, hipStream_t st);
+void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
+                 hipStream_t st);
+void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
+void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt, hipStream_t st);
+void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, const uint64_t* off,
+                        uint64_t* cursor, tgsim_delivery* out, hipStream_t st);
+void launch_dst_sort(const tgsim_delivery* in, const uint64_t* off, const uint64_t* cnt, uint32_t n_dst,
+                     tgsim_delivery* out, void* scratch, hipStream_t st);
+size_t sort_key_bytes();
+
+}  // namespace tgsim

@@ -1,0 +1,192 @@
+"""Python handle over the engine's C ABI (include/tgsim.h).
+
+``Engine`` always drives the HIP library ``libtgsim.so``; it raises ``EngineUnavailable`` when the
+library or a GPU is missing — there is no CPU fallback in the product path.  ``CABIEngine`` is the
+generic wrapper over any library exporting the same function set under a prefix (the tests use it
+to drive the CPU oracle with identical inputs).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import os
+from pathlib import Path
+from typing import Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .network import Config, to_c
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libtgsim.so"
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{msg} (errno {-code}: {errno.errorcode.get(-code, '?')})")
+        self.code = code
+        self.msg = msg
+
+
+class EngineUnavailable(EngineError):
+    pass
+
+
+_LIB: Optional[C.CDLL] = None
+
+
+def load_library(path: Optional[Path] = None) -> C.CDLL:
+    """Loads libtgsim.so (in-tree).  Fails loudly if it has not been built."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = Path(path or os.environ.get("TGSIM_LIB", LIB_PATH))
+    if not p.exists():
+        raise EngineUnavailable(-errno.ENOENT, f"HIP engine library not built: {p} (run __graft_entry__.build())")
+    lib = C.CDLL(str(p))
+    abi.declare(lib, "tgsim_")
+    if lib.tgsim_abi_version() != abi.ABI_VERSION:
+        raise EngineUnavailable(-errno.EPROTO, "libtgsim ABI version mismatch")
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+class CABIEngine:
+    """Engine-shaped C ABI wrapper (prefix 'tgsim_' for the product, 'tgo_' for the oracle)."""
+
+    def __init__(self, lib: C.CDLL, prefix: str, n_peers: int, seed: int = 0x7E576A0D00000001,
+                 tick_ns: int = 1000, queue_limit: int = 0, shard: Tuple[int, int] = (0, 0),
+                 lookahead_ns: int = 0, flags: int = 0, subnet_base: int = 0, device: int = -1):
+        self._lib = lib
+        self._p = prefix
+        o = abi.Opts()
+        o.abi_version = abi.ABI_VERSION
+        o.n_peers = n_peers
+        o.shard_begin, o.shard_end = shard
+        o.seed = seed & 0xFFFFFFFFFFFFFFFF
+        o.tick_ns = tick_ns
+        o.queue_limit = queue_limit
+        o.flags = flags
+        o.lookahead_ns = lookahead_ns
+        o.subnet_base = subnet_base
+        o.device = device
+        self.n_peers = n_peers
+        self.shard = (shard[0], shard[1] if shard[1] else n_peers) if shard != (0, 0) else (0, n_peers)
+        self.tick_ns = tick_ns
+        h = C.c_void_p()
+        rc = self._fn("create")(C.byref(o), C.byref(h))
+        if rc != 0:
+            exc = EngineUnavailable if rc in (-errno.ENODEV, -errno.EPROTO) else EngineError
+            raise exc(rc, f"{prefix}create failed")
+        self._h = h
+
+    def _fn(self, name):
+        return getattr(self._lib, self._p + name)
+
+    def _check(self, rc: int, what: str) -> int:
+        if rc < 0:
+            msg = self._fn("last_error")(self._h)
+            raise EngineError(rc, f"{what}: {msg.decode() if msg else ''}")
+        return rc
+
+    # -- lifecycle -----------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._fn("destroy")(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- configuration -------------------------------------------------------------------------
+    def configure(self, peer: int, cfg: Config) -> None:
+        c, keep = to_c(cfg)
+        self._check(self._fn("configure")(self._h, peer, C.byref(c)), f"configure peer {peer}")
+        del keep
+
+    # -- data path -----------------------------------------------------------------------------
+    def submit(self, pkts: np.ndarray) -> None:
+        pkts = np.ascontiguousarray(pkts, dtype=abi.PKT_DTYPE)
+        self._check(self._fn("submit")(self._h, pkts.ctypes.data, len(pkts)), "submit")
+
+    def gen_storm(self, lam: float, n_ticks: int) -> None:
+        self._check(self._fn("gen_storm")(self._h, float(lam), n_ticks), "gen_storm")
+
+    def step(self, n_ticks: int) -> None:
+        self._check(self._fn("step")(self._h, n_ticks), "step")
+
+    def step_sim(self, n_ticks: int, bounds: Sequence[int], d_out: int, out_cap: int) -> np.ndarray:
+        nr = len(bounds) - 1
+        b = (C.c_uint32 * len(bounds))(*bounds)
+        counts = (C.c_uint64 * nr)()
+        self._check(self._fn("step_sim")(self._h, n_ticks, nr, b, C.c_void_p(d_out), out_cap, counts), "step_sim")
+        return np.array(list(counts), dtype=np.uint64)
+
+    def deliver(self, d_in: int, n: int) -> None:
+        self._check(self._fn("deliver")(self._h, C.c_void_p(d_in), n), "deliver")
+
+    def sim_capacity(self) -> int:
+        return self._check(self._fn("sim_capacity")(self._h), "sim_capacity")
+
+    def pending(self) -> int:
+        return self._check(self._fn("pending_deliveries")(self._h), "pending")
+
+    def drain(self) -> np.ndarray:
+        n = self.pending() if hasattr(self._lib, self._p + "pending_deliveries") else None
+        if n is None:  # oracle: ask with a large buffer
+            out = np.empty(1 << 22, dtype=abi.DELIVERY_DTYPE)
+            k = self._check(self._fn("drain")(self._h, out.ctypes.data, len(out)), "drain")
+            return out[:k].copy()
+        out = np.empty(n, dtype=abi.DELIVERY_DTYPE)
+        k = self._check(self._fn("drain")(self._h, out.ctypes.data, n), "drain")
+        return out[:k]
+
+    def verdicts(self) -> np.ndarray:
+        n = self._check(self._fn("verdicts")(self._h, None, 0), "verdicts")
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            self._check(self._fn("verdicts")(self._h, out.ctypes.data, n), "verdicts")
+        return out
+
+    def stats(self) -> dict:
+        s = abi.Stats()
+        self._check(self._fn("stats")(self._h, C.byref(s)), "stats")
+        d = {k: getattr(s, k) for k in ("offered", "scheduled", "cloned", "corrupted", "bytes_scheduled", "now_tick")}
+        d["by_verdict"] = {abi.VERDICT_NAMES[i]: s.by_verdict[i] for i in range(8)}
+        return d
+
+    # -- sync counters -------------------------------------------------------------------------
+    def signal(self, state: int, n: int = 1) -> int:
+        return self._check(self._fn("signal")(self._h, state, n), "signal")
+
+    def barrier_poll(self, state: int, target: int) -> bool:
+        return bool(self._check(self._fn("barrier_poll")(self._h, state, target), "barrier_poll"))
+
+    # -- instrumentation -----------------------------------------------------------------------
+    def sim_kernel_ms(self, reset: bool = False) -> Tuple[float, int]:
+        n = C.c_uint64()
+        ms = self._fn("sim_kernel_ms")(self._h, C.byref(n), 1 if reset else 0)
+        return ms, n.value
+
+
+class Engine(CABIEngine):
+    """The MI355X engine (libtgsim.so)."""
+
+    def __init__(self, n_peers: int, **kw):
+        super().__init__(load_library(), "tgsim_", n_peers, **kw)
+
+
+def packets(rows: Iterable[tuple]) -> np.ndarray:
+    """Builds a packet array from (src, dst, seq, len, tick) tuples."""
+    return np.array(list(rows), dtype=abi.PKT_DTYPE)

@@ -1,0 +1,162 @@
+"""Synthetic equivalents of the reference's network workloads (SURVEY §8(d) C1–C3).
+
+Each driver talks to an engine-shaped object (``Engine`` or any ``CABIEngine``), so the same
+driver runs the HIP engine on the GPU and, in the tests, the CPU oracle with identical inputs.
+
+  C1 pingpong    plans/network/pingpong.go:16-201 (RTT windows :185, :195)
+  C2 splitbrain  plans/splitbrain/main.go:60-186 (expectErrors :50-58)
+  C3 storm       plans/benchmarks/storm.go:31-197, random all-to-all with heterogeneous shapes
+
+A reaction to a delivery at time d (reply, echo, forward) is offered at tick floor(d/tick) + 1.
+"""
+from __future__ import annotations
+
+import ipaddress
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+from . import abi
+from .network import Config, FilterAction, LinkRule, LinkShape, Millisecond, RoutingPolicyType
+
+SEED = 0x7E576A0D00000001
+
+
+# ---------------------------------------------------------------------------------------------
+# C3: storm — heterogeneous LinkShape per instance.
+def storm_shapes(n_peers: int, seed: int = SEED) -> List[LinkShape]:
+    """L~U[1,100] ms, J~U[0,10] ms, Loss~U[0,5] %, Dup/Corrupt/Reorder~U[0,1] %,
+    Bw in {1,10,100,1000} Mbit/s, correlations 0."""
+    rng = np.random.default_rng(seed & 0xFFFFFFFF)
+    lat = rng.integers(1 * Millisecond, 100 * Millisecond + 1, n_peers)
+    jit = rng.integers(0, 10 * Millisecond + 1, n_peers)
+    loss = rng.uniform(0, 5, n_peers).astype(np.float32)
+    dup = rng.uniform(0, 1, n_peers).astype(np.float32)
+    cor = rng.uniform(0, 1, n_peers).astype(np.float32)
+    reo = rng.uniform(0, 1, n_peers).astype(np.float32)
+    bw = rng.choice(np.array([1, 10, 100, 1000], dtype=np.int64) * 1_000_000, n_peers)
+    return [LinkShape(Latency=int(lat[i]), Jitter=int(jit[i]), Bandwidth=int(bw[i]), Loss=float(loss[i]),
+                      Duplicate=float(dup[i]), Corrupt=float(cor[i]), Reorder=float(reo[i]))
+            for i in range(n_peers)]
+
+
+def configure_storm(eng, n_peers: int, seed: int = SEED) -> List[LinkShape]:
+    shapes = storm_shapes(n_peers, seed)
+    for i, s in enumerate(shapes):
+        eng.configure(i, Config(Network="default", Enable=True, Default=s,
+                                CallbackState="storm-shaped", RoutingPolicy=RoutingPolicyType.DenyAll))
+    return shapes
+
+
+# ---------------------------------------------------------------------------------------------
+# C2: splitbrain.
+REGION_A, REGION_B, REGION_C = 0, 1, 2
+
+
+def splitbrain_regions(n: int) -> np.ndarray:
+    """seq = i + 1 (SignalEntry is 1-based), region = seq % 3 (splitbrain/main.go:84-87)."""
+    return (np.arange(n) + 1) % 3
+
+
+def expect_errors(case: str, ra: int, rb: int) -> bool:
+    """splitbrain/main.go:50-58."""
+    if case == "accept" or ra == REGION_C or rb == REGION_C:
+        return False
+    return (ra == REGION_A and rb == REGION_B) or (ra == REGION_B and rb == REGION_A)
+
+
+def peer_ip(i: int, subnet_base: int = 16 << 24) -> int:
+    return subnet_base + 2 + i
+
+
+def configure_splitbrain(eng, n: int, case: str) -> np.ndarray:
+    action = {"drop": FilterAction.Drop, "reject": FilterAction.Reject, "accept": FilterAction.Accept}[case]
+    region = splitbrain_regions(n)
+    b_peers = np.nonzero(region == REGION_B)[0]
+    for i in np.nonzero(region == REGION_A)[0]:
+        rules = [LinkRule(Subnet=(str(ipaddress.IPv4Address(peer_ip(int(p)))), 32),
+                          LinkShape=LinkShape(Filter=action)) for p in b_peers]
+        eng.configure(int(i), Config(Network="default", Enable=True, Rules=rules,
+                                     CallbackState=f"reconfigured{i}", CallbackTarget=1))
+    return region
+
+
+def run_splitbrain(eng, n: int, case: str, pkt_len: int = 66) -> Tuple[np.ndarray, Dict]:
+    """All ordered pairs send one request at tick 0; each delivered request is answered.
+    Returns ok[i, j] = request i->j and its reply j->i both delivered, plus step artifacts."""
+    region = configure_splitbrain(eng, n, case)
+    src, dst = np.nonzero(~np.eye(n, dtype=bool))
+    req = np.zeros(len(src), dtype=abi.PKT_DTYPE)
+    req["src"], req["dst"], req["len"], req["tick"] = src, dst, pkt_len, 0
+    req["seq"] = dst - (dst > src)  # per-source sequence 0..n-2
+    eng.submit(req)
+    eng.step(1)
+    v_req = eng.verdicts()
+    d_req = eng.drain()
+    tick = eng.tick_ns
+    now = 1
+    rep = np.zeros(len(d_req), dtype=abi.PKT_DTYPE)
+    rep["src"], rep["dst"], rep["len"] = d_req["dst"], d_req["src"], pkt_len
+    rep["seq"] = (n - 1) + d_req["src"]  # fresh per-source sequence numbers
+    rtick = d_req["t_ns"] // tick + 1
+    span = int(rtick.max() - now + 1) if len(rtick) else 1
+    rep["tick"] = rtick - now
+    eng.submit(rep)
+    eng.step(span)
+    v_rep = eng.verdicts()
+    d_rep = eng.drain()
+    ok = np.zeros((n, n), dtype=bool)
+    ok[d_rep["dst"], d_rep["src"]] = True  # reply j->i delivered to i => i->j round trip ok
+    return ok, {"region": region, "v_req": v_req, "d_req": d_req, "v_rep": v_rep, "d_rep": d_rep}
+
+
+def splitbrain_expected(n: int, case: str) -> np.ndarray:
+    region = splitbrain_regions(n)
+    exp = np.zeros((n, n), dtype=bool)
+    for i in range(n):
+        for j in range(n):
+            if i != j:
+                exp[i, j] = not expect_errors(case, int(region[i]), int(region[j]))
+    return exp
+
+
+# ---------------------------------------------------------------------------------------------
+# C1: ping-pong (2 instances).
+def pingpong_config(latency_ns: int, callback: str = "network-configured", ipv4=None) -> Config:
+    """pingpong.go:29-42 (and :61-65 for the re-addressing)."""
+    return Config(Network="default", Enable=True, IPv4=ipv4,
+                  Default=LinkShape(Latency=latency_ns, Bandwidth=1 << 20),
+                  CallbackState=callback, RoutingPolicy=RoutingPolicyType.DenyAll)
+
+
+def pingpong_round(eng, start_tick: int, seq0: int, pkt_len: int = 66, chunk: int = 1000,
+                   max_ticks: int = 2_000_000) -> Tuple[List[int], int]:
+    """One pingPong() exchange (pingpong.go:116-183): both sides write their id at start_tick,
+    echo the other's id on receipt, and stop when their own id comes back.  The engine must have
+    lookahead >= chunk ticks.  Returns (rtt_ns per instance, next free tick)."""
+    tick = eng.tick_ns
+    now = eng.stats()["now_tick"]
+    assert now <= start_tick
+    if start_tick > now:
+        eng.step(start_tick - now)
+        eng.drain()
+        now = start_tick
+    pending: List[tuple] = [(0, 1, seq0, pkt_len, 0), (1, 0, seq0, pkt_len, 0)]  # (src,dst,seq,len,abs tick)
+    pending = [(s, d, q, l, start_tick) for (s, d, q, l, _) in pending]
+    rtt = [None, None]
+    while None in rtt and now - start_tick < max_ticks:
+        window = [p for p in pending if now <= p[4] < now + chunk]
+        pending = [p for p in pending if p[4] >= now + chunk]
+        if window:
+            arr = np.array([(s, d, q, l, t - now) for (s, d, q, l, t) in window], dtype=abi.PKT_DTYPE)
+            eng.submit(arr)
+        eng.step(chunk)
+        now += chunk
+        for r in eng.drain():
+            dst, src, t = int(r["dst"]), int(r["src"]), int(r["t_ns"])
+            react = t // tick + 1
+            if int(r["seq"]) == seq0:  # the other's id arrived: echo it back
+                pending.append((dst, src, seq0 + 1 + dst, pkt_len, react))
+            elif rtt[dst] is None:  # own id came back
+                rtt[dst] = t - start_tick * tick
+    return rtt, now

@@ -1,0 +1,32 @@
+"""Shared fixtures.  `gpu` tests run the HIP engine on an MI355X; everything else runs on CPU."""
+import ctypes
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+from testground_amd import abi  # noqa: E402
+from testground_amd.build import build_oracle  # noqa: E402
+from testground_amd.engine import CABIEngine  # noqa: E402
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X; drives libtgsim.so through its C ABI")
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    """The CPU golden model (oracle/), the checker for every parity test."""
+    lib = ctypes.CDLL(str(build_oracle()))
+    abi.declare(lib, "tgo_")
+    return lib
+
+
+@pytest.fixture
+def make_oracle(oracle_lib):
+    def _make(n_peers, **kw):
+        return CABIEngine(oracle_lib, "tgo_", n_peers, **kw)
+    return _make
