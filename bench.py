@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--window", type=int, default=2000, help="ticks (1 us) per step")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--queue-limit", type=int, default=0, help="netem limit (0 = netlink default 1000)")
+    p.add_argument("--shapes", default="storm", choices=["storm", "fixed"],
+                   help="storm: C3 heterogeneous shapes; fixed: L=5 ms, no jitter/loss/reorder (probe)")
     return p.parse_args()
 
 
@@ -98,9 +101,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     peers_total = a.peers * world
     lo, hi = rank * a.peers, (rank + 1) * a.peers
-    eng = Engine(peers_total, shard=(lo, hi), device=local, flags=abi.OPT_DISCARD_DELIVERIES)
-    shapes = workloads.storm_shapes(peers_total)
-    from testground_amd.network import Config, RoutingPolicyType
+    eng = Engine(peers_total, shard=(lo, hi), device=local, flags=abi.OPT_DISCARD_DELIVERIES,
+                 queue_limit=a.queue_limit)
+    from testground_amd.network import Config, LinkShape, Millisecond, RoutingPolicyType
+    if a.shapes == "storm":
+        shapes = workloads.storm_shapes(peers_total)
+    else:
+        shapes = [LinkShape(Latency=5 * Millisecond)] * peers_total
     for i, s in enumerate(shapes):
         eng.configure(i, Config(Network="default", Enable=True, Default=s, RoutingPolicy=RoutingPolicyType.DenyAll))
     for _ in range(a.warmup + a.steps):
@@ -178,7 +185,7 @@ def main():
         "data": "synthetic (device-generated storm traffic, Philox-keyed)",
         "config": {"workload": "C3 storm: random all-to-all, heterogeneous LinkShape (BASELINE.json configs[2])",
                    "peers_per_gpu": a.peers, "peers_total": peers_total, "lambda_per_tick": a.lam,
-                   "tick_ns": 1000, "window_ticks": a.window,
+                   "tick_ns": 1000, "window_ticks": a.window, "shapes": a.shapes, "queue_limit": a.queue_limit or 1000,
                    "packets_per_step": offered_all / a.steps, "parallelism": f"peer-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

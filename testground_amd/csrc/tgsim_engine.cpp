@@ -450,7 +450,7 @@ int run_sim(Eng* E, uint32_t n_ticks) {
   a.t0_ns = E->now_tick * E->o.tick_ns;
   a.horizon_ns = (E->now_tick + n_ticks) * E->o.tick_ns + E->o.lookahead_ns;
   HIPCHK(hipEventRecord(E->ev0, E->st));
-  launch_sim(a, (E->S + kWave - 1) / kWave, E->st);
+  launch_sim(a, (E->S + kSpw - 1) / kSpw, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(E->ev1, E->st));
   E->n_verdict = E->n_in;
@@ -609,12 +609,11 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
     E->src[s].dirty = false;
   }
   E->any_patch = false;
-  const size_t nwg = (E->S + kWave - 1) / kWave;
   if ((rc = E->hip(E->d_params.ensure(E->S), "alloc params"))) return bail(rc);
   if ((rc = E->hip(E->d_state.ensure(E->S), "alloc state"))) return bail(rc);
   if ((rc = E->hip(E->d_enabled.ensure(E->N), "alloc enabled"))) return bail(rc);
   if ((rc = E->hip(E->d_ip.ensure(E->N), "alloc ip"))) return bail(rc);
-  if ((rc = E->hip(E->d_heap.ensure(nwg * kHeapCap * kWave), "alloc heap"))) return bail(rc);
+  if ((rc = E->hip(E->d_heap.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc heap"))) return bail(rc);
   if ((rc = E->hip(E->d_ring.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc ring"))) return bail(rc);
   if ((rc = E->hip(E->d_gen_seq.ensure(E->S), "alloc gen_seq"))) return bail(rc);
   if ((rc = E->hip(E->d_stats.ensure(kStSlots), "alloc stats"))) return bail(rc);

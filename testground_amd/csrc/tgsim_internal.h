@@ -11,7 +11,12 @@
 namespace tgsim {
 
 constexpr uint32_t kHeapCap = 1024;   // >= queue_limit (netem limit, max 1024)
-constexpr uint32_t kWave = 64;        // sources per simulate workgroup (lane = source)
+constexpr uint32_t kWave = 64;        // lanes per wavefront
+#ifndef TGSIM_SPW
+#define TGSIM_SPW 1
+#endif
+constexpr uint32_t kSpw = TGSIM_SPW;  // sources per simulate wavefront (LDS-resident queues)
+constexpr uint32_t kAhead = kWave / kSpw;  // records per source staged per batch
 constexpr uint64_t kEMask = (1ull << 46) - 1;  // eligibility time field of a queued item
 constexpr uint32_t kStates = 1024;    // sync states
 
@@ -75,8 +80,8 @@ struct SimArgs {
   const uint64_t* off;      // CSR offsets of the step's offered packets (S+1)
   const InRec* in;
   uint8_t* verdict;         // one byte per offered packet
-  uint4* heap;              // [wg][slot][lane] interleaved, 16 B items
-  uint64_t* ring;           // [s][kHeapCap] departure times
+  uint4* heap;              // [s][kHeapCap] eligibility heap, 16 B items
+  uint64_t* ring;           // [s][kHeapCap] departure times, compacted (head at 0)
   tgsim_delivery* emit;     // per-source regions, base 2*off[s] + kHeapCap*s
   uint32_t* emit_n;         // records emitted per source this step
   unsigned long long* stats;

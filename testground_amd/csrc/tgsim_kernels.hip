@@ -45,83 +45,112 @@ __device__ __forceinline__ uint64_t w0_of(const uint4& a) {
   return ((uint64_t)a.y << 32) | a.x;
 }
 __device__ __forceinline__ bool item_lt(const uint4& a, const uint4& b) {
+  // (e, seq, clone first), evaluated without branches: a divergent compare in the sift loop costs
+  // more than the LDS round trip it guards.
   const uint64_t ea = w0_of(a) & kEMask, eb = w0_of(b) & kEMask;
-  if (ea != eb) return ea < eb;
-  if (a.z != b.z) return a.z < b.z;
-  return (a.y >> 30 & 1u) > (b.y >> 30 & 1u);  // DUP flag (bit 62) set sorts first
+  const bool dup_first = (a.y >> 30 & 1u) > (b.y >> 30 & 1u);
+  const bool seq_lt = (a.z < b.z) | ((a.z == b.z) & dup_first);
+  return (ea < eb) | ((ea == eb) & seq_lt);
 }
 
+// Per-workgroup LDS: the eligibility heaps and departure rings of kSpw sources, plus the staging
+// area where all 64 lanes leave the prefetched record + Philox draws for the sequential lanes.
+struct alignas(16) Pre {
+  uint4 rec;   // dst, seq, tick, len | filter verdict << 16
+  uint4 r0;    // draw 0: dup, loss, corrupt, reorder
+  uint4 r2;    // draw 2 (clone): loss, corrupt, reorder, delay
+  uint4 r1;    // draw 1: delay word in .x
+};
+struct SimLds {
+  uint4 heap[kHeapCap * kSpw];     // slot k of source j at k * kSpw + j
+  uint64_t ring[kHeapCap * kSpw];  // departure times, circular per source
+  Pre stage[kWave];
+  uint8_t vst[kWave];              // verdicts of the batch, stored back coalesced
+};
+static_assert(sizeof(SimLds) <= 163840, "simulate workgroup exceeds 160 KiB of LDS");
+
+constexpr uint32_t kFvPass = 0xFFu;
+
 struct Lane {
-  // heap in the workgroup's interleaved block: slot k at hb[k * 64]
-  uint4* hb;
-  uint64_t* ring;
+  uint4* hb;        // LDS heap of this source, stride kSpw
+  uint64_t* rb;     // LDS ring of this source, stride kSpw
   tgsim_delivery* emit;
   uint32_t n_emit;
   SrcState st;
   SrcParams p;
   uint32_t src;
-  // statistics
   uint32_t scheduled, cloned, corrupted, offered;
-  uint32_t verdicts[8];
+  uint32_t v0, v1, v2, v3, v4, v5, v6, v7;
   uint64_t bytes;
   uint32_t err;
+  // register copies of the two values the common (queue-full) path compares against
+  uint64_t top_e;   // eligibility time of the heap root, ~0 when the heap is empty
+  uint64_t head_d;  // departure time at the ring head, ~0 when the ring is empty
 };
 
+__device__ __forceinline__ uint4 hget(const Lane& L, uint32_t k) { return L.hb[k * kSpw]; }
+__device__ __forceinline__ void hset(Lane& L, uint32_t k, const uint4& v) { L.hb[k * kSpw] = v; }
+
 __device__ __forceinline__ void heap_push(Lane& L, uint4 it) {
+  const uint64_t e = w0_of(it) & kEMask;
+  if (e < L.top_e) L.top_e = e;  // ties keep the root's e: only the time is cached
   uint32_t i = L.st.heap_n++;
   while (i > 0) {
     const uint32_t par = (i - 1) >> 1;
-    const uint4 pv = L.hb[(size_t)par * kWave];
+    const uint4 pv = hget(L, par);
     if (!item_lt(it, pv)) break;
-    L.hb[(size_t)i * kWave] = pv;
+    hset(L, i, pv);
     i = par;
   }
-  L.hb[(size_t)i * kWave] = it;
+  hset(L, i, it);
 }
 
-__device__ __forceinline__ uint4 heap_pop(Lane& L) {
-  const uint4 top = L.hb[0];
+__device__ __forceinline__ void heap_pop(Lane& L) {
   const uint32_t n = --L.st.heap_n;
-  const uint4 last = L.hb[(size_t)n * kWave];
+  const uint4 last = hget(L, n);
   uint32_t i = 0;
   for (;;) {
     uint32_t c = 2 * i + 1;
     if (c >= n) break;
-    uint4 cv = L.hb[(size_t)c * kWave];
+    uint4 cv = hget(L, c);
     if (c + 1 < n) {
-      const uint4 rv = L.hb[(size_t)(c + 1) * kWave];
+      const uint4 rv = hget(L, c + 1);
       if (item_lt(rv, cv)) {
         cv = rv;
         ++c;
       }
     }
     if (!item_lt(cv, last)) break;
-    L.hb[(size_t)i * kWave] = cv;
+    hset(L, i, cv);
     i = c;
   }
-  if (n) L.hb[(size_t)i * kWave] = last;
-  return top;
+  if (n) hset(L, i, last);
+  L.top_e = n ? (w0_of(hget(L, 0)) & kEMask) : ~0ull;
+}
+
+__device__ __forceinline__ void count_verdict(Lane& L, uint32_t v) {
+  L.v0 += v == 0; L.v1 += v == 1; L.v2 += v == 2; L.v3 += v == 3;
+  L.v4 += v == 4; L.v5 += v == 5; L.v6 += v == 6; L.v7 += v == 7;
 }
 
 // HTB class serving the netem queue in eligibility order: d = max(e, TAT),
 // TAT' = max(TAT, e - B) + len * mult >> shift.
 __device__ __forceinline__ void htb_until(Lane& L, uint64_t horizon) {
-  while (L.st.heap_n) {
-    const uint4 top = L.hb[0];
-    const uint64_t e = w0_of(top) & kEMask;
+  while (L.top_e < horizon) {
+    const uint4 top = hget(L, 0);
+    const uint64_t w0 = w0_of(top);
+    const uint64_t e = w0 & kEMask;
     if (e >= horizon) break;
     heap_pop(L);
-    const uint64_t w0 = w0_of(top);
     const uint32_t len = (uint32_t)(w0 >> 46) & 0xFFFFu;
     const uint32_t flags = (uint32_t)(w0 >> 62);
     const uint64_t d = e > L.st.tat ? e : L.st.tat;
     const uint64_t fl = e > L.p.burst_ns ? e - L.p.burst_ns : 0;
     const uint64_t base = L.st.tat > fl ? L.st.tat : fl;
     L.st.tat = base + (((uint64_t)len * L.p.mult) >> (L.p.shift_ext & 0xFFu));
-    L.ring[(L.st.ring_head + L.st.ring_n) & (kHeapCap - 1)] = d;
-    L.st.ring_n++;
-    tgsim_delivery* r = L.emit + L.n_emit++;
-    uint64_t* rw = reinterpret_cast<uint64_t*>(r);
+    L.rb[((L.st.ring_head + L.st.ring_n) & (kHeapCap - 1)) * kSpw] = d;
+    if (L.st.ring_n++ == 0) L.head_d = d;
+    uint64_t* rw = reinterpret_cast<uint64_t*>(L.emit + L.n_emit++);
     rw[0] = d;
     rw[1] = ((uint64_t)top.w << 32) | L.src;
     rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | top.z;
@@ -131,16 +160,16 @@ __device__ __forceinline__ void htb_until(Lane& L, uint64_t horizon) {
   }
 }
 
-// netem_enqueue from the queue-limit check on.
-__device__ __forceinline__ uint32_t enqueue(Lane& L, const SimArgs& a, uint64_t T, uint32_t dst,
+// netem_enqueue from the queue-limit check on; `delay_raw` is the (uncorrelated) tabledist word.
+__device__ __forceinline__ uint32_t enqueue(Lane& L, uint32_t limit, uint64_t T, uint32_t dst,
                                             uint32_t seq, uint32_t len, uint32_t reo_raw,
-                                            uint32_t draw, int delay_word, uint32_t flags) {
+                                            uint32_t delay_raw, uint32_t flags) {
   htb_until(L, T);
-  while (L.st.ring_n && L.ring[L.st.ring_head] < T) {
+  while (L.head_d < T) {  // departures before T leave the netem queue
     L.st.ring_head = (L.st.ring_head + 1) & (kHeapCap - 1);
-    L.st.ring_n--;
+    L.head_d = --L.st.ring_n ? L.rb[L.st.ring_head * kSpw] : ~0ull;
   }
-  if (L.st.heap_n + L.st.ring_n >= a.queue_limit) return TGSIM_V_QUEUE_FULL;
+  if (L.st.heap_n + L.st.ring_n >= limit) return TGSIM_V_QUEUE_FULL;
   bool reordered = false;
   if (L.p.thr_reo) reordered = !(L.p.thr_reo < crand(reo_raw, L.p.rho_reo, L.st.last_reo));
   uint64_t e;
@@ -149,73 +178,70 @@ __device__ __forceinline__ uint32_t enqueue(Lane& L, const SimArgs& a, uint64_t 
   } else if (L.p.sigma == 0) {
     e = T + L.p.lat_ns;
   } else {
-    uint32_t r[4];
-    philox(L.src, dst, seq, draw, a.key0, a.key1, r);
     const uint32_t m = 2u * (uint32_t)L.p.sigma;
-    const int64_t delay = (int64_t)(r[delay_word] % m) + (int64_t)L.p.lat_ns - (int64_t)L.p.sigma;
+    const int64_t delay = (int64_t)(delay_raw % m) + (int64_t)L.p.lat_ns - (int64_t)L.p.sigma;
     e = delay > 0 ? T + (uint64_t)delay : T;
   }
   if (e > kEMask) {
     L.err |= kErrTimeOverflow;
     e = kEMask;
   }
-  uint4 it;
   const uint64_t w0 = e | ((uint64_t)(len & 0xFFFFu) << 46) | ((uint64_t)flags << 62);
-  it.x = (uint32_t)w0;
-  it.y = (uint32_t)(w0 >> 32);
-  it.z = seq;
-  it.w = dst;
-  heap_push(L, it);
+  heap_push(L, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst));
   return TGSIM_V_SCHEDULED;
 }
 
-__device__ __forceinline__ uint32_t fib_lookup(const SimArgs& a, const SrcParams& p, uint32_t ip) {
-  // binary search over sorted disjoint intervals
-  uint32_t lo = 0, hi = p.rule_n;
-  const Interval* iv = a.rules + p.rule_off;
+__device__ __forceinline__ uint32_t fib_lookup(const Interval* iv, uint32_t n, uint32_t ip) {
+  uint32_t lo = 0, hi = n;  // binary search over sorted disjoint intervals
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
     if (iv[mid].hi < ip) lo = mid + 1;
     else hi = mid;
   }
-  if (lo < p.rule_n && iv[lo].lo <= ip) return iv[lo].act;
+  if (lo < n && iv[lo].lo <= ip) return iv[lo].act;
   return TGSIM_ACCEPT;
 }
 
-__device__ __forceinline__ uint32_t process(Lane& L, const SimArgs& a, uint64_t T, const InRec& k) {
-  L.offered++;
-  const uint32_t dst = k.dst;
-  const bool ext = dst == TGSIM_EXTERNAL;
-  if (!a.enabled[L.src] || (!ext && !a.enabled[dst])) return 0xF0u | TGSIM_V_DISCONNECTED;
-  if (ext) return 0xF0u | ((L.p.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE);
-  if (L.p.rule_n) {
-    const uint32_t act = fib_lookup(a, L.p, a.ip[dst]);
-    if (act == TGSIM_DROP) return 0xF0u | TGSIM_V_BLACKHOLE;
-    if (act == TGSIM_REJECT) return 0xF0u | TGSIM_V_PROHIBIT;
+// Connectivity, routing policy and FIB rules (no queue state involved): computed by the
+// prefetching lanes.  Returns kFvPass or the verdict.
+__device__ __forceinline__ uint32_t filter(const SimArgs& a, const SrcParams& p, bool src_on, uint32_t dst) {
+  if (dst == TGSIM_EXTERNAL) {
+    if (!src_on) return TGSIM_V_DISCONNECTED;
+    return (p.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE;
   }
-  uint32_t r0[4];
-  philox(L.src, dst, k.seq, 0, a.key0, a.key1, r0);
+  if (!src_on || !a.enabled[dst]) return TGSIM_V_DISCONNECTED;
+  if (p.rule_n) {
+    const uint32_t act = fib_lookup(a.rules + p.rule_off, p.rule_n, a.ip[dst]);
+    if (act == TGSIM_DROP) return TGSIM_V_BLACKHOLE;
+    if (act == TGSIM_REJECT) return TGSIM_V_PROHIBIT;
+  }
+  return kFvPass;
+}
+
+// The sequential part of netem_enqueue for one offered packet, with its draws precomputed.
+__device__ __forceinline__ uint32_t process(Lane& L, uint32_t limit, uint64_t T, const Pre& pre) {
+  L.offered++;
+  const uint32_t dst = pre.rec.x, seq = pre.rec.y, len = pre.rec.w & 0xFFFFu;
+  const uint32_t fv = pre.rec.w >> 16;
+  if (fv != kFvPass) return 0xF0u | fv;
   int count = 1;
-  if (L.p.thr_dup && L.p.thr_dup >= crand(r0[0], L.p.rho_dup, L.st.last_dup)) ++count;
-  if (L.p.thr_loss && L.p.thr_loss >= r0[1]) --count;
+  if (L.p.thr_dup && L.p.thr_dup >= crand(pre.r0.x, L.p.rho_dup, L.st.last_dup)) ++count;
+  if (L.p.thr_loss && L.p.thr_loss >= pre.r0.y) --count;
   if (count == 0) return 0xF0u | TGSIM_V_LOSS;
   uint32_t cv = TGSIM_V_NONE;
-  const uint32_t len = k.len & 0xFFFFu;
-  if (count == 2) {
+  if (count == 2) {  // the clone re-enters the root qdisc with duplicate = 0
     L.cloned++;
-    uint32_t r2[4];
-    philox(L.src, dst, k.seq, 2, a.key0, a.key1, r2);
-    if (L.p.thr_loss && L.p.thr_loss >= r2[0]) {
+    if (L.p.thr_loss && L.p.thr_loss >= pre.r2.x) {
       cv = TGSIM_V_LOSS;
     } else {
       uint32_t fl = TGSIM_FLAG_DUP;
-      if (L.p.thr_cor && L.p.thr_cor >= crand(r2[1], L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
-      cv = enqueue(L, a, T, dst, k.seq, len, r2[2], 2, 3, fl);
+      if (L.p.thr_cor && L.p.thr_cor >= crand(pre.r2.y, L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+      cv = enqueue(L, limit, T, dst, seq, len, pre.r2.z, pre.r2.w, fl);
     }
   }
   uint32_t fl = 0;
-  if (L.p.thr_cor && L.p.thr_cor >= crand(r0[2], L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
-  const uint32_t ov = enqueue(L, a, T, dst, k.seq, len, r0[3], 1, 0, fl);
+  if (L.p.thr_cor && L.p.thr_cor >= crand(pre.r0.z, L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+  const uint32_t ov = enqueue(L, limit, T, dst, seq, len, pre.r0.w, pre.r1.x, fl);
   return (cv << 4) | ov;
 }
 
@@ -229,48 +255,155 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
+  return v;
+}
+
+// One wave per workgroup owns kSpw sources.  Per batch every lane (j, r) = (lane % kSpw,
+// lane / kSpw) loads record r of source j's next kAhead records, evaluates the filter and the
+// three Philox blocks the packet may need, and stages them in LDS; then lane j replays its
+// source's kAhead packets through the queue-limit / eligibility-heap / HTB recurrence, which lives
+// in LDS.  The next batch's records are requested before the sequential phase starts.
 __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
+  __shared__ SimLds lds;
   const uint32_t lane = threadIdx.x;
-  const uint32_t s = blockIdx.x * kWave + lane;
-  const bool active = s < a.n_src;
+  const uint32_t s0 = blockIdx.x * kSpw;
+  // ---- load heaps and rings of the workgroup's sources into LDS
+  for (uint32_t j = 0; j < kSpw; ++j) {
+    const uint32_t s = s0 + j;
+    if (s >= a.n_src) break;
+    const uint32_t hn = a.state[s].heap_n, rn = a.state[s].ring_n;
+    for (uint32_t k = lane; k < hn; k += kWave) lds.heap[k * kSpw + j] = a.heap[(size_t)s * kHeapCap + k];
+    for (uint32_t k = lane; k < rn; k += kWave) lds.ring[k * kSpw + j] = a.ring[(size_t)s * kHeapCap + k];
+  }
+  // ---- per-lane roles
+  const uint32_t pj = lane % kSpw, pr = lane / kSpw;
+  const bool prefetcher = pr < kAhead && s0 + pj < a.n_src;
+  SrcParams pp;
+  uint64_t pbeg = 0, pend = 0;
+  bool src_on = false;
+  if (prefetcher) {
+    pp = a.params[s0 + pj];
+    pbeg = a.off[s0 + pj];
+    pend = a.off[s0 + pj + 1];
+    src_on = a.enabled[a.shard_begin + s0 + pj] != 0;
+  }
+  const bool seq_lane = lane < kSpw && s0 + lane < a.n_src;
   Lane L;
   L.offered = L.scheduled = L.cloned = L.corrupted = 0;
+  L.v0 = L.v1 = L.v2 = L.v3 = L.v4 = L.v5 = L.v6 = L.v7 = 0;
   L.bytes = 0;
   L.err = 0;
   L.n_emit = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) L.verdicts[i] = 0;
-  if (active) {
+  uint64_t sbeg = 0, send = 0;
+  uint32_t nb = 0;
+  if (seq_lane) {
+    const uint32_t s = s0 + lane;
     L.p = a.params[s];
     L.st = a.state[s];
+    L.st.ring_head = 0;  // rings are stored compacted
     L.src = a.shard_begin + s;
-    L.hb = a.heap + (size_t)blockIdx.x * kHeapCap * kWave + lane;
-    L.ring = a.ring + (size_t)s * kHeapCap;
-    const uint64_t b = a.off[s], e = a.off[s + 1];
-    L.emit = a.emit + 2 * b + (uint64_t)kHeapCap * s;
-    for (uint64_t i = b; i < e; ++i) {
-      const InRec k = a.in[i];
-      const uint64_t T = a.t0_ns + (uint64_t)k.tick * a.tick_ns;
-      const uint32_t v = process(L, a, T, k);
-      a.verdict[i] = (uint8_t)v;
-      L.verdicts[v & 15u]++;
-      if ((v >> 4) != TGSIM_V_NONE) L.verdicts[v >> 4]++;
-    }
-    htb_until(L, a.horizon_ns);
-    a.state[s] = L.st;
-    a.emit_n[s] = L.n_emit;
+    L.hb = lds.heap + lane;
+    L.rb = lds.ring + lane;
+    sbeg = a.off[s];
+    send = a.off[s + 1];
+    L.emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
+    nb = (uint32_t)((send - sbeg + kAhead - 1) / kAhead);
   }
-  uint64_t sums[kStSlots];
+  const uint32_t n_batches = wave_max(nb);
+  __syncthreads();
+  if (seq_lane) {
+    L.top_e = L.st.heap_n ? (w0_of(lds.heap[lane]) & kEMask) : ~0ull;
+    L.head_d = L.st.ring_n ? lds.ring[lane] : ~0ull;
+  }
+  // ---- batch loop
+  uint64_t idx = pbeg + pr;
+  InRec rec = {};
+  if (prefetcher && idx < pend) rec = a.in[idx];
+  for (uint32_t b = 0; b < n_batches; ++b) {
+    const uint64_t my_idx = idx;  // the record this lane stages in this batch
+    const bool staged = prefetcher && my_idx < pend;
+    if (staged) {
+      Pre pre;
+      const uint32_t fv = filter(a, pp, src_on, rec.dst);
+      pre.rec = make_uint4(rec.dst, rec.seq, rec.tick, (rec.len & 0xFFFFu) | (fv << 16));
+      pre.r0 = pre.r1 = pre.r2 = make_uint4(0, 0, 0, 0);
+      if (fv == kFvPass) {
+        const uint32_t src = a.shard_begin + s0 + pj;
+        uint32_t r[4];
+        philox(src, rec.dst, rec.seq, 0, a.key0, a.key1, r);
+        pre.r0 = make_uint4(r[0], r[1], r[2], r[3]);
+        if (pp.thr_dup) {
+          philox(src, rec.dst, rec.seq, 2, a.key0, a.key1, r);
+          pre.r2 = make_uint4(r[0], r[1], r[2], r[3]);
+        }
+        if (pp.sigma) {
+          philox(src, rec.dst, rec.seq, 1, a.key0, a.key1, r);
+          pre.r1.x = r[0];
+        }
+      }
+      lds.stage[lane] = pre;
+    }
+    __syncthreads();
+    idx += kAhead;
+    if (prefetcher && idx < pend) rec = a.in[idx];  // in flight during the sequential phase
+    if (seq_lane) {
+      const uint64_t first = sbeg + (uint64_t)b * kAhead;
+      const uint32_t nr = first < send ? (uint32_t)min((uint64_t)kAhead, send - first) : 0u;
+      Pre nxt;
+      if (nr) nxt = lds.stage[lane];
+      for (uint32_t r = 0; r < nr; ++r) {
+        const Pre pre = nxt;
+        if (r + 1 < nr) nxt = lds.stage[(r + 1) * kSpw + lane];  // next record's LDS read in flight
+        const uint64_t T = a.t0_ns + (uint64_t)pre.rec.z * a.tick_ns;
+        const uint32_t v = process(L, a.queue_limit, T, pre);
+        lds.vst[r * kSpw + lane] = (uint8_t)v;
+        count_verdict(L, v & 15u);
+        if ((v >> 4) != TGSIM_V_NONE) count_verdict(L, v >> 4);
+      }
+    }
+    __syncthreads();
+    if (staged) a.verdict[my_idx] = lds.vst[lane];
+  }
+  if (seq_lane) {
+    htb_until(L, a.horizon_ns);
+    a.emit_n[s0 + lane] = L.n_emit;
+  }
+  __syncthreads();
+  // ---- write back state, heaps and (compacted) rings
+  for (uint32_t j = 0; j < kSpw; ++j) {
+    const uint32_t s = s0 + j;
+    if (s >= a.n_src) break;
+    const uint32_t hn = __shfl(L.st.heap_n, j, 64);
+    const uint32_t rn = __shfl(L.st.ring_n, j, 64);
+    const uint32_t rh = __shfl(L.st.ring_head, j, 64);
+    for (uint32_t k = lane; k < hn; k += kWave) a.heap[(size_t)s * kHeapCap + k] = lds.heap[k * kSpw + j];
+    for (uint32_t k = lane; k < rn; k += kWave)
+      a.ring[(size_t)s * kHeapCap + k] = lds.ring[((rh + k) & (kHeapCap - 1)) * kSpw + j];
+  }
+  if (seq_lane) {
+    L.st.ring_head = 0;
+    a.state[s0 + lane] = L.st;
+  }
+  uint64_t sums[kStBytes + 1];
   sums[kStOffered] = wave_sum(L.offered);
   sums[kStScheduled] = wave_sum(L.scheduled);
   sums[kStCloned] = wave_sum(L.cloned);
   sums[kStCorrupted] = wave_sum(L.corrupted);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) sums[kStVerdict0 + i] = wave_sum(L.verdicts[i]);
+  sums[kStVerdict0 + 0] = wave_sum(L.v0);
+  sums[kStVerdict0 + 1] = wave_sum(L.v1);
+  sums[kStVerdict0 + 2] = wave_sum(L.v2);
+  sums[kStVerdict0 + 3] = wave_sum(L.v3);
+  sums[kStVerdict0 + 4] = wave_sum(L.v4);
+  sums[kStVerdict0 + 5] = wave_sum(L.v5);
+  sums[kStVerdict0 + 6] = wave_sum(L.v6);
+  sums[kStVerdict0 + 7] = wave_sum(L.v7);
   sums[kStBytes] = wave_sum(L.bytes);
-  const uint32_t err = (uint32_t)wave_sum(L.err ? 1u : 0u);
+  const uint64_t err = wave_sum(L.err ? 1u : 0u);
   if (lane == 0) {
-    for (int i = 0; i < kStBytes + 1; ++i)
+    for (int i = 0; i <= kStBytes; ++i)
       if (sums[i]) atomicAdd(&a.stats[i], (unsigned long long)sums[i]);
     if (err) atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
   }
@@ -561,7 +694,7 @@ __global__ __launch_bounds__(256) void k_dst_sort(const tgsim_delivery* in, cons
 // ---------------------------------------------------------------------------------------------
 // Host-side launchers.
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
-  hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);
+  hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
 }
 
 void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st) {

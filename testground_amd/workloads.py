@@ -81,28 +81,31 @@ def configure_splitbrain(eng, n: int, case: str) -> np.ndarray:
     return region
 
 
-def run_splitbrain(eng, n: int, case: str, pkt_len: int = 66) -> Tuple[np.ndarray, Dict]:
-    """All ordered pairs send one request at tick 0; each delivered request is answered.
-    Returns ok[i, j] = request i->j and its reply j->i both delivered, plus step artifacts."""
+def run_splitbrain(eng, n: int, case: str, pkt_len: int = 66, gap: int = 8) -> Tuple[np.ndarray, Dict]:
+    """Every instance contacts every other instance once, sequentially (one request every `gap`
+    ticks, as the plan's `for _, p := range nodes { httpclient.Get(...) }`, main.go:159-175), and
+    every delivered request is answered.  Replies run in a second window on the same relative time
+    axis (reply tick = floor(d / tick) + 1).  Returns ok[i, j] = request i->j and its reply j->i
+    both delivered, plus the step artifacts."""
     region = configure_splitbrain(eng, n, case)
     src, dst = np.nonzero(~np.eye(n, dtype=bool))
+    k = dst - (dst > src)  # per-source request index 0..n-2
     req = np.zeros(len(src), dtype=abi.PKT_DTYPE)
-    req["src"], req["dst"], req["len"], req["tick"] = src, dst, pkt_len, 0
-    req["seq"] = dst - (dst > src)  # per-source sequence 0..n-2
+    req["src"], req["dst"], req["len"] = src, dst, pkt_len
+    req["seq"], req["tick"] = k, k * gap
+    span = (n - 1) * gap
+    t0 = eng.stats()["now_tick"]
     eng.submit(req)
-    eng.step(1)
+    eng.step(span)
     v_req = eng.verdicts()
     d_req = eng.drain()
     tick = eng.tick_ns
-    now = 1
     rep = np.zeros(len(d_req), dtype=abi.PKT_DTYPE)
     rep["src"], rep["dst"], rep["len"] = d_req["dst"], d_req["src"], pkt_len
     rep["seq"] = (n - 1) + d_req["src"]  # fresh per-source sequence numbers
-    rtick = d_req["t_ns"] // tick + 1
-    span = int(rtick.max() - now + 1) if len(rtick) else 1
-    rep["tick"] = rtick - now
+    rep["tick"] = (d_req["t_ns"] // tick + 1) - t0
     eng.submit(rep)
-    eng.step(span)
+    eng.step(span + 2)
     v_rep = eng.verdicts()
     d_rep = eng.drain()
     ok = np.zeros((n, n), dtype=bool)
