@@ -79,8 +79,7 @@ struct Lane {
   SrcState st;
   SrcParams p;
   uint32_t src;
-  uint32_t scheduled, cloned, corrupted, offered;
-  uint32_t v0, v1, v2, v3, v4, v5, v6, v7;
+  uint32_t scheduled, corrupted;
   uint64_t bytes;
   uint32_t err;
   // register copies of the two values the common (queue-full) path compares against
@@ -128,10 +127,6 @@ __device__ __forceinline__ void heap_pop(Lane& L) {
   L.top_e = n ? (w0_of(hget(L, 0)) & kEMask) : ~0ull;
 }
 
-__device__ __forceinline__ void count_verdict(Lane& L, uint32_t v) {
-  L.v0 += v == 0; L.v1 += v == 1; L.v2 += v == 2; L.v3 += v == 3;
-  L.v4 += v == 4; L.v5 += v == 5; L.v6 += v == 6; L.v7 += v == 7;
-}
 
 // HTB class serving the netem queue in eligibility order: d = max(e, TAT),
 // TAT' = max(TAT, e - B) + len * mult >> shift.
@@ -160,28 +155,42 @@ __device__ __forceinline__ void htb_until(Lane& L, uint64_t horizon) {
   }
 }
 
-// netem_enqueue from the queue-limit check on; `delay_raw` is the (uncorrelated) tabledist word.
-__device__ __forceinline__ uint32_t enqueue(Lane& L, uint32_t limit, uint64_t T, uint32_t dst,
-                                            uint32_t seq, uint32_t len, uint32_t reo_raw,
-                                            uint32_t delay_raw, uint32_t flags) {
+// Queue-limit check and insertion of one netem item whose eligibility time e is already known.
+__device__ __forceinline__ uint32_t admit(Lane& L, uint32_t limit, uint64_t T, uint64_t e, uint32_t dst,
+                                          uint32_t seq, uint32_t len, uint32_t flags) {
   htb_until(L, T);
   while (L.head_d < T) {  // departures before T leave the netem queue
     L.st.ring_head = (L.st.ring_head + 1) & (kHeapCap - 1);
     L.head_d = --L.st.ring_n ? L.rb[L.st.ring_head * kSpw] : ~0ull;
   }
   if (L.st.heap_n + L.st.ring_n >= limit) return TGSIM_V_QUEUE_FULL;
+  const uint64_t w0 = e | ((uint64_t)(len & 0xFFFFu) << 46) | ((uint64_t)flags << 62);
+  heap_push(L, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst));
+  return TGSIM_V_SCHEDULED;
+}
+
+// tabledist() uniform branch: e = T + max(0, L - sigma + raw mod 2 sigma), or T + L when sigma = 0.
+__device__ __forceinline__ uint64_t delayed(const SrcParams& p, uint64_t T, uint32_t raw) {
+  if (p.sigma == 0) return T + p.lat_ns;
+  const uint32_t m = 2u * (uint32_t)p.sigma;
+  const int64_t delay = (int64_t)(raw % m) + (int64_t)p.lat_ns - (int64_t)p.sigma;
+  return delay > 0 ? T + (uint64_t)delay : T;
+}
+
+// netem_enqueue from the queue-limit check on, for sources with correlated draws: the reorder
+// decision consumes correlated state only when the packet passes the limit check.
+__device__ __forceinline__ uint32_t enqueue(Lane& L, uint32_t limit, uint64_t T, uint32_t dst,
+                                            uint32_t seq, uint32_t len, uint32_t reo_raw,
+                                            uint32_t delay_raw, uint32_t flags) {
+  htb_until(L, T);
+  while (L.head_d < T) {
+    L.st.ring_head = (L.st.ring_head + 1) & (kHeapCap - 1);
+    L.head_d = --L.st.ring_n ? L.rb[L.st.ring_head * kSpw] : ~0ull;
+  }
+  if (L.st.heap_n + L.st.ring_n >= limit) return TGSIM_V_QUEUE_FULL;
   bool reordered = false;
   if (L.p.thr_reo) reordered = !(L.p.thr_reo < crand(reo_raw, L.p.rho_reo, L.st.last_reo));
-  uint64_t e;
-  if (reordered) {
-    e = T;
-  } else if (L.p.sigma == 0) {
-    e = T + L.p.lat_ns;
-  } else {
-    const uint32_t m = 2u * (uint32_t)L.p.sigma;
-    const int64_t delay = (int64_t)(delay_raw % m) + (int64_t)L.p.lat_ns - (int64_t)L.p.sigma;
-    e = delay > 0 ? T + (uint64_t)delay : T;
-  }
+  uint64_t e = reordered ? T : delayed(L.p, T, delay_raw);
   if (e > kEMask) {
     L.err |= kErrTimeOverflow;
     e = kEMask;
@@ -202,8 +211,8 @@ __device__ __forceinline__ uint32_t fib_lookup(const Interval* iv, uint32_t n, u
   return TGSIM_ACCEPT;
 }
 
-// Connectivity, routing policy and FIB rules (no queue state involved): computed by the
-// prefetching lanes.  Returns kFvPass or the verdict.
+// Connectivity, routing policy and FIB rules (no queue state involved).  Returns kFvPass or the
+// verdict.
 __device__ __forceinline__ uint32_t filter(const SimArgs& a, const SrcParams& p, bool src_on, uint32_t dst) {
   if (dst == TGSIM_EXTERNAL) {
     if (!src_on) return TGSIM_V_DISCONNECTED;
@@ -218,9 +227,8 @@ __device__ __forceinline__ uint32_t filter(const SimArgs& a, const SrcParams& p,
   return kFvPass;
 }
 
-// The sequential part of netem_enqueue for one offered packet, with its draws precomputed.
-__device__ __forceinline__ uint32_t process(Lane& L, uint32_t limit, uint64_t T, const Pre& pre) {
-  L.offered++;
+// Sequential netem_enqueue for one offered packet of a correlated source (raw draws staged).
+__device__ __forceinline__ uint32_t process_corr(Lane& L, uint32_t limit, uint64_t T, const Pre& pre) {
   const uint32_t dst = pre.rec.x, seq = pre.rec.y, len = pre.rec.w & 0xFFFFu;
   const uint32_t fv = pre.rec.w >> 16;
   if (fv != kFvPass) return 0xF0u | fv;
@@ -230,7 +238,6 @@ __device__ __forceinline__ uint32_t process(Lane& L, uint32_t limit, uint64_t T,
   if (count == 0) return 0xF0u | TGSIM_V_LOSS;
   uint32_t cv = TGSIM_V_NONE;
   if (count == 2) {  // the clone re-enters the root qdisc with duplicate = 0
-    L.cloned++;
     if (L.p.thr_loss && L.p.thr_loss >= pre.r2.x) {
       cv = TGSIM_V_LOSS;
     } else {
@@ -261,11 +268,19 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
   return v;
 }
 
-// One wave per workgroup owns kSpw sources.  Per batch every lane (j, r) = (lane % kSpw,
-// lane / kSpw) loads record r of source j's next kAhead records, evaluates the filter and the
-// three Philox blocks the packet may need, and stages them in LDS; then lane j replays its
-// source's kAhead packets through the queue-limit / eligibility-heap / HTB recurrence, which lives
-// in LDS.  The next batch's records are requested before the sequential phase starts.
+// Staged candidate of an uncorrelated source (48 B of a Pre slot): everything netem decides
+// without queue state is resolved by the lane that loaded the packet.
+//   rec = {T lo, T hi, e_orig lo, e_orig hi}, r0 = {e_clone lo, e_clone hi, dst, seq},
+//   r2.x = len | orig flags << 16 | clone flags << 18 | clone state << 20 | batch slot << 24
+// clone state: 0 none, 1 lost, 2 queue candidate.
+
+// One wavefront per workgroup owns kSpw sources (kSpw = 1: one netem queue per wavefront, so the
+// sequential recurrences of different sources are independent waves the SIMDs interleave).  Per
+// batch every lane (j, r) = (lane % kSpw, lane / kSpw) loads record r of source j's next kAhead
+// records and resolves the filter and all Philox-driven decisions; lane j then replays the queue
+// candidates (compacted with a ballot) through the netem-limit / eligibility-heap / HTB
+// recurrence held in LDS.  Sources with correlated draws (get_crandom, rho != 0) replay the raw
+// draws sequentially instead.  The next batch's records are in flight during the sequential phase.
 __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   __shared__ SimLds lds;
   const uint32_t lane = threadIdx.x;
@@ -284,16 +299,20 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   SrcParams pp;
   uint64_t pbeg = 0, pend = 0;
   bool src_on = false;
+  uint32_t psrc = 0;
   if (prefetcher) {
     pp = a.params[s0 + pj];
     pbeg = a.off[s0 + pj];
     pend = a.off[s0 + pj + 1];
-    src_on = a.enabled[a.shard_begin + s0 + pj] != 0;
+    psrc = a.shard_begin + s0 + pj;
+    src_on = a.enabled[psrc] != 0;
   }
+  // correlated sources replay raw draws; with kSpw = 1 this is uniform across the wavefront
+  const bool corr = kSpw != 1 || (prefetcher && (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0);
+  const bool any_corr = __any(corr);
   const bool seq_lane = lane < kSpw && s0 + lane < a.n_src;
   Lane L;
-  L.offered = L.scheduled = L.cloned = L.corrupted = 0;
-  L.v0 = L.v1 = L.v2 = L.v3 = L.v4 = L.v5 = L.v6 = L.v7 = 0;
+  L.scheduled = L.corrupted = 0;
   L.bytes = 0;
   L.err = 0;
   L.n_emit = 0;
@@ -313,6 +332,8 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     nb = (uint32_t)((send - sbeg + kAhead - 1) / kAhead);
   }
   const uint32_t n_batches = wave_max(nb);
+  uint64_t c_off = 0, c_clone = 0, c_v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t perr = 0;
   __syncthreads();
   if (seq_lane) {
     L.top_e = L.st.heap_n ? (w0_of(lds.heap[lane]) & kEMask) : ~0ull;
@@ -325,47 +346,142 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   for (uint32_t b = 0; b < n_batches; ++b) {
     const uint64_t my_idx = idx;  // the record this lane stages in this batch
     const bool staged = prefetcher && my_idx < pend;
-    if (staged) {
-      Pre pre;
-      const uint32_t fv = filter(a, pp, src_on, rec.dst);
-      pre.rec = make_uint4(rec.dst, rec.seq, rec.tick, (rec.len & 0xFFFFu) | (fv << 16));
-      pre.r0 = pre.r1 = pre.r2 = make_uint4(0, 0, 0, 0);
-      if (fv == kFvPass) {
-        const uint32_t src = a.shard_begin + s0 + pj;
-        uint32_t r[4];
-        philox(src, rec.dst, rec.seq, 0, a.key0, a.key1, r);
-        pre.r0 = make_uint4(r[0], r[1], r[2], r[3]);
-        if (pp.thr_dup) {
-          philox(src, rec.dst, rec.seq, 2, a.key0, a.key1, r);
-          pre.r2 = make_uint4(r[0], r[1], r[2], r[3]);
+    uint32_t n_cand = 0;
+    if (any_corr) {
+      // ---------- correlated path: stage raw draws, replay every packet in order
+      if (staged) {
+        Pre pre;
+        const uint32_t fv = filter(a, pp, src_on, rec.dst);
+        pre.rec = make_uint4(rec.dst, rec.seq, rec.tick, (rec.len & 0xFFFFu) | (fv << 16));
+        pre.r0 = pre.r1 = pre.r2 = make_uint4(0, 0, 0, 0);
+        if (fv == kFvPass) {
+          uint32_t r[4];
+          philox(psrc, rec.dst, rec.seq, 0, a.key0, a.key1, r);
+          pre.r0 = make_uint4(r[0], r[1], r[2], r[3]);
+          if (pp.thr_dup) {
+            philox(psrc, rec.dst, rec.seq, 2, a.key0, a.key1, r);
+            pre.r2 = make_uint4(r[0], r[1], r[2], r[3]);
+          }
+          if (pp.sigma) {
+            philox(psrc, rec.dst, rec.seq, 1, a.key0, a.key1, r);
+            pre.r1.x = r[0];
+          }
         }
-        if (pp.sigma) {
-          philox(src, rec.dst, rec.seq, 1, a.key0, a.key1, r);
-          pre.r1.x = r[0];
+        lds.stage[lane] = pre;
+      }
+    } else {
+      // ---------- uncorrelated path: resolve everything but the queue in parallel
+      uint32_t fin = 0;  // final verdict when no queue decision is needed
+      bool cand = false;
+      Pre pre;
+      if (staged) {
+        const uint64_t T = a.t0_ns + (uint64_t)rec.tick * a.tick_ns;
+        const uint32_t fv = filter(a, pp, src_on, rec.dst);
+        if (fv != kFvPass) {
+          fin = 0xF0u | fv;
+        } else {
+          uint32_t r0[4];
+          philox(psrc, rec.dst, rec.seq, 0, a.key0, a.key1, r0);
+          const int count = 1 + (pp.thr_dup && pp.thr_dup >= r0[0]) - (pp.thr_loss && pp.thr_loss >= r0[1]);
+          if (count == 0) {
+            fin = 0xF0u | TGSIM_V_LOSS;
+          } else {
+            uint32_t cstate = 0, flc = TGSIM_FLAG_DUP;
+            uint64_t ec = ~0ull;
+            if (count == 2) {
+              uint32_t r2[4];
+              philox(psrc, rec.dst, rec.seq, 2, a.key0, a.key1, r2);
+              if (pp.thr_loss && pp.thr_loss >= r2[0]) {
+                cstate = 1;
+              } else {
+                cstate = 2;
+                if (pp.thr_cor && pp.thr_cor >= r2[1]) flc |= TGSIM_FLAG_CORRUPT;
+                ec = (pp.thr_reo && pp.thr_reo >= r2[2]) ? T : delayed(pp, T, r2[3]);
+              }
+            }
+            const uint32_t flo = (pp.thr_cor && pp.thr_cor >= r0[2]) ? TGSIM_FLAG_CORRUPT : 0u;
+            uint64_t eo;
+            if (pp.thr_reo && pp.thr_reo >= r0[3]) {
+              eo = T;
+            } else if (pp.sigma) {
+              uint32_t r1[4];
+              philox(psrc, rec.dst, rec.seq, 1, a.key0, a.key1, r1);
+              eo = delayed(pp, T, r1[0]);
+            } else {
+              eo = T + pp.lat_ns;
+            }
+            if (eo > kEMask || (cstate == 2 && ec > kEMask)) perr = 1;
+            pre.rec = make_uint4((uint32_t)T, (uint32_t)(T >> 32), (uint32_t)eo, (uint32_t)(eo >> 32));
+            pre.r0 = make_uint4((uint32_t)ec, (uint32_t)(ec >> 32), rec.dst, rec.seq);
+            pre.r2 = make_uint4((rec.len & 0xFFFFu) | (flo << 16) | (flc << 18) | (cstate << 20) | (pr << 24),
+                                0, 0, 0);
+            cand = true;
+          }
         }
       }
-      lds.stage[lane] = pre;
+      const uint64_t m = __ballot(cand);
+      n_cand = __popcll(m);
+      if (cand) {
+        const Pre p2 = pre;
+        const uint32_t slot = __popcll(m & ((1ull << lane) - 1));
+        lds.stage[slot].rec = p2.rec;
+        lds.stage[slot].r0 = p2.r0;
+        lds.stage[slot].r2 = p2.r2;
+      } else if (staged) {
+        lds.vst[lane] = (uint8_t)fin;
+      }
     }
     __syncthreads();
     idx += kAhead;
     if (prefetcher && idx < pend) rec = a.in[idx];  // in flight during the sequential phase
     if (seq_lane) {
-      const uint64_t first = sbeg + (uint64_t)b * kAhead;
-      const uint32_t nr = first < send ? (uint32_t)min((uint64_t)kAhead, send - first) : 0u;
-      Pre nxt;
-      if (nr) nxt = lds.stage[lane];
-      for (uint32_t r = 0; r < nr; ++r) {
-        const Pre pre = nxt;
-        if (r + 1 < nr) nxt = lds.stage[(r + 1) * kSpw + lane];  // next record's LDS read in flight
-        const uint64_t T = a.t0_ns + (uint64_t)pre.rec.z * a.tick_ns;
-        const uint32_t v = process(L, a.queue_limit, T, pre);
-        lds.vst[r * kSpw + lane] = (uint8_t)v;
-        count_verdict(L, v & 15u);
-        if ((v >> 4) != TGSIM_V_NONE) count_verdict(L, v >> 4);
+      if (any_corr) {
+        const uint64_t first = sbeg + (uint64_t)b * kAhead;
+        const uint32_t nr = first < send ? (uint32_t)min((uint64_t)kAhead, send - first) : 0u;
+        for (uint32_t r = 0; r < nr; ++r) {
+          const Pre pre = lds.stage[r * kSpw + lane];
+          const uint64_t T = a.t0_ns + (uint64_t)pre.rec.z * a.tick_ns;
+          lds.vst[r * kSpw + lane] = (uint8_t)process_corr(L, a.queue_limit, T, pre);
+        }
+      } else {
+        uint4 n_rec, n_r0, n_r2;
+        if (n_cand) {
+          n_rec = lds.stage[0].rec;
+          n_r0 = lds.stage[0].r0;
+          n_r2 = lds.stage[0].r2;
+        }
+        for (uint32_t c = 0; c < n_cand; ++c) {
+          const uint4 crec = n_rec, cr0 = n_r0, cr2 = n_r2;
+          if (c + 1 < n_cand) {  // next candidate's LDS reads in flight
+            n_rec = lds.stage[c + 1].rec;
+            n_r0 = lds.stage[c + 1].r0;
+            n_r2 = lds.stage[c + 1].r2;
+          }
+          const uint64_t T = ((uint64_t)crec.y << 32) | crec.x;
+          const uint64_t eo = ((uint64_t)crec.w << 32) | crec.z;
+          const uint32_t info = cr2.x, len = info & 0xFFFFu, cstate = (info >> 20) & 3u;
+          uint32_t cv = cstate == 0 ? TGSIM_V_NONE : TGSIM_V_LOSS;
+          if (cstate == 2) {
+            const uint64_t ec = ((uint64_t)cr0.y << 32) | cr0.x;
+            cv = admit(L, a.queue_limit, T, ec, cr0.z, cr0.w, len, (info >> 18) & 3u);
+          }
+          const uint32_t ov = admit(L, a.queue_limit, T, eo, cr0.z, cr0.w, len, (info >> 16) & 3u);
+          lds.vst[info >> 24] = (uint8_t)((cv << 4) | ov);
+        }
       }
     }
     __syncthreads();
-    if (staged) a.verdict[my_idx] = lds.vst[lane];
+    if (staged) {
+      const uint32_t v = lds.vst[lane];
+      a.verdict[my_idx] = (uint8_t)v;
+    }
+    // statistics from the verdict bytes (wave-uniform ballot counts)
+    const uint32_t v = staged ? lds.vst[lane] : 0xFFu;
+    c_off += __popcll(__ballot(staged));
+    c_clone += __popcll(__ballot(staged && (v >> 4) != TGSIM_V_NONE));
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+      c_v[k] += __popcll(__ballot(staged && (v & 15u) == k)) + __popcll(__ballot(staged && (v >> 4) == k));
   }
   if (seq_lane) {
     htb_until(L, a.horizon_ns);
@@ -387,24 +503,18 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     L.st.ring_head = 0;
     a.state[s0 + lane] = L.st;
   }
-  uint64_t sums[kStBytes + 1];
-  sums[kStOffered] = wave_sum(L.offered);
-  sums[kStScheduled] = wave_sum(L.scheduled);
-  sums[kStCloned] = wave_sum(L.cloned);
-  sums[kStCorrupted] = wave_sum(L.corrupted);
-  sums[kStVerdict0 + 0] = wave_sum(L.v0);
-  sums[kStVerdict0 + 1] = wave_sum(L.v1);
-  sums[kStVerdict0 + 2] = wave_sum(L.v2);
-  sums[kStVerdict0 + 3] = wave_sum(L.v3);
-  sums[kStVerdict0 + 4] = wave_sum(L.v4);
-  sums[kStVerdict0 + 5] = wave_sum(L.v5);
-  sums[kStVerdict0 + 6] = wave_sum(L.v6);
-  sums[kStVerdict0 + 7] = wave_sum(L.v7);
-  sums[kStBytes] = wave_sum(L.bytes);
-  const uint64_t err = wave_sum(L.err ? 1u : 0u);
+  const uint64_t sched = wave_sum(seq_lane ? L.scheduled : 0u);
+  const uint64_t corrupted = wave_sum(seq_lane ? L.corrupted : 0u);
+  const uint64_t bytes = wave_sum(seq_lane ? L.bytes : 0ull);
+  const uint64_t err = wave_sum((seq_lane && L.err) || perr ? 1u : 0u);
   if (lane == 0) {
-    for (int i = 0; i <= kStBytes; ++i)
-      if (sums[i]) atomicAdd(&a.stats[i], (unsigned long long)sums[i]);
+    atomicAdd(&a.stats[kStOffered], (unsigned long long)c_off);
+    if (sched) atomicAdd(&a.stats[kStScheduled], (unsigned long long)sched);
+    if (c_clone) atomicAdd(&a.stats[kStCloned], (unsigned long long)c_clone);
+    if (corrupted) atomicAdd(&a.stats[kStCorrupted], (unsigned long long)corrupted);
+    for (int k = 0; k < 8; ++k)
+      if (c_v[k]) atomicAdd(&a.stats[kStVerdict0 + k], (unsigned long long)c_v[k]);
+    if (bytes) atomicAdd(&a.stats[kStBytes], (unsigned long long)bytes);
     if (err) atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
   }
 }

@@ -225,4 +225,3 @@ def test_full_size_storm_properties():
     assert (np.diff(d["dst"].astype(np.int64)) >= 0).all()
     same = d["dst"][1:] == d["dst"][:-1]
     assert (d["t_ns"][1:][same] >= d["t_ns"][:-1][same]).all()
-    assert (d["t_ns"] > 0).all()
