@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--peers", type=int, default=10_000, help="instances per GPU")
     p.add_argument("--lam", type=float, default=0.5)
     p.add_argument("--window", type=int, default=2000, help="ticks (1 us) per step")
+    p.add_argument("--settle-ms", type=float, default=120.0,
+                   help="untimed simulated time before warm-up so every netem queue is in its sustained "
+                        "storm state (> max latency + jitter = 110 ms); queues start empty otherwise")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--queue-limit", type=int, default=0, help="netem limit (0 = netlink default 1000)")
@@ -110,8 +113,6 @@ def main():
         shapes = [LinkShape(Latency=5 * Millisecond)] * peers_total
     for i, s in enumerate(shapes):
         eng.configure(i, Config(Network="default", Enable=True, Default=s, RoutingPolicy=RoutingPolicyType.DenyAll))
-    for _ in range(a.warmup + a.steps):
-        eng.gen_storm(a.lam, a.window)  # inputs resident in HBM before the timed region
     bounds = [r * a.peers for r in range(world)] + [peers_total]
     out_buf = None
 
@@ -133,6 +134,13 @@ def main():
                                [int(x) * 24 for x in rc], [int(x) * 24 for x in cnt])
         eng.deliver(inbuf.data_ptr(), int(rc.sum()))
 
+    settle = int(a.settle_ms * 1000 / a.window + 0.999)
+    for _ in range(settle):  # untimed: bring every netem queue to its sustained state
+        eng.gen_storm(a.lam, a.window)
+        one_step()
+    eng.drain()
+    for _ in range(a.warmup + a.steps):
+        eng.gen_storm(a.lam, a.window)  # inputs resident in HBM before the timed region
     for _ in range(a.warmup):
         one_step()
     eng.drain()
@@ -185,7 +193,7 @@ def main():
         "data": "synthetic (device-generated storm traffic, Philox-keyed)",
         "config": {"workload": "C3 storm: random all-to-all, heterogeneous LinkShape (BASELINE.json configs[2])",
                    "peers_per_gpu": a.peers, "peers_total": peers_total, "lambda_per_tick": a.lam,
-                   "tick_ns": 1000, "window_ticks": a.window, "shapes": a.shapes, "queue_limit": a.queue_limit or 1000,
+                   "tick_ns": 1000, "window_ticks": a.window, "settle_sim_ms": settle * a.window / 1000, "shapes": a.shapes, "queue_limit": a.queue_limit or 1000,
                    "packets_per_step": offered_all / a.steps, "parallelism": f"peer-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

@@ -201,6 +201,10 @@ int tgsim_barrier_poll(void* engine, uint32_t state, uint64_t target);
  * with HIP events on the engine's stream. */
 double tgsim_sim_kernel_ms(void* engine, uint64_t* n_launches, int reset);
 void* tgsim_stream(void* engine);
+/* Diagnostics: with TGSIM_STAMPS set at create time, the simulate kernel records 8 words per
+ * workgroup (s_memrealtime at its phase boundaries, batch count, HW_ID, queue sizes); copies them
+ * for the last step and returns the word count (0 when disabled). */
+int64_t tgsim_debug_stamps(void* engine, uint64_t* out, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -94,7 +94,7 @@ EXPORTS = [
     "tgsim_create", "tgsim_destroy", "tgsim_last_error", "tgsim_abi_version", "tgsim_configure",
     "tgsim_submit", "tgsim_gen_storm", "tgsim_step", "tgsim_step_sim", "tgsim_deliver",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
-    "tgsim_signal", "tgsim_barrier_poll", "tgsim_sim_kernel_ms", "tgsim_stream",
+    "tgsim_signal", "tgsim_barrier_poll", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
 ]
 
 
@@ -128,5 +128,6 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("barrier_poll", C.c_int, vp, C.c_uint32, C.c_uint64)
     f("sim_kernel_ms", C.c_double, vp, C.POINTER(C.c_uint64), C.c_int)
     f("stream", vp, vp)
+    f("debug_stamps", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("abi_version", C.c_uint32)
     f("offered", C.c_int64, vp, C.c_void_p, C.c_size_t)

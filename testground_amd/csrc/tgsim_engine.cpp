@@ -6,6 +6,7 @@
 // + the kernel would install it, staged, and scattered into HBM by the
 // config-apply kernel at the next step.
 #include <errno.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -202,6 +203,7 @@ struct tgsim_engine_s {
   uint32_t key0 = 0, key1 = 0;
 
   std::vector<uint8_t> enabled;
+  uint32_t n_disabled = 0;  // peers with Enable=false (0 lets k_sim skip the enabled[dst] gather)
   std::vector<uint32_t> ip;
   std::vector<HostSrc> src;
   bool peers_dirty = true, rules_dirty = true, any_patch = false, params_dirty = true;
@@ -250,6 +252,11 @@ struct tgsim_engine_s {
 
   double sim_ms = 0;
   uint64_t sim_launches = 0;
+  bool stamps_on = false;
+  DevBuf<uint32_t> d_order;
+  bool order_valid = false;
+  DevBuf<uint64_t> d_stamps;
+  uint64_t n_stamp_wg = 0;
 
   int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -446,13 +453,28 @@ int run_sim(Eng* E, uint32_t n_ticks) {
   a.shard_begin = E->o.shard_begin;
   a.n_peers = E->N;
   a.queue_limit = E->o.queue_limit;
+  a.any_disabled = E->n_disabled ? 1u : 0u;
   a.tick_ns = E->o.tick_ns;
   a.t0_ns = E->now_tick * E->o.tick_ns;
   a.horizon_ns = (E->now_tick + n_ticks) * E->o.tick_ns + E->o.lookahead_ns;
+  const uint32_t n_wg = (E->S + kSpw - 1) / kSpw;
+  a.order = (kSpw == 1 && E->order_valid) ? E->d_order.p : nullptr;
+  a.stamps = nullptr;
+  if (E->stamps_on) {
+    HIPCHK(E->d_stamps.ensure(static_cast<size_t>(n_wg) * kStampSlots));
+    a.stamps = E->d_stamps.p;
+    E->n_stamp_wg = n_wg;
+  }
   HIPCHK(hipEventRecord(E->ev0, E->st));
-  launch_sim(a, (E->S + kSpw - 1) / kSpw, E->st);
+  launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(E->ev1, E->st));
+  if (kSpw == 1) {  // heavy-first dispatch order for the next step
+    HIPCHK(E->d_order.ensure(E->S));
+    launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
+    HIPCHK(hipGetLastError());
+    E->order_valid = true;
+  }
   E->n_verdict = E->n_in;
   E->last_perm.swap(E->perm);
   E->perm.clear();
@@ -599,6 +621,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking), "stream"))) return bail(rc);
   if ((rc = E->hip(hipEventCreate(&E->ev0), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreate(&E->ev1), "event"))) return bail(rc);
+  E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
   E->ip.resize(E->N);
   for (uint32_t i = 0; i < E->N; ++i) E->ip[i] = E->o.subnet_base + 2 + i;
@@ -641,7 +664,7 @@ void tgsim_destroy(void* e) {
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rank.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dcur.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_sortkeys.release(); E->d_drain.release(); E->d_stats.release();
+  E->d_sortkeys.release(); E->d_drain.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
   if (E->ev0) (void)hipEventDestroy(E->ev0);
@@ -674,6 +697,7 @@ int tgsim_configure(void* e, uint32_t peer, const tgsim_config* cfg) {
   if (!cfg->enable) {  // NetworkDisconnect; shape and rules untouched
     if (E->enabled[peer]) {
       E->enabled[peer] = 0;
+      E->n_disabled++;
       E->peers_dirty = true;
     }
     return 0;
@@ -685,6 +709,7 @@ int tgsim_configure(void* e, uint32_t peer, const tgsim_config* cfg) {
   }
   if (!E->enabled[peer]) {
     E->enabled[peer] = 1;
+    E->n_disabled--;
     E->peers_dirty = true;
   }
   if (!owned) return 0;
@@ -926,6 +951,17 @@ double tgsim_sim_kernel_ms(void* e, uint64_t* n, int reset) {
     E->sim_launches = 0;
   }
   return avg;
+}
+
+int64_t tgsim_debug_stamps(void* e, uint64_t* out, size_t cap) {
+  Eng* E = as_eng(e);
+  if (!E) return -EINVAL;
+  const uint64_t n = E->stamps_on ? E->n_stamp_wg * kStampSlots : 0;
+  if (out && cap >= n && n) {
+    HIPCHK(hipSetDevice(E->dev));
+    HIPCHK(hipMemcpy(out, E->d_stamps.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  }
+  return static_cast<int64_t>(n);
 }
 
 void* tgsim_stream(void* e) {

@@ -87,7 +87,11 @@ struct SimArgs {
   unsigned long long* stats;
   uint32_t key0, key1;
   uint32_t n_src, shard_begin, n_peers, queue_limit;
+  uint32_t any_disabled;    // 0: every peer is connected, the per-packet enabled[dst] gather is skipped
   uint64_t t0_ns, tick_ns, horizon_ns;
+  const uint32_t* order;    // k_sim dispatch order (workgroup -> source), or null for identity
+  uint64_t* stamps;         // diagnostics: kStampSlots s_memrealtime stamps per workgroup, or null
 };
+constexpr uint32_t kStampSlots = 8;
 
 }  // namespace tgsim

@@ -62,7 +62,7 @@ struct alignas(16) Pre {
   uint4 r1;    // draw 1: delay word in .x
 };
 struct SimLds {
-  uint4 heap[kHeapCap * kSpw];     // slot k of source j at k * kSpw + j
+  uint4 heap[(kHeapCap + 4) * kSpw];  // slot k of source j at k * kSpw + j (+4: child reads past n)
   uint64_t ring[kHeapCap * kSpw];  // departure times, circular per source
   Pre stage[kWave];
   uint8_t vst[kWave];              // verdicts of the batch, stored back coalesced
@@ -90,12 +90,14 @@ struct Lane {
 __device__ __forceinline__ uint4 hget(const Lane& L, uint32_t k) { return L.hb[k * kSpw]; }
 __device__ __forceinline__ void hset(Lane& L, uint32_t k, const uint4& v) { L.hb[k * kSpw] = v; }
 
+// 4-ary min-heap on (e, seq, clone first) in LDS: the four children of a node are read together,
+// so a sift-down level costs one LDS round trip and the depth is log4(1024) = 5.
 __device__ __forceinline__ void heap_push(Lane& L, uint4 it) {
   const uint64_t e = w0_of(it) & kEMask;
   if (e < L.top_e) L.top_e = e;  // ties keep the root's e: only the time is cached
   uint32_t i = L.st.heap_n++;
   while (i > 0) {
-    const uint32_t par = (i - 1) >> 1;
+    const uint32_t par = (i - 1) >> 2;
     const uint4 pv = hget(L, par);
     if (!item_lt(it, pv)) break;
     hset(L, i, pv);
@@ -109,24 +111,21 @@ __device__ __forceinline__ void heap_pop(Lane& L) {
   const uint4 last = hget(L, n);
   uint32_t i = 0;
   for (;;) {
-    uint32_t c = 2 * i + 1;
+    const uint32_t c = 4 * i + 1;
     if (c >= n) break;
-    uint4 cv = hget(L, c);
-    if (c + 1 < n) {
-      const uint4 rv = hget(L, c + 1);
-      if (item_lt(rv, cv)) {
-        cv = rv;
-        ++c;
-      }
-    }
-    if (!item_lt(cv, last)) break;
-    hset(L, i, cv);
-    i = c;
+    const uint4 v0 = hget(L, c), v1 = hget(L, c + 1), v2 = hget(L, c + 2), v3 = hget(L, c + 3);
+    uint4 best = v0;
+    uint32_t bi = c;
+    if (c + 1 < n && item_lt(v1, best)) { best = v1; bi = c + 1; }
+    if (c + 2 < n && item_lt(v2, best)) { best = v2; bi = c + 2; }
+    if (c + 3 < n && item_lt(v3, best)) { best = v3; bi = c + 3; }
+    if (!item_lt(best, last)) break;
+    hset(L, i, best);
+    i = bi;
   }
   if (n) hset(L, i, last);
   L.top_e = n ? (w0_of(hget(L, 0)) & kEMask) : ~0ull;
 }
-
 
 // HTB class serving the netem queue in eligibility order: d = max(e, TAT),
 // TAT' = max(TAT, e - B) + len * mult >> shift.
@@ -218,7 +217,7 @@ __device__ __forceinline__ uint32_t filter(const SimArgs& a, const SrcParams& p,
     if (!src_on) return TGSIM_V_DISCONNECTED;
     return (p.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE;
   }
-  if (!src_on || !a.enabled[dst]) return TGSIM_V_DISCONNECTED;
+  if (!src_on || (a.any_disabled && !a.enabled[dst])) return TGSIM_V_DISCONNECTED;
   if (p.rule_n) {
     const uint32_t act = fib_lookup(a.rules + p.rule_off, p.rule_n, a.ip[dst]);
     if (act == TGSIM_DROP) return TGSIM_V_BLACKHOLE;
@@ -281,17 +280,50 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // candidates (compacted with a ballot) through the netem-limit / eligibility-heap / HTB
 // recurrence held in LDS.  Sources with correlated draws (get_crandom, rho != 0) replay the raw
 // draws sequentially instead.  The next batch's records are in flight during the sequential phase.
+// The simulate workgroup is a single wavefront: cross-lane LDS hand-offs only need this wave's
+// LDS operations to have landed (lgkmcnt(0)), not the vmcnt(0) drain of outstanding global stores
+// and prefetch loads that __syncthreads() implies.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  __asm__ volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void stamp(const SimArgs& a, uint32_t lane, uint32_t k, uint64_t v) {
+  if (a.stamps && lane == 0) a.stamps[(size_t)blockIdx.x * kStampSlots + k] = v;
+}
+
 __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   __shared__ SimLds lds;
   const uint32_t lane = threadIdx.x;
-  const uint32_t s0 = blockIdx.x * kSpw;
+  // heavy-first dispatch order (previous step's HTB work per source), identity when absent
+  const uint32_t s0 = (kSpw == 1 && a.order) ? a.order[blockIdx.x] : blockIdx.x * kSpw;
+  stamp(a, lane, 0, __builtin_amdgcn_s_memrealtime());
   // ---- load heaps and rings of the workgroup's sources into LDS
   for (uint32_t j = 0; j < kSpw; ++j) {
     const uint32_t s = s0 + j;
     if (s >= a.n_src) break;
     const uint32_t hn = a.state[s].heap_n, rn = a.state[s].ring_n;
-    for (uint32_t k = lane; k < hn; k += kWave) lds.heap[k * kSpw + j] = a.heap[(size_t)s * kHeapCap + k];
-    for (uint32_t k = lane; k < rn; k += kWave) lds.ring[k * kSpw + j] = a.ring[(size_t)s * kHeapCap + k];
+    const uint4* gh = a.heap + (size_t)s * kHeapCap;
+    const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+    for (uint32_t k0 = 0; k0 < hn; k0 += 4 * kWave) {  // four loads in flight per lane
+      const uint32_t k = k0 + lane;
+      const uint4 v0 = gh[min(k, hn - 1)], v1 = gh[min(k + kWave, hn - 1)];
+      const uint4 v2 = gh[min(k + 2 * kWave, hn - 1)], v3 = gh[min(k + 3 * kWave, hn - 1)];
+      if (k < hn) lds.heap[k * kSpw + j] = v0;
+      if (k + kWave < hn) lds.heap[(k + kWave) * kSpw + j] = v1;
+      if (k + 2 * kWave < hn) lds.heap[(k + 2 * kWave) * kSpw + j] = v2;
+      if (k + 3 * kWave < hn) lds.heap[(k + 3 * kWave) * kSpw + j] = v3;
+    }
+    for (uint32_t k0 = 0; k0 < rn; k0 += 4 * kWave) {
+      const uint32_t k = k0 + lane;
+      const uint64_t v0 = gr[min(k, rn - 1)], v1 = gr[min(k + kWave, rn - 1)];
+      const uint64_t v2 = gr[min(k + 2 * kWave, rn - 1)], v3 = gr[min(k + 3 * kWave, rn - 1)];
+      if (k < rn) lds.ring[k * kSpw + j] = v0;
+      if (k + kWave < rn) lds.ring[(k + kWave) * kSpw + j] = v1;
+      if (k + 2 * kWave < rn) lds.ring[(k + 2 * kWave) * kSpw + j] = v2;
+      if (k + 3 * kWave < rn) lds.ring[(k + 3 * kWave) * kSpw + j] = v3;
+    }
   }
   // ---- per-lane roles
   const uint32_t pj = lane % kSpw, pr = lane / kSpw;
@@ -334,15 +366,17 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   const uint32_t n_batches = wave_max(nb);
   uint64_t c_off = 0, c_clone = 0, c_v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t perr = 0;
-  __syncthreads();
+  wave_lds_sync();
   if (seq_lane) {
     L.top_e = L.st.heap_n ? (w0_of(lds.heap[lane]) & kEMask) : ~0ull;
     L.head_d = L.st.ring_n ? lds.ring[lane] : ~0ull;
   }
+  stamp(a, lane, 1, __builtin_amdgcn_s_memrealtime());
   // ---- batch loop
   uint64_t idx = pbeg + pr;
-  InRec rec = {};
+  InRec rec = {}, rec2 = {};  // records of batches b and b + 1 (two batches in flight)
   if (prefetcher && idx < pend) rec = a.in[idx];
+  if (prefetcher && idx + kAhead < pend) rec2 = a.in[idx + kAhead];
   for (uint32_t b = 0; b < n_batches; ++b) {
     const uint64_t my_idx = idx;  // the record this lane stages in this batch
     const bool staged = prefetcher && my_idx < pend;
@@ -431,9 +465,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         lds.vst[lane] = (uint8_t)fin;
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     idx += kAhead;
-    if (prefetcher && idx < pend) rec = a.in[idx];  // in flight during the sequential phase
+    rec = rec2;
+    if (prefetcher && idx + kAhead < pend) rec2 = a.in[idx + kAhead];  // in flight two batches ahead
     if (seq_lane) {
       if (any_corr) {
         const uint64_t first = sbeg + (uint64_t)b * kAhead;
@@ -443,20 +478,45 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
           const uint64_t T = a.t0_ns + (uint64_t)pre.rec.z * a.tick_ns;
           lds.vst[r * kSpw + lane] = (uint8_t)process_corr(L, a.queue_limit, T, pre);
         }
-      } else {
-        uint4 n_rec, n_r0, n_r2;
-        if (n_cand) {
-          n_rec = lds.stage[0].rec;
-          n_r0 = lds.stage[0].r0;
-          n_r2 = lds.stage[0].r2;
+      }
+    }
+    if (!any_corr) {
+      // Uniform replay of the compacted candidates.  While the netem queue is full its state
+      // cannot change before min(next departure, next eligibility), so every candidate offered
+      // up to that instant is a QUEUE_FULL drop: the whole run is resolved with one ballot
+      // (T is non-decreasing over the candidates); the remaining candidates go through the
+      // sequential lane one by one.
+      uint64_t Tc = ~0ull;
+      uint32_t cinfo = 0;
+      if (lane < n_cand) {
+        const uint4 r = lds.stage[lane].rec;
+        Tc = ((uint64_t)r.y << 32) | r.x;
+        cinfo = lds.stage[lane].r2.x;
+      }
+      uint32_t c = 0;
+      while (c < n_cand) {
+        uint64_t thr = 0;
+        uint32_t full = 0;
+        if (lane == 0) {
+          thr = L.top_e < L.head_d ? L.top_e : L.head_d;
+          full = L.st.heap_n + L.st.ring_n >= a.queue_limit;
         }
-        for (uint32_t c = 0; c < n_cand; ++c) {
-          const uint4 crec = n_rec, cr0 = n_r0, cr2 = n_r2;
-          if (c + 1 < n_cand) {  // next candidate's LDS reads in flight
-            n_rec = lds.stage[c + 1].rec;
-            n_r0 = lds.stage[c + 1].r0;
-            n_r2 = lds.stage[c + 1].r2;
+        full = __builtin_amdgcn_readfirstlane(full);
+        if (full) {
+          thr = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(thr >> 32)) << 32) |
+                __builtin_amdgcn_readfirstlane((uint32_t)thr);
+          const bool drop = lane >= c && lane < n_cand && Tc <= thr;
+          const uint64_t m = __ballot(drop);
+          if (drop) {
+            const uint32_t cst = (cinfo >> 20) & 3u;
+            const uint32_t cv = cst == 0 ? TGSIM_V_NONE : (cst == 1 ? TGSIM_V_LOSS : TGSIM_V_QUEUE_FULL);
+            lds.vst[cinfo >> 24] = (uint8_t)((cv << 4) | TGSIM_V_QUEUE_FULL);
           }
+          c += __popcll(m);
+          if (c >= n_cand) break;
+        }
+        if (lane == 0) {
+          const uint4 crec = lds.stage[c].rec, cr0 = lds.stage[c].r0, cr2 = lds.stage[c].r2;
           const uint64_t T = ((uint64_t)crec.y << 32) | crec.x;
           const uint64_t eo = ((uint64_t)crec.w << 32) | crec.z;
           const uint32_t info = cr2.x, len = info & 0xFFFFu, cstate = (info >> 20) & 3u;
@@ -468,9 +528,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
           const uint32_t ov = admit(L, a.queue_limit, T, eo, cr0.z, cr0.w, len, (info >> 16) & 3u);
           lds.vst[info >> 24] = (uint8_t)((cv << 4) | ov);
         }
+        ++c;
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     if (staged) {
       const uint32_t v = lds.vst[lane];
       a.verdict[my_idx] = (uint8_t)v;
@@ -483,11 +544,13 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     for (uint32_t k = 0; k < 8; ++k)
       c_v[k] += __popcll(__ballot(staged && (v & 15u) == k)) + __popcll(__ballot(staged && (v >> 4) == k));
   }
+  stamp(a, lane, 2, __builtin_amdgcn_s_memrealtime());
   if (seq_lane) {
     htb_until(L, a.horizon_ns);
     a.emit_n[s0 + lane] = L.n_emit;
   }
-  __syncthreads();
+  wave_lds_sync();
+  stamp(a, lane, 3, __builtin_amdgcn_s_memrealtime());
   // ---- write back state, heaps and (compacted) rings
   for (uint32_t j = 0; j < kSpw; ++j) {
     const uint32_t s = s0 + j;
@@ -503,6 +566,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     L.st.ring_head = 0;
     a.state[s0 + lane] = L.st;
   }
+  stamp(a, lane, 4, __builtin_amdgcn_s_memrealtime());
+  stamp(a, lane, 5, ((uint64_t)s0 << 32) | n_batches);
+  stamp(a, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
+  stamp(a, lane, 7, seq_lane ? ((uint64_t)L.st.heap_n << 32 | L.st.ring_n) : 0);
   const uint64_t sched = wave_sum(seq_lane ? L.scheduled : 0u);
   const uint64_t corrupted = wave_sum(seq_lane ? L.corrupted : 0u);
   const uint64_t bytes = wave_sum(seq_lane ? L.bytes : 0ull);
@@ -516,6 +583,30 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       if (c_v[k]) atomicAdd(&a.stats[kStVerdict0 + k], (unsigned long long)c_v[k]);
     if (bytes) atomicAdd(&a.stats[kStBytes], (unsigned long long)bytes);
     if (err) atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Longest-processing-time-first dispatch order for the next k_sim: sources bucketed by
+// log2(HTB records emitted this step), heaviest bucket first (one workgroup, LDS counting sort).
+// Only the dispatch order changes; every source's result is independent of it.
+__global__ __launch_bounds__(1024) void k_order(const uint32_t* emit_n, uint32_t n, uint32_t* order) {
+  __shared__ uint32_t cnt[33], base[33];
+  for (uint32_t i = threadIdx.x; i < 33; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) atomicAdd(&cnt[__clz(emit_n[s])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int b = 0; b < 33; ++b) {
+      base[b] = acc;
+      acc += cnt[b];
+    }
+  }
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) {
+    const uint32_t b = __clz(emit_n[s]);
+    order[atomicAdd(&base[b], 1u)] = s;
   }
 }
 
@@ -805,6 +896,10 @@ __global__ __launch_bounds__(256) void k_dst_sort(const tgsim_delivery* in, cons
 // Host-side launchers.
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
+}
+
+void launch_order(const uint32_t* emit_n, uint32_t n, uint32_t* order, hipStream_t st) {
+  hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, st, emit_n, n, order);
 }
 
 void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st) {
