@@ -114,25 +114,16 @@ def main():
     for i, s in enumerate(shapes):
         eng.configure(i, Config(Network="default", Enable=True, Default=s, RoutingPolicy=RoutingPolicyType.DenyAll))
     bounds = [r * a.peers for r in range(world)] + [peers_total]
-    out_buf = None
+    stepper = None
+    if world > 1:
+        from testground_amd.shard import ShardedStepper
+        stepper = ShardedStepper(eng, bounds, device=f"cuda:{local}")
 
     def one_step():
-        nonlocal out_buf
-        if world == 1:
+        if stepper is None:
             eng.step(a.window)
-            return
-        cap = eng.sim_capacity()
-        if out_buf is None or out_buf.numel() < cap * 24:
-            out_buf = torch.empty(int(cap * 1.25) * 24, dtype=torch.uint8, device="cuda")
-        cnt = eng.step_sim(a.window, bounds, out_buf.data_ptr(), out_buf.numel() // 24)
-        send = torch.tensor(cnt.astype(np.int64), device="cuda")
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send)
-        rc = recv.cpu().numpy()
-        inbuf = torch.empty(int(rc.sum()) * 24 + 24, dtype=torch.uint8, device="cuda")
-        dist.all_to_all_single(inbuf[: int(rc.sum()) * 24], out_buf[: int(cnt.sum()) * 24],
-                               [int(x) * 24 for x in rc], [int(x) * 24 for x in cnt])
-        eng.deliver(inbuf.data_ptr(), int(rc.sum()))
+        else:
+            stepper.step(a.window)
 
     settle = int(a.settle_ms * 1000 / a.window + 0.999)
     for _ in range(settle):  # untimed: bring every netem queue to its sustained state

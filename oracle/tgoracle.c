@@ -608,9 +608,10 @@ static int cmp_del(const void* a, const void* b) {
     return yd - xd; /* clone first */
 }
 
-int tgo_step(void* p, uint32_t n_ticks) {
-    oracle* o = (oracle*)p;
-    if (!o || n_ticks == 0) return -EINVAL;
+/* Runs the window's offered packets through filter -> netem -> HTB; leaves the scheduled records
+ * of the step (unsorted) in o->step_out. */
+static int step_core(oracle* o, uint32_t n_ticks) {
+    if (n_ticks == 0) return -EINVAL;
     for (size_t i = 0; i < o->n_off; ++i)
         if (o->off[i].p.tick >= n_ticks)
             return fail(o, -EINVAL, "packet %zu: tick %u beyond step of %u ticks", i, o->off[i].p.tick, n_ticks);
@@ -631,14 +632,71 @@ int tgo_step(void* p, uint32_t n_ticks) {
     }
     uint64_t T1 = (o->now_tick + n_ticks) * o->o.tick_ns;
     for (uint32_t s = 0; s < o->nsrc; ++s) htb_until(o, s, T1 + o->o.lookahead_ns);
-    qsort(o->step_out, o->n_step, sizeof(tgsim_delivery), cmp_del);
-    o->out = (tgsim_delivery*)grow(o->out, &o->cap_out, o->n_out + o->n_step, sizeof(tgsim_delivery));
-    memcpy(o->out + o->n_out, o->step_out, o->n_step * sizeof(tgsim_delivery));
-    o->n_out += o->n_step;
     o->n_off = 0;
     o->now_tick += n_ticks;
     o->st.now_tick = o->now_tick;
     return 0;
+}
+
+/* Sorts records into delivery order and appends them to the drain queue. */
+static void deliver_records(oracle* o, const tgsim_delivery* recs, size_t n) {
+    o->out = (tgsim_delivery*)grow(o->out, &o->cap_out, o->n_out + n, sizeof(tgsim_delivery));
+    memcpy(o->out + o->n_out, recs, n * sizeof(tgsim_delivery));
+    qsort(o->out + o->n_out, n, sizeof(tgsim_delivery), cmp_del);
+    o->n_out += n;
+}
+
+int tgo_step(void* p, uint32_t n_ticks) {
+    oracle* o = (oracle*)p;
+    if (!o) return -EINVAL;
+    int rc = step_core(o, n_ticks);
+    if (rc) return rc;
+    deliver_records(o, o->step_out, o->n_step);
+    return 0;
+}
+
+/* Multi-shard form: scheduled records grouped by the destination's shard into `out` (host
+ * memory here), counts per shard in `counts`. */
+int tgo_step_sim(void* p, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out,
+                 size_t cap, uint64_t* counts) {
+    oracle* o = (oracle*)p;
+    if (!o || !n_ranks || n_ranks > 8 || !bounds || !counts) return -EINVAL;
+    if (bounds[0] != 0 || bounds[n_ranks] != o->o.n_peers) return fail(o, -EINVAL, "rank bounds must cover [0, n_peers)");
+    int rc = step_core(o, n_ticks);
+    if (rc) return rc;
+    if (o->n_step > cap) return fail(o, -ENOSPC, "step_sim: %zu records exceed capacity %zu", o->n_step, cap);
+    tgsim_delivery* dst = (tgsim_delivery*)out;
+    size_t w = 0;
+    for (uint32_t r = 0; r < n_ranks; ++r) {
+        counts[r] = 0;
+        for (size_t i = 0; i < o->n_step; ++i)
+            if (o->step_out[i].dst >= bounds[r] && o->step_out[i].dst < bounds[r + 1]) {
+                dst[w++] = o->step_out[i];
+                counts[r]++;
+            }
+    }
+    return 0;
+}
+
+int tgo_deliver(void* p, const void* in, size_t n) {
+    oracle* o = (oracle*)p;
+    if (!o || (!in && n)) return -EINVAL;
+    const tgsim_delivery* r = (const tgsim_delivery*)in;
+    for (size_t i = 0; i < n; ++i)
+        if (r[i].dst < o->o.shard_begin || r[i].dst >= o->o.shard_end)
+            return fail(o, -EINVAL, "deliver: record %zu addresses dst %u outside this shard", i, r[i].dst);
+    deliver_records(o, r, n);
+    return 0;
+}
+
+int64_t tgo_sim_capacity(void* p) {
+    oracle* o = (oracle*)p;
+    return (int64_t)(2 * o->n_off + 1024ull * o->nsrc);
+}
+
+int64_t tgo_pending_deliveries(void* p) {
+    oracle* o = (oracle*)p;
+    return (int64_t)(o->n_out - o->out_head);
 }
 
 int64_t tgo_drain(void* p, tgsim_delivery* out, size_t cap) {

@@ -33,6 +33,11 @@ int tgo_configure(void* o, uint32_t peer, const tgsim_config* cfg);
 int tgo_submit(void* o, const tgsim_pkt* pkts, size_t n);
 int tgo_gen_storm(void* o, double lambda, uint32_t n_ticks);
 int tgo_step(void* o, uint32_t n_ticks);
+int tgo_step_sim(void* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out, size_t cap,
+                 uint64_t* counts);
+int tgo_deliver(void* o, const void* in, size_t n);
+int64_t tgo_sim_capacity(void* o);
+int64_t tgo_pending_deliveries(void* o);
 int64_t tgo_drain(void* o, tgsim_delivery* out, size_t cap);
 int64_t tgo_verdicts(void* o, uint8_t* out, size_t cap);
 int tgo_stats(void* o, tgsim_stats_t* out);
