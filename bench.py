@@ -25,10 +25,11 @@ METRIC = "simulated packets/sec (whole node) at 10k & 1M peers; % of HBM rooflin
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # Algorithmic HBM bytes of k_sim: per offered packet 16 B record read + 1 B verdict
-# write; per scheduled record 24 B delivery write + 16 B queue item write + 16 B read + 8 B departure
-# ring write + 8 B read; per source 64 B params + 32 B state read + 32 B state write + 8 B offsets
-# + 4 B emit count.
-B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 72, 140
+# write; per scheduled record 24 B delivery write; per source 64 B params + 32 B state read + 32 B
+# state write + 16 B CSR offsets + 4 B emit count; plus the netem queue state each source carries
+# across steps (16 B per queued item, 8 B per departing item, loaded at step start and stored at
+# step end: the engine's queue_state_bytes counter).
+B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 24, 148
 
 
 def parse():
@@ -163,7 +164,8 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
-    per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled) / max(1, a.steps) + B_SOURCE * a.peers
+    qbytes = s1["queue_state_bytes"] - s0["queue_state_bytes"]
+    per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled + qbytes) / max(1, a.steps) + B_SOURCE * a.peers
     achieved = per_launch / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else None
     pmc = load_pmc()
     traffic = None

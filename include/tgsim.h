@@ -148,6 +148,9 @@ typedef struct {
     uint64_t by_verdict[8];   /* originals+clones per enum tgsim_verdict         */
     uint64_t bytes_scheduled; /* sum of len over scheduled records               */
     uint64_t now_tick;        /* engine time after the last step                 */
+    uint64_t queue_state_bytes; /* netem queue state carried across steps: 16 B per
+                                   queued item + 8 B per departing item, summed at
+                                   every step start and end (the HBM round trip)   */
 } tgsim_stats_t;
 
 /* ---- lifecycle ---------------------------------------------------------------------------- */

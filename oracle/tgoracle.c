@@ -610,12 +610,19 @@ static int cmp_del(const void* a, const void* b) {
 
 /* Runs the window's offered packets through filter -> netem -> HTB; leaves the scheduled records
  * of the step (unsorted) in o->step_out. */
+static uint64_t queue_bytes(const oracle* o) {
+    uint64_t b = 0;
+    for (uint32_t s = 0; s < o->nsrc; ++s) b += 16ull * o->src[s].heap_n + 8ull * o->src[s].ring_n;
+    return b;
+}
+
 static int step_core(oracle* o, uint32_t n_ticks) {
     if (n_ticks == 0) return -EINVAL;
     for (size_t i = 0; i < o->n_off; ++i)
         if (o->off[i].p.tick >= n_ticks)
             return fail(o, -EINVAL, "packet %zu: tick %u beyond step of %u ticks", i, o->off[i].p.tick, n_ticks);
     qsort(o->off, o->n_off, sizeof(offered), cmp_off);
+    o->st.queue_state_bytes += queue_bytes(o);
     free(o->verdicts);
     o->verdicts = (uint8_t*)malloc(o->n_off ? o->n_off : 1);
     o->n_verdicts = o->n_off;
@@ -632,6 +639,7 @@ static int step_core(oracle* o, uint32_t n_ticks) {
     }
     uint64_t T1 = (o->now_tick + n_ticks) * o->o.tick_ns;
     for (uint32_t s = 0; s < o->nsrc; ++s) htb_until(o, s, T1 + o->o.lookahead_ns);
+    o->st.queue_state_bytes += queue_bytes(o);
     o->n_off = 0;
     o->now_tick += n_ticks;
     o->st.now_tick = o->now_tick;

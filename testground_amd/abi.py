@@ -80,6 +80,7 @@ class Stats(C.Structure):
         ("by_verdict", C.c_uint64 * 8),
         ("bytes_scheduled", C.c_uint64),
         ("now_tick", C.c_uint64),
+        ("queue_state_bytes", C.c_uint64),
     ]
 
 

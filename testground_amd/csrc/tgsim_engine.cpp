@@ -242,7 +242,7 @@ struct tgsim_engine_s {
   // step output
   DevBuf<tgsim_delivery> d_emit;
   DevBuf<uint32_t> d_emit_n;
-  DevBuf<unsigned long long> d_rank;  // [0..7] counts, [8..15] offsets
+  DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts and their scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dcur, d_dblk, d_dtot;
   DevBuf<uint8_t> d_sortkeys;
@@ -504,27 +504,29 @@ int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out,
   h.n_src = E->S;
   h.n_ranks = n_ranks;
   for (uint32_t i = 0; i <= n_ranks && i < 9; ++i) h.bounds[i] = bounds[i];
-  HIPCHK(E->d_rank.ensure(16));
-  HIPCHK(hipMemsetAsync(E->d_rank.p, 0, 16 * sizeof(unsigned long long), E->st));
-  h.rank_cnt = E->d_rank.p;
-  h.rank_off = E->d_rank.p + 8;
+  const uint64_t m = static_cast<uint64_t>(n_ranks) * E->S;
+  HIPCHK(E->d_rcnt.ensure(m));
+  HIPCHK(E->d_rpos.ensure(m + 1));
+  HIPCHK(E->d_rblk.ensure((m + 1023) / 1024 + 1));
+  HIPCHK(E->d_rtot.ensure(1));
+  h.cnt = E->d_rcnt.p;
+  h.pos = E->d_rpos.p;
   h.out = out;
   launch_route(h, 0, E->st);
   HIPCHK(hipGetLastError());
-  unsigned long long cnt[8] = {0};
-  HIPCHK(hipMemcpyAsync(cnt, E->d_rank.p, sizeof cnt, hipMemcpyDeviceToHost, E->st));
+  launch_scan(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(E->d_rpos.p + m, E->d_rtot.p, sizeof(uint64_t), hipMemcpyDeviceToDevice, E->st));
+  // per-rank totals: pos[r * S] .. pos[(r + 1) * S]
+  std::vector<uint64_t> edges(n_ranks + 1);
+  for (uint32_t r = 0; r <= n_ranks; ++r)
+    HIPCHK(hipMemcpyAsync(&edges[r], E->d_rpos.p + static_cast<uint64_t>(r) * E->S, sizeof(uint64_t),
+                          hipMemcpyDeviceToHost, E->st));
   HIPCHK(hipStreamSynchronize(E->st));
-  unsigned long long offs[8] = {0};
-  uint64_t total = 0;
-  for (uint32_t r = 0; r < n_ranks; ++r) {
-    offs[r] = total;
-    total += cnt[r];
-    counts[r] = cnt[r];
-  }
-  if (total > out_cap) return E->fail(-ENOSPC, "route: %llu records exceed capacity %zu",
-                                      static_cast<unsigned long long>(total), out_cap);
-  HIPCHK(hipMemcpyAsync(E->d_rank.p + 8, offs, sizeof offs, hipMemcpyHostToDevice, E->st));
-  HIPCHK(hipMemsetAsync(E->d_rank.p, 0, 8 * sizeof(unsigned long long), E->st));
+  for (uint32_t r = 0; r < n_ranks; ++r) counts[r] = edges[r + 1] - edges[r];
+  if (edges[n_ranks] > out_cap)
+    return E->fail(-ENOSPC, "route: %llu records exceed capacity %zu",
+                   static_cast<unsigned long long>(edges[n_ranks]), out_cap);
   launch_route(h, 1, E->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -661,7 +663,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rank.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dcur.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_sortkeys.release(); E->d_drain.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
@@ -925,6 +927,7 @@ int tgsim_stats(void* e, tgsim_stats_t* out) {
   for (int i = 0; i < 8; ++i) out->by_verdict[i] = s[kStVerdict0 + i];
   out->bytes_scheduled = s[kStBytes];
   out->now_tick = E->now_tick;
+  out->queue_state_bytes = s[kStQueue];
   return 0;
 }
 

@@ -67,7 +67,7 @@ struct CfgPatch {
 
 enum StatSlot {
   kStOffered = 0, kStScheduled, kStCloned, kStCorrupted, kStVerdict0,  // 4..11 verdicts
-  kStBytes = 12, kStErr = 13, kStSlots = 16
+  kStBytes = 12, kStErr = 13, kStQueue = 14, kStSlots = 16
 };
 constexpr uint32_t kErrTimeOverflow = 1u;
 

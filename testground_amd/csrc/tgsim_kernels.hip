@@ -364,6 +364,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     nb = (uint32_t)((send - sbeg + kAhead - 1) / kAhead);
   }
   const uint32_t n_batches = wave_max(nb);
+  const uint64_t qbytes_in = seq_lane ? 16ull * L.st.heap_n + 8ull * L.st.ring_n : 0;
   uint64_t c_off = 0, c_clone = 0, c_v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t perr = 0;
   wave_lds_sync();
@@ -573,6 +574,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   const uint64_t sched = wave_sum(seq_lane ? L.scheduled : 0u);
   const uint64_t corrupted = wave_sum(seq_lane ? L.corrupted : 0u);
   const uint64_t bytes = wave_sum(seq_lane ? L.bytes : 0ull);
+  const uint64_t qbytes = wave_sum(seq_lane ? qbytes_in + 16ull * L.st.heap_n + 8ull * L.st.ring_n : 0ull);
   const uint64_t err = wave_sum((seq_lane && L.err) || perr ? 1u : 0u);
   if (lane == 0) {
     atomicAdd(&a.stats[kStOffered], (unsigned long long)c_off);
@@ -582,6 +584,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     for (int k = 0; k < 8; ++k)
       if (c_v[k]) atomicAdd(&a.stats[kStVerdict0 + k], (unsigned long long)c_v[k]);
     if (bytes) atomicAdd(&a.stats[kStBytes], (unsigned long long)bytes);
+    if (qbytes) atomicAdd(&a.stats[kStQueue], (unsigned long long)qbytes);
     if (err) atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
   }
 }
@@ -754,7 +757,9 @@ __global__ __launch_bounds__(256) void k_scan_add(uint64_t* out, uint64_t n, con
 }
 
 // ---------------------------------------------------------------------------------------------
-// Route: group the emitted records by the destination shard (wave-aggregated atomics).
+// Route: group the emitted records by the destination shard, deterministically and without
+// contended atomics: per (rank, source) counts -> one exclusive scan over [rank][source] -> every
+// source writes its records of rank r at off[r * S + s] in emission order.
 struct RouteArgs {
   const tgsim_delivery* emit;
   const uint32_t* emit_n;
@@ -762,8 +767,8 @@ struct RouteArgs {
   uint32_t n_src;
   uint32_t n_ranks;
   uint32_t bounds[9];
-  unsigned long long* rank_cnt;  // [n_ranks] counts (phase 0) / cursors (phase 1)
-  const unsigned long long* rank_off;
+  uint64_t* cnt;                 // [n_ranks][n_src] records per (rank, source)
+  const uint64_t* pos;           // exclusive scan of cnt
   tgsim_delivery* out;
 };
 
@@ -773,34 +778,55 @@ __device__ __forceinline__ uint32_t rank_of(const RouteArgs& a, uint32_t dst) {
   return r;
 }
 
-template <int PHASE>
-__global__ __launch_bounds__(256) void k_route(RouteArgs a) {
+__global__ __launch_bounds__(256) void k_route_count(RouteArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * 4;
-  for (uint32_t s = wave; s < a.n_src; s += nw) {
+  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < a.n_src; s += nw) {
+    const uint32_t n = a.emit_n[s];
+    if (a.n_ranks == 1) {
+      if (lane == 0) a.cnt[s] = n;
+      continue;
+    }
+    const tgsim_delivery* base = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
+    uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const uint32_t rk = i < n ? rank_of(a, base[i].dst) : 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) c[q] += __popcll(__ballot(rk == q));
+    }
+    if (lane < a.n_ranks) {
+      uint32_t v = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) v = lane == q ? c[q] : v;
+      a.cnt[(size_t)lane * a.n_src + s] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < a.n_src; s += nw) {
     const uint32_t n = a.emit_n[s];
     const tgsim_delivery* base = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
-    for (uint32_t i = lane; i < ((n + 63u) & ~63u); i += 64) {
-      const bool valid = i < n;
+    uint64_t run[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) run[q] = q < a.n_ranks ? a.pos[(size_t)q * a.n_src + s] : 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+      const uint32_t i = i0 + lane;
       tgsim_delivery r;
       uint32_t rk = 0xFFFFFFFFu;
-      if (valid) {
+      if (i < n) {
         r = base[i];
         rk = rank_of(a, r.dst);
       }
-      for (uint32_t q = 0; q < a.n_ranks; ++q) {
+      const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) {
         const uint64_t m = __ballot(rk == q);
-        if (!m) continue;
-        const uint32_t leader = __ffsll((long long)m) - 1;
-        unsigned long long bpos = 0;
-        if (lane == leader) bpos = atomicAdd(&a.rank_cnt[q], (unsigned long long)__popcll(m));
-        if (PHASE == 1) {
-          const uint32_t lo = __shfl((uint32_t)bpos, leader, 64);
-          const uint32_t hi = __shfl((uint32_t)(bpos >> 32), leader, 64);
-          const uint64_t pos = ((uint64_t)hi << 32 | lo) + __popcll(m & ((1ull << lane) - 1));
-          if (rk == q) a.out[a.rank_off[q] + pos] = r;
-        }
+        if (rk == q) a.out[run[q] + __popcll(m & below)] = r;
+        run[q] += __popcll(m);
       }
     }
   }
@@ -938,14 +964,14 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
   a.n_src = h.n_src;
   a.n_ranks = h.n_ranks;
   for (int i = 0; i < 9; ++i) a.bounds[i] = h.bounds[i];
-  a.rank_cnt = h.rank_cnt;
-  a.rank_off = h.rank_off;
+  a.cnt = h.cnt;
+  a.pos = h.pos;
   a.out = h.out;
   uint32_t grid = (h.n_src + 3) / 4;
-  if (grid > 2048) grid = 2048;
+  if (grid > 4096) grid = 4096;
   if (grid == 0) grid = 1;
-  if (phase == 0) hipLaunchKernelGGL(k_route<0>, dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(k_route<1>, dim3(grid), dim3(256), 0, st, a);
+  if (phase == 0) hipLaunchKernelGGL(k_route_count, dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(k_route_scatter, dim3(grid), dim3(256), 0, st, a);
 }
 
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt, hipStream_t st) {

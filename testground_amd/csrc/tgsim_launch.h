@@ -17,8 +17,8 @@ struct RouteArgsHost {
   uint32_t n_src;
   uint32_t n_ranks;
   uint32_t bounds[9];
-  unsigned long long* rank_cnt;
-  const unsigned long long* rank_off;
+  uint64_t* cnt;        // [n_ranks][n_src]
+  const uint64_t* pos;  // exclusive scan of cnt
   tgsim_delivery* out;
 };
 

@@ -162,7 +162,8 @@ class CABIEngine:
     def stats(self) -> dict:
         s = abi.Stats()
         self._check(self._fn("stats")(self._h, C.byref(s)), "stats")
-        d = {k: getattr(s, k) for k in ("offered", "scheduled", "cloned", "corrupted", "bytes_scheduled", "now_tick")}
+        d = {k: getattr(s, k) for k in ("offered", "scheduled", "cloned", "corrupted", "bytes_scheduled", "now_tick",
+                                   "queue_state_bytes")}
         d["by_verdict"] = {abi.VERDICT_NAMES[i]: s.by_verdict[i] for i in range(8)}
         return d
 

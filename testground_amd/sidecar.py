@@ -1,0 +1,295 @@
+"""Mirror of the reference sidecar's instance handling (pkg/sidecar) over the engine.
+
+The reference's plugin surface is kept with the same names, argument meaning and errors:
+
+  Network{ConfigureNetwork, ListActive, Close}     pkg/sidecar/instance.go:37-42
+  Reactor{Handle, Close}, InstanceHandler          pkg/sidecar/instance.go:16-23
+  Instance{Hostname, Client, RunEnv, Network}      pkg/sidecar/instance.go:25-60
+  handler                                          pkg/sidecar/sidecar_handler.go:15-83
+  MockReactor / MockNetwork                        pkg/sidecar/mock.go:27-118
+
+plus the sdk-go pieces the handler and the plans talk to: an in-memory sync client (the role of
+sync.NewInmemClient, used by mock.go:41) and network.Client (WaitNetworkInitialized,
+ConfigureNetwork).  ``SimNetwork`` is the new implementation of ``Network``: one per simulated
+instance, all funnelled into one engine handle (the C engine is not re-entrant, so calls are
+serialised with a lock, as INTEGRATION.md's Go binding does).
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+import queue
+import threading
+import time
+from typing import Callable, Dict, List, Optional
+
+from .engine import EngineError
+from .network import Config
+
+DEFAULT_DATA_NETWORK = "default"   # sidecar_handler.go:11
+NET_INIT_STATE = "network-initialized"  # sidecar_handler.go:39
+
+
+class Context:
+    """Minimal context.Context: cancellation plus an optional deadline."""
+
+    def __init__(self, timeout: Optional[float] = None):
+        self._done = threading.Event()
+        self._deadline = time.monotonic() + timeout if timeout else None
+
+    def cancel(self) -> None:
+        self._done.set()
+
+    def done(self) -> bool:
+        if self._deadline is not None and time.monotonic() > self._deadline:
+            self._done.set()
+        return self._done.is_set()
+
+    def err(self) -> Optional[str]:
+        return "context canceled" if self.done() else None
+
+
+class SyncClient:
+    """In-memory sync service: signal (1-based sequence numbers), barrier, pub/sub topics."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._counts: Dict[str, int] = {}
+        self._topics: Dict[str, List] = {}
+        self._subs: Dict[str, List[queue.Queue]] = {}
+
+    def SignalEntry(self, ctx: Context, state: str) -> int:
+        with self._cv:
+            self._counts[state] = self._counts.get(state, 0) + 1
+            self._cv.notify_all()
+            return self._counts[state]
+
+    def Barrier(self, ctx: Context, state: str, target: int) -> None:
+        with self._cv:
+            while self._counts.get(state, 0) < target:
+                if ctx.done():
+                    raise TimeoutError(f"barrier {state!r}: {ctx.err()}")
+                self._cv.wait(timeout=0.05)
+
+    def SignalAndWait(self, ctx: Context, state: str, target: int) -> int:
+        seq = self.SignalEntry(ctx, state)
+        self.Barrier(ctx, state, target)
+        return seq
+
+    def Publish(self, ctx: Context, topic: str, payload) -> int:
+        with self._cv:
+            self._topics.setdefault(topic, []).append(payload)
+            for q in self._subs.get(topic, []):
+                q.put(payload)
+            return len(self._topics[topic])
+
+    def Subscribe(self, ctx: Context, topic: str) -> "queue.Queue":
+        q: queue.Queue = queue.Queue(maxsize=0)
+        with self._cv:
+            for p in self._topics.get(topic, []):  # subscribers see the whole topic history
+                q.put(p)
+            self._subs.setdefault(topic, []).append(q)
+        return q
+
+    def PublishAndWait(self, ctx: Context, topic: str, payload, state: str, target: int) -> int:
+        seq = self.Publish(ctx, topic, payload)
+        self.Barrier(ctx, state, target)
+        return seq
+
+    def Close(self) -> None:
+        pass
+
+
+@dataclasses.dataclass
+class RunEnv:
+    TestInstanceCount: int = 1
+    TestSidecar: bool = True
+    TestRun: str = "run"
+    TestSubnet: str = "16.0.0.0/8"
+
+
+class NetClient:
+    """sdk-go network.Client as used by the plans (pingpong.go:21-22, splitbrain/main.go:73-74)."""
+
+    def __init__(self, sync_client: SyncClient, runenv: RunEnv, hostname: str):
+        self.sync = sync_client
+        self.runenv = runenv
+        self.hostname = hostname
+
+    def WaitNetworkInitialized(self, ctx: Context) -> None:
+        self.sync.Barrier(ctx, NET_INIT_STATE, self.runenv.TestInstanceCount)
+
+    def ConfigureNetwork(self, ctx: Context, config: Config) -> None:
+        if not config.CallbackState:  # pinned by sidecar_test.go:59
+            raise ValueError("failed to configure network; no callback state provided")
+        target = config.CallbackTarget or self.runenv.TestInstanceCount
+        self.sync.PublishAndWait(ctx, "network:" + self.hostname, config, config.CallbackState, target)
+
+
+class Network:
+    """sidecar.Network (instance.go:37-42)."""
+
+    def ConfigureNetwork(self, ctx: Context, cfg: Config) -> None:
+        raise NotImplementedError
+
+    def ListActive(self) -> List[str]:
+        raise NotImplementedError
+
+    def Close(self) -> None:
+        raise NotImplementedError
+
+
+class MockNetwork(Network):
+    """mock.go:88-118: records every config; closed networks refuse configuration."""
+
+    def __init__(self):
+        self.Active: Dict[str, Config] = {"default": Config()}
+        self.Configured: List[Config] = []
+        self.Closed = False
+        self.L = threading.Lock()
+
+    def Close(self) -> None:
+        self.Closed = True
+
+    def ConfigureNetwork(self, ctx: Context, cfg: Config) -> None:
+        if self.Closed:
+            raise RuntimeError("mock network is closed.")
+        with self.L:
+            self.Configured.append(cfg)
+            self.Active[cfg.Network] = cfg
+
+    def ListActive(self) -> List[str]:
+        return list(self.Active)
+
+
+class SimNetwork(Network):
+    """sidecar.Network backed by the engine: the instance is simulated peer `peer`.  The engine
+    applies DockerNetwork.ConfigureNetwork's order of operations and errors (docker_network.go:51-148);
+    the config is copied into engine state and never mutated (sidecar_test.go:91-92)."""
+
+    def __init__(self, engine, peer: int, lock: threading.Lock):
+        self.engine = engine
+        self.peer = peer
+        self.lock = lock
+        self.active: Dict[str, bool] = {DEFAULT_DATA_NETWORK: True}
+        self.closed = False
+
+    def ConfigureNetwork(self, ctx: Context, cfg: Config) -> None:
+        if self.closed:
+            raise RuntimeError("network is closed")
+        with self.lock:
+            self.engine.configure(self.peer, cfg)
+        self.active[cfg.Network] = bool(cfg.Enable)
+
+    def ListActive(self) -> List[str]:
+        return [n for n, on in self.active.items() if on]
+
+    def Close(self) -> None:
+        self.closed = True
+
+
+@dataclasses.dataclass
+class Instance:
+    """instance.go:25-60."""
+    Hostname: str
+    Client: SyncClient
+    RunEnv: RunEnv
+    Network: Network
+
+    def Close(self) -> None:
+        self.Network.Close()
+
+
+InstanceHandler = Callable[[Context, Instance], None]
+
+
+class HandlerError(RuntimeError):
+    pass
+
+
+def handler(ctx: Context, instance: Instance) -> None:
+    """sidecar_handler.go:15-83: configure the default network, wait for every sidecar, then
+    apply each config published on network:<hostname> and signal its callback state."""
+    try:
+        instance.Network.ConfigureNetwork(ctx, Config(Network=DEFAULT_DATA_NETWORK, Enable=True))
+        instance.Client.SignalAndWait(ctx, NET_INIT_STATE, instance.RunEnv.TestInstanceCount)
+        changes = instance.Client.Subscribe(ctx, "network:" + instance.Hostname)
+        while not ctx.done():
+            try:
+                cfg = changes.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            try:
+                instance.Network.ConfigureNetwork(ctx, cfg)
+            except (EngineError, RuntimeError) as e:
+                raise HandlerError(f"failed to update network {cfg.Network}: {e}") from e
+            if cfg.CallbackState:
+                instance.Client.SignalEntry(ctx, cfg.CallbackState)
+    finally:
+        instance.Close()
+
+
+class Reactor:
+    """sidecar.Reactor (instance.go:18-23)."""
+
+    def Handle(self, ctx: Context, h: InstanceHandler) -> None:
+        raise NotImplementedError
+
+    def Close(self) -> None:
+        pass
+
+
+class MockReactor(Reactor):
+    """mock.go:27-73: a single instance with a MockNetwork and an in-memory sync client."""
+
+    def __init__(self, hostname: str = "mock-host"):
+        self.RunEnv = RunEnv(TestInstanceCount=1)
+        self.Network = MockNetwork()
+        self.Client = SyncClient()
+        self.Hostname = hostname
+
+    def Handle(self, ctx: Context, h: InstanceHandler) -> None:
+        h(ctx, Instance(self.Hostname, self.Client, self.RunEnv, self.Network))
+
+
+class SimReactor(Reactor):
+    """The `mi355x-sim` reactor: one Instance per simulated peer, all on one engine, each served
+    by `handler` on its own thread (the docker reactor runs one goroutine per container,
+    pkg/docker/manager.go:154-178)."""
+
+    def __init__(self, engine, n_instances: int, client: Optional[SyncClient] = None):
+        self.engine = engine
+        self.n = n_instances
+        self.Client = client or SyncClient()
+        self.RunEnv = RunEnv(TestInstanceCount=n_instances)
+        self.lock = threading.Lock()
+        self.threads: List[threading.Thread] = []
+        self.errors: List[BaseException] = []
+        self.networks = [SimNetwork(engine, p, self.lock) for p in range(n_instances)]
+
+    def hostname(self, peer: int) -> str:
+        return f"instance-{peer}"
+
+    def Handle(self, ctx: Context, h: InstanceHandler) -> None:
+        def run(p):
+            try:
+                h(ctx, Instance(self.hostname(p), self.Client, self.RunEnv, self.networks[p]))
+            except BaseException as e:  # noqa: BLE001 - reported to the caller
+                self.errors.append(e)
+
+        for p in range(self.n):
+            t = threading.Thread(target=run, args=(p,), daemon=True)
+            t.start()
+            self.threads.append(t)
+
+    def net_client(self, peer: int) -> NetClient:
+        return NetClient(self.Client, self.RunEnv, self.hostname(peer))
+
+    def Close(self) -> None:
+        for t in self.threads:
+            t.join(timeout=5)
+
+
+def snapshot(cfg: Config) -> Config:
+    """Deep copy used by tests to check configs pass through unmodified."""
+    return copy.deepcopy(cfg)
