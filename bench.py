@@ -1,14 +1,21 @@
 """Benchmark: simulated packets/sec of the network.Config enforcement path (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2]): storm-style random all-to-all traffic over
-10,000 instances per GPU, heterogeneous LinkShape (latency/jitter/loss/dup/corrupt/reorder/
+Default workload (BASELINE.json configs[2]): storm-style random all-to-all traffic
+over 10,000 instances per GPU, heterogeneous LinkShape (latency/jitter/loss/dup/corrupt/reorder/
 bandwidth), Poisson(0.5) packets per instance per 1 µs tick.  One step = one pass of the hot path
 over one window of `--window` ticks of offered traffic that is already resident in HBM (generated
 on the device before the timed region): filter -> netem -> HTB (k_sim), routing by destination
 shard, RCCL all-to-all (N > 1), per-destination delivery sort.
 
+`--workload gossip` (C4, BASELINE.json configs[3]): flood of 64 messages over --peers instances per
+GPU (125,000 per GPU = 1M at 8 GPUs), degree 8, 1 KiB, L~U[5,50] ms, loss 1 %.  A step is one 5 ms
+window: forwards of the previous window's receipts generated on the device, then the hot path.
+`--workload epochs` (C5, configs[4]): 100,000 instances per GPU, C3 shapes and traffic at
+lambda 0.2, 1,000-tick epochs; a step reshapes 10 % of the instances (batched ConfigureNetwork),
+runs the epoch and passes the `epoch-k` barrier (counters summed over ranks).
+
 N = 1 runs directly; N > 1 is launched by torch.distributed.run, one rank per GPU, each rank owning
-10,000 instances (weak scaling), cross-shard deliveries exchanged with all_to_all_single (RCCL).
+--peers instances (weak scaling), cross-shard deliveries exchanged with all_to_all_single (RCCL).
 """
 import argparse
 import ctypes
@@ -35,9 +42,13 @@ B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 24, 148
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--peers", type=int, default=10_000, help="instances per GPU")
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default: 10; gossip: 70 windows)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; gossip: 0)")
+    p.add_argument("--workload", default="storm", choices=["storm", "gossip", "epochs"])
+    p.add_argument("--peers", type=int, default=0,
+                   help="instances per GPU (default: storm 10,000; gossip 125,000; epochs 100,000)")
+    p.add_argument("--floods", type=int, default=64, help="gossip: flood messages")
+    p.add_argument("--flood-gap", type=int, default=1000, help="gossip: ticks between flood starts")
     p.add_argument("--lam", type=float, default=0.5)
     p.add_argument("--window", type=int, default=2000, help="ticks (1 us) per step")
     p.add_argument("--settle-ms", type=float, default=120.0,
@@ -48,43 +59,85 @@ def parse():
     p.add_argument("--queue-limit", type=int, default=0, help="netem limit (0 = netlink default 1000)")
     p.add_argument("--shapes", default="storm", choices=["storm", "fixed"],
                    help="storm: C3 heterogeneous shapes; fixed: L=5 ms, no jitter/loss/reorder (probe)")
-    return p.parse_args()
+    a = p.parse_args()
+    if not a.peers:
+        a.peers = {"storm": 10_000, "gossip": 125_000, "epochs": 100_000}[a.workload]
+    if a.workload == "epochs":
+        a.lam, a.window = 0.2, 1000
+    if a.workload == "gossip":
+        a.window = 5000
+    if a.steps is None:
+        a.steps = 70 if a.workload == "gossip" else 10
+    if a.warmup is None:
+        a.warmup = 0 if a.workload == "gossip" else 3
+    return a
 
 
-def cpu_baseline(peers_total, lam, window, seconds):
+def cpu_baseline(a, peers_total):
     """The CPU oracle (a 'port' of the reference semantics) timed on this host, single thread, on a
-    bounded sample: sources 0..999 of the same storm workload."""
+    bounded sample of the same workload."""
     from testground_amd import abi, workloads
     from testground_amd.build import build_oracle
     from testground_amd.engine import CABIEngine
 
     lib = ctypes.CDLL(str(build_oracle()))
     abi.declare(lib, "tgo_")
-    sample_src = min(1000, peers_total)
-    e = CABIEngine(lib, "tgo_", peers_total, shard=(0, sample_src))
-    workloads.configure_storm(e, peers_total)
-    busy, pkts, steps = 0.0, 0, 0
-    while busy < seconds:
-        e.gen_storm(lam, window)
-        t0 = time.perf_counter()
-        e.step(window)
-        busy += time.perf_counter() - t0
-        steps += 1
-        e.drain()
+    busy, steps = 0.0, 0
+    if a.workload == "gossip":  # closed loop: needs every peer, so the sample is a smaller flood
+        n = min(peers_total, 20_000)
+        e = CABIEngine(lib, "tgo_", n, lookahead_ns=workloads.GOSSIP_MIN_LAT)
+        workloads.configure_gossip(e, n)
+        e.gossip_init(n_floods=a.floods, degree=8, msg_len=1024, start_gap_ticks=a.flood_gap, start_tick=0)
+        while busy < a.cpu_seconds and steps < 400:
+            t0 = time.perf_counter()
+            e.gen_gossip(a.window)
+            e.step(a.window)
+            busy += time.perf_counter() - t0
+            steps += 1
+            e.drain()
         pkts = e.stats()["offered"]
-    return {"value": pkts / busy, "unit": "packets/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/tgoracle.c, sources 0..{sample_src - 1} of the {peers_total}-instance storm, "
-                      f"lambda={lam}, {steps} windows of {window} ticks, {pkts} packets, {busy:.1f} s"}
+        sample = (f"oracle/tgoracle.c, the same flood over {n} instances ({a.floods} floods, degree 8), "
+                  f"{steps} windows of {a.window} ticks incl. forward generation, {pkts} packets, {busy:.1f} s")
+    else:
+        sample_src = min(1000, peers_total)
+        e = CABIEngine(lib, "tgo_", peers_total, shard=(0, sample_src))
+        workloads.configure_storm(e, peers_total)
+        while busy < a.cpu_seconds:
+            if a.workload == "epochs" and steps:
+                r0 = time.perf_counter()
+                workloads.epoch_reshape(e, peers_total, steps)
+                busy += time.perf_counter() - r0
+            e.gen_storm(a.lam, a.window)
+            t0 = time.perf_counter()
+            e.step(a.window)
+            busy += time.perf_counter() - t0
+            steps += 1
+            e.drain()
+        pkts = e.stats()["offered"]
+        sample = (f"oracle/tgoracle.c, sources 0..{sample_src - 1} of the {peers_total}-instance {a.workload} "
+                  f"workload, lambda={a.lam}, {steps} windows of {a.window} ticks, {pkts} packets, {busy:.1f} s")
+    return {"value": pkts / busy, "unit": "packets/s", "cores": 1, "kind": "port", "sample": sample}
 
 
-def load_pmc(kernel="k_sim"):
-    f = ROOT / "profiles" / "pmc_k_sim.json"
+def load_pmc(a):
+    f = ROOT / "profiles" / ("pmc_k_sim.json" if a.workload == "storm" else f"pmc_k_sim_{a.workload}.json")
     if not f.exists():
         return None
     try:
-        return json.loads(f.read_text())
+        pmc = json.loads(f.read_text())
     except Exception:
         return None
+    if pmc.get("window") == a.window and pmc.get("peers") == a.peers and pmc.get("lam", a.lam) == a.lam:
+        return pmc.get("hbm_bytes_per_launch")
+    return None
+
+
+WORKLOAD_NAMES = {
+    "storm": "C3 storm: random all-to-all, heterogeneous LinkShape (BASELINE.json configs[2])",
+    "gossip": "C4 gossip flood: degree 8, 1 KiB, L~U[5,50] ms, loss 1 % (BASELINE.json configs[3])",
+    "epochs": "C5 epochs: C3 traffic at lambda 0.2, 10 % reshaped per 1,000-tick epoch, barrier per epoch "
+              "(BASELINE.json configs[4])",
+}
 
 
 def main():
@@ -97,6 +150,7 @@ def main():
 
     from testground_amd import abi, workloads
     from testground_amd.engine import Engine
+    from testground_amd.network import configs_array
 
     torch.cuda.set_device(local)
     dist = None
@@ -105,34 +159,52 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     peers_total = a.peers * world
     lo, hi = rank * a.peers, (rank + 1) * a.peers
+    kw = dict(lookahead_ns=workloads.GOSSIP_MIN_LAT) if a.workload == "gossip" else {}
     eng = Engine(peers_total, shard=(lo, hi), device=local, flags=abi.OPT_DISCARD_DELIVERIES,
-                 queue_limit=a.queue_limit)
-    from testground_amd.network import Config, LinkShape, Millisecond, RoutingPolicyType
-    if a.shapes == "storm":
-        shapes = workloads.storm_shapes(peers_total)
+                 queue_limit=a.queue_limit, **kw)
+    if a.workload == "gossip":
+        workloads.configure_gossip(eng, peers_total)
+    elif a.shapes == "storm":
+        workloads.configure_storm(eng, peers_total)
     else:
-        shapes = [LinkShape(Latency=5 * Millisecond)] * peers_total
-    for i, s in enumerate(shapes):
-        eng.configure(i, Config(Network="default", Enable=True, Default=s, RoutingPolicy=RoutingPolicyType.DenyAll))
+        eng.configure_batch(np.arange(peers_total), configs_array(np.full(peers_total, 5_000_000), routing_policy=2))
     bounds = [r * a.peers for r in range(world)] + [peers_total]
     stepper = None
     if world > 1:
         from testground_amd.shard import ShardedStepper
         stepper = ShardedStepper(eng, bounds, device=f"cuda:{local}")
+    step = eng.step if stepper is None else stepper.step
+    barrier = None if stepper is None else stepper.barrier
+    epoch = [0]
 
     def one_step():
-        if stepper is None:
-            eng.step(a.window)
+        if a.workload == "gossip":
+            eng.gen_gossip(a.window)
+            step(a.window)
+        elif a.workload == "epochs":  # traffic pre-generated; reshape + epoch + barrier
+            k = epoch[0]
+            if k:
+                workloads.epoch_reshape(eng, peers_total, k)
+            step(a.window)
+            state, rnd = workloads.epoch_state(k)
+            eng.signal(state, a.peers)
+            ok = barrier(state, rnd * peers_total) if barrier else eng.barrier_poll(state, rnd * peers_total)
+            if not ok:
+                raise RuntimeError(f"barrier epoch-{k} did not release")
+            epoch[0] += 1
         else:
-            stepper.step(a.window)
+            step(a.window)
 
-    settle = int(a.settle_ms * 1000 / a.window + 0.999)
-    for _ in range(settle):  # untimed: bring every netem queue to its sustained state
-        eng.gen_storm(a.lam, a.window)
-        one_step()
-    eng.drain()
-    for _ in range(a.warmup + a.steps):
-        eng.gen_storm(a.lam, a.window)  # inputs resident in HBM before the timed region
+    if a.workload == "gossip":
+        eng.gossip_init(n_floods=a.floods, degree=8, msg_len=1024, start_gap_ticks=a.flood_gap, start_tick=0)
+        settle = 0  # a flood is a transient by nature: the timed windows cover it from the start
+    else:
+        settle = int(a.settle_ms * 1000 / a.window + 0.999)
+        for _ in range(settle):  # untimed: bring every netem queue to its sustained state
+            eng.gen_storm(a.lam, a.window)
+            one_step()
+        for _ in range(a.warmup + a.steps):
+            eng.gen_storm(a.lam, a.window)  # inputs resident in HBM before the timed region
     for _ in range(a.warmup):
         one_step()
     eng.drain()
@@ -161,16 +233,22 @@ def main():
         offered_all = float(t[1])
     else:
         offered_all = float(offered)
+    extra = {}
+    if a.workload == "gossip":
+        reached = eng.gossip_reached()
+        if dist:
+            r = torch.as_tensor(reached.astype(np.int64), device="cuda")
+            dist.all_reduce(r)
+            reached = r.cpu().numpy()
+        extra = {"floods": a.floods, "flood_gap_ticks": a.flood_gap,
+                 "reached_min_frac": float(reached.min()) / peers_total,
+                 "sim_ms_covered": (a.warmup + a.steps) * a.window / 1000}
     if rank != 0:
         dist.destroy_process_group()
         return
     qbytes = s1["queue_state_bytes"] - s0["queue_state_bytes"]
     per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled + qbytes) / max(1, a.steps) + B_SOURCE * a.peers
     achieved = per_launch / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else None
-    pmc = load_pmc()
-    traffic = None
-    if pmc and pmc.get("window") == a.window and pmc.get("peers") == a.peers and pmc.get("lam") == a.lam:
-        traffic = pmc.get("hbm_bytes_per_launch")
     res = {
         "metric": METRIC,
         "value": offered_all / el,
@@ -183,19 +261,21 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
-        "data": "synthetic (device-generated storm traffic, Philox-keyed)",
-        "config": {"workload": "C3 storm: random all-to-all, heterogeneous LinkShape (BASELINE.json configs[2])",
-                   "peers_per_gpu": a.peers, "peers_total": peers_total, "lambda_per_tick": a.lam,
-                   "tick_ns": 1000, "window_ticks": a.window, "settle_sim_ms": settle * a.window / 1000, "shapes": a.shapes, "queue_limit": a.queue_limit or 1000,
-                   "packets_per_step": offered_all / a.steps, "parallelism": f"peer-sharded x{world}"},
+        "data": f"synthetic (device-generated {a.workload} traffic, Philox-keyed)",
+        "config": dict({"workload": WORKLOAD_NAMES[a.workload],
+                        "peers_per_gpu": a.peers, "peers_total": peers_total, "lambda_per_tick": a.lam,
+                        "tick_ns": 1000, "window_ticks": a.window, "settle_sim_ms": settle * a.window / 1000,
+                        "shapes": a.shapes if a.workload == "storm" else a.workload,
+                        "queue_limit": a.queue_limit or 1000, "packets_per_step": offered_all / a.steps,
+                        "parallelism": f"peer-sharded x{world}"}, **extra),
         "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": per_launch,
+                     "traffic": load_pmc(a), "algorithmic_bytes_per_launch": per_launch,
                      "kernel_ms_avg": sim_ms, "launches": n_launch},
         "cpu_baseline": None,
     }
     if world == 1 and not a.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(peers_total, a.lam, a.window, a.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(a, peers_total)
         res["cpu_baseline"]["gpu_over_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     print(json.dumps(res))
     if dist:

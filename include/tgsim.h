@@ -153,6 +153,19 @@ typedef struct {
                                    every step start and end (the HBM round trip)   */
 } tgsim_stats_t;
 
+/* Closed-loop gossip flood workload, generated and consumed on the device.
+ * Flood f (0 <= f < n_floods) starts at tick start_tick + f * start_gap_ticks at its origin peer;
+ * every peer forwards a flood once, on its first receipt, to its `degree` out-neighbours
+ * (a fixed hash of (seed, peer, k)), one msg_len-byte packet each, seq = f * degree + k, offered
+ * at the tick after the receipt's delivery time.  Corrupted deliveries are not receipts. */
+typedef struct {
+    uint32_t n_floods;         /* 1..64                                                      */
+    uint32_t degree;           /* out-neighbours per peer, 1..64                             */
+    uint32_t msg_len;          /* bytes per message, 1..65535                                */
+    uint32_t start_gap_ticks;  /* ticks between flood starts                                 */
+    uint64_t start_tick;       /* absolute tick of flood 0 (>= the engine's next window)     */
+} tgsim_gossip;
+
 /* ---- lifecycle ---------------------------------------------------------------------------- */
 int tgsim_create(const tgsim_opts* opts, void** out_engine);
 void tgsim_destroy(void* engine);
@@ -164,6 +177,11 @@ uint32_t tgsim_abi_version(void);
  * the next step).  Follows DockerNetwork.ConfigureNetwork's order of operations.  Every shard of a
  * multi-GPU run must receive every call (peer tables are replicated). */
 int tgsim_configure(void* engine, uint32_t peer, const tgsim_config* cfg);
+/* n tgsim_configure calls in order (cfgs[i] to peers[i]): the Go host funnels the per-instance
+ * ConfigureNetwork calls into one engine goroutine, which drains its queue in one batch.
+ * rcs[i] (optional) receives each call's return code; returns the number of failed calls. */
+int64_t tgsim_configure_batch(void* engine, const uint32_t* peers, const tgsim_config* cfgs, size_t n,
+                              int32_t* rcs);
 
 /* ---- data path ---------------------------------------------------------------------------- */
 int tgsim_submit(void* engine, const tgsim_pkt* pkts, size_t n);
@@ -192,6 +210,19 @@ int64_t tgsim_pending_deliveries(void* engine);
 /* Per-packet verdict bytes of the last step, in submit order (host packets) or generation order. */
 int64_t tgsim_verdicts(void* engine, uint8_t* out, size_t cap);
 int tgsim_stats(void* engine, tgsim_stats_t* out);
+
+/* ---- gossip workload (C4) ------------------------------------------------------------------ */
+/* Arms the gossip driver: resets the per-peer receipt state of this shard and schedules the
+ * floods whose origin it owns.  Requires lookahead_ns >= the window of every later step and
+ * <= the minimum netem delay, so that a window's receipts are known before the next window. */
+int tgsim_gossip_init(void* engine, const tgsim_gossip* g);
+/* Generates the next n_ticks window of gossip traffic on the device (origins + forwards of the
+ * receipts delivered so far), like tgsim_gen_storm.  -EINVAL when a receipt precedes the window
+ * (lookahead shorter than the window). */
+int tgsim_gen_gossip(void* engine, uint32_t n_ticks);
+/* Per flood, the number of this shard's peers that have the flood (received or originated);
+ * out[0..n_floods).  Returns n_floods. */
+int64_t tgsim_gossip_reached(void* engine, uint64_t* out, size_t cap);
 
 /* ---- sync counters (sync-service SignalEntry / Barrier) ------------------------------------ */
 /* Increments state `state` (0..1023) by n and returns the new value (1-based sequence). */

@@ -209,6 +209,11 @@ typedef struct {
     tgsim_stats_t st;
     uint64_t counters[1024];
     uint32_t* gen_seq;
+    /* gossip workload (C4): receipt tick per (local peer, flood), forwarded-flood bitmask */
+    int gossip_on;
+    tgsim_gossip g;
+    uint32_t* g_first;
+    uint64_t* g_fwd;
 } oracle;
 
 #define HCAP 1024u
@@ -291,7 +296,7 @@ void tgo_destroy(void* p) {
         free(o->src[s].rules);
     }
     free(o->src); free(o->enabled); free(o->ip); free(o->off); free(o->verdicts);
-    free(o->out); free(o->step_out); free(o->gen_seq);
+    free(o->out); free(o->step_out); free(o->gen_seq); free(o->g_first); free(o->g_fwd);
     free(o);
 }
 
@@ -391,6 +396,17 @@ int tgo_submit(void* p, const tgsim_pkt* pkts, size_t n) {
         o->n_off++;
     }
     return 0;
+}
+
+int64_t tgo_configure_batch(void* p, const uint32_t* peers, const tgsim_config* cfgs, size_t n, int32_t* rcs) {
+    if (!p || (n && (!peers || !cfgs))) return -EINVAL;
+    int64_t failed = 0;
+    for (size_t i = 0; i < n; ++i) {
+        int rc = tgo_configure(p, peers[i], &cfgs[i]);
+        if (rcs) rcs[i] = rc;
+        failed += rc != 0;
+    }
+    return failed;
 }
 
 /* Storm generator restatement: per (src, tick) Poisson count, uniform dst != src,
@@ -647,7 +663,10 @@ static int step_core(oracle* o, uint32_t n_ticks) {
 }
 
 /* Sorts records into delivery order and appends them to the drain queue. */
+static void gossip_receive(oracle* o, const tgsim_delivery* recs, size_t n);
+
 static void deliver_records(oracle* o, const tgsim_delivery* recs, size_t n) {
+    if (o->gossip_on) gossip_receive(o, recs, n);
     o->out = (tgsim_delivery*)grow(o->out, &o->cap_out, o->n_out + n, sizeof(tgsim_delivery));
     memcpy(o->out + o->n_out, recs, n * sizeof(tgsim_delivery));
     qsort(o->out + o->n_out, n, sizeof(tgsim_delivery), cmp_del);
@@ -740,4 +759,101 @@ int tgo_barrier_poll(void* p, uint32_t state, uint64_t target) {
     oracle* o = (oracle*)p;
     if (state >= 1024) return -EINVAL;
     return o->counters[state] >= target;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Gossip flood workload (include/tgsim.h tgsim_gossip).  A peer forwards flood
+ * f once, at the tick after its earliest receipt, to its `degree` hashed out-neighbours. */
+static uint32_t gossip_hash(const oracle* o, uint32_t a, uint32_t b, uint32_t tag) {
+    uint32_t gk[2] = {o->key[0] ^ 0x3C6EF372u, o->key[1] ^ 0xA54FF53Au};
+    uint32_t ctr[4] = {a, b, tag, 0}, r[4];
+    tgo_philox4x32_10(ctr, gk, r);
+    return r[0];
+}
+
+static uint32_t gossip_neighbour(const oracle* o, uint32_t peer, uint32_t k) {
+    uint32_t N = o->o.n_peers;
+    uint32_t d = gossip_hash(o, peer, k, 0x474F5350u) % (N - 1);
+    return d >= peer ? d + 1 : d;
+}
+
+int tgo_gossip_init(void* p, const tgsim_gossip* g) {
+    oracle* o = (oracle*)p;
+    if (!o || !g || g->n_floods == 0 || g->n_floods > 64 || g->degree == 0 || g->degree > 64 ||
+        g->msg_len == 0 || g->msg_len > 65535 || o->o.n_peers < 2)
+        return -EINVAL;
+    if (g->start_tick < o->now_tick) return fail(o, -EINVAL, "gossip: start tick in the past");
+    o->g = *g;
+    free(o->g_first);
+    free(o->g_fwd);
+    o->g_first = (uint32_t*)malloc(sizeof(uint32_t) * 64 * o->nsrc);
+    o->g_fwd = (uint64_t*)calloc(o->nsrc, sizeof(uint64_t));
+    for (size_t i = 0; i < 64ull * o->nsrc; ++i) o->g_first[i] = 0xFFFFFFFFu;
+    for (uint32_t f = 0; f < g->n_floods; ++f) {
+        uint32_t origin = gossip_hash(o, f, 0, 0x4F524947u) % o->o.n_peers;
+        if (origin < o->o.shard_begin || origin >= o->o.shard_end) continue;
+        o->g_first[64ull * (origin - o->o.shard_begin) + f] = (uint32_t)(g->start_tick + (uint64_t)f * g->start_gap_ticks);
+    }
+    o->gossip_on = 1;
+    return 0;
+}
+
+static void gossip_receive(oracle* o, const tgsim_delivery* recs, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        const tgsim_delivery* r = &recs[i];
+        uint32_t f = r->seq / o->g.degree;
+        if (f >= o->g.n_floods || (r->flags & TGSIM_FLAG_CORRUPT)) continue;
+        uint32_t s = r->dst - o->o.shard_begin;
+        if (o->g_fwd[s] >> f & 1) continue;
+        uint64_t t = r->t_ns / o->o.tick_ns + 1;
+        if (t > 0xFFFFFFFEull) t = 0xFFFFFFFEull;
+        if (t < o->g_first[64ull * s + f]) o->g_first[64ull * s + f] = (uint32_t)t;
+    }
+}
+
+int tgo_gen_gossip(void* p, uint32_t n_ticks) {
+    oracle* o = (oracle*)p;
+    if (!o || !o->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
+    uint64_t A = o->now_tick, B = o->now_tick + n_ticks;
+    for (uint32_t s = 0; s < o->nsrc; ++s) {
+        uint32_t src = o->o.shard_begin + s;
+        for (;;) { /* floods due in the window, earliest receipt first, then by flood id */
+            int best = -1;
+            for (uint32_t f = 0; f < o->g.n_floods; ++f) {
+                if (o->g_fwd[s] >> f & 1) continue;
+                uint32_t t = o->g_first[64ull * s + f];
+                if (t >= B) continue;
+                if (t < A) return fail(o, -EINVAL, "gossip: receipt at tick %u precedes the window at %llu", t,
+                                       (unsigned long long)A);
+                if (best < 0 || t < o->g_first[64ull * s + (uint32_t)best]) best = (int)f;
+            }
+            if (best < 0) break;
+            o->g_fwd[s] |= 1ull << best;
+            uint32_t t = o->g_first[64ull * s + (uint32_t)best];
+            for (uint32_t k = 0; k < o->g.degree; ++k) {
+                tgsim_pkt pk;
+                pk.src = src;
+                pk.dst = gossip_neighbour(o, src, k);
+                pk.seq = (uint32_t)best * o->g.degree + k;
+                pk.len = (uint16_t)o->g.msg_len;
+                pk.tick = (uint16_t)(t - A);
+                o->off = (offered*)grow(o->off, &o->cap_off, o->n_off + 1, sizeof(offered));
+                o->off[o->n_off].p = pk;
+                o->off[o->n_off].idx = o->n_off;
+                o->n_off++;
+            }
+        }
+    }
+    return 0;
+}
+
+int64_t tgo_gossip_reached(void* p, uint64_t* out, size_t cap) {
+    oracle* o = (oracle*)p;
+    if (!o || !o->gossip_on) return -EINVAL;
+    for (uint32_t f = 0; f < o->g.n_floods && f < cap; ++f) {
+        uint64_t c = 0;
+        for (uint32_t s = 0; s < o->nsrc; ++s) c += o->g_fwd[s] >> f & 1;
+        out[f] = c;
+    }
+    return o->g.n_floods;
 }

@@ -30,6 +30,7 @@ int tgo_create(const tgsim_opts* opts, void** out);
 void tgo_destroy(void* o);
 const char* tgo_last_error(const void* o);
 int tgo_configure(void* o, uint32_t peer, const tgsim_config* cfg);
+int64_t tgo_configure_batch(void* o, const uint32_t* peers, const tgsim_config* cfgs, size_t n, int32_t* rcs);
 int tgo_submit(void* o, const tgsim_pkt* pkts, size_t n);
 int tgo_gen_storm(void* o, double lambda, uint32_t n_ticks);
 int tgo_step(void* o, uint32_t n_ticks);
@@ -43,6 +44,9 @@ int64_t tgo_verdicts(void* o, uint8_t* out, size_t cap);
 int tgo_stats(void* o, tgsim_stats_t* out);
 int64_t tgo_signal(void* o, uint32_t state, uint32_t n);
 int tgo_barrier_poll(void* o, uint32_t state, uint64_t target);
+int tgo_gossip_init(void* o, const tgsim_gossip* g);
+int tgo_gen_gossip(void* o, uint32_t n_ticks);
+int64_t tgo_gossip_reached(void* o, uint64_t* out, size_t cap);
 
 /* Building blocks exposed for known-answer tests. */
 void tgo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -84,18 +84,38 @@ class Stats(C.Structure):
     ]
 
 
+class Gossip(C.Structure):
+    _fields_ = [
+        ("n_floods", C.c_uint32),
+        ("degree", C.c_uint32),
+        ("msg_len", C.c_uint32),
+        ("start_gap_ticks", C.c_uint32),
+        ("start_tick", C.c_uint64),
+    ]
+
+
 PKT_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("len", "<u2"), ("tick", "<u2")])
 DELIVERY_DTYPE = np.dtype([("t_ns", "<u8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"),
                            ("len", "<u2"), ("flags", "<u2")])
+# tgsim_config as a numpy record (batch configuration without per-peer ctypes objects).
+SHAPE_DTYPE = np.dtype([("latency_ns", "<i8"), ("jitter_ns", "<i8"), ("bandwidth_bps", "<u8"), ("loss", "<f4"),
+                        ("corrupt", "<f4"), ("corrupt_corr", "<f4"), ("reorder", "<f4"), ("reorder_corr", "<f4"),
+                        ("duplicate", "<f4"), ("duplicate_corr", "<f4"), ("_pad", "<u4")])
+CONFIG_DTYPE = np.dtype([("network", "<u8"), ("enable", "u1"), ("routing_policy", "u1"), ("has_ipv4", "u1"),
+                         ("_pad", "u1"), ("ipv4", "<u4"), ("shape", SHAPE_DTYPE), ("rules", "<u8"),
+                         ("n_rules", "<u4"), ("_pad2", "<u4")])
+assert SHAPE_DTYPE.itemsize == 56 and CONFIG_DTYPE.itemsize == 88
 assert PKT_DTYPE.itemsize == 16 and DELIVERY_DTYPE.itemsize == 24
-assert C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56 and C.sizeof(Config) == 88
+assert C.sizeof(Gossip) == 24 and C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56 and C.sizeof(Config) == 88
 
 # Every symbol include/tgsim.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "tgsim_create", "tgsim_destroy", "tgsim_last_error", "tgsim_abi_version", "tgsim_configure",
+    "tgsim_configure_batch",
     "tgsim_submit", "tgsim_gen_storm", "tgsim_step", "tgsim_step_sim", "tgsim_deliver",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_barrier_poll", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
+    "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached",
 ]
 
 
@@ -114,6 +134,7 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("destroy", None, vp)
     f("last_error", C.c_char_p, vp)
     f("configure", C.c_int, vp, C.c_uint32, C.POINTER(Config))
+    f("configure_batch", C.c_int64, vp, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
     f("submit", C.c_int, vp, C.c_void_p, C.c_size_t)
     f("gen_storm", C.c_int, vp, C.c_double, C.c_uint32)
     f("step", C.c_int, vp, C.c_uint32)
@@ -131,4 +152,7 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("stream", vp, vp)
     f("debug_stamps", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("abi_version", C.c_uint32)
+    f("gossip_init", C.c_int, vp, C.POINTER(Gossip))
+    f("gen_gossip", C.c_int, vp, C.c_uint32)
+    f("gossip_reached", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("offered", C.c_int64, vp, C.c_void_p, C.c_size_t)

@@ -258,6 +258,12 @@ struct tgsim_engine_s {
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
 
+  // gossip workload (C4)
+  bool gossip_on = false;
+  tgsim_gossip gossip{};
+  DevBuf<uint32_t> d_gfirst, d_gerr;
+  DevBuf<uint64_t> d_gfwd;
+
   int fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -532,6 +538,25 @@ int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out,
   return 0;
 }
 
+GossipArgs gossip_args(Eng* E, uint64_t win0, uint32_t n_ticks) {
+  GossipArgs g;
+  g.first = E->d_gfirst.p;
+  g.fwd = E->d_gfwd.p;
+  g.err = E->d_gerr.p;
+  g.k0 = E->key0 ^ 0x3C6EF372u;
+  g.k1 = E->key1 ^ 0xA54FF53Au;
+  g.n_src = E->S;
+  g.shard_begin = E->o.shard_begin;
+  g.n_peers = E->N;
+  g.n_floods = E->gossip.n_floods;
+  g.degree = E->gossip.degree;
+  g.msg_len = E->gossip.msg_len;
+  g.n_ticks = n_ticks;
+  g.tick_ns = E->o.tick_ns;
+  g.win0 = win0;
+  return g;
+}
+
 int deliver(Eng* E, const tgsim_delivery* in, uint64_t n) {
   const uint32_t nd = E->S;  // destinations owned by this shard
   HIPCHK(E->d_dcnt.ensure(nd));
@@ -572,10 +597,15 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n) {
   }
   launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->d_sortkeys.p, E->st);
   HIPCHK(hipGetLastError());
+  if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
+    launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, E->st);
+    HIPCHK(hipGetLastError());
+  }
   return 0;
 }
 
 Eng* as_eng(void* e) { return static_cast<Eng*>(e); }
+
 
 }  // namespace
 
@@ -666,7 +696,7 @@ void tgsim_destroy(void* e) {
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dcur.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_sortkeys.release(); E->d_drain.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
+  E->d_sortkeys.release(); E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
   if (E->ev0) (void)hipEventDestroy(E->ev0);
@@ -771,6 +801,17 @@ int tgsim_configure(void* e, uint32_t peer, const tgsim_config* cfg) {
   return 0;
 }
 
+int64_t tgsim_configure_batch(void* e, const uint32_t* peers, const tgsim_config* cfgs, size_t n, int32_t* rcs) {
+  if (!e || (n && (!peers || !cfgs))) return -EINVAL;
+  int64_t failed = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const int rc = tgsim_configure(e, peers[i], &cfgs[i]);
+    if (rcs) rcs[i] = rc;
+    failed += rc != 0;
+  }
+  return failed;
+}
+
 int tgsim_submit(void* e, const tgsim_pkt* pkts, size_t n) {
   Eng* E = as_eng(e);
   if (!E || (!pkts && n)) return -EINVAL;
@@ -826,6 +867,86 @@ int tgsim_gen_storm(void* e, double lambda, uint32_t n_ticks) {
   E->gen_q_ticks += n_ticks;
   E->gen_q.push_back(std::move(w));
   return 0;
+}
+
+// Gossip flood workload, see include/tgsim.h.
+int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
+  Eng* E = as_eng(e);
+  if (!E || !g || g->n_floods == 0 || g->n_floods > 64 || g->degree == 0 || g->degree > 64 ||
+      g->msg_len == 0 || g->msg_len > 65535 || E->N < 2)
+    return -EINVAL;
+  if (g->start_tick < E->now_tick + E->gen_q_ticks) return E->fail(-EINVAL, "gossip: start tick in the past");
+  HIPCHK(hipSetDevice(E->dev));
+  E->gossip = *g;
+  HIPCHK(E->d_gfirst.ensure(static_cast<size_t>(E->S) * 64));
+  HIPCHK(E->d_gfwd.ensure(E->S));
+  HIPCHK(E->d_gerr.ensure(1));
+  HIPCHK(hipMemsetAsync(E->d_gfirst.p, 0xFF, sizeof(uint32_t) * 64 * E->S, E->st));
+  HIPCHK(hipMemsetAsync(E->d_gfwd.p, 0, sizeof(uint64_t) * E->S, E->st));
+  HIPCHK(hipMemsetAsync(E->d_gerr.p, 0, sizeof(uint32_t), E->st));
+  for (uint32_t f = 0; f < g->n_floods; ++f) {
+    uint32_t r[4];
+    philox_host(f, 0, 0x4F524947u, 0, E->key0 ^ 0x3C6EF372u, E->key1 ^ 0xA54FF53Au, r);
+    const uint32_t origin = r[0] % E->N;
+    if (origin < E->o.shard_begin || origin >= E->o.shard_end) continue;
+    const uint32_t t = static_cast<uint32_t>(g->start_tick + static_cast<uint64_t>(f) * g->start_gap_ticks);
+    HIPCHK(hipMemcpyAsync(E->d_gfirst.p + static_cast<uint64_t>(origin - E->o.shard_begin) * 64 + f, &t,
+                          sizeof t, hipMemcpyHostToDevice, E->st));
+    HIPCHK(hipStreamSynchronize(E->st));  // `t` lives on this stack frame
+  }
+  HIPCHK(hipStreamSynchronize(E->st));
+  E->gossip_on = true;
+  return 0;
+}
+
+int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
+  Eng* E = as_eng(e);
+  if (!E || !E->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
+  if (!E->staged.empty()) return E->fail(-EBUSY, "host packets already pending for the next step");
+  HIPCHK(hipSetDevice(E->dev));
+  const uint64_t win0 = E->now_tick + E->gen_q_ticks;
+  const GossipArgs g = gossip_args(E, win0, n_ticks);
+  Eng::GenWindow w;
+  if (!E->gen_free.empty()) {
+    w = std::move(E->gen_free.back());
+    E->gen_free.pop_back();
+  }
+  HIPCHK(E->d_cnt.ensure(E->S));
+  launch_gossip(g, nullptr, 0, E->d_cnt.p, nullptr, nullptr, 1, E->st);
+  HIPCHK(hipGetLastError());
+  uint64_t total = 0;
+  int rc = scan_counts(E, E->d_cnt, w.off, E->d_blk, E->d_tot, E->S, &total);
+  if (rc) return rc;
+  uint32_t errw = 0;
+  HIPCHK(hipMemcpy(&errw, E->d_gerr.p, sizeof errw, hipMemcpyDeviceToHost));
+  if (errw) {
+    E->gen_free.push_back(std::move(w));
+    return E->fail(-EINVAL, "gossip: a receipt precedes the window at tick %llu (lookahead shorter than the window)",
+                   static_cast<unsigned long long>(win0));
+  }
+  HIPCHK(w.in.ensure(total ? total : 1));
+  launch_gossip(g, nullptr, 0, nullptr, w.off.p, w.in.p, 2, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(E->st));
+  w.n = total;
+  w.ticks = n_ticks;
+  E->gen_q_ticks += n_ticks;
+  E->gen_q.push_back(std::move(w));
+  return 0;
+}
+
+int64_t tgsim_gossip_reached(void* e, uint64_t* out, size_t cap) {
+  Eng* E = as_eng(e);
+  if (!E || !E->gossip_on || (!out && cap)) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  std::vector<uint64_t> fwd(E->S);
+  HIPCHK(hipMemcpy(fwd.data(), E->d_gfwd.p, sizeof(uint64_t) * E->S, hipMemcpyDeviceToHost));
+  for (uint32_t f = 0; f < E->gossip.n_floods && f < cap; ++f) {
+    uint64_t c = 0;
+    for (uint32_t s = 0; s < E->S; ++s) c += fwd[s] >> f & 1u;
+    out[f] = c;
+  }
+  return E->gossip.n_floods;
 }
 
 int64_t tgsim_sim_capacity(void* e) {

@@ -94,4 +94,15 @@ struct SimArgs {
 };
 constexpr uint32_t kStampSlots = 8;
 
+// Gossip workload state (C4) of one shard.
+struct GossipArgs {
+  uint32_t* first;          // [s][64] earliest receipt tick (0xFFFFFFFF: none)
+  uint64_t* fwd;            // [s] floods already forwarded (or originated)
+  uint32_t* err;            // bit 0: a receipt precedes the generated window
+  uint32_t k0, k1;          // neighbour hash key
+  uint32_t n_src, shard_begin, n_peers;
+  uint32_t n_floods, degree, msg_len, n_ticks;
+  uint64_t tick_ns, win0;   // window start (absolute tick)
+};
+
 }  // namespace tgsim

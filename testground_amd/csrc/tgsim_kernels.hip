@@ -7,6 +7,7 @@
 //                  carries millions of packets.
 //   k_apply_cfg    K9: scatters compiled LinkShape deltas into the SoA parameter/state arrays.
 //   k_gen_*        synthetic storm traffic written straight into the CSR input.
+//   k_gossip_*     closed-loop gossip flood traffic (C4): receipts at delivery, forwards per window.
 //   k_route_*      groups scheduled records by the destination's shard (input of the RCCL
 //                  all-to-all; plain compaction on one GPU).
 //   k_dst_*        K5: counting sort of deliveries by destination, then a per-destination sort
@@ -687,6 +688,76 @@ __global__ void k_gen_write(GenArgs g, const uint64_t* off, uint32_t* gen_seq, I
 }
 
 // ---------------------------------------------------------------------------------------------
+// Gossip flood workload (C4): receipts are folded into a per-(peer, flood) earliest-receipt tick
+// at delivery; each window emits, per peer, the floods first received in it, earliest first.
+__device__ __forceinline__ uint32_t gossip_neighbour(const GossipArgs& g, uint32_t peer, uint32_t k) {
+  uint32_t r[4];
+  philox(peer, k, 0x474F5350u, 0, g.k0, g.k1, r);
+  const uint32_t d = r[0] % (g.n_peers - 1);
+  return d + (d >= peer);
+}
+
+__global__ void k_gossip_recv(GossipArgs g, const tgsim_delivery* in, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const tgsim_delivery r = in[i];
+  const uint32_t f = r.seq / g.degree;
+  if (f >= g.n_floods || (r.flags & TGSIM_FLAG_CORRUPT)) return;
+  const uint32_t s = r.dst - g.shard_begin;
+  if (g.fwd[s] >> f & 1ull) return;
+  uint64_t t = r.t_ns / g.tick_ns + 1;
+  if (t > 0xFFFFFFFEull) t = 0xFFFFFFFEull;
+  atomicMin(&g.first[(uint64_t)s * 64 + f], (uint32_t)t);
+}
+
+// Floods due in [win0, win0 + n_ticks) for local peer s, as a bitmask; flags late receipts.
+__device__ __forceinline__ uint64_t gossip_due(const GossipArgs& g, uint32_t s) {
+  const uint64_t done = g.fwd[s];
+  const uint32_t* fs = g.first + (uint64_t)s * 64;
+  uint64_t due = 0;
+  for (uint32_t f = 0; f < g.n_floods; ++f) {
+    const uint32_t t = fs[f];
+    if ((done >> f & 1ull) || t == 0xFFFFFFFFu || (uint64_t)t >= g.win0 + g.n_ticks) continue;
+    if ((uint64_t)t < g.win0) atomicOr(g.err, 1u);
+    due |= 1ull << f;
+  }
+  return due;
+}
+
+__global__ void k_gossip_count(GossipArgs g, uint64_t* counts) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.n_src) return;
+  counts[s] = (uint64_t)__popcll(gossip_due(g, s)) * g.degree;
+}
+
+__global__ void k_gossip_write(GossipArgs g, const uint64_t* off, InRec* out) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.n_src) return;
+  uint64_t due = gossip_due(g, s);
+  if (!due) return;
+  g.fwd[s] |= due;
+  const uint32_t src = g.shard_begin + s;
+  const uint32_t* fs = g.first + (uint64_t)s * 64;
+  uint64_t o = off[s];
+  while (due) {  // earliest receipt first, ties by flood id (seq order within a tick)
+    uint32_t best = __ffsll((unsigned long long)due) - 1, bt = fs[best];
+    for (uint64_t m = due & (due - 1); m; m &= m - 1) {
+      const uint32_t f = __ffsll((unsigned long long)m) - 1;
+      if (fs[f] < bt) { best = f; bt = fs[f]; }
+    }
+    due &= ~(1ull << best);
+    for (uint32_t k = 0; k < g.degree; ++k) {
+      InRec rec;
+      rec.dst = gossip_neighbour(g, src, k);
+      rec.seq = best * g.degree + k;
+      rec.tick = (uint32_t)(bt - g.win0);
+      rec.len = g.msg_len;
+      out[o++] = rec;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Exclusive scan (u64), three phases, 1024 elements per block.
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, uint64_t& total) {
   const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
@@ -942,6 +1013,17 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
   const dim3 grid((h.n_src + 63) / 64), blk(64);
   if (phase == 0) hipLaunchKernelGGL(k_gen_count, grid, blk, 0, st, g, counts);
   else hipLaunchKernelGGL(k_gen_write, grid, blk, 0, st, g, off, gen_seq, out);
+}
+
+void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
+                   const uint64_t* off, InRec* out, int phase, hipStream_t st) {
+  if (phase == 0) {
+    if (n) hipLaunchKernelGGL(k_gossip_recv, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, g, recs, n);
+    return;
+  }
+  const dim3 grid((g.n_src + 255) / 256), blk(256);
+  if (phase == 1) hipLaunchKernelGGL(k_gossip_count, grid, blk, 0, st, g, counts);
+  else hipLaunchKernelGGL(k_gossip_write, grid, blk, 0, st, g, off, out);
 }
 
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums,

@@ -27,6 +27,9 @@ void launch_order(const uint32_t* emit_n, uint32_t n, uint32_t* order, hipStream
 void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st);
 void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uint32_t* gen_seq,
                 InRec* out, int phase, hipStream_t st);
+// phase 0: fold delivered records into receipts; 1: per-source counts; 2: write the window.
+void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
+                   const uint64_t* off, InRec* out, int phase, hipStream_t st);
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
                  hipStream_t st);
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);

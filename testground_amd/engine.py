@@ -115,6 +115,20 @@ class CABIEngine:
         self._check(self._fn("configure")(self._h, peer, C.byref(c)), f"configure peer {peer}")
         del keep
 
+    def configure_batch(self, peers: np.ndarray, cfgs: np.ndarray) -> None:
+        """Batch of ConfigureNetwork calls; cfgs is an abi.CONFIG_DTYPE array whose `network`
+        pointers reference live buffers (see network.configs_array)."""
+        peers = np.ascontiguousarray(peers, dtype=np.uint32)
+        cfgs = np.ascontiguousarray(cfgs, dtype=abi.CONFIG_DTYPE)
+        if len(peers) != len(cfgs):
+            raise ValueError("peers and cfgs differ in length")
+        rcs = np.zeros(len(peers), dtype=np.int32)
+        failed = self._fn("configure_batch")(self._h, peers.ctypes.data, cfgs.ctypes.data, len(peers),
+                                             rcs.ctypes.data)
+        if failed:
+            i = int(np.nonzero(rcs)[0][0])
+            self._check(int(rcs[i]), f"configure_batch: peer {int(peers[i])} (and {failed - 1} more)")
+
     # -- data path -----------------------------------------------------------------------------
     def submit(self, pkts: np.ndarray) -> None:
         pkts = np.ascontiguousarray(pkts, dtype=abi.PKT_DTYPE)
@@ -122,6 +136,21 @@ class CABIEngine:
 
     def gen_storm(self, lam: float, n_ticks: int) -> None:
         self._check(self._fn("gen_storm")(self._h, float(lam), n_ticks), "gen_storm")
+
+    def gossip_init(self, n_floods: int = 64, degree: int = 8, msg_len: int = 1024, start_gap_ticks: int = 0,
+                    start_tick: Optional[int] = None) -> None:
+        g = abi.Gossip(n_floods, degree, msg_len, start_gap_ticks, self.stats()["now_tick"] if start_tick is None
+                       else start_tick)
+        self._check(self._fn("gossip_init")(self._h, C.byref(g)), "gossip_init")
+        self.n_floods = n_floods
+
+    def gen_gossip(self, n_ticks: int) -> None:
+        self._check(self._fn("gen_gossip")(self._h, n_ticks), "gen_gossip")
+
+    def gossip_reached(self) -> np.ndarray:
+        out = np.zeros(64, dtype=np.uint64)
+        n = self._check(self._fn("gossip_reached")(self._h, out.ctypes.data, 64), "gossip_reached")
+        return out[:n]
 
     def step(self, n_ticks: int) -> None:
         self._check(self._fn("step")(self._h, n_ticks), "step")

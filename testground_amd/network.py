@@ -8,10 +8,13 @@ plans/network/pingpong.go:29-42, plans/splitbrain/main.go:111-131.  Durations ar
 """
 from __future__ import annotations
 
+import ctypes as C
 import dataclasses
 import enum
 import ipaddress
 from typing import List, Optional, Union
+
+import numpy as np
 
 from . import abi
 
@@ -120,3 +123,29 @@ def to_c(cfg: Config):
 
 def shape_to_c(s: LinkShape) -> abi.Shape:
     return to_c(Config(Network="default", Enable=True, Default=s))[0].shape
+
+
+_DEFAULT_NET = b"default"
+_DEFAULT_NET_BUF = C.create_string_buffer(_DEFAULT_NET)
+
+
+def configs_array(latency_ns, jitter_ns=0, bandwidth_bps=0, loss=0.0, corrupt=0.0, reorder=0.0, duplicate=0.0,
+                  routing_policy: int = 0) -> np.ndarray:
+    """Vectorised Config{Network: "default", Enable: true, Default: LinkShape{...}} records (no
+    rules, no re-addressing) for tgsim_configure_batch; correlations 0."""
+    lat = np.asarray(latency_ns, dtype=np.int64)
+    n = lat.shape[0]
+    a = np.zeros(n, dtype=abi.CONFIG_DTYPE)
+    a["network"] = C.addressof(_DEFAULT_NET_BUF)
+    a["enable"] = 1
+    a["routing_policy"] = routing_policy
+    sh = a["shape"]
+    sh["latency_ns"] = lat
+    sh["jitter_ns"] = jitter_ns
+    sh["bandwidth_bps"] = bandwidth_bps
+    sh["loss"] = loss
+    sh["corrupt"] = corrupt
+    sh["reorder"] = reorder
+    sh["duplicate"] = duplicate
+    a["shape"] = sh
+    return a

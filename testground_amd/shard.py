@@ -63,3 +63,11 @@ class ShardedStepper:
             torch.cuda.current_stream(self.device).synchronize()
         self.engine.deliver(inb.data_ptr(), n_in)
         return n_in
+
+    def barrier(self, state: int, target: int) -> bool:
+        """Global barrier over the shards' sync counters: the per-rank counts of `state` are summed
+        with an all-reduce (RCCL on GPUs) and compared with target (SignalAndWait semantics)."""
+        local = self.engine.signal(state, 0)
+        t = torch.tensor([local], dtype=torch.int64, device=self.device)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item()) >= target

@@ -6,6 +6,8 @@ driver runs the HIP engine on the GPU and, in the tests, the CPU oracle with ide
   C1 pingpong    plans/network/pingpong.go:16-201 (RTT windows :185, :195)
   C2 splitbrain  plans/splitbrain/main.go:60-186 (expectErrors :50-58)
   C3 storm       plans/benchmarks/storm.go:31-197, random all-to-all with heterogeneous shapes
+  C4 gossip      SURVEY §8(d): 1M-peer flood, degree 8, 1 KiB messages, L~U[5,50] ms, loss 1 %
+  C5 epochs      SURVEY §8(d): C3 traffic, mid-run reshaping of 10 % of peers per epoch, barriers
 
 A reaction to a delivery at time d (reply, echo, forward) is offered at tick floor(d/tick) + 1.
 """
@@ -17,14 +19,14 @@ from typing import Dict, List, Tuple
 import numpy as np
 
 from . import abi
-from .network import Config, FilterAction, LinkRule, LinkShape, Millisecond, RoutingPolicyType
+from .network import Config, FilterAction, LinkRule, LinkShape, Millisecond, RoutingPolicyType, configs_array
 
 SEED = 0x7E576A0D00000001
 
 
 # ---------------------------------------------------------------------------------------------
 # C3: storm — heterogeneous LinkShape per instance.
-def storm_shapes(n_peers: int, seed: int = SEED) -> List[LinkShape]:
+def storm_shape_arrays(n_peers: int, seed: int = SEED) -> Dict[str, np.ndarray]:
     """L~U[1,100] ms, J~U[0,10] ms, Loss~U[0,5] %, Dup/Corrupt/Reorder~U[0,1] %,
     Bw in {1,10,100,1000} Mbit/s, correlations 0."""
     rng = np.random.default_rng(seed & 0xFFFFFFFF)
@@ -35,17 +37,26 @@ def storm_shapes(n_peers: int, seed: int = SEED) -> List[LinkShape]:
     cor = rng.uniform(0, 1, n_peers).astype(np.float32)
     reo = rng.uniform(0, 1, n_peers).astype(np.float32)
     bw = rng.choice(np.array([1, 10, 100, 1000], dtype=np.int64) * 1_000_000, n_peers)
-    return [LinkShape(Latency=int(lat[i]), Jitter=int(jit[i]), Bandwidth=int(bw[i]), Loss=float(loss[i]),
-                      Duplicate=float(dup[i]), Corrupt=float(cor[i]), Reorder=float(reo[i]))
+    return dict(latency_ns=lat, jitter_ns=jit, bandwidth_bps=bw, loss=loss, duplicate=dup, corrupt=cor,
+                reorder=reo)
+
+
+def storm_shapes(n_peers: int, seed: int = SEED) -> List[LinkShape]:
+    a = storm_shape_arrays(n_peers, seed)
+    return [LinkShape(Latency=int(a["latency_ns"][i]), Jitter=int(a["jitter_ns"][i]),
+                      Bandwidth=int(a["bandwidth_bps"][i]), Loss=float(a["loss"][i]),
+                      Duplicate=float(a["duplicate"][i]), Corrupt=float(a["corrupt"][i]),
+                      Reorder=float(a["reorder"][i]))
             for i in range(n_peers)]
 
 
-def configure_storm(eng, n_peers: int, seed: int = SEED) -> List[LinkShape]:
-    shapes = storm_shapes(n_peers, seed)
-    for i, s in enumerate(shapes):
-        eng.configure(i, Config(Network="default", Enable=True, Default=s,
-                                CallbackState="storm-shaped", RoutingPolicy=RoutingPolicyType.DenyAll))
-    return shapes
+def storm_configs(n_peers: int, seed: int = SEED) -> np.ndarray:
+    """The storm shapes as tgsim_config records (RoutingPolicy DenyAll), for configure_batch."""
+    return configs_array(routing_policy=2, **storm_shape_arrays(n_peers, seed))
+
+
+def configure_storm(eng, n_peers: int, seed: int = SEED) -> None:
+    eng.configure_batch(np.arange(n_peers), storm_configs(n_peers, seed))
 
 
 # ---------------------------------------------------------------------------------------------
@@ -163,3 +174,86 @@ def pingpong_round(eng, start_tick: int, seq0: int, pkt_len: int = 66, chunk: in
             elif rtt[dst] is None:  # own id came back
                 rtt[dst] = t - start_tick * tick
     return rtt, now
+
+
+# ---------------------------------------------------------------------------------------------
+# C4: gossip flood.  The engine generates and consumes the traffic on the device
+# (tgsim_gossip_init / tgsim_gen_gossip); this module only shapes the peers and runs windows.
+GOSSIP_MIN_LAT = 5 * Millisecond
+
+
+def gossip_shapes(n_peers: int, seed: int = SEED) -> Tuple[np.ndarray, float]:
+    """Per-peer latency L~U[5,50] ms in whole microseconds (what toMicroseconds keeps), loss 1 %."""
+    rng = np.random.default_rng((seed >> 32) & 0xFFFFFFFF)
+    lat_us = rng.integers(5_000, 50_001, n_peers)
+    return lat_us * 1000, 1.0
+
+
+def configure_gossip(eng, n_peers: int, seed: int = SEED) -> None:
+    lat, loss = gossip_shapes(n_peers, seed)
+    eng.configure_batch(np.arange(n_peers), configs_array(lat, loss=loss))
+
+
+def gossip_window_ticks(eng) -> int:
+    """The largest window whose receipts are all known before the next window: the engine serves
+    items eligible before T_end + lookahead, so lookahead = window = the minimum latency."""
+    return GOSSIP_MIN_LAT // eng.tick_ns
+
+
+def gossip_run(eng, n_windows: int, window: int, collect: bool = True):
+    """Runs n_windows gossip windows; returns per-window (verdicts, deliveries) when collect."""
+    out = []
+    for _ in range(n_windows):
+        eng.gen_gossip(window)
+        eng.step(window)
+        if collect:
+            out.append((eng.verdicts(), eng.drain()))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# C5: epochs of C3 traffic with mid-run reshaping and a barrier per epoch.
+EPOCH_TICKS = 1000
+EPOCH_LAMBDA = 0.2
+EPOCH_RESHAPE_FRAC = 0.1
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    x = (x + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def epoch_selection(n_peers: int, epoch: int, frac: float = EPOCH_RESHAPE_FRAC, seed: int = SEED) -> np.ndarray:
+    """Peers reshaped at the start of `epoch` (hash-selected, ~frac of all peers)."""
+    with np.errstate(over="ignore"):
+        x = _splitmix64(np.arange(n_peers, dtype=np.uint64) ^ np.uint64((seed ^ (epoch << 40)) & (2**64 - 1)))
+    return np.nonzero((x >> np.uint64(32)) < np.uint64(int(frac * 2**32)))[0].astype(np.uint32)
+
+
+def epoch_reshape(eng, n_peers: int, epoch: int, seed: int = SEED) -> int:
+    """Fresh C3-style shapes for the epoch's selected peers; every shard receives every call."""
+    sel = epoch_selection(n_peers, epoch, seed=seed)
+    eng.configure_batch(sel, storm_configs(len(sel), (seed + 0x1000 * (epoch + 1)) & 0xFFFFFFFF))
+    return len(sel)
+
+
+def epoch_state(epoch: int) -> Tuple[int, int]:
+    """Sync state id of barrier `epoch-k` and the round of that id (states are 1024 counters)."""
+    return epoch % 1024, epoch // 1024 + 1
+
+
+def run_epoch(eng, n_peers: int, epoch: int, n_local: int, step=None, barrier=None,
+              lam: float = EPOCH_LAMBDA, ticks: int = EPOCH_TICKS, seed: int = SEED) -> None:
+    """One C5 epoch: reshape (from epoch 1), traffic window, then every local peer signals
+    `epoch-k` and the barrier must release with all n_peers signals (summed over shards)."""
+    if epoch:
+        epoch_reshape(eng, n_peers, epoch, seed)
+    eng.gen_storm(lam, ticks)
+    (step or eng.step)(ticks)
+    state, rnd = epoch_state(epoch)
+    eng.signal(state, n_local)
+    ok = barrier(state, rnd * n_peers) if barrier else eng.barrier_poll(state, rnd * n_peers)
+    if not ok:
+        raise RuntimeError(f"barrier epoch-{epoch} did not release")

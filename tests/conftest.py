@@ -22,6 +22,8 @@ def oracle_lib():
     """The CPU golden model (oracle/), the checker for every parity test."""
     lib = ctypes.CDLL(str(build_oracle()))
     abi.declare(lib, "tgo_")
+    lib.tgo_percentage2u32.restype = ctypes.c_uint32
+    lib.tgo_percentage2u32.argtypes = [ctypes.c_float]
     return lib
 
 

@@ -1,0 +1,121 @@
+"""C4 gossip flood workload on the CPU oracle: the driver's semantics checked
+against an independent restatement.
+
+* Reachability: a peer has flood f iff a path of non-lost edges leads to it from f's origin.
+  Loss is keyed by (seed, src, dst, seq) only, so the reached set is a pure graph property,
+  recomputed here by BFS from the Philox draws.
+* Forward-on-first-receipt: every forward of (peer, flood) is offered at floor(d/tick) + 1 of the
+  peer's earliest receipt of that flood, exactly once, to the `degree` hashed neighbours.
+"""
+import numpy as np
+import pytest
+
+from testground_amd import abi
+from testground_amd import workloads as wl
+from testground_amd.engine import EngineError
+
+N, FLOODS, DEG = 600, 6, 8
+
+
+def _philox(oracle_lib, ctr, key):
+    import ctypes as C
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    oracle_lib.tgo_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def _run(make_oracle, n=N, floods=FLOODS, windows=40):
+    e = make_oracle(n, lookahead_ns=wl.GOSSIP_MIN_LAT)
+    wl.configure_gossip(e, n)
+    e.gossip_init(n_floods=floods, degree=DEG, msg_len=1024, start_gap_ticks=700, start_tick=0)
+    W = wl.gossip_window_ticks(e)
+    offered = []
+    delivered = []
+    import ctypes as C
+    for k in range(windows):
+        e.gen_gossip(W)
+        pk = np.zeros(1 << 20, dtype=abi.PKT_DTYPE)
+        m = e._lib.tgo_offered(e._h, pk.ctypes.data, len(pk))
+        pk = pk[:m].copy()
+        pk_abs = pk["tick"].astype(np.int64) + k * W
+        offered.append((pk, pk_abs))
+        e.step(W)
+        delivered.append(e.drain())
+    return e, W, offered, delivered
+
+
+def test_gossip_reachability_and_first_receipt(oracle_lib, make_oracle):
+    e, W, offered, delivered = _run(make_oracle)
+    key = [wl.SEED & 0xFFFFFFFF, wl.SEED >> 32]
+    gk = [key[0] ^ 0x3C6EF372, key[1] ^ 0xA54FF53A]
+    thr = oracle_lib.tgo_percentage2u32(1.0)
+
+    def nbr(p, k):
+        d = _philox(oracle_lib, [p, k, 0x474F5350, 0], gk)[0] % (N - 1)
+        return d + (d >= p)
+
+    nb = [[nbr(p, k) for k in range(DEG)] for p in range(N)]
+    reached = e.gossip_reached()
+    for f in range(FLOODS):
+        origin = _philox(oracle_lib, [f, 0, 0x4F524947, 0], gk)[0] % N
+        seen = {origin}
+        stack = [origin]
+        while stack:
+            p = stack.pop()
+            for k, q in enumerate(nb[p]):
+                lost = thr >= _philox(oracle_lib, [p, q, f * DEG + k, 0], key)[1]
+                if not lost and q not in seen:
+                    seen.add(q)
+                    stack.append(q)
+        assert reached[f] == len(seen), f"flood {f}: {reached[f]} reached vs BFS {len(seen)}"
+        assert len(seen) > 0.99 * N
+
+    allp = np.concatenate([p for p, _ in offered])
+    ticks = np.concatenate([t for _, t in offered])
+    alld = np.concatenate(delivered)
+    assert len(alld) > 0
+    # every (src, flood) forwards exactly once, to its hashed neighbours
+    flood = allp["seq"] // DEG
+    k = allp["seq"] % DEG
+    pairs = allp["src"].astype(np.int64) * 64 + flood
+    u, cnt = np.unique(pairs, return_counts=True)
+    assert (cnt == DEG).all()
+    assert sum(reached) == len(u)
+    nb_arr = np.array(nb)
+    assert (allp["dst"] == nb_arr[allp["src"], k]).all()
+    # forward tick = tick after the earliest receipt (origins: their start tick)
+    first = {}
+    rf = alld["seq"] // DEG
+    rt = alld["t_ns"] // 1000 + 1
+    for dst, f, t in zip(alld["dst"], rf, rt):
+        key_ = int(dst) * 64 + int(f)
+        if key_ not in first or t < first[key_]:
+            first[key_] = int(t)
+    for s, f, t in zip(allp["src"], flood, ticks):
+        key_ = int(s) * 64 + int(f)
+        if key_ in first:
+            assert t == first[key_] or t == 700 * int(f), (s, f, t, first[key_])
+        else:
+            assert t == 700 * int(f)  # the origin
+
+
+def test_gossip_window_longer_than_lookahead_is_rejected(make_oracle):
+    e = make_oracle(200, lookahead_ns=wl.GOSSIP_MIN_LAT)
+    wl.configure_gossip(e, 200)
+    e.gossip_init(n_floods=2, degree=4, msg_len=512, start_tick=0)
+    W = 2 * wl.gossip_window_ticks(e)  # receipts land inside windows already simulated
+    with pytest.raises(EngineError, match="precedes the window"):
+        for _ in range(20):
+            e.gen_gossip(W)
+            e.step(W)
+
+
+def test_gossip_init_contract(make_oracle):
+    e = make_oracle(10)
+    for bad in (dict(n_floods=0), dict(n_floods=65), dict(degree=0), dict(degree=65), dict(msg_len=0)):
+        kw = dict(n_floods=1, degree=1, msg_len=100, start_tick=0)
+        kw.update(bad)
+        with pytest.raises(EngineError):
+            e.gossip_init(**kw)

@@ -225,3 +225,77 @@ def test_full_size_storm_properties():
     assert (np.diff(d["dst"].astype(np.int64)) >= 0).all()
     same = d["dst"][1:] == d["dst"][:-1]
     assert (d["t_ns"][1:][same] >= d["t_ns"][:-1][same]).all()
+
+
+def _manual_sharded_step(shards, bounds, window):
+    """step_sim on every shard, exchange through device buffers, deliver (one GPU, no collective)."""
+    outs = []
+    for s in shards:
+        buf = torch.empty(max(1, s.sim_capacity()) * 24, dtype=torch.uint8, device="cuda")
+        cnt = s.step_sim(window, bounds, buf.data_ptr(), s.sim_capacity())
+        outs.append((buf, cnt))
+    for k, s in enumerate(shards):
+        parts = [buf[int(cnt[:k].sum()) * 24: int(cnt[:k + 1].sum()) * 24] for buf, cnt in outs]
+        inbound = torch.cat(parts)
+        s.deliver(inbound.data_ptr(), inbound.numel() // 24)
+
+
+def test_gossip_gpu_equals_oracle(make_oracle):
+    """C4 at small scale: device-generated floods whose receipts drive the next window; every
+    window's verdicts and deliveries, and the per-flood reach, bit-exact with the oracle."""
+    n, floods = 3000, 16
+    g, c = both(make_oracle, n, lookahead_ns=wl.GOSSIP_MIN_LAT)
+    for e in (g, c):
+        wl.configure_gossip(e, n)
+        e.gossip_init(n_floods=floods, degree=8, msg_len=1024, start_gap_ticks=500, start_tick=0)
+    w = wl.gossip_window_ticks(g)
+    total = 0
+    for k in range(40):
+        g.gen_gossip(w)
+        c.gen_gossip(w)
+        g.step(w)
+        c.step(w)
+        v, _ = assert_same(g, c, f"gossip window {k}")
+        total += len(v)
+    rg, rc = g.gossip_reached(), c.gossip_reached()
+    assert (rg == rc).all() and (rg > 0.99 * n).all()
+    assert total == 8 * int(rg.sum())  # every reached peer forwarded once (floods drained)
+
+
+def test_gossip_two_shards_equal_one():
+    """C4 sharded: receipts are folded on the destination's shard and forwarded from there."""
+    n, floods, half = 2000, 8, 1000
+    ref = Engine(n, lookahead_ns=wl.GOSSIP_MIN_LAT)
+    shards = [Engine(n, shard=(0, half), lookahead_ns=wl.GOSSIP_MIN_LAT),
+              Engine(n, shard=(half, n), lookahead_ns=wl.GOSSIP_MIN_LAT)]
+    for e in [ref] + shards:
+        wl.configure_gossip(e, n)
+        e.gossip_init(n_floods=floods, degree=8, msg_len=1024, start_gap_ticks=300, start_tick=0)
+    w = wl.gossip_window_ticks(ref)
+    for k in range(30):
+        ref.gen_gossip(w)
+        ref.step(w)
+        for s in shards:
+            s.gen_gossip(w)
+        _manual_sharded_step(shards, [0, half, n], w)
+        d_sh = np.concatenate([s.drain() for s in shards])
+        d_ref = ref.drain()
+        assert len(d_sh) == len(d_ref) and (d_sh == d_ref).all(), f"window {k}"
+        v_sh = np.concatenate([s.verdicts() for s in shards])
+        assert (v_sh == ref.verdicts()).all(), f"window {k}"
+    assert (shards[0].gossip_reached() + shards[1].gossip_reached() == ref.gossip_reached()).all()
+
+
+def test_epochs_reshaping_and_barriers(make_oracle):
+    """C5 at small scale: 10 % of the peers get a fresh shape every epoch, all peers pass the
+    epoch barrier; every epoch bit-exact with the oracle."""
+    n = 2000
+    g, c = both(make_oracle, n)
+    for e in (g, c):
+        wl.configure_storm(e, n)
+    for k in range(6):
+        for e in (g, c):
+            wl.run_epoch(e, n, k, n)
+        v, _ = assert_same(g, c, f"epoch {k}")
+        assert len(v) > 300_000
+    assert g.barrier_poll(wl.epoch_state(5)[0], n) and not g.barrier_poll(wl.epoch_state(6)[0], 1)

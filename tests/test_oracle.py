@@ -173,3 +173,27 @@ def test_netem_distributions(make_oracle):
     assert delays.min() >= L - J and delays.max() < L + J
     assert _ks_uniform(delays, L - J, L + J) <= 0.02
     assert abs(lost / sent - 0.03) <= 0.005
+
+
+def test_configure_batch_equals_sequential(make_oracle):
+    """tgsim_configure_batch is n tgsim_configure calls: the vectorised records give the same run as
+    per-instance Config objects, and a failing record reports its peer and the reference's error."""
+    import ctypes
+
+    from testground_amd import network as nw
+    from testground_amd import workloads as wl
+    n = 120
+    a, b = make_oracle(n), make_oracle(n)
+    for i, s in enumerate(wl.storm_shapes(n)):
+        a.configure(i, nw.Config(Network="default", Enable=True, Default=s,
+                                 RoutingPolicy=nw.RoutingPolicyType.DenyAll))
+    wl.configure_storm(b, n)
+    for e in (a, b):
+        e.gen_storm(0.5, 800)
+        e.step(800)
+    assert (a.verdicts() == b.verdicts()).all() and (a.drain() == b.drain()).all()
+    bogus = ctypes.create_string_buffer(b"bogus")
+    recs = nw.configs_array([1000, 2000])
+    recs["network"][1] = ctypes.addressof(bogus)
+    with pytest.raises(Exception, match="peer 7.*unsupported network: bogus"):
+        b.configure_batch([3, 7], recs)

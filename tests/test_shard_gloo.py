@@ -1,6 +1,8 @@
 """World-size-2 `gloo` run of the sharded step (testground_amd/shard.py) on CPU: each rank owns half
 of the sources (an oracle shard), records are exchanged with all_to_all, and the result must equal
-a single engine over all sources, step by step: verdicts per shard and deliveries per destination."""
+a single engine over all sources, step by step: verdicts per shard and deliveries per destination.
+Device-generated workloads: C3 storm, C4 gossip (receipts feed the next window) and C5 epochs
+(reshaping every epoch, barrier counters summed over the ranks with all_reduce)."""
 import ctypes
 import os
 import tempfile
@@ -22,7 +24,32 @@ def _oracle(n, **kw):
     return CABIEngine(lib, "tgo_", n, **kw)
 
 
-def _rank(rank, world, port, outdir):
+def _window(eng, workload, k, step, barrier=None):
+    """Runs window k of `workload` on eng with the given step function (sharded or single)."""
+    if workload == "storm":
+        if k == 0:
+            workloads.configure_storm(eng, N)
+        eng.gen_storm(LAM, WINDOW)
+        step(WINDOW)
+    elif workload == "gossip":
+        if k == 0:
+            workloads.configure_gossip(eng, N)
+            eng.gossip_init(n_floods=4, degree=8, msg_len=1024, start_gap_ticks=900, start_tick=0)
+        w = workloads.gossip_window_ticks(eng)
+        eng.gen_gossip(w)
+        step(w)
+    else:  # C5 epochs: reshaping + barrier reduced over the ranks
+        if k == 0:
+            workloads.configure_storm(eng, N)
+        lo, hi = eng.shard
+        workloads.run_epoch(eng, N, k, hi - lo, step=step, barrier=barrier)
+
+
+def _kw(workload):
+    return dict(lookahead_ns=workloads.GOSSIP_MIN_LAT) if workload == "gossip" else {}
+
+
+def _rank(rank, world, port, outdir, workload="storm", steps=STEPS):
     import torch.distributed as dist
 
     from testground_amd.shard import ShardedStepper, shard_bounds
@@ -30,29 +57,29 @@ def _rank(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     b = shard_bounds(N, world)
-    eng = _oracle(N, shard=(b[rank], b[rank + 1]))
-    workloads.configure_storm(eng, N)
+    eng = _oracle(N, shard=(b[rank], b[rank + 1]), **_kw(workload))
     st = ShardedStepper(eng, b, device="cpu")
-    for k in range(STEPS):
-        eng.gen_storm(LAM, WINDOW)
-        st.step(WINDOW)
+    for k in range(steps):
+        _window(eng, workload, k, st.step, st.barrier)
         np.save(os.path.join(outdir, f"v{rank}_{k}.npy"), eng.verdicts())
         np.save(os.path.join(outdir, f"d{rank}_{k}.npy"), eng.drain())
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_equals_single_engine():
+@pytest.mark.parametrize("workload,steps,min_pkts",
+                         [("storm", STEPS, 10_000), ("gossip", 16, 100), ("epochs", 4, 10_000)])
+def test_two_rank_gloo_equals_single_engine(workload, steps, min_pkts):
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_rank, args=(world, 29600 + os.getpid() % 300, d), nprocs=world,
-                           start_method="spawn", join=True)
-        ref = _oracle(N)
-        workloads.configure_storm(ref, N)
-        for k in range(STEPS):
-            ref.gen_storm(LAM, WINDOW)
-            ref.step(WINDOW)
+        mp.start_processes(_rank, args=(world, 29600 + os.getpid() % 300 + 7 * ["storm", "gossip", "epochs"].index(workload), d,
+                                        workload, steps), nprocs=world, start_method="spawn", join=True)
+        ref = _oracle(N, **_kw(workload))
+        for k in range(steps):
+            _window(ref, workload, k, ref.step)
             v = np.concatenate([np.load(os.path.join(d, f"v{r}_{k}.npy")) for r in range(world)])
             dl = np.concatenate([np.load(os.path.join(d, f"d{r}_{k}.npy")) for r in range(world)])
             vr, dr = ref.verdicts(), ref.drain()
-            assert len(v) == len(vr) > 10_000 and (v == vr).all(), f"step {k}: verdicts"
+            assert len(v) == len(vr) and (v == vr).all(), f"step {k}: verdicts"
+            total = total + len(v) if k else len(v)
             assert len(dl) == len(dr) and (dl == dr).all(), f"step {k}: deliveries"
+        assert total > min_pkts
