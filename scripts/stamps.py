@@ -1,51 +1,92 @@
-"""k_sim phase breakdown from in-kernel s_memrealtime stamps (diagnostic build path)."""
-import ctypes as C
+"""k_sim phase breakdown from in-kernel stamps (diagnostic library libtgsim_prof.so).
+
+Phase stamps (s_memrealtime, 100 MHz) per workgroup plus, in the profile build, s_memtime cycle
+counters of the sequential recurrence: admit / heap_pop / heap_push (cycles and counts), the
+parallel phase, the replay loop and the number of queue-full runs resolved by ballot.
+"""
+import argparse
 import os
 import sys
 from pathlib import Path
 
 import numpy as np
 
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
 os.environ["TGSIM_STAMPS"] = "1"
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+os.environ.setdefault("TGSIM_LIB", str(ROOT / "testground_amd" / "libtgsim_prof.so"))
 import torch  # noqa: E402
 
 torch.cuda.init()
 from testground_amd import abi, workloads  # noqa: E402
 from testground_amd.engine import Engine  # noqa: E402
 
-peers = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
-lam = float(sys.argv[2]) if len(sys.argv) > 2 else 0.5
-ql = int(sys.argv[3]) if len(sys.argv) > 3 else 0
-nsteps = int(sys.argv[4]) if len(sys.argv) > 4 else 4
-e = Engine(peers, flags=abi.OPT_DISCARD_DELIVERIES, queue_limit=ql)
-workloads.configure_storm(e, peers)
-for _ in range(nsteps):
-    e.gen_storm(lam, 2000)
-    e.step(2000)
+ap = argparse.ArgumentParser()
+ap.add_argument("--peers", type=int, default=10000)
+ap.add_argument("--lam", type=float, default=0.5)
+ap.add_argument("--ql", type=int, default=0)
+ap.add_argument("--steps", type=int, default=65, help="steps of --window ticks (the last one is reported)")
+ap.add_argument("--window", type=int, default=2000)
+ap.add_argument("--workload", default="storm", choices=["storm", "gossip"])
+ap.add_argument("--top", type=int, default=12)
+a = ap.parse_args()
+
+kw = dict(lookahead_ns=workloads.GOSSIP_MIN_LAT) if a.workload == "gossip" else {}
+e = Engine(a.peers, flags=abi.OPT_DISCARD_DELIVERIES, queue_limit=a.ql, **kw)
+if a.workload == "gossip":
+    workloads.configure_gossip(e, a.peers)
+    e.gossip_init(n_floods=64, degree=8, msg_len=1024, start_gap_ticks=1000, start_tick=0)
+    a.window = workloads.gossip_window_ticks(e)
+else:
+    workloads.configure_storm(e, a.peers)
+for _ in range(a.steps):
+    if a.workload == "gossip":
+        e.gen_gossip(a.window)
+    else:
+        e.gen_storm(a.lam, a.window)
+    e.step(a.window)
 n = e._lib.tgsim_debug_stamps(e._h, None, 0)
 st = np.zeros(n, dtype=np.uint64)
 e._lib.tgsim_debug_stamps(e._h, st.ctypes.data, n)
-st = st.reshape(-1, 8).astype(np.int64)
+st = st.reshape(-1, 16).astype(np.int64)
 t0 = st[:, 0].min()
 ph = np.diff(st[:, :5], axis=1) * 10 / 1000  # us (100 MHz)
 tot = (st[:, 4] - st[:, 0]) * 10 / 1000
-print(f"steps={nsteps} peers={peers} lam={lam} ql={ql} wgs={len(st)} kernel span {(st[:, 4].max() - t0) * 10 / 1e6:.3f} ms")
+print(f"{a.workload} steps={a.steps} peers={a.peers} lam={a.lam} ql={a.ql} wgs={len(st)} "
+      f"kernel span {(st[:, 4].max() - t0) * 10 / 1e6:.3f} ms")
 for name, col in zip(["load", "batches", "end_htb", "writeback"], ph.T):
     print(f"  {name:10s} mean {col.mean():8.2f} us  p50 {np.median(col):8.2f}  max {col.max():8.2f}")
 print(f"  total      mean {tot.mean():8.2f} us  p50 {np.median(tot):8.2f}  max {tot.max():8.2f}")
 src_of = st[:, 5] >> 32
 nbat = st[:, 5] & 0xFFFFFFFF
-print(f"  batches/wg mean {nbat.mean():.1f}; queue (heap, ring) mean {np.mean(st[:, 7] >> 32):.0f}, {np.mean(st[:, 7] & 0xffffffff):.0f}")
+print(f"  batches/wg mean {nbat.mean():.1f}; queue (heap, ring) mean {np.mean(st[:, 7] >> 32):.0f}, "
+      f"{np.mean(st[:, 7] & 0xffffffff):.0f}")
 start = (st[:, 0] - t0) * 10 / 1000
 end = (st[:, 4] - t0) * 10 / 1000
 ts = np.linspace(0, end.max(), 20)
-conc = [int(((start <= t) & (end > t)).sum()) for t in ts]
-print("  concurrency over time:", conc)
-shapes = workloads.storm_shapes(peers)
-order = np.argsort(-tot)[:12]
+print("  concurrency over time:", [int(((start <= t) & (end > t)).sum()) for t in ts])
+cyc = st[:, 8:14]
+par, rep, runs = st[:, 14], st[:, 15] >> 20, st[:, 15] & 0xFFFFF
+
+
+def per(c, k):
+    return c / np.maximum(k, 1)
+
+
+print(f"  all wgs: admit {cyc[:, 1].sum():.3g} x {per(cyc[:, 0].sum(), cyc[:, 1].sum()):.0f} cyc, "
+      f"pop {cyc[:, 3].sum():.3g} x {per(cyc[:, 2].sum(), cyc[:, 3].sum()):.0f} cyc, "
+      f"push {cyc[:, 5].sum():.3g} x {per(cyc[:, 4].sum(), cyc[:, 5].sum()):.0f} cyc; "
+      f"parallel {par.sum() / max(1, nbat.sum()):.0f} cyc/batch, replay {rep.sum() / max(1, nbat.sum()):.0f} "
+      f"cyc/batch, runs {runs.sum() / max(1, nbat.sum()):.1f}/batch")
+shapes = workloads.storm_shapes(a.peers) if a.workload == "storm" else None
 print("  slowest workgroups (= sources):")
-for i in order:
-    s = shapes[src_of[i]]
-    print(f"    wg {i:5d} src {src_of[i]:5d} start {start[i]:7.1f} us {tot[i]:8.1f} us  batches {nbat[i]}  heap {st[i,7]>>32} ring {st[i,7]&0xffffffff}  "
-          f"L {s.Latency/1e6:6.2f} ms J {s.Jitter/1e6:5.2f} ms bw {s.Bandwidth/1e6:5.0f} Mb loss {s.Loss:.2f} reo {s.Reorder:.2f} dup {s.Duplicate:.2f}")
+for i in np.argsort(-tot)[:a.top]:
+    line = (f"    src {src_of[i]:7d} start {start[i]:7.1f} us {tot[i]:8.1f} us  batches {nbat[i]:3d}  "
+            f"q {st[i, 7] >> 32}/{st[i, 7] & 0xffffffff}  admit {cyc[i, 1]}x{per(cyc[i, 0], cyc[i, 1]):.0f}  "
+            f"pop {cyc[i, 3]}x{per(cyc[i, 2], cyc[i, 3]):.0f}  push {cyc[i, 5]}x{per(cyc[i, 4], cyc[i, 5]):.0f}  "
+            f"par {par[i] / max(1, nbat[i]):.0f}/b  rep {rep[i]} runs {runs[i]}")
+    if shapes:
+        s = shapes[src_of[i]]
+        line += (f"  L {s.Latency / 1e6:6.2f} J {s.Jitter / 1e6:5.2f} bw {s.Bandwidth / 1e6:5.0f} "
+                 f"reo {s.Reorder:.2f}")
+    print(line)

@@ -29,26 +29,31 @@ def _stale(target: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def build_engine(force: bool = False, verbose: bool = False) -> Path:
-    """Compiles the HIP engine (kernels + host runtime) into libtgsim.so."""
-    if not force and not _stale(LIB, SOURCES + HEADERS):
-        return LIB
+PROF_LIB = PKG / "libtgsim_prof.so"
+
+
+def build_engine(force: bool = False, verbose: bool = False, profile: bool = False) -> Path:
+    """Compiles the HIP engine (kernels + host runtime) into libtgsim.so.  profile=True builds the
+    diagnostic variant libtgsim_prof.so (k_sim cycle counters in the stamp slots; scripts only)."""
+    lib = PROF_LIB if profile else LIB
+    if not force and not _stale(lib, SOURCES + HEADERS):
+        return lib
     objs = []
-    build_dir = PKG / "build"
+    build_dir = PKG / ("build_prof" if profile else "build")
     build_dir.mkdir(exist_ok=True)
     for src in SOURCES:
         obj = build_dir / (src.stem + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-result", "-c", str(src), "-o", str(obj)]
+               "-Wno-unused-result", *(["-DTGSIM_PROFILE"] if profile else []), "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         objs.append(str(obj))
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 def build_oracle(force: bool = False) -> Path:

@@ -86,7 +86,20 @@ struct Lane {
   // register copies of the two values the common (queue-full) path compares against
   uint64_t top_e;   // eligibility time of the heap root, ~0 when the heap is empty
   uint64_t head_d;  // departure time at the ring head, ~0 when the ring is empty
+#ifdef TGSIM_PROFILE
+  uint64_t pc[6];   // diagnostic build: cycles in admit / heap_pop / heap_push and their counts
+#endif
 };
+
+// Diagnostic build (-DTGSIM_PROFILE, libtgsim_prof.so): s_memtime cycle accounting of the
+// sequential recurrence, reported through the stamp slots.  Compiled out of the product.
+#ifdef TGSIM_PROFILE
+#define PROF_T0() const uint64_t _pt0 = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(L, k) do { (L).pc[2 * (k)] += __builtin_amdgcn_s_memtime() - _pt0; (L).pc[2 * (k) + 1]++; } while (0)
+#else
+#define PROF_T0() do {} while (0)
+#define PROF_ADD(L, k) do {} while (0)
+#endif
 
 __device__ __forceinline__ uint4 hget(const Lane& L, uint32_t k) { return L.hb[k * kSpw]; }
 __device__ __forceinline__ void hset(Lane& L, uint32_t k, const uint4& v) { L.hb[k * kSpw] = v; }
@@ -94,6 +107,7 @@ __device__ __forceinline__ void hset(Lane& L, uint32_t k, const uint4& v) { L.hb
 // 4-ary min-heap on (e, seq, clone first) in LDS: the four children of a node are read together,
 // so a sift-down level costs one LDS round trip and the depth is log4(1024) = 5.
 __device__ __forceinline__ void heap_push(Lane& L, uint4 it) {
+  PROF_T0();
   const uint64_t e = w0_of(it) & kEMask;
   if (e < L.top_e) L.top_e = e;  // ties keep the root's e: only the time is cached
   uint32_t i = L.st.heap_n++;
@@ -105,9 +119,11 @@ __device__ __forceinline__ void heap_push(Lane& L, uint4 it) {
     i = par;
   }
   hset(L, i, it);
+  PROF_ADD(L, 2);
 }
 
 __device__ __forceinline__ void heap_pop(Lane& L) {
+  PROF_T0();
   const uint32_t n = --L.st.heap_n;
   const uint4 last = hget(L, n);
   uint32_t i = 0;
@@ -126,6 +142,7 @@ __device__ __forceinline__ void heap_pop(Lane& L) {
   }
   if (n) hset(L, i, last);
   L.top_e = n ? (w0_of(hget(L, 0)) & kEMask) : ~0ull;
+  PROF_ADD(L, 1);
 }
 
 // HTB class serving the netem queue in eligibility order: d = max(e, TAT),
@@ -158,14 +175,19 @@ __device__ __forceinline__ void htb_until(Lane& L, uint64_t horizon) {
 // Queue-limit check and insertion of one netem item whose eligibility time e is already known.
 __device__ __forceinline__ uint32_t admit(Lane& L, uint32_t limit, uint64_t T, uint64_t e, uint32_t dst,
                                           uint32_t seq, uint32_t len, uint32_t flags) {
+  PROF_T0();
   htb_until(L, T);
   while (L.head_d < T) {  // departures before T leave the netem queue
     L.st.ring_head = (L.st.ring_head + 1) & (kHeapCap - 1);
     L.head_d = --L.st.ring_n ? L.rb[L.st.ring_head * kSpw] : ~0ull;
   }
-  if (L.st.heap_n + L.st.ring_n >= limit) return TGSIM_V_QUEUE_FULL;
+  if (L.st.heap_n + L.st.ring_n >= limit) {
+    PROF_ADD(L, 0);
+    return TGSIM_V_QUEUE_FULL;
+  }
   const uint64_t w0 = e | ((uint64_t)(len & 0xFFFFu) << 46) | ((uint64_t)flags << 62);
   heap_push(L, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst));
+  PROF_ADD(L, 0);
   return TGSIM_V_SCHEDULED;
 }
 
@@ -345,6 +367,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   const bool any_corr = __any(corr);
   const bool seq_lane = lane < kSpw && s0 + lane < a.n_src;
   Lane L;
+#ifdef TGSIM_PROFILE
+  for (int k = 0; k < 6; ++k) L.pc[k] = 0;
+  uint64_t prof_par = 0, prof_rep = 0, prof_runs = 0;
+#endif
   L.scheduled = L.corrupted = 0;
   L.bytes = 0;
   L.err = 0;
@@ -380,6 +406,9 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   if (prefetcher && idx < pend) rec = a.in[idx];
   if (prefetcher && idx + kAhead < pend) rec2 = a.in[idx + kAhead];
   for (uint32_t b = 0; b < n_batches; ++b) {
+#ifdef TGSIM_PROFILE
+    const uint64_t pb0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint64_t my_idx = idx;  // the record this lane stages in this batch
     const bool staged = prefetcher && my_idx < pend;
     uint32_t n_cand = 0;
@@ -468,6 +497,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       }
     }
     wave_lds_sync();
+#ifdef TGSIM_PROFILE
+    const uint64_t pb1 = __builtin_amdgcn_s_memtime();
+    prof_par += pb1 - pb0;
+#endif
     idx += kAhead;
     rec = rec2;
     if (prefetcher && idx + kAhead < pend) rec2 = a.in[idx + kAhead];  // in flight two batches ahead
@@ -515,6 +548,9 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
             lds.vst[cinfo >> 24] = (uint8_t)((cv << 4) | TGSIM_V_QUEUE_FULL);
           }
           c += __popcll(m);
+#ifdef TGSIM_PROFILE
+          prof_runs++;
+#endif
           if (c >= n_cand) break;
         }
         if (lane == 0) {
@@ -534,6 +570,9 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       }
     }
     wave_lds_sync();
+#ifdef TGSIM_PROFILE
+    prof_rep += __builtin_amdgcn_s_memtime() - pb1;
+#endif
     if (staged) {
       const uint32_t v = lds.vst[lane];
       a.verdict[my_idx] = (uint8_t)v;
@@ -572,6 +611,11 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   stamp(a, lane, 5, ((uint64_t)s0 << 32) | n_batches);
   stamp(a, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
   stamp(a, lane, 7, seq_lane ? ((uint64_t)L.st.heap_n << 32 | L.st.ring_n) : 0);
+#ifdef TGSIM_PROFILE
+  for (int k = 0; k < 6; ++k) stamp(a, lane, 8 + k, L.pc[k]);
+  stamp(a, lane, 14, prof_par);
+  stamp(a, lane, 15, (prof_rep << 20) | (prof_runs & 0xFFFFF));
+#endif
   const uint64_t sched = wave_sum(seq_lane ? L.scheduled : 0u);
   const uint64_t corrupted = wave_sum(seq_lane ? L.corrupted : 0u);
   const uint64_t bytes = wave_sum(seq_lane ? L.bytes : 0ull);
