@@ -65,26 +65,17 @@ start = (st[:, 0] - t0) * 10 / 1000
 end = (st[:, 4] - t0) * 10 / 1000
 ts = np.linspace(0, end.max(), 20)
 print("  concurrency over time:", [int(((start <= t) & (end > t)).sum()) for t in ts])
-cyc = st[:, 8:14]
-par, rep, runs = st[:, 14], st[:, 15] >> 20, st[:, 15] & 0xFFFFF
-
-
-def per(c, k):
-    return c / np.maximum(k, 1)
-
-
-print(f"  all wgs: admit {cyc[:, 1].sum():.3g} x {per(cyc[:, 0].sum(), cyc[:, 1].sum()):.0f} cyc, "
-      f"pop {cyc[:, 3].sum():.3g} x {per(cyc[:, 2].sum(), cyc[:, 3].sum()):.0f} cyc, "
-      f"push {cyc[:, 5].sum():.3g} x {per(cyc[:, 4].sum(), cyc[:, 5].sum()):.0f} cyc; "
-      f"parallel {par.sum() / max(1, nbat.sum()):.0f} cyc/batch, replay {rep.sum() / max(1, nbat.sum()):.0f} "
-      f"cyc/batch, runs {runs.sum() / max(1, nbat.sum()):.1f}/batch")
+pf = st[:, 8:16]  # profile build: [parallel cyc, window cyc, -, windows, insert cyc, inserted items, shift chunks, -]
+nb = np.maximum(nbat, 1)
+print(f"  per batch (mean over wgs): parallel {np.mean(pf[:, 0] / nb):.0f} cyc, windows {np.mean(pf[:, 1] / nb):.0f} cyc, "
+      f"{np.mean(pf[:, 3] / nb):.2f} windows, insert {np.mean(pf[:, 4] / nb):.0f} cyc, "
+      f"{np.mean(pf[:, 5] / nb):.2f} items, {np.mean(pf[:, 6] / nb):.2f} shift chunks")
 shapes = workloads.storm_shapes(a.peers) if a.workload == "storm" else None
 print("  slowest workgroups (= sources):")
 for i in np.argsort(-tot)[:a.top]:
     line = (f"    src {src_of[i]:7d} start {start[i]:7.1f} us {tot[i]:8.1f} us  batches {nbat[i]:3d}  "
-            f"q {st[i, 7] >> 32}/{st[i, 7] & 0xffffffff}  admit {cyc[i, 1]}x{per(cyc[i, 0], cyc[i, 1]):.0f}  "
-            f"pop {cyc[i, 3]}x{per(cyc[i, 2], cyc[i, 3]):.0f}  push {cyc[i, 5]}x{per(cyc[i, 4], cyc[i, 5]):.0f}  "
-            f"par {par[i] / max(1, nbat[i]):.0f}/b  rep {rep[i]} runs {runs[i]}")
+            f"q {st[i, 7] >> 32}/{st[i, 7] & 0xffffffff}  par {pf[i, 0] // nb[i]}/b  win {pf[i, 1] // nb[i]}/b "
+            f"x{pf[i, 3]}  ins {pf[i, 4] // max(1, pf[i, 5])}/item x{pf[i, 5]} chunks {pf[i, 6]}")
     if shapes:
         s = shapes[src_of[i]]
         line += (f"  L {s.Latency / 1e6:6.2f} J {s.Jitter / 1e6:5.2f} bw {s.Bandwidth / 1e6:5.0f} "

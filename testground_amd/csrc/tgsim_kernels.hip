@@ -54,141 +54,116 @@ __device__ __forceinline__ bool item_lt(const uint4& a, const uint4& b) {
   return (ea < eb) | ((ea == eb) & seq_lt);
 }
 
-// Per-workgroup LDS: the eligibility heaps and departure rings of kSpw sources, plus the staging
-// area where all 64 lanes leave the prefetched record + Philox draws for the sequential lanes.
-struct alignas(16) Pre {
-  uint4 rec;   // dst, seq, tick, len | filter verdict << 16
-  uint4 r0;    // draw 0: dup, loss, corrupt, reorder
-  uint4 r2;    // draw 2 (clone): loss, corrupt, reorder, delay
-  uint4 r1;    // draw 1: delay word in .x
-};
+// ---------------------------------------------------------------------------------------------
+// k_sim: one wavefront owns one source's netem queue for the whole step.
+//
+// The queue lives in LDS as ONE circular buffer of kHeapCap 16-B slots: the departure ring (items
+// already given a departure time by HTB, d in .x/.y, oldest first) immediately followed by the
+// eligibility queue (items waiting for their netem time e, kept SORTED by (e, seq, clone first)).
+// HTB serves the eligibility queue from its head, so serving an item turns the slot at the
+// boundary into the ring's newest entry in place; the netem limit bounds ring + queue <= 1024.
+//
+// The sequential recurrence of netem_enqueue (limit check) + HTB is resolved a WINDOW of offered
+// packets at a time, wave-parallel:
+//   1. the queue-head items that may become eligible before the batch's last packet are served
+//      optimistically with a max-plus scan (TAT' = max(TAT + c, e - B + c));
+//   2. every candidate counts the departures before its offer time (binary search over the ring
+//      ++ the newly served items, both sorted by d);
+//   3. the netem limit is a saturating counter x -> min(x + a, limit), whose prefix composition is
+//      closed-form (prefix sum + prefix max), so all admission decisions come from two scans;
+//   4. the window ends before the first packet whose offer time is after the eligibility time of
+//      an item admitted earlier in the window (only then could the optimistic HTB service be
+//      wrong): reordered (e = T) and near-zero-delay admissions split windows, nothing else does;
+//   5. admitted items are merged into the sorted queue (binary search + tail shift).
+// Sources with correlated draws (get_crandom, rho != 0) consume state in admission order and take
+// the per-packet path built from the same wave-wide primitives.
 struct SimLds {
-  uint4 heap[(kHeapCap + 4) * kSpw];  // slot k of source j at k * kSpw + j (+4: child reads past n)
-  uint64_t ring[kHeapCap * kSpw];  // departure times, circular per source
-  Pre stage[kWave];
-  uint8_t vst[kWave];              // verdicts of the batch, stored back coalesced
+  uint4 slot[kHeapCap];     // circular: departure ring, then the sorted eligibility queue
+  uint32_t pos[kWave];      // insertion positions of new items, by rank
 };
-static_assert(sizeof(SimLds) <= 163840, "simulate workgroup exceeds 160 KiB of LDS");
+static_assert(sizeof(SimLds) <= 65536, "simulate workgroup LDS");
 
 constexpr uint32_t kFvPass = 0xFFu;
+constexpr uint32_t kSlotMask = kHeapCap - 1;
 
-struct Lane {
-  uint4* hb;        // LDS heap of this source, stride kSpw
-  uint64_t* rb;     // LDS ring of this source, stride kSpw
-  tgsim_delivery* emit;
-  uint32_t n_emit;
-  SrcState st;
-  SrcParams p;
-  uint32_t src;
-  uint32_t scheduled, corrupted;
-  uint64_t bytes;
-  uint32_t err;
-  // register copies of the two values the common (queue-full) path compares against
-  uint64_t top_e;   // eligibility time of the heap root, ~0 when the heap is empty
-  uint64_t head_d;  // departure time at the ring head, ~0 when the ring is empty
-#ifdef TGSIM_PROFILE
-  uint64_t pc[6];   // diagnostic build: cycles in admit / heap_pop / heap_push and their counts
-#endif
-};
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  return ((uint64_t)readlane32((uint32_t)(v >> 32), l) << 32) | readlane32((uint32_t)v, l);
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t ballot_count(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
-// Diagnostic build (-DTGSIM_PROFILE, libtgsim_prof.so): s_memtime cycle accounting of the
-// sequential recurrence, reported through the stamp slots.  Compiled out of the product.
-#ifdef TGSIM_PROFILE
-#define PROF_T0() const uint64_t _pt0 = __builtin_amdgcn_s_memtime()
-#define PROF_ADD(L, k) do { (L).pc[2 * (k)] += __builtin_amdgcn_s_memtime() - _pt0; (L).pc[2 * (k) + 1]++; } while (0)
-#else
-#define PROF_T0() do {} while (0)
-#define PROF_ADD(L, k) do {} while (0)
-#endif
+// Inclusive wave scans (lane order = packet / queue order) on DPP: row_shr 1/2/4/8 inside each
+// row of 16 lanes, then row_bcast:15 and row_bcast:31 carry the row totals (GFX9 wave64 pattern).
+// Lanes without a source lane read the identity.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp(uint32_t id, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t id, uint64_t v) {
+  return ((uint64_t)dpp<CTRL, ROWS>((uint32_t)(id >> 32), (uint32_t)(v >> 32)) << 32) |
+         dpp<CTRL, ROWS>((uint32_t)id, (uint32_t)v);
+}
+#define TG_SCAN_STEPS(STEP) STEP(0x111, 0xF) STEP(0x112, 0xF) STEP(0x114, 0xF) STEP(0x118, 0xF) \
+                            STEP(0x142, 0xA) STEP(0x143, 0xC)
+constexpr int kDppWaveShr1 = 0x138;  // wave_shr:1 (lane i reads lane i - 1; lane 0 the identity)
 
-__device__ __forceinline__ uint4 hget(const Lane& L, uint32_t k) { return L.hb[k * kSpw]; }
-__device__ __forceinline__ void hset(Lane& L, uint32_t k, const uint4& v) { L.hb[k * kSpw] = v; }
-
-// 4-ary min-heap on (e, seq, clone first) in LDS: the four children of a node are read together,
-// so a sift-down level costs one LDS round trip and the depth is log4(1024) = 5.
-__device__ __forceinline__ void heap_push(Lane& L, uint4 it) {
-  PROF_T0();
-  const uint64_t e = w0_of(it) & kEMask;
-  if (e < L.top_e) L.top_e = e;  // ties keep the root's e: only the time is cached
-  uint32_t i = L.st.heap_n++;
-  while (i > 0) {
-    const uint32_t par = (i - 1) >> 2;
-    const uint4 pv = hget(L, par);
-    if (!item_lt(it, pv)) break;
-    hset(L, i, pv);
-    i = par;
-  }
-  hset(L, i, it);
-  PROF_ADD(L, 2);
+// wave_shr:1 must stay a plain v_mov_b32_dpp: folded into a VOP2 ALU op (v_sub_u32_dpp ...
+// wave_shr:1) it gave wrong results on gfx950, so the asm barrier keeps the DPP combiner off it.
+__device__ __forceinline__ uint32_t shr1_u32(uint32_t v, uint32_t id) {
+  uint32_t r = dpp<kDppWaveShr1, 0xF>(id, v);
+  __asm__ volatile("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ uint64_t shr1_u64(uint64_t v, uint64_t id) {
+  return ((uint64_t)shr1_u32((uint32_t)(v >> 32), (uint32_t)(id >> 32)) << 32) | shr1_u32((uint32_t)v, (uint32_t)id);
 }
 
-__device__ __forceinline__ void heap_pop(Lane& L) {
-  PROF_T0();
-  const uint32_t n = --L.st.heap_n;
-  const uint4 last = hget(L, n);
-  uint32_t i = 0;
-  for (;;) {
-    const uint32_t c = 4 * i + 1;
-    if (c >= n) break;
-    const uint4 v0 = hget(L, c), v1 = hget(L, c + 1), v2 = hget(L, c + 2), v3 = hget(L, c + 3);
-    uint4 best = v0;
-    uint32_t bi = c;
-    if (c + 1 < n && item_lt(v1, best)) { best = v1; bi = c + 1; }
-    if (c + 2 < n && item_lt(v2, best)) { best = v2; bi = c + 2; }
-    if (c + 3 < n && item_lt(v3, best)) { best = v3; bi = c + 3; }
-    if (!item_lt(best, last)) break;
-    hset(L, i, best);
-    i = bi;
-  }
-  if (n) hset(L, i, last);
-  L.top_e = n ? (w0_of(hget(L, 0)) & kEMask) : ~0ull;
-  PROF_ADD(L, 1);
+__device__ __forceinline__ void scan_maxplus(uint64_t& a, uint64_t& b) {
+  // maps x -> max(x + a, b); earlier (pa, pb) then later (a, b) = (pa + a, max(pb + a, b))
+#define STEP(C, R) { const uint64_t pa = dpp64<C, R>(0, a), pb = dpp64<C, R>(0, b); \
+                     const uint64_t nb = pb + a; b = nb > b ? nb : b; a = pa + a; }
+  TG_SCAN_STEPS(STEP)
+#undef STEP
+}
+__device__ __forceinline__ int32_t scan_sum_i32(int32_t v) {
+#define STEP(C, R) v += (int32_t)dpp<C, R>(0u, (uint32_t)v);
+  TG_SCAN_STEPS(STEP)
+#undef STEP
+  return v;
+}
+__device__ __forceinline__ int32_t scan_max_i32(int32_t v) {
+#define STEP(C, R) v = max(v, (int32_t)dpp<C, R>(0x80000000u, (uint32_t)v));
+  TG_SCAN_STEPS(STEP)
+#undef STEP
+  return v;
+}
+__device__ __forceinline__ uint32_t scan_max_u32(uint32_t v) {
+#define STEP(C, R) v = max(v, dpp<C, R>(0u, v));
+  TG_SCAN_STEPS(STEP)
+#undef STEP
+  return v;
+}
+__device__ __forceinline__ uint64_t scan_min_u64(uint64_t v) {
+#define STEP(C, R) { const uint64_t p = dpp64<C, R>(~0ull, v); v = p < v ? p : v; }
+  TG_SCAN_STEPS(STEP)
+#undef STEP
+  return v;
 }
 
-// HTB class serving the netem queue in eligibility order: d = max(e, TAT),
-// TAT' = max(TAT, e - B) + len * mult >> shift.
-__device__ __forceinline__ void htb_until(Lane& L, uint64_t horizon) {
-  while (L.top_e < horizon) {
-    const uint4 top = hget(L, 0);
-    const uint64_t w0 = w0_of(top);
-    const uint64_t e = w0 & kEMask;
-    if (e >= horizon) break;
-    heap_pop(L);
-    const uint32_t len = (uint32_t)(w0 >> 46) & 0xFFFFu;
-    const uint32_t flags = (uint32_t)(w0 >> 62);
-    const uint64_t d = e > L.st.tat ? e : L.st.tat;
-    const uint64_t fl = e > L.p.burst_ns ? e - L.p.burst_ns : 0;
-    const uint64_t base = L.st.tat > fl ? L.st.tat : fl;
-    L.st.tat = base + (((uint64_t)len * L.p.mult) >> (L.p.shift_ext & 0xFFu));
-    L.rb[((L.st.ring_head + L.st.ring_n) & (kHeapCap - 1)) * kSpw] = d;
-    if (L.st.ring_n++ == 0) L.head_d = d;
-    uint64_t* rw = reinterpret_cast<uint64_t*>(L.emit + L.n_emit++);
-    rw[0] = d;
-    rw[1] = ((uint64_t)top.w << 32) | L.src;
-    rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | top.z;
-    L.scheduled++;
-    L.bytes += len;
-    L.corrupted += (flags >> 1) & 1u;
-  }
-}
-
-// Queue-limit check and insertion of one netem item whose eligibility time e is already known.
-__device__ __forceinline__ uint32_t admit(Lane& L, uint32_t limit, uint64_t T, uint64_t e, uint32_t dst,
-                                          uint32_t seq, uint32_t len, uint32_t flags) {
-  PROF_T0();
-  htb_until(L, T);
-  while (L.head_d < T) {  // departures before T leave the netem queue
-    L.st.ring_head = (L.st.ring_head + 1) & (kHeapCap - 1);
-    L.head_d = --L.st.ring_n ? L.rb[L.st.ring_head * kSpw] : ~0ull;
-  }
-  if (L.st.heap_n + L.st.ring_n >= limit) {
-    PROF_ADD(L, 0);
-    return TGSIM_V_QUEUE_FULL;
-  }
-  const uint64_t w0 = e | ((uint64_t)(len & 0xFFFFu) << 46) | ((uint64_t)flags << 62);
-  heap_push(L, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst));
-  PROF_ADD(L, 0);
-  return TGSIM_V_SCHEDULED;
+// Count of the 64 lane values v (sorted ascending over lanes) that are <= t, for every lane's t.
+__device__ __forceinline__ uint32_t count_le_sorted_u32(uint32_t v, uint32_t t) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t s = 32; s; s >>= 1)
+    if ((uint32_t)__shfl(v, (int)(lo + s - 1), 64) <= t) lo += s;
+  return lo + ((uint32_t)__shfl(v, (int)lo, 64) <= t ? 1u : 0u);
 }
 
 // tabledist() uniform branch: e = T + max(0, L - sigma + raw mod 2 sigma), or T + L when sigma = 0.
@@ -197,29 +172,6 @@ __device__ __forceinline__ uint64_t delayed(const SrcParams& p, uint64_t T, uint
   const uint32_t m = 2u * (uint32_t)p.sigma;
   const int64_t delay = (int64_t)(raw % m) + (int64_t)p.lat_ns - (int64_t)p.sigma;
   return delay > 0 ? T + (uint64_t)delay : T;
-}
-
-// netem_enqueue from the queue-limit check on, for sources with correlated draws: the reorder
-// decision consumes correlated state only when the packet passes the limit check.
-__device__ __forceinline__ uint32_t enqueue(Lane& L, uint32_t limit, uint64_t T, uint32_t dst,
-                                            uint32_t seq, uint32_t len, uint32_t reo_raw,
-                                            uint32_t delay_raw, uint32_t flags) {
-  htb_until(L, T);
-  while (L.head_d < T) {
-    L.st.ring_head = (L.st.ring_head + 1) & (kHeapCap - 1);
-    L.head_d = --L.st.ring_n ? L.rb[L.st.ring_head * kSpw] : ~0ull;
-  }
-  if (L.st.heap_n + L.st.ring_n >= limit) return TGSIM_V_QUEUE_FULL;
-  bool reordered = false;
-  if (L.p.thr_reo) reordered = !(L.p.thr_reo < crand(reo_raw, L.p.rho_reo, L.st.last_reo));
-  uint64_t e = reordered ? T : delayed(L.p, T, delay_raw);
-  if (e > kEMask) {
-    L.err |= kErrTimeOverflow;
-    e = kEMask;
-  }
-  const uint64_t w0 = e | ((uint64_t)(len & 0xFFFFu) << 46) | ((uint64_t)flags << 62);
-  heap_push(L, make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst));
-  return TGSIM_V_SCHEDULED;
 }
 
 __device__ __forceinline__ uint32_t fib_lookup(const Interval* iv, uint32_t n, uint32_t ip) {
@@ -249,31 +201,6 @@ __device__ __forceinline__ uint32_t filter(const SimArgs& a, const SrcParams& p,
   return kFvPass;
 }
 
-// Sequential netem_enqueue for one offered packet of a correlated source (raw draws staged).
-__device__ __forceinline__ uint32_t process_corr(Lane& L, uint32_t limit, uint64_t T, const Pre& pre) {
-  const uint32_t dst = pre.rec.x, seq = pre.rec.y, len = pre.rec.w & 0xFFFFu;
-  const uint32_t fv = pre.rec.w >> 16;
-  if (fv != kFvPass) return 0xF0u | fv;
-  int count = 1;
-  if (L.p.thr_dup && L.p.thr_dup >= crand(pre.r0.x, L.p.rho_dup, L.st.last_dup)) ++count;
-  if (L.p.thr_loss && L.p.thr_loss >= pre.r0.y) --count;
-  if (count == 0) return 0xF0u | TGSIM_V_LOSS;
-  uint32_t cv = TGSIM_V_NONE;
-  if (count == 2) {  // the clone re-enters the root qdisc with duplicate = 0
-    if (L.p.thr_loss && L.p.thr_loss >= pre.r2.x) {
-      cv = TGSIM_V_LOSS;
-    } else {
-      uint32_t fl = TGSIM_FLAG_DUP;
-      if (L.p.thr_cor && L.p.thr_cor >= crand(pre.r2.y, L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
-      cv = enqueue(L, limit, T, dst, seq, len, pre.r2.z, pre.r2.w, fl);
-    }
-  }
-  uint32_t fl = 0;
-  if (L.p.thr_cor && L.p.thr_cor >= crand(pre.r0.z, L.p.rho_cor, L.st.last_cor)) fl |= TGSIM_FLAG_CORRUPT;
-  const uint32_t ov = enqueue(L, limit, T, dst, seq, len, pre.r0.w, pre.r1.x, fl);
-  return (cv << 4) | ov;
-}
-
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -284,28 +211,8 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
   return v;
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
-  return v;
-}
-
-// Staged candidate of an uncorrelated source (48 B of a Pre slot): everything netem decides
-// without queue state is resolved by the lane that loaded the packet.
-//   rec = {T lo, T hi, e_orig lo, e_orig hi}, r0 = {e_clone lo, e_clone hi, dst, seq},
-//   r2.x = len | orig flags << 16 | clone flags << 18 | clone state << 20 | batch slot << 24
-// clone state: 0 none, 1 lost, 2 queue candidate.
-
-// One wavefront per workgroup owns kSpw sources (kSpw = 1: one netem queue per wavefront, so the
-// sequential recurrences of different sources are independent waves the SIMDs interleave).  Per
-// batch every lane (j, r) = (lane % kSpw, lane / kSpw) loads record r of source j's next kAhead
-// records and resolves the filter and all Philox-driven decisions; lane j then replays the queue
-// candidates (compacted with a ballot) through the netem-limit / eligibility-heap / HTB
-// recurrence held in LDS.  Sources with correlated draws (get_crandom, rho != 0) replay the raw
-// draws sequentially instead.  The next batch's records are in flight during the sequential phase.
-// The simulate workgroup is a single wavefront: cross-lane LDS hand-offs only need this wave's
-// LDS operations to have landed (lgkmcnt(0)), not the vmcnt(0) drain of outstanding global stores
-// and prefetch loads that __syncthreads() implies.
+// Cross-lane LDS hand-off inside the single-wavefront workgroup: this wave's LDS operations have
+// landed (lgkmcnt(0)); no vmcnt drain of the outstanding global stores and prefetch loads.
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
   __builtin_amdgcn_wave_barrier();
@@ -316,311 +223,491 @@ __device__ __forceinline__ void stamp(const SimArgs& a, uint32_t lane, uint32_t 
   if (a.stamps && lane == 0) a.stamps[(size_t)blockIdx.x * kStampSlots + k] = v;
 }
 
+#ifdef TGSIM_PROFILE
+#define PROF_T0(n) const uint64_t _pt##n = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(k, n) (pf[k] += __builtin_amdgcn_s_memtime() - _pt##n)
+#define PROF_CNT(k, v) (pf[k] += (v))
+#else
+#define PROF_T0(n) do {} while (0)
+#define PROF_ADD(k, n) do {} while (0)
+#define PROF_CNT(k, v) do {} while (0)
+#endif
+
+// Wave-uniform queue state of the source plus the helpers that operate on it.  Every member is
+// identical in all 64 lanes; per-lane scratch is passed in and out.
+struct SimQueue {
+  SimLds& lds;
+  const SrcParams& p;
+  uint32_t lane;
+  uint32_t rh, rn, qn;      // ring head slot, ring length, eligibility-queue length
+  uint64_t tat;             // HTB theoretical arrival time
+  tgsim_delivery* emit;
+  uint32_t n_emit, src;
+  // per-lane accumulators (summed over the wave at the end)
+  uint32_t sched, corrupted;
+  uint64_t bytes;
+#ifdef TGSIM_PROFILE
+  uint64_t pf[8];
+#endif
+
+  __device__ __forceinline__ uint4& slot(uint32_t k) { return lds.slot[(rh + k) & kSlotMask]; }
+  __device__ __forceinline__ uint64_t ring_d(uint32_t k) {
+    const uint2 v = *reinterpret_cast<const uint2*>(&lds.slot[(rh + k) & kSlotMask]);
+    return ((uint64_t)v.y << 32) | v.x;
+  }
+
+  // HTB departure times of the queue-head items held one per lane (in = lane < n, e/len of the
+  // lane's item): d = max(e, TAT_before), and the TAT after each item.
+  __device__ __forceinline__ void htb_scan(bool in, uint64_t e, uint32_t len, uint64_t& d,
+                                           uint64_t& tat_after) const {
+    const uint64_t c = ((uint64_t)len * p.mult) >> (p.shift_ext & 0xFFu);
+    uint64_t A = in ? c : 0, B = in ? (e > p.burst_ns ? e - p.burst_ns : 0) + c : 0;
+    scan_maxplus(A, B);
+    const uint64_t ta = tat + A;
+    tat_after = ta > B ? ta : B;
+    const uint64_t before = shr1_u64(tat_after, tat);
+    d = e > before ? e : before;
+  }
+
+  // Commits the HTB service of the first n queue items (lanes < n): slot -> ring entry, record.
+  __device__ __forceinline__ void commit(bool c, uint32_t n, const uint4& qi, uint64_t d, uint64_t tat_after) {
+    if (c) {
+      *reinterpret_cast<uint2*>(&slot(rn + lane)) = make_uint2((uint32_t)d, (uint32_t)(d >> 32));
+      const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
+      uint64_t* rw = reinterpret_cast<uint64_t*>(emit + n_emit + lane);
+      rw[0] = d;
+      rw[1] = ((uint64_t)qi.w << 32) | src;
+      rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
+      sched++;
+      bytes += len;
+      corrupted += (flags >> 1) & 1u;
+    }
+    tat = readlane64(tat_after, n - 1);
+    rn += n;
+    qn -= n;
+    n_emit += n;
+    wave_lds_sync();
+  }
+
+  // HTB serves every queued item eligible before h (e < h), in (e, seq, clone first) order.
+  __device__ void serve_until(uint64_t h) {
+    for (;;) {
+      const bool hq = lane < qn;
+      const uint4 qi = hq ? slot(rn + lane) : make_uint4(0, 0, 0, 0);
+      const uint64_t qe = hq ? (w0_of(qi) & kEMask) : ~0ull;
+      const bool in = qe < h;
+      const uint32_t n = ballot_count(in);
+      if (!n) break;
+      uint64_t d, ta;
+      htb_scan(in, qe, qi.y >> 14 & 0xFFFFu, d, ta);
+      commit(in, n, qi, d, ta);
+      if (n < kWave) break;
+    }
+  }
+
+  // Items whose departure time is before T leave the netem queue.
+  __device__ void depart_before(uint64_t T) {
+    for (;;) {
+      const uint64_t dep = lane < rn ? ring_d(lane) : ~0ull;
+      const uint32_t k = ballot_count(dep < T);
+      rh = (rh + k) & kSlotMask;
+      rn -= k;
+      if (k < kWave) break;
+    }
+  }
+
+  // Merges the lanes' new items (has) into the sorted eligibility queue.
+  __device__ void insert(bool has, const uint4& it) {
+    const uint64_t m = __ballot(has);
+    if (!m) return;
+    PROF_T0(i);
+    const uint32_t nm = (uint32_t)__popcll(m);
+    // position among the queued items: lower bound of the item's key
+    uint32_t pos = 0;
+    if (has && qn) {
+      if (item_lt(slot(rn + qn - 1), it)) {
+        pos = qn;
+      } else {
+        uint32_t lo = 0, hi = qn - 1;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (item_lt(slot(rn + mid), it)) lo = mid + 1;
+          else hi = mid;
+        }
+        pos = lo;
+      }
+    }
+    // rank among the new items (equal keys: lane order)
+    uint32_t rank = 0;
+    if (nm > 1) {
+      uint64_t mm = m;
+      while (mm) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(mm);
+        mm &= mm - 1;
+        const uint4 o = make_uint4(readlane32(it.x, b), readlane32(it.y, b), readlane32(it.z, b), 0u);
+        rank += (has && (item_lt(o, it) || (!item_lt(it, o) && b < lane))) ? 1u : 0u;
+      }
+    }
+    if (has) lds.pos[rank] = pos;
+    wave_lds_sync();
+    const uint32_t sp = lane < nm ? lds.pos[lane] : 0xFFFFFFFFu;  // ascending
+    const uint32_t minpos = readlane32(sp, 0);
+    // queued items at index r >= minpos move up by the number of new items placed before them;
+    // chunks from the tail down, so no chunk reads a slot an earlier chunk wrote
+    for (int32_t hi = (int32_t)qn; hi > (int32_t)minpos; hi -= (int32_t)kWave) {
+      const int32_t r = hi - (int32_t)kWave + (int32_t)lane;
+      const bool mv = r >= (int32_t)minpos;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (mv) v = slot(rn + (uint32_t)r);
+      uint32_t sh = 0;
+      if (nm <= 8) {
+        for (uint32_t k = 0; k < nm; ++k) sh += readlane32(sp, k) <= (uint32_t)r ? 1u : 0u;
+      } else {
+        sh = count_le_sorted_u32(sp, mv ? (uint32_t)r : 0u);
+      }
+      if (mv) slot(rn + (uint32_t)r + sh) = v;
+      PROF_CNT(6, 1);
+    }
+    if (has) slot(rn + pos + rank) = it;
+    qn += nm;
+    wave_lds_sync();
+    PROF_ADD(4, i);
+    PROF_CNT(5, nm);
+  }
+};
+
+__device__ __forceinline__ uint4 make_item(uint64_t e, uint32_t len, uint32_t flags, uint32_t seq, uint32_t dst) {
+  const uint64_t w0 = e | ((uint64_t)(len & 0xFFFFu) << 46) | ((uint64_t)flags << 62);
+  return make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst);
+}
+
 __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   __shared__ SimLds lds;
   const uint32_t lane = threadIdx.x;
   // heavy-first dispatch order (previous step's HTB work per source), identity when absent
-  const uint32_t s0 = (kSpw == 1 && a.order) ? a.order[blockIdx.x] : blockIdx.x * kSpw;
+  const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
+  if (s >= a.n_src) return;
   stamp(a, lane, 0, __builtin_amdgcn_s_memrealtime());
-  // ---- load heaps and rings of the workgroup's sources into LDS
-  for (uint32_t j = 0; j < kSpw; ++j) {
-    const uint32_t s = s0 + j;
-    if (s >= a.n_src) break;
-    const uint32_t hn = a.state[s].heap_n, rn = a.state[s].ring_n;
-    const uint4* gh = a.heap + (size_t)s * kHeapCap;
-    const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
-    for (uint32_t k0 = 0; k0 < hn; k0 += 4 * kWave) {  // four loads in flight per lane
-      const uint32_t k = k0 + lane;
-      const uint4 v0 = gh[min(k, hn - 1)], v1 = gh[min(k + kWave, hn - 1)];
-      const uint4 v2 = gh[min(k + 2 * kWave, hn - 1)], v3 = gh[min(k + 3 * kWave, hn - 1)];
-      if (k < hn) lds.heap[k * kSpw + j] = v0;
-      if (k + kWave < hn) lds.heap[(k + kWave) * kSpw + j] = v1;
-      if (k + 2 * kWave < hn) lds.heap[(k + 2 * kWave) * kSpw + j] = v2;
-      if (k + 3 * kWave < hn) lds.heap[(k + 3 * kWave) * kSpw + j] = v3;
-    }
-    for (uint32_t k0 = 0; k0 < rn; k0 += 4 * kWave) {
-      const uint32_t k = k0 + lane;
-      const uint64_t v0 = gr[min(k, rn - 1)], v1 = gr[min(k + kWave, rn - 1)];
-      const uint64_t v2 = gr[min(k + 2 * kWave, rn - 1)], v3 = gr[min(k + 3 * kWave, rn - 1)];
-      if (k < rn) lds.ring[k * kSpw + j] = v0;
-      if (k + kWave < rn) lds.ring[(k + kWave) * kSpw + j] = v1;
-      if (k + 2 * kWave < rn) lds.ring[(k + 2 * kWave) * kSpw + j] = v2;
-      if (k + 3 * kWave < rn) lds.ring[(k + 3 * kWave) * kSpw + j] = v3;
-    }
-  }
-  // ---- per-lane roles
-  const uint32_t pj = lane % kSpw, pr = lane / kSpw;
-  const bool prefetcher = pr < kAhead && s0 + pj < a.n_src;
-  SrcParams pp;
-  uint64_t pbeg = 0, pend = 0;
-  bool src_on = false;
-  uint32_t psrc = 0;
-  if (prefetcher) {
-    pp = a.params[s0 + pj];
-    pbeg = a.off[s0 + pj];
-    pend = a.off[s0 + pj + 1];
-    psrc = a.shard_begin + s0 + pj;
-    src_on = a.enabled[psrc] != 0;
-  }
-  // correlated sources replay raw draws; with kSpw = 1 this is uniform across the wavefront
-  const bool corr = kSpw != 1 || (prefetcher && (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0);
-  const bool any_corr = __any(corr);
-  const bool seq_lane = lane < kSpw && s0 + lane < a.n_src;
-  Lane L;
+  const SrcParams pp = a.params[s];
+  SrcState st = a.state[s];
+  SimQueue Q{lds, pp, lane};
+  Q.rh = 0;
+  Q.rn = st.ring_n;
+  Q.qn = st.heap_n;
+  Q.tat = st.tat;
+  Q.src = a.shard_begin + s;
+  Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
+  Q.n_emit = 0;
+  Q.sched = Q.corrupted = 0;
+  Q.bytes = 0;
 #ifdef TGSIM_PROFILE
-  for (int k = 0; k < 6; ++k) L.pc[k] = 0;
-  uint64_t prof_par = 0, prof_rep = 0, prof_runs = 0;
+  for (int k = 0; k < 8; ++k) Q.pf[k] = 0;
+  uint64_t* pf = Q.pf;
 #endif
-  L.scheduled = L.corrupted = 0;
-  L.bytes = 0;
-  L.err = 0;
-  L.n_emit = 0;
-  uint64_t sbeg = 0, send = 0;
-  uint32_t nb = 0;
-  if (seq_lane) {
-    const uint32_t s = s0 + lane;
-    L.p = a.params[s];
-    L.st = a.state[s];
-    L.st.ring_head = 0;  // rings are stored compacted
-    L.src = a.shard_begin + s;
-    L.hb = lds.heap + lane;
-    L.rb = lds.ring + lane;
-    sbeg = a.off[s];
-    send = a.off[s + 1];
-    L.emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
-    nb = (uint32_t)((send - sbeg + kAhead - 1) / kAhead);
+  // ---- load the departure ring (compacted) and the sorted eligibility queue into LDS
+  {
+    const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+    const uint4* gh = a.heap + (size_t)s * kHeapCap;
+    const uint32_t rn = Q.rn, qn = Q.qn;
+    for (uint32_t k0 = 0; k0 < rn + qn; k0 += 4 * kWave) {  // four loads in flight per lane
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = k0 + u * kWave + lane;
+        if (k < rn) {
+          const uint64_t d = gr[k];
+          v[u] = make_uint4((uint32_t)d, (uint32_t)(d >> 32), 0, 0);
+        } else if (k < rn + qn) {
+          v[u] = gh[k - rn];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = k0 + u * kWave + lane;
+        if (k < rn + qn) lds.slot[k] = v[u];
+      }
+    }
   }
-  const uint32_t n_batches = wave_max(nb);
-  const uint64_t qbytes_in = seq_lane ? 16ull * L.st.heap_n + 8ull * L.st.ring_n : 0;
+  const uint64_t qbytes_in = 16ull * Q.qn + 8ull * Q.rn;
+  const uint64_t sbeg = a.off[s], send = a.off[s + 1];
+  const bool src_on = a.enabled[Q.src] != 0;
+  const bool corr = (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0;
+  const uint32_t lim = a.queue_limit;
+  uint32_t last_dup = st.last_dup, last_cor = st.last_cor, last_reo = st.last_reo;
   uint64_t c_off = 0, c_clone = 0, c_v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t perr = 0;
   wave_lds_sync();
-  if (seq_lane) {
-    L.top_e = L.st.heap_n ? (w0_of(lds.heap[lane]) & kEMask) : ~0ull;
-    L.head_d = L.st.ring_n ? lds.ring[lane] : ~0ull;
-  }
   stamp(a, lane, 1, __builtin_amdgcn_s_memrealtime());
-  // ---- batch loop
-  uint64_t idx = pbeg + pr;
+
+  const uint32_t n_batches = (uint32_t)((send - sbeg + kWave - 1) / kWave);
+  uint64_t idx = sbeg + lane;
   InRec rec = {}, rec2 = {};  // records of batches b and b + 1 (two batches in flight)
-  if (prefetcher && idx < pend) rec = a.in[idx];
-  if (prefetcher && idx + kAhead < pend) rec2 = a.in[idx + kAhead];
+  if (idx < send) rec = a.in[idx];
+  if (idx + kWave < send) rec2 = a.in[idx + kWave];
   for (uint32_t b = 0; b < n_batches; ++b) {
-#ifdef TGSIM_PROFILE
-    const uint64_t pb0 = __builtin_amdgcn_s_memtime();
-#endif
-    const uint64_t my_idx = idx;  // the record this lane stages in this batch
-    const bool staged = prefetcher && my_idx < pend;
-    uint32_t n_cand = 0;
-    if (any_corr) {
-      // ---------- correlated path: stage raw draws, replay every packet in order
-      if (staged) {
-        Pre pre;
-        const uint32_t fv = filter(a, pp, src_on, rec.dst);
-        pre.rec = make_uint4(rec.dst, rec.seq, rec.tick, (rec.len & 0xFFFFu) | (fv << 16));
-        pre.r0 = pre.r1 = pre.r2 = make_uint4(0, 0, 0, 0);
-        if (fv == kFvPass) {
-          uint32_t r[4];
-          philox(psrc, rec.dst, rec.seq, 0, a.key0, a.key1, r);
-          pre.r0 = make_uint4(r[0], r[1], r[2], r[3]);
-          if (pp.thr_dup) {
-            philox(psrc, rec.dst, rec.seq, 2, a.key0, a.key1, r);
-            pre.r2 = make_uint4(r[0], r[1], r[2], r[3]);
-          }
-          if (pp.sigma) {
-            philox(psrc, rec.dst, rec.seq, 1, a.key0, a.key1, r);
-            pre.r1.x = r[0];
-          }
-        }
-        lds.stage[lane] = pre;
-      }
-    } else {
-      // ---------- uncorrelated path: resolve everything but the queue in parallel
-      uint32_t fin = 0;  // final verdict when no queue decision is needed
-      bool cand = false;
-      Pre pre;
-      if (staged) {
-        const uint64_t T = a.t0_ns + (uint64_t)rec.tick * a.tick_ns;
-        const uint32_t fv = filter(a, pp, src_on, rec.dst);
-        if (fv != kFvPass) {
-          fin = 0xF0u | fv;
-        } else {
-          uint32_t r0[4];
-          philox(psrc, rec.dst, rec.seq, 0, a.key0, a.key1, r0);
-          const int count = 1 + (pp.thr_dup && pp.thr_dup >= r0[0]) - (pp.thr_loss && pp.thr_loss >= r0[1]);
-          if (count == 0) {
-            fin = 0xF0u | TGSIM_V_LOSS;
-          } else {
-            uint32_t cstate = 0, flc = TGSIM_FLAG_DUP;
-            uint64_t ec = ~0ull;
-            if (count == 2) {
-              uint32_t r2[4];
-              philox(psrc, rec.dst, rec.seq, 2, a.key0, a.key1, r2);
-              if (pp.thr_loss && pp.thr_loss >= r2[0]) {
-                cstate = 1;
-              } else {
-                cstate = 2;
-                if (pp.thr_cor && pp.thr_cor >= r2[1]) flc |= TGSIM_FLAG_CORRUPT;
-                ec = (pp.thr_reo && pp.thr_reo >= r2[2]) ? T : delayed(pp, T, r2[3]);
-              }
-            }
-            const uint32_t flo = (pp.thr_cor && pp.thr_cor >= r0[2]) ? TGSIM_FLAG_CORRUPT : 0u;
-            uint64_t eo;
-            if (pp.thr_reo && pp.thr_reo >= r0[3]) {
-              eo = T;
-            } else if (pp.sigma) {
-              uint32_t r1[4];
-              philox(psrc, rec.dst, rec.seq, 1, a.key0, a.key1, r1);
-              eo = delayed(pp, T, r1[0]);
-            } else {
-              eo = T + pp.lat_ns;
-            }
-            if (eo > kEMask || (cstate == 2 && ec > kEMask)) perr = 1;
-            pre.rec = make_uint4((uint32_t)T, (uint32_t)(T >> 32), (uint32_t)eo, (uint32_t)(eo >> 32));
-            pre.r0 = make_uint4((uint32_t)ec, (uint32_t)(ec >> 32), rec.dst, rec.seq);
-            pre.r2 = make_uint4((rec.len & 0xFFFFu) | (flo << 16) | (flc << 18) | (cstate << 20) | (pr << 24),
-                                0, 0, 0);
-            cand = true;
-          }
-        }
-      }
-      const uint64_t m = __ballot(cand);
-      n_cand = __popcll(m);
-      if (cand) {
-        const Pre p2 = pre;
-        const uint32_t slot = __popcll(m & ((1ull << lane) - 1));
-        lds.stage[slot].rec = p2.rec;
-        lds.stage[slot].r0 = p2.r0;
-        lds.stage[slot].r2 = p2.r2;
-      } else if (staged) {
-        lds.vst[lane] = (uint8_t)fin;
-      }
-    }
-    wave_lds_sync();
-#ifdef TGSIM_PROFILE
-    const uint64_t pb1 = __builtin_amdgcn_s_memtime();
-    prof_par += pb1 - pb0;
-#endif
-    idx += kAhead;
+    PROF_T0(b);
+    const uint64_t my_idx = idx;
+    const bool staged = my_idx < send;
+    const InRec r = rec;
+    idx += kWave;
     rec = rec2;
-    if (prefetcher && idx + kAhead < pend) rec2 = a.in[idx + kAhead];  // in flight two batches ahead
-    if (seq_lane) {
-      if (any_corr) {
-        const uint64_t first = sbeg + (uint64_t)b * kAhead;
-        const uint32_t nr = first < send ? (uint32_t)min((uint64_t)kAhead, send - first) : 0u;
-        for (uint32_t r = 0; r < nr; ++r) {
-          const Pre pre = lds.stage[r * kSpw + lane];
-          const uint64_t T = a.t0_ns + (uint64_t)pre.rec.z * a.tick_ns;
-          lds.vst[r * kSpw + lane] = (uint8_t)process_corr(L, a.queue_limit, T, pre);
-        }
-      }
-    }
-    if (!any_corr) {
-      // Uniform replay of the compacted candidates.  While the netem queue is full its state
-      // cannot change before min(next departure, next eligibility), so every candidate offered
-      // up to that instant is a QUEUE_FULL drop: the whole run is resolved with one ballot
-      // (T is non-decreasing over the candidates); the remaining candidates go through the
-      // sequential lane one by one.
-      uint64_t Tc = ~0ull;
-      uint32_t cinfo = 0;
-      if (lane < n_cand) {
-        const uint4 r = lds.stage[lane].rec;
-        Tc = ((uint64_t)r.y << 32) | r.x;
-        cinfo = lds.stage[lane].r2.x;
-      }
-      uint32_t c = 0;
-      while (c < n_cand) {
-        uint64_t thr = 0;
-        uint32_t full = 0;
-        if (lane == 0) {
-          thr = L.top_e < L.head_d ? L.top_e : L.head_d;
-          full = L.st.heap_n + L.st.ring_n >= a.queue_limit;
-        }
-        full = __builtin_amdgcn_readfirstlane(full);
-        if (full) {
-          thr = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(thr >> 32)) << 32) |
-                __builtin_amdgcn_readfirstlane((uint32_t)thr);
-          const bool drop = lane >= c && lane < n_cand && Tc <= thr;
-          const uint64_t m = __ballot(drop);
-          if (drop) {
-            const uint32_t cst = (cinfo >> 20) & 3u;
-            const uint32_t cv = cst == 0 ? TGSIM_V_NONE : (cst == 1 ? TGSIM_V_LOSS : TGSIM_V_QUEUE_FULL);
-            lds.vst[cinfo >> 24] = (uint8_t)((cv << 4) | TGSIM_V_QUEUE_FULL);
+    if (idx + kWave < send) rec2 = a.in[idx + kWave];  // in flight two batches ahead
+    const uint64_t T = a.t0_ns + (uint64_t)r.tick * a.tick_ns;
+    const uint32_t len = r.len & 0xFFFFu;
+    const uint32_t fv = staged ? filter(a, pp, src_on, r.dst) : 0u;
+    uint32_t vout = 0xF0u | fv;  // verdict byte (final for filtered packets)
+    if (!corr) {
+      // ---------- parallel phase: every decision that does not depend on queue state
+      bool cand = false, reo_o = false;
+      uint32_t cst = 0, flo = 0, flc = TGSIM_FLAG_DUP;
+      uint64_t ec = ~0ull;
+      if (staged && fv == kFvPass) {
+        uint32_t r0[4];
+        philox(Q.src, r.dst, r.seq, 0, a.key0, a.key1, r0);
+        const int count = 1 + (pp.thr_dup && pp.thr_dup >= r0[0]) - (pp.thr_loss && pp.thr_loss >= r0[1]);
+        if (count == 0) {
+          vout = 0xF0u | TGSIM_V_LOSS;
+        } else {
+          cand = true;
+          if (count == 2) {  // the clone re-enters the root qdisc with duplicate = 0
+            uint32_t r2[4];
+            philox(Q.src, r.dst, r.seq, 2, a.key0, a.key1, r2);
+            if (pp.thr_loss && pp.thr_loss >= r2[0]) {
+              cst = 1;
+            } else {
+              cst = 2;
+              if (pp.thr_cor && pp.thr_cor >= r2[1]) flc |= TGSIM_FLAG_CORRUPT;
+              ec = (pp.thr_reo && pp.thr_reo >= r2[2]) ? T : delayed(pp, T, r2[3]);
+              if (ec > kEMask) { perr = 1; ec = kEMask; }
+            }
           }
-          c += __popcll(m);
-#ifdef TGSIM_PROFILE
-          prof_runs++;
-#endif
-          if (c >= n_cand) break;
+          flo = (pp.thr_cor && pp.thr_cor >= r0[2]) ? TGSIM_FLAG_CORRUPT : 0u;
+          reo_o = pp.thr_reo && pp.thr_reo >= r0[3];
         }
-        if (lane == 0) {
-          const uint4 crec = lds.stage[c].rec, cr0 = lds.stage[c].r0, cr2 = lds.stage[c].r2;
-          const uint64_t T = ((uint64_t)crec.y << 32) | crec.x;
-          const uint64_t eo = ((uint64_t)crec.w << 32) | crec.z;
-          const uint32_t info = cr2.x, len = info & 0xFFFFu, cstate = (info >> 20) & 3u;
-          uint32_t cv = cstate == 0 ? TGSIM_V_NONE : TGSIM_V_LOSS;
-          if (cstate == 2) {
-            const uint64_t ec = ((uint64_t)cr0.y << 32) | cr0.x;
-            cv = admit(L, a.queue_limit, T, ec, cr0.z, cr0.w, len, (info >> 18) & 3u);
+      }
+      PROF_ADD(0, b);
+      PROF_T0(w);
+      // ---------- windows
+      uint64_t pend = __ballot(cand);
+      while (pend) {
+        PROF_CNT(3, 1);
+        const uint32_t w0 = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t wl = 63u - (uint32_t)__builtin_clzll(pend);
+        const uint64_t T_last = readlane64(T, wl);
+        // (1) queue-head items eligible before the last pending packet, served optimistically
+        const bool hq = lane < Q.qn;
+        const uint4 qi = hq ? Q.slot(Q.rn + lane) : make_uint4(0, 0, 0, 0);
+        const uint64_t qe = hq ? (w0_of(qi) & kEMask) : ~0ull;
+        const bool inS = qe < T_last;
+        const uint32_t nS = ballot_count(inS);
+        uint64_t T_cut = ~0ull;  // packets offered after the 65th queued item's e wait for the next window
+        if (nS == kWave && Q.qn > kWave) {
+          const uint64_t e64 = w0_of(Q.slot(Q.rn + kWave)) & kEMask;
+          if (e64 < T_last) T_cut = e64;
+        }
+        uint64_t dS = 0, tatS = 0;
+        if (nS) Q.htb_scan(inS, qe, qi.y >> 14 & 0xFFFFu, dS, tatS);
+        // (2) departures before each candidate's offer time: ring ++ newly served, sorted by d;
+        //     only the prefix with d < the window's last offer time matters
+        const bool inw = cand && ((pend >> lane) & 1ull) && T <= T_cut;
+        const uint64_t mw = __ballot(inw);
+        uint32_t D = 0;
+        if (mw) {
+          const uint64_t T_max = readlane64(T, 63u - (uint32_t)__builtin_clzll(mw));
+          for (uint32_t base = 0;; base += kWave) {
+            const uint32_t k = base + lane;
+            const uint32_t ks = k - Q.rn;  // index among the newly served items when k >= rn
+            const uint64_t dfs = shfl64(dS, (k >= Q.rn && ks < kWave) ? ks : 0u);
+            uint64_t dep = ~0ull;
+            if (k < Q.rn) dep = Q.ring_d(k);
+            else if (ks < nS) dep = dfs;
+            const uint32_t nd = ballot_count(dep < T_max);
+            for (uint32_t l = 0; l < nd; ++l) D += readlane64(dep, l) < T ? 1u : 0u;
+            if (nd < kWave) break;
           }
-          const uint32_t ov = admit(L, a.queue_limit, T, eo, cr0.z, cr0.w, len, (info >> 16) & 3u);
-          lds.vst[info >> 24] = (uint8_t)((cv << 4) | ov);
+          PROF_CNT(7, 1);
         }
-        ++c;
+        // (3) netem limit: saturating occupancy counter, prefix-composed
+        const uint32_t Dm = scan_max_u32(inw ? D : 0u);
+        const int32_t delta = (int32_t)(Dm - shr1_u32(Dm, 0u));
+        const int32_t cnt = inw ? 1 + (cst == 2) : 0;
+        const int32_t P = scan_sum_i32(cnt - delta);
+        const int32_t M = scan_max_i32(P);
+        const int32_t x0 = (int32_t)(Q.rn + Q.qn), ilim = (int32_t)lim;
+        const int32_t Pex = (int32_t)shr1_u32((uint32_t)P, 0u);
+        const int32_t Mex = (int32_t)shr1_u32((uint32_t)M, 0u);  // lane 0: 0 = identity here
+        const int32_t xb = Pex + min(x0, ilim - Mex);
+        const int32_t y = xb - delta;
+        const bool clone_adm = inw && cst == 2 && y < ilim;
+        const bool orig_adm = inw && y + (cst == 2 ? 1 : 0) < ilim;
+        // delay draw only for admitted originals
+        uint64_t eo = reo_o ? T : T + pp.lat_ns;
+        const bool need1 = orig_adm && !reo_o && pp.sigma != 0;
+        if (__ballot(need1)) {
+          if (need1) {
+            uint32_t r1[4];
+            philox(Q.src, r.dst, r.seq, 1, a.key0, a.key1, r1);
+            eo = delayed(pp, T, r1[0]);
+          }
+        }
+        if (orig_adm && eo > kEMask) { perr = 1; eo = kEMask; }
+        // (4) window end.  An admitted item i can change a later packet j's departure count only
+        //     if its own departure, or that of a queued item it is served before, precedes T_j.
+        //     Lower bound of both (HTB's TAT only grows when items are added):
+        //       beta_i = min(d of the first queued item with e >= e_i, max(e_i, TAT before it)).
+        //     The window ends before the first packet j with beta_i < T_j for an earlier i.
+        uint64_t ea = clone_adm ? ec : ~0ull;
+        if (orig_adm && eo < ea) ea = eo;
+        uint64_t beta = ~0ull;
+        for (uint64_t madm = __ballot(orig_adm || clone_adm); madm; madm &= madm - 1) {
+          const uint32_t i = (uint32_t)__builtin_ctzll(madm);
+          const uint64_t ei = readlane64(ea, i);
+          const uint32_t pe = ballot_count(inS && qe < ei);
+          const uint64_t b1 = pe < nS ? readlane64(dS, pe) : ~0ull;
+          const uint64_t tb = pe == 0 ? Q.tat : readlane64(tatS, pe - 1);
+          const uint64_t b2 = ei > tb ? ei : tb;
+          if (lane == i) beta = b1 < b2 ? b1 : b2;
+        }
+        const uint64_t Bex = shr1_u64(scan_min_u64(beta), ~0ull);
+        const uint64_t mv = __ballot(inw && Bex < T);
+        const uint32_t wend = mv ? (uint32_t)__builtin_ctzll(mv) : kWave;
+        const bool inwin = inw && lane < wend;
+        const uint64_t mwin = __ballot(inwin);
+        uint64_t T_w, e_new = ~0ull;
+        uint32_t Dw = 0, lw = 0;
+        if (mwin) {
+          lw = 63u - (uint32_t)__builtin_clzll(mwin);
+          T_w = readlane64(T, lw);
+          Dw = readlane32(D, lw);
+          e_new = readlane64(scan_min_u64(inwin ? ea : ~0ull), kWave - 1);
+        } else {
+          T_w = readlane64(T, w0);
+        }
+        // commit the optimistic HTB service of the items served before every new item and
+        // eligible before the window's last packet (the rest is served after the merge)
+        const uint64_t t_c = e_new < T_w ? e_new : T_w;
+        const bool inC = inS && qe < t_c;
+        const uint32_t nC = ballot_count(inC);
+        if (nC) Q.commit(inC, nC, qi, dS, tatS);
+        Q.rh = (Q.rh + Dw) & kSlotMask;
+        Q.rn -= Dw;
+        if (inwin) {
+          const uint32_t cv = cst == 0 ? TGSIM_V_NONE
+                            : cst == 1 ? TGSIM_V_LOSS
+                                       : (clone_adm ? TGSIM_V_SCHEDULED : TGSIM_V_QUEUE_FULL);
+          vout = (cv << 4) | (orig_adm ? TGSIM_V_SCHEDULED : TGSIM_V_QUEUE_FULL);
+        }
+        // (5) merge the admitted items into the sorted queue
+        Q.insert(inwin && orig_adm, make_item(eo, len, flo, r.seq, r.dst));
+        Q.insert(inwin && clone_adm, make_item(ec, len, flc, r.seq, r.dst));
+        if (e_new < T_w) Q.serve_until(T_w);
+        if (mwin) pend &= lw >= 63u ? 0ull : ~((1ull << (lw + 1)) - 1);
+      }
+      PROF_ADD(1, w);
+    } else {
+      // ---------- correlated draws: per-packet netem_enqueue in order, wave-wide queue ops
+      uint4 r0 = make_uint4(0, 0, 0, 0), r2 = make_uint4(0, 0, 0, 0);
+      uint32_t r1x = 0;
+      if (staged && fv == kFvPass) {
+        uint32_t t[4];
+        philox(Q.src, r.dst, r.seq, 0, a.key0, a.key1, t);
+        r0 = make_uint4(t[0], t[1], t[2], t[3]);
+        if (pp.thr_dup) {
+          philox(Q.src, r.dst, r.seq, 2, a.key0, a.key1, t);
+          r2 = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+        if (pp.sigma) {
+          philox(Q.src, r.dst, r.seq, 1, a.key0, a.key1, t);
+          r1x = t[0];
+        }
+      }
+      const uint32_t n_st = ballot_count(staged);
+      for (uint32_t j = 0; j < n_st; ++j) {
+        if (readlane32(fv, j) != kFvPass) continue;
+        const uint64_t Tj = readlane64(T, j);
+        const uint32_t dj = readlane32(r.dst, j), sj = readlane32(r.seq, j), lj = readlane32(len, j);
+        const uint4 a0 = make_uint4(readlane32(r0.x, j), readlane32(r0.y, j), readlane32(r0.z, j), readlane32(r0.w, j));
+        int count = 1;
+        if (pp.thr_dup && pp.thr_dup >= crand(a0.x, pp.rho_dup, last_dup)) ++count;
+        if (pp.thr_loss && pp.thr_loss >= a0.y) --count;
+        uint32_t vj;
+        if (count == 0) {
+          vj = 0xF0u | TGSIM_V_LOSS;
+        } else {
+          // netem_enqueue from the limit check on; reorder consumes correlated state only when
+          // the packet passes the limit
+          auto enq = [&](uint32_t reo_raw, uint32_t delay_raw, uint32_t fl) -> uint32_t {
+            Q.serve_until(Tj);
+            Q.depart_before(Tj);
+            if (Q.rn + Q.qn >= lim) return TGSIM_V_QUEUE_FULL;
+            bool reordered = false;
+            if (pp.thr_reo) reordered = !(pp.thr_reo < crand(reo_raw, pp.rho_reo, last_reo));
+            uint64_t e = reordered ? Tj : delayed(pp, Tj, delay_raw);
+            if (e > kEMask) { perr = 1; e = kEMask; }
+            Q.insert(lane == 0, make_item(e, lj, fl, sj, dj));
+            return TGSIM_V_SCHEDULED;
+          };
+          uint32_t cv = TGSIM_V_NONE;
+          if (count == 2) {
+            const uint4 a2 = make_uint4(readlane32(r2.x, j), readlane32(r2.y, j), readlane32(r2.z, j), readlane32(r2.w, j));
+            if (pp.thr_loss && pp.thr_loss >= a2.x) {
+              cv = TGSIM_V_LOSS;
+            } else {
+              uint32_t fl = TGSIM_FLAG_DUP;
+              if (pp.thr_cor && pp.thr_cor >= crand(a2.y, pp.rho_cor, last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+              cv = enq(a2.z, a2.w, fl);
+            }
+          }
+          uint32_t fl = 0;
+          if (pp.thr_cor && pp.thr_cor >= crand(a0.z, pp.rho_cor, last_cor)) fl |= TGSIM_FLAG_CORRUPT;
+          const uint32_t ov = enq(a0.w, readlane32(r1x, j), fl);
+          vj = (cv << 4) | ov;
+        }
+        if (lane == j) vout = vj;
       }
     }
-    wave_lds_sync();
-#ifdef TGSIM_PROFILE
-    prof_rep += __builtin_amdgcn_s_memtime() - pb1;
-#endif
-    if (staged) {
-      const uint32_t v = lds.vst[lane];
-      a.verdict[my_idx] = (uint8_t)v;
-    }
+    if (staged) a.verdict[my_idx] = (uint8_t)vout;
     // statistics from the verdict bytes (wave-uniform ballot counts)
-    const uint32_t v = staged ? lds.vst[lane] : 0xFFu;
-    c_off += __popcll(__ballot(staged));
-    c_clone += __popcll(__ballot(staged && (v >> 4) != TGSIM_V_NONE));
+    const uint32_t v = staged ? vout : 0xFFu;
+    c_off += ballot_count(staged);
+    c_clone += ballot_count(staged && (v >> 4) != TGSIM_V_NONE);
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k)
-      c_v[k] += __popcll(__ballot(staged && (v & 15u) == k)) + __popcll(__ballot(staged && (v >> 4) == k));
+      c_v[k] += ballot_count(staged && (v & 15u) == k) + ballot_count(staged && (v >> 4) == k);
   }
   stamp(a, lane, 2, __builtin_amdgcn_s_memrealtime());
-  if (seq_lane) {
-    htb_until(L, a.horizon_ns);
-    a.emit_n[s0 + lane] = L.n_emit;
-  }
-  wave_lds_sync();
+  Q.serve_until(a.horizon_ns);
+  if (lane == 0) a.emit_n[s] = Q.n_emit;
   stamp(a, lane, 3, __builtin_amdgcn_s_memrealtime());
-  // ---- write back state, heaps and (compacted) rings
-  for (uint32_t j = 0; j < kSpw; ++j) {
-    const uint32_t s = s0 + j;
-    if (s >= a.n_src) break;
-    const uint32_t hn = __shfl(L.st.heap_n, j, 64);
-    const uint32_t rn = __shfl(L.st.ring_n, j, 64);
-    const uint32_t rh = __shfl(L.st.ring_head, j, 64);
-    for (uint32_t k = lane; k < hn; k += kWave) a.heap[(size_t)s * kHeapCap + k] = lds.heap[k * kSpw + j];
-    for (uint32_t k = lane; k < rn; k += kWave)
-      a.ring[(size_t)s * kHeapCap + k] = lds.ring[((rh + k) & (kHeapCap - 1)) * kSpw + j];
+  // ---- write back the compacted ring, the sorted queue and the state
+  {
+    uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+    uint4* gh = a.heap + (size_t)s * kHeapCap;
+    for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
+    for (uint32_t k = lane; k < Q.qn; k += kWave) gh[k] = Q.slot(Q.rn + k);
   }
-  if (seq_lane) {
-    L.st.ring_head = 0;
-    a.state[s0 + lane] = L.st;
+  if (lane == 0) {
+    st.tat = Q.tat;
+    st.heap_n = Q.qn;
+    st.ring_n = Q.rn;
+    st.ring_head = 0;
+    st.last_dup = last_dup;
+    st.last_cor = last_cor;
+    st.last_reo = last_reo;
+    a.state[s] = st;
   }
   stamp(a, lane, 4, __builtin_amdgcn_s_memrealtime());
-  stamp(a, lane, 5, ((uint64_t)s0 << 32) | n_batches);
+  stamp(a, lane, 5, ((uint64_t)s << 32) | n_batches);
   stamp(a, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
-  stamp(a, lane, 7, seq_lane ? ((uint64_t)L.st.heap_n << 32 | L.st.ring_n) : 0);
+  stamp(a, lane, 7, ((uint64_t)Q.qn << 32) | Q.rn);
 #ifdef TGSIM_PROFILE
-  for (int k = 0; k < 6; ++k) stamp(a, lane, 8 + k, L.pc[k]);
-  stamp(a, lane, 14, prof_par);
-  stamp(a, lane, 15, (prof_rep << 20) | (prof_runs & 0xFFFFF));
+  for (int k = 0; k < 8; ++k) stamp(a, lane, 8 + k, Q.pf[k]);
 #endif
-  const uint64_t sched = wave_sum(seq_lane ? L.scheduled : 0u);
-  const uint64_t corrupted = wave_sum(seq_lane ? L.corrupted : 0u);
-  const uint64_t bytes = wave_sum(seq_lane ? L.bytes : 0ull);
-  const uint64_t qbytes = wave_sum(seq_lane ? qbytes_in + 16ull * L.st.heap_n + 8ull * L.st.ring_n : 0ull);
-  const uint64_t err = wave_sum((seq_lane && L.err) || perr ? 1u : 0u);
+  const uint64_t sched = wave_sum(Q.sched);
+  const uint64_t corrupted = wave_sum(Q.corrupted);
+  const uint64_t bytes = wave_sum(Q.bytes);
+  const uint64_t qbytes = qbytes_in + 16ull * Q.qn + 8ull * Q.rn;
+  const uint64_t err = wave_sum(perr ? 1u : 0u);
   if (lane == 0) {
     atomicAdd(&a.stats[kStOffered], (unsigned long long)c_off);
     if (sched) atomicAdd(&a.stats[kStScheduled], (unsigned long long)sched);
