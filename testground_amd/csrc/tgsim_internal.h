@@ -92,7 +92,7 @@ struct SimArgs {
   const uint32_t* order;    // k_sim dispatch order (workgroup -> source), or null for identity
   uint64_t* stamps;         // diagnostics: kStampSlots s_memrealtime stamps per workgroup, or null
 };
-constexpr uint32_t kStampSlots = 16;  // 8 phase stamps + 8 profile counters (TGSIM_PROFILE)
+constexpr uint32_t kStampSlots = 24;  // 8 phase stamps + 16 profile counters (TGSIM_PROFILE)
 
 // Gossip workload state (C4) of one shard.
 struct GossipArgs {

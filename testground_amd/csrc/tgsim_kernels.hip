@@ -22,8 +22,10 @@ __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, ui
                                        uint32_t k0, uint32_t k1, uint32_t r[4]) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const uint32_t h0 = __umulhi(0xD2511F53u, c0), l0 = 0xD2511F53u * c0;
-    const uint32_t h1 = __umulhi(0xCD9E8D57u, c2), l1 = 0xCD9E8D57u * c2;
+    // one v_mad_u64_u32 per product instead of a v_mul_hi_u32 + v_mul_lo_u32 pair
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
     const uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
     c0 = n0; c1 = l1; c2 = n2; c3 = l0;
     k0 += 0x9E3779B9u;
@@ -247,7 +249,7 @@ struct SimQueue {
   uint32_t sched, corrupted;
   uint64_t bytes;
 #ifdef TGSIM_PROFILE
-  uint64_t pf[8];
+  uint64_t pf[16];
 #endif
 
   __device__ __forceinline__ uint4& slot(uint32_t k) { return lds.slot[(rh + k) & kSlotMask]; }
@@ -316,58 +318,105 @@ struct SimQueue {
     }
   }
 
-  // Merges the lanes' new items (has) into the sorted eligibility queue.
+  // Merges the lanes' new items (has) into the sorted eligibility queue: each item's position
+  // among the queued items (lower bound of its key), its rank among the new items, then the
+  // queued items from the first position on move up by the number of new items before them.
   __device__ void insert(bool has, const uint4& it) {
     const uint64_t m = __ballot(has);
     if (!m) return;
     PROF_T0(i);
     const uint32_t nm = (uint32_t)__popcll(m);
-    // position among the queued items: lower bound of the item's key
-    uint32_t pos = 0;
-    if (has && qn) {
-      if (item_lt(slot(rn + qn - 1), it)) {
-        pos = qn;
-      } else {
-        uint32_t lo = 0, hi = qn - 1;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (item_lt(slot(rn + mid), it)) lo = mid + 1;
-          else hi = mid;
+    uint32_t pos = 0, minpos = 0;
+    if (nm <= 8) {
+      if (qn) {
+        // two-level search, one item at a time: a sample every 16th queued key (one read per
+        // lane), then the 15 keys between the two samples that bracket the item
+        const uint4 last = slot(rn + qn - 1);
+        const bool hs = 16 * lane < qn;
+        const uint4 smp = hs ? slot(rn + 16 * lane) : make_uint4(0, 0, 0, 0);
+        minpos = qn;
+        for (uint64_t mm = m; mm; mm &= mm - 1) {
+          const uint32_t b = (uint32_t)__builtin_ctzll(mm);
+          const uint4 k = make_uint4(readlane32(it.x, b), readlane32(it.y, b), readlane32(it.z, b), 0u);
+          uint32_t p = qn;  // appended: the common case (e grows with the offer time)
+          if (!item_lt(last, k)) {
+            const uint32_t c = ballot_count(hs && item_lt(smp, k));
+            p = 0;
+            if (c) {
+              const uint32_t base = 16 * (c - 1);
+              const bool hb = lane >= 1 && lane < 16 && base + lane < qn;
+              const uint4 blk = hb ? slot(rn + base + lane) : make_uint4(0, 0, 0, 0);
+              p = base + 1 + ballot_count(hb && item_lt(blk, k));
+            }
+          }
+          if (lane == b) pos = p;
+          minpos = min(minpos, p);
         }
-        pos = lo;
+      }
+    } else {
+      if (has && qn) {
+        if (item_lt(slot(rn + qn - 1), it)) {
+          pos = qn;
+        } else {
+          uint32_t lo = 0, hi = qn - 1;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (item_lt(slot(rn + mid), it)) lo = mid + 1;
+            else hi = mid;
+          }
+          pos = lo;
+        }
       }
     }
     // rank among the new items (equal keys: lane order)
     uint32_t rank = 0;
     if (nm > 1) {
-      uint64_t mm = m;
-      while (mm) {
+      for (uint64_t mm = m; mm; mm &= mm - 1) {
         const uint32_t b = (uint32_t)__builtin_ctzll(mm);
-        mm &= mm - 1;
         const uint4 o = make_uint4(readlane32(it.x, b), readlane32(it.y, b), readlane32(it.z, b), 0u);
         rank += (has && (item_lt(o, it) || (!item_lt(it, o) && b < lane))) ? 1u : 0u;
       }
     }
-    if (has) lds.pos[rank] = pos;
-    wave_lds_sync();
-    const uint32_t sp = lane < nm ? lds.pos[lane] : 0xFFFFFFFFu;  // ascending
-    const uint32_t minpos = readlane32(sp, 0);
-    // queued items at index r >= minpos move up by the number of new items placed before them;
-    // chunks from the tail down, so no chunk reads a slot an earlier chunk wrote
-    for (int32_t hi = (int32_t)qn; hi > (int32_t)minpos; hi -= (int32_t)kWave) {
-      const int32_t r = hi - (int32_t)kWave + (int32_t)lane;
-      const bool mv = r >= (int32_t)minpos;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (mv) v = slot(rn + (uint32_t)r);
-      uint32_t sh = 0;
-      if (nm <= 8) {
-        for (uint32_t k = 0; k < nm; ++k) sh += readlane32(sp, k) <= (uint32_t)r ? 1u : 0u;
-      } else {
-        sh = count_le_sorted_u32(sp, mv ? (uint32_t)r : 0u);
+    if (nm <= 8) {
+      // queued item r >= minpos moves up by #{new items with pos <= r}; passes of four chunks from
+      // the tail down, all reads of a pass before its writes (no pass reads a slot a previous
+      // pass wrote; within a pass the LDS executes this wave's operations in order)
+      for (int32_t hi = (int32_t)qn; hi > (int32_t)minpos; hi -= 4 * (int32_t)kWave) {
+        uint4 v[4];
+        int32_t r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          r[u] = hi - (u + 1) * (int32_t)kWave + (int32_t)lane;
+          v[u] = r[u] >= (int32_t)minpos ? slot(rn + (uint32_t)r[u]) : make_uint4(0, 0, 0, 0);
+        }
+        uint32_t sh[4] = {0, 0, 0, 0};
+        for (uint64_t mm = m; mm; mm &= mm - 1) {
+          const int32_t pb = (int32_t)readlane32(pos, (uint32_t)__builtin_ctzll(mm));
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sh[u] += pb <= r[u] ? 1u : 0u;
+        }
+        __asm__ volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (r[u] >= (int32_t)minpos) slot(rn + (uint32_t)r[u] + sh[u]) = v[u];
+        PROF_CNT(6, 1);
       }
-      if (mv) slot(rn + (uint32_t)r + sh) = v;
-      PROF_CNT(6, 1);
+    } else {
+      if (has) lds.pos[rank] = pos;
+      wave_lds_sync();
+      const uint32_t sp = lane < nm ? lds.pos[lane] : 0xFFFFFFFFu;  // ascending
+      const uint32_t mp = readlane32(sp, 0);
+      for (int32_t hi = (int32_t)qn; hi > (int32_t)mp; hi -= (int32_t)kWave) {
+        const int32_t r = hi - (int32_t)kWave + (int32_t)lane;
+        const bool mv = r >= (int32_t)mp;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (mv) v = slot(rn + (uint32_t)r);
+        const uint32_t sh = count_le_sorted_u32(sp, mv ? (uint32_t)r : 0u);
+        if (mv) slot(rn + (uint32_t)r + sh) = v;
+        PROF_CNT(6, 1);
+      }
     }
+    __asm__ volatile("" ::: "memory");
     if (has) slot(rn + pos + rank) = it;
     qn += nm;
     wave_lds_sync();
@@ -401,7 +450,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   Q.sched = Q.corrupted = 0;
   Q.bytes = 0;
 #ifdef TGSIM_PROFILE
-  for (int k = 0; k < 8; ++k) Q.pf[k] = 0;
+  for (int k = 0; k < 16; ++k) Q.pf[k] = 0;
   uint64_t* pf = Q.pf;
 #endif
   // ---- load the departure ring (compacted) and the sorted eligibility queue into LDS
@@ -409,23 +458,21 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     const uint4* gh = a.heap + (size_t)s * kHeapCap;
     const uint32_t rn = Q.rn, qn = Q.qn;
-    for (uint32_t k0 = 0; k0 < rn + qn; k0 += 4 * kWave) {  // four loads in flight per lane
-      uint4 v[4];
+    // every load of the ring and the queue in flight before the first LDS write (one HBM
+    // latency instead of one per 256 slots)
+    uint64_t rv[kHeapCap / kWave];
+    uint4 qv[kHeapCap / kWave];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t k = k0 + u * kWave + lane;
-        if (k < rn) {
-          const uint64_t d = gr[k];
-          v[u] = make_uint4((uint32_t)d, (uint32_t)(d >> 32), 0, 0);
-        } else if (k < rn + qn) {
-          v[u] = gh[k - rn];
-        }
-      }
+    for (uint32_t u = 0; u < kHeapCap / kWave; ++u) {
+      const uint32_t k = u * kWave + lane;
+      rv[u] = k < rn ? gr[k] : 0ull;
+      qv[u] = k < qn ? gh[k] : make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t k = k0 + u * kWave + lane;
-        if (k < rn + qn) lds.slot[k] = v[u];
-      }
+    for (uint32_t u = 0; u < kHeapCap / kWave; ++u) {
+      const uint32_t k = u * kWave + lane;
+      if (k < rn) *reinterpret_cast<uint2*>(&lds.slot[k]) = make_uint2((uint32_t)rv[u], (uint32_t)(rv[u] >> 32));
+      if (k < qn) lds.slot[(rn + k) & kSlotMask] = qv[u];
     }
   }
   const uint64_t qbytes_in = 16ull * Q.qn + 8ull * Q.rn;
@@ -491,9 +538,27 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       uint64_t pend = __ballot(cand);
       while (pend) {
         PROF_CNT(3, 1);
+        if (Q.rn + Q.qn >= lim) {
+          // full queue: nothing changes before the next eligibility or departure time, so every
+          // packet offered up to then is a QUEUE_FULL drop
+          const uint64_t qh = Q.qn ? (w0_of(Q.slot(Q.rn)) & kEMask) : ~0ull;
+          const uint64_t dh = Q.rn ? Q.ring_d(0) : ~0ull;
+          const uint64_t t_ev = qh < dh ? qh : dh;
+          const uint64_t mf = __ballot(((pend >> lane) & 1ull) && T <= t_ev);
+          if (mf) {
+            if ((mf >> lane) & 1ull) {
+              const uint32_t cv = cst == 0 ? TGSIM_V_NONE : cst == 1 ? TGSIM_V_LOSS : TGSIM_V_QUEUE_FULL;
+              vout = (cv << 4) | TGSIM_V_QUEUE_FULL;
+            }
+            pend &= ~mf;
+            PROF_CNT(2, 1);
+            continue;
+          }
+        }
         const uint32_t w0 = (uint32_t)__builtin_ctzll(pend);
         const uint32_t wl = 63u - (uint32_t)__builtin_clzll(pend);
         const uint64_t T_last = readlane64(T, wl);
+        PROF_T0(s1);
         // (1) queue-head items eligible before the last pending packet, served optimistically
         const bool hq = lane < Q.qn;
         const uint4 qi = hq ? Q.slot(Q.rn + lane) : make_uint4(0, 0, 0, 0);
@@ -507,13 +572,16 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         }
         uint64_t dS = 0, tatS = 0;
         if (nS) Q.htb_scan(inS, qe, qi.y >> 14 & 0xFFFFu, dS, tatS);
+        PROF_ADD(7, s1);
+        PROF_T0(s2);
         // (2) departures before each candidate's offer time: ring ++ newly served, sorted by d;
         //     only the prefix with d < the window's last offer time matters
         const bool inw = cand && ((pend >> lane) & 1ull) && T <= T_cut;
         const uint64_t mw = __ballot(inw);
         uint32_t D = 0;
+        const uint64_t T_mx = mw ? readlane64(T, 63u - (uint32_t)__builtin_clzll(mw)) : 0ull;
         if (mw) {
-          const uint64_t T_max = readlane64(T, 63u - (uint32_t)__builtin_clzll(mw));
+          const uint64_t T_max = T_mx;
           for (uint32_t base = 0;; base += kWave) {
             const uint32_t k = base + lane;
             const uint32_t ks = k - Q.rn;  // index among the newly served items when k >= rn
@@ -525,8 +593,9 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
             for (uint32_t l = 0; l < nd; ++l) D += readlane64(dep, l) < T ? 1u : 0u;
             if (nd < kWave) break;
           }
-          PROF_CNT(7, 1);
         }
+        PROF_ADD(8, s2);
+        PROF_T0(s3);
         // (3) netem limit: saturating occupancy counter, prefix-composed
         const uint32_t Dm = scan_max_u32(inw ? D : 0u);
         const int32_t delta = (int32_t)(Dm - shr1_u32(Dm, 0u));
@@ -551,6 +620,8 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
           }
         }
         if (orig_adm && eo > kEMask) { perr = 1; eo = kEMask; }
+        PROF_ADD(9, s3);
+        PROF_T0(s4);
         // (4) window end.  An admitted item i can change a later packet j's departure count only
         //     if its own departure, or that of a queued item it is served before, precedes T_j.
         //     Lower bound of both (HTB's TAT only grows when items are added):
@@ -558,31 +629,38 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         //     The window ends before the first packet j with beta_i < T_j for an earlier i.
         uint64_t ea = clone_adm ? ec : ~0ull;
         if (orig_adm && eo < ea) ea = eo;
-        uint64_t beta = ~0ull;
-        for (uint64_t madm = __ballot(orig_adm || clone_adm); madm; madm &= madm - 1) {
-          const uint32_t i = (uint32_t)__builtin_ctzll(madm);
-          const uint64_t ei = readlane64(ea, i);
-          const uint32_t pe = ballot_count(inS && qe < ei);
-          const uint64_t b1 = pe < nS ? readlane64(dS, pe) : ~0ull;
-          const uint64_t tb = pe == 0 ? Q.tat : readlane64(tatS, pe - 1);
-          const uint64_t b2 = ei > tb ? ei : tb;
-          if (lane == i) beta = b1 < b2 ? b1 : b2;
+        // only items eligible before the last packet of the window can end it (beta_i >= e_i)
+        const uint64_t madm = __ballot((orig_adm || clone_adm) && ea < T_mx);
+        uint32_t wend = kWave;
+        if (madm) {
+          uint64_t beta = ~0ull;
+          for (uint64_t mm = madm; mm; mm &= mm - 1) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(mm);
+            const uint64_t ei = readlane64(ea, i);
+            const uint32_t pe = ballot_count(inS && qe < ei);
+            const uint64_t b1 = pe < nS ? readlane64(dS, pe) : ~0ull;
+            const uint64_t tb = pe == 0 ? Q.tat : readlane64(tatS, pe - 1);
+            const uint64_t b2 = ei > tb ? ei : tb;
+            if (lane == i) beta = b1 < b2 ? b1 : b2;
+          }
+          const uint64_t Bex = shr1_u64(scan_min_u64(beta), ~0ull);
+          const uint64_t mv = __ballot(inw && Bex < T);
+          if (mv) wend = (uint32_t)__builtin_ctzll(mv);
         }
-        const uint64_t Bex = shr1_u64(scan_min_u64(beta), ~0ull);
-        const uint64_t mv = __ballot(inw && Bex < T);
-        const uint32_t wend = mv ? (uint32_t)__builtin_ctzll(mv) : kWave;
         const bool inwin = inw && lane < wend;
         const uint64_t mwin = __ballot(inwin);
-        uint64_t T_w, e_new = ~0ull;
+        uint64_t T_w, e_new = ~0ull;  // e_new: earliest new item (>= T_w unless madm)
         uint32_t Dw = 0, lw = 0;
         if (mwin) {
           lw = 63u - (uint32_t)__builtin_clzll(mwin);
           T_w = readlane64(T, lw);
           Dw = readlane32(D, lw);
-          e_new = readlane64(scan_min_u64(inwin ? ea : ~0ull), kWave - 1);
+          if (madm) e_new = readlane64(scan_min_u64(inwin ? ea : ~0ull), kWave - 1);
         } else {
           T_w = readlane64(T, w0);
         }
+        PROF_ADD(10, s4);
+        PROF_T0(s5);
         // commit the optimistic HTB service of the items served before every new item and
         // eligible before the window's last packet (the rest is served after the merge)
         const uint64_t t_c = e_new < T_w ? e_new : T_w;
@@ -591,6 +669,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         if (nC) Q.commit(inC, nC, qi, dS, tatS);
         Q.rh = (Q.rh + Dw) & kSlotMask;
         Q.rn -= Dw;
+        PROF_ADD(11, s5);
         if (inwin) {
           const uint32_t cv = cst == 0 ? TGSIM_V_NONE
                             : cst == 1 ? TGSIM_V_LOSS
@@ -600,7 +679,11 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         // (5) merge the admitted items into the sorted queue
         Q.insert(inwin && orig_adm, make_item(eo, len, flo, r.seq, r.dst));
         Q.insert(inwin && clone_adm, make_item(ec, len, flc, r.seq, r.dst));
-        if (e_new < T_w) Q.serve_until(T_w);
+        if (e_new < T_w) {
+          PROF_T0(s6);
+          Q.serve_until(T_w);
+          PROF_ADD(12, s6);
+        }
         if (mwin) pend &= lw >= 63u ? 0ull : ~((1ull << (lw + 1)) - 1);
       }
       PROF_ADD(1, w);
@@ -676,7 +759,9 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       c_v[k] += ballot_count(staged && (v & 15u) == k) + ballot_count(staged && (v >> 4) == k);
   }
   stamp(a, lane, 2, __builtin_amdgcn_s_memrealtime());
+  PROF_T0(e);
   Q.serve_until(a.horizon_ns);
+  PROF_ADD(13, e);
   if (lane == 0) a.emit_n[s] = Q.n_emit;
   stamp(a, lane, 3, __builtin_amdgcn_s_memrealtime());
   // ---- write back the compacted ring, the sorted queue and the state
@@ -701,7 +786,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   stamp(a, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
   stamp(a, lane, 7, ((uint64_t)Q.qn << 32) | Q.rn);
 #ifdef TGSIM_PROFILE
-  for (int k = 0; k < 8; ++k) stamp(a, lane, 8 + k, Q.pf[k]);
+  for (int k = 0; k < 16; ++k) stamp(a, lane, 8 + k, Q.pf[k]);
 #endif
   const uint64_t sched = wave_sum(Q.sched);
   const uint64_t corrupted = wave_sum(Q.corrupted);
