@@ -197,7 +197,10 @@ struct tgsim_engine_s {
   std::string err;
   int dev = 0;
   hipStream_t st = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+  std::vector<hipEvent_t> ev_pool;
+  uint64_t* h_err = nullptr;  // pinned copy of the sticky device error word, refreshed every step
   uint32_t S = 0, N = 0;
   uint64_t now_tick = 0;
   uint32_t key0 = 0, key1 = 0;
@@ -244,8 +247,8 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_emit_n;
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts and their scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
-  DevBuf<uint64_t> d_dcnt, d_doff, d_dcur, d_dblk, d_dtot;
-  DevBuf<uint8_t> d_sortkeys;
+  DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
+  uint64_t h_dtot = 0;
   DevBuf<tgsim_delivery> d_drain;
   uint64_t drain_head = 0, drain_n = 0;
   DevBuf<unsigned long long> d_stats;
@@ -404,19 +407,66 @@ int stage_host_input(Eng* E, uint32_t n_ticks) {
 
 // Device exclusive scan of cnt[0..n) into off[0..n] (off[n] = total); returns total on host.
 int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uint64_t>& blk,
-                DevBuf<uint64_t>& tot, uint64_t n, uint64_t* total) {
+                DevBuf<uint64_t>& tot, uint64_t n, uint64_t* total, uint64_t* pos = nullptr) {
   HIPCHK(off.ensure(n + 1));
   HIPCHK(blk.ensure((n + 1023) / 1024 + 1));
   HIPCHK(tot.ensure(1));
-  launch_scan(cnt.p, off.p, n, blk.p, tot.p, E->st);
+  launch_scan(cnt.p, off.p, n, blk.p, tot.p, E->st, pos);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(off.p + n, tot.p, sizeof(uint64_t), hipMemcpyDeviceToDevice, E->st));
   HIPCHK(hipMemcpyAsync(total, tot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
   HIPCHK(hipStreamSynchronize(E->st));
   return 0;
 }
 
-int run_sim(Eng* E, uint32_t n_ticks) {
+hipError_t take_event(Eng* E, hipEvent_t* ev) {
+  if (!E->ev_pool.empty()) {
+    *ev = E->ev_pool.back();
+    E->ev_pool.pop_back();
+    return hipSuccess;
+  }
+  return hipEventCreate(ev);
+}
+
+// Folds finished k_sim event pairs into the running average (wait: block until all are done).
+int harvest_timing(Eng* E, bool wait) {
+  size_t k = 0;
+  for (; k < E->ev_pending.size(); ++k) {
+    auto& pr = E->ev_pending[k];
+    if (wait) {
+      HIPCHK(hipEventSynchronize(pr.second));
+    } else if (hipEventQuery(pr.second) != hipSuccess) {
+      break;
+    }
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+    E->sim_ms += ms;
+    E->sim_launches++;
+    E->ev_pool.push_back(pr.first);
+    E->ev_pool.push_back(pr.second);
+  }
+  E->ev_pending.erase(E->ev_pending.begin(), E->ev_pending.begin() + k);
+  return 0;
+}
+
+// The sticky error word of k_sim (simulated time past 2^46 ns), as last copied to pinned memory:
+// exact after a stream synchronization, possibly one step late otherwise.
+int check_sim_error(Eng* E) {
+  if (E->h_err && (__atomic_load_n(E->h_err, __ATOMIC_RELAXED) & kErrTimeOverflow))
+    return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
+  return 0;
+}
+
+// Every reader of device results goes through here: the step itself does not synchronize.
+int sync_stream(Eng* E) {
+  HIPCHK(hipStreamSynchronize(E->st));
+  return harvest_timing(E, true);
+}
+
+int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
+  int erc = check_sim_error(E);
+  if (erc) return erc;
+  erc = harvest_timing(E, false);
+  if (erc) return erc;
   if (!E->gen_q.empty()) {
     if (!E->staged.empty()) return E->fail(-EBUSY, "host packets and generated traffic in one step");
     Eng::GenWindow& w = E->gen_q.front();
@@ -471,10 +521,23 @@ int run_sim(Eng* E, uint32_t n_ticks) {
     a.stamps = E->d_stamps.p;
     E->n_stamp_wg = n_wg;
   }
-  HIPCHK(hipEventRecord(E->ev0, E->st));
+  a.dst_cnt = nullptr;
+  if (local_hist) {
+    if (E->d_dcnt.cap < E->N) {
+      HIPCHK(E->d_dcnt.ensure(E->N));
+      HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, E->st));
+    }
+    a.dst_cnt = reinterpret_cast<unsigned long long*>(E->d_dcnt.p);
+  }
+  hipEvent_t ev0, ev1;
+  HIPCHK(take_event(E, &ev0));
+  HIPCHK(take_event(E, &ev1));
+  HIPCHK(hipEventRecord(ev0, E->st));
   launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(E->ev1, E->st));
+  HIPCHK(hipEventRecord(ev1, E->st));
+  E->ev_pending.emplace_back(ev0, ev1);
+  HIPCHK(hipMemcpyAsync(E->h_err, E->d_stats.p + kStErr, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
   if (kSpw == 1) {  // heavy-first dispatch order for the next step
     HIPCHK(E->d_order.ensure(E->S));
     launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
@@ -489,15 +552,9 @@ int run_sim(Eng* E, uint32_t n_ticks) {
 }
 
 int finish_sim_timing(Eng* E) {
-  HIPCHK(hipEventSynchronize(E->ev1));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, E->ev0, E->ev1));
-  E->sim_ms += ms;
-  E->sim_launches++;
-  unsigned long long errw = 0;
-  HIPCHK(hipMemcpy(&errw, E->d_stats.p + kStErr, sizeof errw, hipMemcpyDeviceToHost));
-  if (errw & kErrTimeOverflow) return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
-  return 0;
+  int rc = sync_stream(E);
+  if (rc) return rc;
+  return check_sim_error(E);
 }
 
 int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap,
@@ -522,7 +579,6 @@ int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out,
   HIPCHK(hipGetLastError());
   launch_scan(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, E->st);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(E->d_rpos.p + m, E->d_rtot.p, sizeof(uint64_t), hipMemcpyDeviceToDevice, E->st));
   // per-rank totals: pos[r * S] .. pos[(r + 1) * S]
   std::vector<uint64_t> edges(n_ranks + 1);
   for (uint32_t r = 0; r <= n_ranks; ++r)
@@ -557,48 +613,90 @@ GossipArgs gossip_args(Eng* E, uint64_t win0, uint32_t n_ticks) {
   return g;
 }
 
+// Output of a delivery sort of n records: the drain buffer (grown, undrained tail compacted to the
+// front) or, with TGSIM_OPT_DISCARD_DELIVERIES, a scratch buffer.
+int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out) {
+  if (E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) {
+    HIPCHK(E->d_sorted.ensure(n ? n : 1));
+    *out = E->d_sorted.p;
+    return 0;
+  }
+  const uint64_t need = E->drain_head + E->drain_n + n;
+  if (need > E->d_drain.cap) {
+    DevBuf<tgsim_delivery> nb;
+    HIPCHK(nb.ensure(E->drain_n + n));
+    if (E->drain_n)
+      HIPCHK(hipMemcpyAsync(nb.p, E->d_drain.p + E->drain_head, sizeof(tgsim_delivery) * E->drain_n,
+                            hipMemcpyDeviceToDevice, E->st));
+    HIPCHK(hipStreamSynchronize(E->st));
+    E->d_drain.release();
+    E->d_drain = nb;
+    E->drain_head = 0;
+  }
+  *out = E->d_drain.p + E->drain_head + E->drain_n;
+  E->drain_n += n;
+  return 0;
+}
+
+// Records received by this shard (tgsim_deliver, or the routed records of tgsim_step on a
+// partial shard): histogram -> scan -> scatter -> per-destination order.
 int deliver(Eng* E, const tgsim_delivery* in, uint64_t n) {
   const uint32_t nd = E->S;  // destinations owned by this shard
-  HIPCHK(E->d_dcnt.ensure(nd));
-  HIPCHK(E->d_dcur.ensure(nd));
-  HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * nd, E->st));
-  HIPCHK(hipMemsetAsync(E->d_dcur.p, 0, sizeof(uint64_t) * nd, E->st));
+  if (E->d_dcnt.cap < nd) {
+    HIPCHK(E->d_dcnt.ensure(nd));
+    HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, E->st));
+  }
+  HIPCHK(E->d_dpos.ensure(nd));
   launch_dst_hist(in, n, E->o.shard_begin, E->d_dcnt.p, E->st);
   HIPCHK(hipGetLastError());
   uint64_t total = 0;
-  int rc = scan_counts(E, E->d_dcnt, E->d_doff, E->d_dblk, E->d_dtot, nd, &total);
+  int rc = scan_counts(E, E->d_dcnt, E->d_doff, E->d_dblk, E->d_dtot, nd, &total, E->d_dpos.p);
   if (rc) return rc;
   if (total != n) return E->fail(-EINVAL, "deliver: %llu of %llu records address other shards",
                                  static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  HIPCHK(E->d_sortkeys.ensure((2 * n + 1) * sort_key_bytes()));
-  launch_dst_scatter(in, n, E->o.shard_begin, E->d_doff.p, E->d_dcur.p, E->d_scatter.p, E->st);
+  launch_dst_scatter(in, n, E->o.shard_begin, E->d_dpos.p, E->d_scatter.p, E->st);
   HIPCHK(hipGetLastError());
-  tgsim_delivery* dst;
-  if (E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) {
-    HIPCHK(E->d_sorted.ensure(n ? n : 1));
-    dst = E->d_sorted.p;
-  } else {
-    const uint64_t need = E->drain_head + E->drain_n + n;
-    if (need > E->d_drain.cap) {
-      // grow, compacting the undrained tail to the front
-      DevBuf<tgsim_delivery> nb;
-      HIPCHK(nb.ensure(E->drain_n + n));
-      if (E->drain_n)
-        HIPCHK(hipMemcpyAsync(nb.p, E->d_drain.p + E->drain_head, sizeof(tgsim_delivery) * E->drain_n,
-                              hipMemcpyDeviceToDevice, E->st));
-      HIPCHK(hipStreamSynchronize(E->st));
-      E->d_drain.release();
-      E->d_drain = nb;
-      E->drain_head = 0;
-    }
-    dst = E->d_drain.p + E->drain_head + E->drain_n;
-    E->drain_n += n;
-  }
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->d_sortkeys.p, E->st);
+  tgsim_delivery* dst = nullptr;
+  rc = delivery_out(E, n, &dst);
+  if (rc) return rc;
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->st);
   HIPCHK(hipGetLastError());
   if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
     launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, E->st);
+    HIPCHK(hipGetLastError());
+  }
+  return 0;
+}
+
+// Single shard: k_sim counted every emitted record per destination, so the step needs no host
+// round trip: scan -> scatter straight from the emit regions -> per-destination order.  Only the
+// drain bookkeeping (and the gossip receipts) need the record count on the host.
+int deliver_local(Eng* E) {
+  const uint32_t nd = E->N;
+  HIPCHK(E->d_doff.ensure(nd + 1));
+  HIPCHK(E->d_dpos.ensure(nd));
+  HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
+  HIPCHK(E->d_dtot.ensure(1));
+  launch_scan(E->d_dcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, E->st, E->d_dpos.p);
+  HIPCHK(hipGetLastError());
+  const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) || E->gossip_on;
+  uint64_t n = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;  // upper bound
+  if (need_n) {
+    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
+    HIPCHK(hipStreamSynchronize(E->st));
+    n = E->h_dtot;
+  }
+  HIPCHK(E->d_scatter.ensure(n ? n : 1));
+  launch_local_scatter(E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, 0, E->d_dpos.p, E->d_scatter.p, E->st);
+  HIPCHK(hipGetLastError());
+  tgsim_delivery* dst = nullptr;
+  int rc = delivery_out(E, n, &dst);
+  if (rc) return rc;
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->st);
+  HIPCHK(hipGetLastError());
+  if (E->gossip_on) {
+    launch_gossip(gossip_args(E, 0, 0), E->d_scatter.p, n, nullptr, nullptr, nullptr, 0, E->st);
     HIPCHK(hipGetLastError());
   }
   return 0;
@@ -651,8 +749,8 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   };
   if ((rc = E->hip(hipSetDevice(E->dev), "hipSetDevice"))) return bail(rc);
   if ((rc = E->hip(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking), "stream"))) return bail(rc);
-  if ((rc = E->hip(hipEventCreate(&E->ev0), "event"))) return bail(rc);
-  if ((rc = E->hip(hipEventCreate(&E->ev1), "event"))) return bail(rc);
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_err), sizeof(uint64_t)), "pinned"))) return bail(rc);
+  *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
   E->ip.resize(E->N);
@@ -695,12 +793,16 @@ void tgsim_destroy(void* e) {
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
-  E->d_doff.release(); E->d_dcur.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_sortkeys.release(); E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
+  E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
+  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
-  if (E->ev0) (void)hipEventDestroy(E->ev0);
-  if (E->ev1) (void)hipEventDestroy(E->ev1);
+  for (auto& pr : E->ev_pending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
+  if (E->h_err) (void)hipHostFree(E->h_err);
   if (E->st) (void)hipStreamDestroy(E->st);
   delete E;
 }
@@ -939,6 +1041,8 @@ int64_t tgsim_gossip_reached(void* e, uint64_t* out, size_t cap) {
   Eng* E = as_eng(e);
   if (!E || !E->gossip_on || (!out && cap)) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
   std::vector<uint64_t> fwd(E->S);
   HIPCHK(hipMemcpy(fwd.data(), E->d_gfwd.p, sizeof(uint64_t) * E->S, hipMemcpyDeviceToHost));
   for (uint32_t f = 0; f < E->gossip.n_floods && f < cap; ++f) {
@@ -985,6 +1089,11 @@ int tgsim_step(void* e, uint32_t n_ticks) {
   Eng* E = as_eng(e);
   if (!E || n_ticks == 0) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
+  if (E->S == E->N) {  // whole population on this engine: asynchronous local delivery
+    int rc = run_sim(E, n_ticks, true);
+    if (rc) return rc;
+    return deliver_local(E);
+  }
   int rc = run_sim(E, n_ticks);
   if (rc) return rc;
   const uint64_t cap = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;
@@ -995,7 +1104,6 @@ int tgsim_step(void* e, uint32_t n_ticks) {
   if (rc) return rc;
   rc = deliver(E, E->d_bucket.p, count);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(E->st));
   return finish_sim_timing(E);
 }
 
@@ -1003,6 +1111,8 @@ int64_t tgsim_drain(void* e, tgsim_delivery* out, size_t cap) {
   Eng* E = as_eng(e);
   if (!E || (!out && cap)) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
   const uint64_t n = std::min<uint64_t>(cap, E->drain_n);
   if (n) {
     HIPCHK(hipMemcpy(out, E->d_drain.p + E->drain_head, sizeof(tgsim_delivery) * n, hipMemcpyDeviceToHost));
@@ -1022,6 +1132,8 @@ int64_t tgsim_verdicts(void* e, uint8_t* out, size_t cap) {
   Eng* E = as_eng(e);
   if (!E || (!out && cap)) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
   if (cap >= E->n_verdict && E->n_verdict) {
     std::vector<uint8_t> tmp(E->n_verdict);
     HIPCHK(hipMemcpy(tmp.data(), E->d_verdict.p, E->n_verdict, hipMemcpyDeviceToHost));
@@ -1038,6 +1150,8 @@ int tgsim_stats(void* e, tgsim_stats_t* out) {
   Eng* E = as_eng(e);
   if (!E || !out) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
   unsigned long long s[kStSlots];
   HIPCHK(hipMemcpy(s, E->d_stats.p, sizeof s, hipMemcpyDeviceToHost));
   memset(out, 0, sizeof *out);
@@ -1068,6 +1182,7 @@ int tgsim_barrier_poll(void* e, uint32_t state, uint64_t target) {
 double tgsim_sim_kernel_ms(void* e, uint64_t* n, int reset) {
   Eng* E = as_eng(e);
   if (!E) return -1;
+  if (hipSetDevice(E->dev) != hipSuccess || sync_stream(E)) return -1;
   const double avg = E->sim_launches ? E->sim_ms / static_cast<double>(E->sim_launches) : 0.0;
   if (n) *n = E->sim_launches;
   if (reset) {
@@ -1083,6 +1198,8 @@ int64_t tgsim_debug_stamps(void* e, uint64_t* out, size_t cap) {
   const uint64_t n = E->stamps_on ? E->n_stamp_wg * kStampSlots : 0;
   if (out && cap >= n && n) {
     HIPCHK(hipSetDevice(E->dev));
+    int rc = sync_stream(E);
+    if (rc) return rc;
     HIPCHK(hipMemcpy(out, E->d_stamps.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   }
   return static_cast<int64_t>(n);

@@ -91,6 +91,7 @@ struct SimArgs {
   uint64_t t0_ns, tick_ns, horizon_ns;
   const uint32_t* order;    // k_sim dispatch order (workgroup -> source), or null for identity
   uint64_t* stamps;         // diagnostics: kStampSlots s_memrealtime stamps per workgroup, or null
+  unsigned long long* dst_cnt;  // single shard: per-destination histogram of the emitted records, or null
 };
 constexpr uint32_t kStampSlots = 24;  // 8 phase stamps + 16 profile counters (TGSIM_PROFILE)
 

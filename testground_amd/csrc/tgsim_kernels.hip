@@ -244,6 +244,7 @@ struct SimQueue {
   uint32_t rh, rn, qn;      // ring head slot, ring length, eligibility-queue length
   uint64_t tat;             // HTB theoretical arrival time
   tgsim_delivery* emit;
+  unsigned long long* dcnt;  // per-destination histogram (single shard) or null
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
   uint32_t sched, corrupted;
@@ -280,6 +281,7 @@ struct SimQueue {
       rw[0] = d;
       rw[1] = ((uint64_t)qi.w << 32) | src;
       rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
+      if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
       sched++;
       bytes += len;
       corrupted += (flags >> 1) & 1u;
@@ -311,7 +313,8 @@ struct SimQueue {
   __device__ void depart_before(uint64_t T) {
     for (;;) {
       const uint64_t dep = lane < rn ? ring_d(lane) : ~0ull;
-      const uint32_t k = ballot_count(dep < T);
+      const uint64_t stop = __ballot(dep >= T);  // released from the head while head < T
+      const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) : kWave;
       rh = (rh + k) & kSlotMask;
       rn -= k;
       if (k < kWave) break;
@@ -447,6 +450,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   Q.src = a.shard_begin + s;
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
   Q.n_emit = 0;
+  Q.dcnt = a.dst_cnt;
   Q.sched = Q.corrupted = 0;
   Q.bytes = 0;
 #ifdef TGSIM_PROFILE
@@ -589,8 +593,15 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
             uint64_t dep = ~0ull;
             if (k < Q.rn) dep = Q.ring_d(k);
             else if (ks < nS) dep = dfs;
-            const uint32_t nd = ballot_count(dep < T_max);
-            for (uint32_t l = 0; l < nd; ++l) D += readlane64(dep, l) < T ? 1u : 0u;
+            // the netem queue releases departures from the ring head while head < T (a prefix:
+            // with a lookahead the ring need not be sorted across a step boundary)
+            const uint64_t stop = __ballot(dep >= T_max);
+            const uint32_t nd = stop ? (uint32_t)__builtin_ctzll(stop) : kWave;
+            bool alive = true;
+            for (uint32_t l = 0; l < nd; ++l) {
+              alive = alive && readlane64(dep, l) < T;
+              D += alive ? 1u : 0u;
+            }
             if (nd < kWave) break;
           }
         }
@@ -861,32 +872,43 @@ __device__ __forceinline__ uint32_t poisson_count(const GenArgs& g, uint32_t u) 
   return c;
 }
 
-__global__ void k_gen_count(GenArgs g, uint64_t* counts) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+// One wavefront per source, one lane per tick: the per-tick Poisson counts of 64 ticks are drawn
+// in parallel and turned into record positions by a wave prefix sum.
+__global__ __launch_bounds__(256) void k_gen_count(GenArgs g, uint64_t* counts) {
+  const uint32_t s = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const uint32_t lane = threadIdx.x % kWave;
   if (s >= g.n_src) return;
   const uint32_t src = g.shard_begin + s;
-  uint64_t total = 0;
+  uint32_t total = 0;
   if (g.n_peers >= 2) {
-    for (uint32_t t = 0; t < g.n_ticks; ++t) {
+    for (uint32_t t = lane; t < g.n_ticks; t += kWave) {
       uint32_t r[4];
       philox(src, (uint32_t)(g.now_tick + t), 0x53544F52u, 0, g.k0, g.k1, r);
       total += poisson_count(g, r[0]);
     }
   }
-  counts[s] = total;
+  const uint64_t sum = wave_sum(total);
+  if (lane == 0) counts[s] = sum;
 }
 
-__global__ void k_gen_write(GenArgs g, const uint64_t* off, uint32_t* gen_seq, InRec* out) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_gen_write(GenArgs g, const uint64_t* off, uint32_t* gen_seq, InRec* out) {
+  const uint32_t s = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const uint32_t lane = threadIdx.x % kWave;
   if (s >= g.n_src || g.n_peers < 2) return;
   const uint32_t src = g.shard_begin + s;
   uint64_t o = off[s];
   uint32_t seq = gen_seq[s];
-  for (uint32_t t = 0; t < g.n_ticks; ++t) {
+  for (uint32_t t0 = 0; t0 < g.n_ticks; t0 += kWave) {
+    const uint32_t t = t0 + lane;
     const uint32_t at = (uint32_t)(g.now_tick + t);
-    uint32_t r[4];
-    philox(src, at, 0x53544F52u, 0, g.k0, g.k1, r);
-    const uint32_t cnt = poisson_count(g, r[0]);
+    uint32_t cnt = 0;
+    if (t < g.n_ticks) {
+      uint32_t r[4];
+      philox(src, at, 0x53544F52u, 0, g.k0, g.k1, r);
+      cnt = poisson_count(g, r[0]);
+    }
+    const int32_t incl = scan_sum_i32((int32_t)cnt);
+    const uint32_t excl = (uint32_t)incl - cnt;
     for (uint32_t j = 0; j < cnt; ++j) {
       uint32_t q[4];
       philox(src, at, 0x53544F52u, j + 1, g.k0, g.k1, q);
@@ -894,13 +916,16 @@ __global__ void k_gen_write(GenArgs g, const uint64_t* off, uint32_t* gen_seq, I
       d += d >= src;
       InRec rec;
       rec.dst = d;
-      rec.seq = seq++;
+      rec.seq = seq + excl + j;
       rec.tick = t;
       rec.len = 64u + q[1] % 1437u;
-      out[o++] = rec;
+      out[o + excl + j] = rec;
     }
+    const uint32_t tot = readlane32((uint32_t)incl, kWave - 1);
+    o += tot;
+    seq += tot;
   }
-  gen_seq[s] = seq;
+  if (lane == 0) gen_seq[s] = seq;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -992,10 +1017,10 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, ui
       sh[i] = acc;
       acc += s;
     }
-    sh[15] = acc;
+    sh[16] = acc;
   }
   __syncthreads();
-  total = sh[15];
+  total = sh[16];
   const uint64_t r = x - v + sh[w];
   __syncthreads();
   return r;
@@ -1003,7 +1028,7 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, ui
 
 __global__ __launch_bounds__(256) void k_scan_local(const uint64_t* in, uint64_t* out, uint64_t n,
                                                     uint64_t* block_sums) {
-  __shared__ uint64_t sh[16];
+  __shared__ uint64_t sh[17];
   const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x * 4;
   uint64_t v[4], s = 0;
 #pragma unroll
@@ -1022,7 +1047,7 @@ __global__ __launch_bounds__(256) void k_scan_local(const uint64_t* in, uint64_t
 }
 
 __global__ __launch_bounds__(256) void k_scan_sums(uint64_t* sums, uint64_t nb, uint64_t* total_out) {
-  __shared__ uint64_t sh[16];
+  __shared__ uint64_t sh[17];
   uint64_t carry = 0;
   for (uint64_t base = 0; base < nb; base += 256) {
     const uint64_t i = base + threadIdx.x;
@@ -1035,12 +1060,47 @@ __global__ __launch_bounds__(256) void k_scan_sums(uint64_t* sums, uint64_t nb, 
   if (threadIdx.x == 0) *total_out = carry;
 }
 
-__global__ __launch_bounds__(256) void k_scan_add(uint64_t* out, uint64_t n, const uint64_t* sums) {
+__global__ __launch_bounds__(256) void k_scan_add(uint64_t* out, uint64_t n, const uint64_t* sums,
+                                                  uint64_t* pos, const uint64_t* total) {
   const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x * 4;
   const uint64_t add = sums[blockIdx.x];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (base + i < n) out[base + i] += add;
+    if (base + i < n) {
+      const uint64_t v = out[base + i] + add;
+      out[base + i] = v;
+      if (pos) pos[base + i] = v;
+    }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = *total;
+}
+
+// Exclusive scan of up to kSmallScan counts in one workgroup (out[n] = total; pos = a copy).
+constexpr uint32_t kSmallScan = 16384;
+__global__ __launch_bounds__(1024) void k_scan_small(const uint64_t* in, uint64_t* out, uint64_t n,
+                                                     uint64_t* pos, uint64_t* total_out) {
+  __shared__ uint64_t sh[17];
+  const uint32_t per = (uint32_t)((n + 1023) / 1024);  // <= 16
+  const uint64_t base = (uint64_t)threadIdx.x * per;
+  uint64_t v[16], s = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i) {
+    v[i] = (i < per && base + i < n) ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t pre = block_excl_scan(s, sh, total);
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i) {
+    if (i < per && base + i < n) {
+      out[base + i] = pre;
+      if (pos) pos[base + i] = pre;
+    }
+    pre += v[i];
+  }
+  if (threadIdx.x == 0) {
+    out[n] = total;
+    if (total_out) *total_out = total;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1120,89 +1180,134 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Delivery: counting sort by destination, then per-destination ordering.
+// Delivery: counting sort by destination (counts -> exclusive scan -> scatter through per-dst
+// cursors), then each destination's records ordered by (t, src, seq, clone first).
 __global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[in[i].dst - dst_begin]), 1ull);
 }
 
-__global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin,
-                              const uint64_t* off, uint64_t* cursor, tgsim_delivery* out) {
+// Flat input (records received from every shard): pos[] starts as the exclusive scan of counts.
+__global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* pos,
+                              tgsim_delivery* out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const tgsim_delivery r = in[i];
-  const uint32_t d = r.dst - dst_begin;
-  const uint64_t p = atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[d]), 1ull);
-  out[off[d] + p] = r;
+  out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[r.dst - dst_begin]), 1ull)] = r;
 }
 
-struct SortKey {
-  uint64_t t;
-  uint64_t sq;   // src << 32 | seq
-  uint32_t idx;  // (clone ? 0 : 1) << 31 | position in the segment
+// Single shard: straight from k_sim's per-source emit regions (counts were taken by k_sim).
+__global__ __launch_bounds__(256) void k_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n,
+                                                       const uint64_t* off, uint32_t n_src, uint32_t dst_begin,
+                                                       uint64_t* pos, tgsim_delivery* out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
+    const uint32_t n = emit_n[s];
+    const tgsim_delivery* base = emit + 2 * off[s] + (uint64_t)kHeapCap * s;
+    for (uint32_t i = lane; i < n; i += kWave) {
+      const tgsim_delivery r = base[i];
+      out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[r.dst - dst_begin]), 1ull)] = r;
+    }
+  }
+}
+
+// Delivery order inside a destination: (t, src, seq, clone first).
+__device__ __forceinline__ bool rec_lt(uint64_t ta, uint64_t qa, uint32_t ca, uint64_t tb, uint64_t qb, uint32_t cb) {
+  return ta != tb ? ta < tb : (qa != qb ? qa < qb : ca < cb);
+}
+struct RecKey {
+  uint64_t t, sq;
+  uint32_t c;  // 0 for the clone, 1 for the original
 };
-
-__device__ __forceinline__ bool key_lt(const SortKey& a, const SortKey& b) {
-  if (a.t != b.t) return a.t < b.t;
-  if (a.sq != b.sq) return a.sq < b.sq;
-  return a.idx < b.idx;
+__device__ __forceinline__ RecKey rec_key(const tgsim_delivery& r) {
+  return RecKey{r.t_ns, ((uint64_t)r.src << 32) | r.seq, (r.flags & TGSIM_FLAG_DUP) ? 0u : 1u};
 }
 
-__device__ __forceinline__ SortKey make_key(const tgsim_delivery& r, uint32_t i) {
-  SortKey k;
-  k.t = r.t_ns;
-  k.sq = ((uint64_t)r.src << 32) | r.seq;
-  k.idx = ((r.flags & TGSIM_FLAG_DUP) ? 0u : 0x80000000u) | i;
-  return k;
+// Sorts the (up to) 64 records of [b, b + n) held one per lane: each lane counts the keys before
+// its own (ties: lane order, which keeps runs stable).
+__device__ __forceinline__ uint32_t wave_rank(const RecKey& k, uint32_t n, uint32_t lane) {
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t t = readlane64(k.t, j), q = readlane64(k.sq, j);
+    const uint32_t c = readlane32(k.c, j);
+    rank += (rec_lt(t, q, c, k.t, k.sq, k.c) || (!rec_lt(k.t, k.sq, k.c, t, q, c) && j < lane)) ? 1u : 0u;
+  }
+  return rank;
 }
 
-constexpr uint32_t kSegLds = 2048;
-
-// One workgroup per destination segment: bitonic sort of (t, src, seq, clone-first) keys in LDS
-// (global scratch for segments longer than kSegLds), then a gather into delivery order.
-__global__ __launch_bounds__(256) void k_dst_sort(const tgsim_delivery* in, const uint64_t* off,
-                                                  const uint64_t* cnt, tgsim_delivery* out,
-                                                  SortKey* scratch) {
-  __shared__ SortKey sk[kSegLds];
-  const uint32_t d = blockIdx.x;
-  const uint64_t b = off[d];
+// One wavefront per destination.  Up to 64 records: ranked in registers and stored at their rank.
+// Longer segments: runs of 64 ranked the same way, then bottom-up merge passes between the scatter
+// buffer and the output (each element's place = its index in its run + its rank in the other
+// run, a binary search), so no scratch memory is needed.  The destination's count is reset to
+// zero for the next step's histogram.
+__global__ __launch_bounds__(256) void k_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
+                                                  uint32_t n_dst, tgsim_delivery* out) {
+  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (d >= n_dst) return;
   const uint32_t n = (uint32_t)cnt[d];
   if (n == 0) return;
-  if (n == 1) {
-    if (threadIdx.x == 0) out[b] = in[b];
-    return;
-  }
-  uint32_t P = 1;
-  while (P < n) P <<= 1;
-  SortKey* k = P <= kSegLds ? sk : scratch + 2 * b;  // P < 2n: disjoint per segment
-  for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-    if (i < n) {
-      k[i] = make_key(in[b + i], i);
-    } else {
-      k[i].t = ~0ull;
-      k[i].sq = ~0ull;
-      k[i].idx = 0xFFFFFFFFu;
+  const uint64_t b = off[d];
+  if (n <= kWave) {
+    tgsim_delivery r;
+    RecKey k{~0ull, ~0ull, 1u};
+    if (lane < n) {
+      r = in[b + lane];
+      k = rec_key(r);
     }
-  }
-  __syncthreads();
-  for (uint32_t size = 2; size <= P; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-        const uint32_t j = i ^ stride;
-        if (j > i) {
-          const bool up = (i & size) == 0;
-          const SortKey x = k[i], y = k[j];
-          if (key_lt(y, x) == up) {
-            k[i] = y;
-            k[j] = x;
+    const uint32_t rank = wave_rank(k, n, lane);
+    if (lane < n) out[b + rank] = r;
+  } else {
+    // runs of 64, sorted in place in the scatter buffer
+    for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
+      const uint32_t m = min(kWave, n - c0);
+      tgsim_delivery r;
+      RecKey k{~0ull, ~0ull, 1u};
+      if (lane < m) {
+        r = in[b + c0 + lane];
+        k = rec_key(r);
+      }
+      const uint32_t rank = wave_rank(k, m, lane);
+      __builtin_amdgcn_s_waitcnt(0);  // every lane's read of the run lands before any write
+      if (lane < m) in[b + c0 + rank] = r;
+    }
+    tgsim_delivery* src = in + b;
+    tgsim_delivery* dst = out + b;
+    for (uint32_t w = kWave; w < n; w <<= 1) {
+      __threadfence();  // device scope: also drops stale vL1D lines of the other buffer
+      for (uint32_t lo = 0; lo < n; lo += 2 * w) {
+        const uint32_t mid = min(lo + w, n), hi = min(lo + 2 * w, n);
+        for (uint32_t i = lo + lane; i < hi; i += kWave) {
+          const tgsim_delivery r = src[i];
+          const RecKey k = rec_key(r);
+          const bool inA = i < mid;
+          // rank in the other run: A elements count B keys < k, B elements count A keys <= k
+          uint32_t a0 = inA ? mid : lo, a1 = inA ? hi : mid;
+          while (a0 < a1) {
+            const uint32_t m2 = (a0 + a1) >> 1;
+            const RecKey o = rec_key(src[m2]);
+            const bool before = inA ? rec_lt(o.t, o.sq, o.c, k.t, k.sq, k.c)
+                                    : !rec_lt(k.t, k.sq, k.c, o.t, o.sq, o.c);
+            if (before) a0 = m2 + 1;
+            else a1 = m2;
           }
+          const uint32_t other = inA ? a0 - mid : a0 - lo;
+          const uint32_t own = inA ? i - lo : i - mid;
+          dst[lo + own + other] = r;
         }
       }
-      __syncthreads();
+      tgsim_delivery* t = src;
+      src = dst;
+      dst = t;
+    }
+    if (src != out + b) {
+      __threadfence();  // device scope: also drops stale vL1D lines of the other buffer
+      for (uint32_t i = lane; i < n; i += kWave) out[b + i] = src[i];
     }
   }
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[b + i] = in[b + (k[i].idx & 0x7FFFFFFFu)];
+  if (lane == 0) cnt[d] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1226,9 +1331,9 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
   for (int i = 0; i < 16; ++i) g.tab[i] = h.tab[i];
   g.k0 = h.k0; g.k1 = h.k1; g.n_src = h.n_src; g.shard_begin = h.shard_begin;
   g.n_peers = h.n_peers; g.n_ticks = h.n_ticks; g.now_tick = h.now_tick;
-  const dim3 grid((h.n_src + 63) / 64), blk(64);
-  if (phase == 0) hipLaunchKernelGGL(k_gen_count, grid, blk, 0, st, g, counts);
-  else hipLaunchKernelGGL(k_gen_write, grid, blk, 0, st, g, off, gen_seq, out);
+  const dim3 wgrid((h.n_src + 3) / 4), wblk(256);  // one wavefront per source
+  if (phase == 0) hipLaunchKernelGGL(k_gen_count, wgrid, wblk, 0, st, g, counts);
+  else hipLaunchKernelGGL(k_gen_write, wgrid, wblk, 0, st, g, off, gen_seq, out);
 }
 
 void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
@@ -1243,15 +1348,21 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
 }
 
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums,
-                 uint64_t* total, hipStream_t st) {
-  const uint64_t nb = (n + 1023) / 1024;
-  if (nb == 0) {
-    (void)hipMemsetAsync(total, 0, sizeof(uint64_t), st);
+                 uint64_t* total, hipStream_t st, uint64_t* pos) {
+  if (n == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    if (total) (void)hipMemsetAsync(total, 0, sizeof(uint64_t), st);
     return;
   }
+  if (n <= kSmallScan) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, pos, total);
+    return;
+  }
+  const uint64_t nb = (n + 1023) / 1024;
   hipLaunchKernelGGL(k_scan_local, dim3((uint32_t)nb), dim3(256), 0, st, in, out, n, block_sums);
   hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, block_sums, nb, total);
-  hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)nb), dim3(256), 0, st, out, n, block_sums);
+  hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)nb), dim3(256), 0, st, out, n, block_sums, pos,
+                     (const uint64_t*)total);
 }
 
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
@@ -1277,20 +1388,24 @@ void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, u
   hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, cnt);
 }
 
-void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, const uint64_t* off,
-                        uint64_t* cursor, tgsim_delivery* out, hipStream_t st) {
+void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* pos,
+                        tgsim_delivery* out, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n,
-                     dst_begin, off, cursor, out);
+  hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, pos, out);
 }
 
-void launch_dst_sort(const tgsim_delivery* in, const uint64_t* off, const uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, void* scratch, hipStream_t st) {
+void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
+                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st) {
+  if (!n_src) return;
+  const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);
+  hipLaunchKernelGGL(k_local_scatter, dim3(wgs), dim3(256), 0, st, emit, emit_n, off, n_src, dst_begin, pos, out);
+}
+
+void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
+                     tgsim_delivery* out, hipStream_t st) {
   if (!n_dst) return;
-  hipLaunchKernelGGL(k_dst_sort, dim3(n_dst), dim3(256), 0, st, in, off, cnt, out,
-                     reinterpret_cast<SortKey*>(scratch));
+  hipLaunchKernelGGL(k_dst_sort, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
 }
 
-size_t sort_key_bytes() { return sizeof(SortKey); }
 
 }  // namespace tgsim

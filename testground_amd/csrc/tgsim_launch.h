@@ -30,14 +30,19 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
 // phase 0: fold delivered records into receipts; 1: per-source counts; 2: write the window.
 void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
                    const uint64_t* off, InRec* out, int phase, hipStream_t st);
+// Exclusive scan of in[0..n) into out[0..n] (out[n] = total, also stored at *total when non-null);
+// pos (optional) receives a copy of out[0..n), the scatter cursors.
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
-                 hipStream_t st);
+                 hipStream_t st, uint64_t* pos = nullptr);
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt, hipStream_t st);
-void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, const uint64_t* off,
-                        uint64_t* cursor, tgsim_delivery* out, hipStream_t st);
-void launch_dst_sort(const tgsim_delivery* in, const uint64_t* off, const uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, void* scratch, hipStream_t st);
-size_t sort_key_bytes();
+void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* pos,
+                        tgsim_delivery* out, hipStream_t st);
+void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
+                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st);
+// Orders each destination's records; resets cnt[] to zero for the next histogram.
+// (in, the scatter buffer, is overwritten for segments longer than 64.)
+void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
+                     tgsim_delivery* out, hipStream_t st);
 
 }  // namespace tgsim

@@ -113,6 +113,48 @@ def test_host_packets_all_features(make_oracle):
         assert_same(g, c, f"host step {step}")
 
 
+@pytest.mark.parametrize("queue_limit,lookahead", [(1000, 0), (32, 0), (200, 300_000)])
+def test_window_edge_shapes(make_oracle, queue_limit, lookahead):
+    """Uncorrelated shapes that stress the windowed netem/HTB resolution of k_sim: zero and
+    sub-tick latency, jitter larger than the latency (delays clamped to 0, items eligible at once),
+    heavy reorder and duplication, every bandwidth class, bursts of packets in one tick, and
+    sequence numbers that are not monotone across ticks (ties in e resolved by seq)."""
+    n = 128
+    rng = np.random.default_rng(11 + queue_limit)
+    g, c = both(make_oracle, n, queue_limit=queue_limit, lookahead_ns=lookahead)
+    lat = [0, 50 * nw.Microsecond, 1 * nw.Millisecond, 20 * nw.Millisecond]
+    for i in range(n):
+        L = lat[i % 4]
+        J = [0, L // 2, 2 * L, 5 * nw.Millisecond][(i // 4) % 4]
+        s = nw.LinkShape(Latency=L, Jitter=J,
+                         Bandwidth=int([0, 1 << 20, 10**7, 10**8, 10**9][(i // 16) % 5]),
+                         Reorder=float([0, 5, 50][(i // 3) % 3]), Duplicate=float([0, 20][(i // 7) % 2]),
+                         Loss=float([0, 5][(i // 11) % 2]), Corrupt=float([0, 10][(i // 5) % 2]))
+        cfg = nw.Config(Network="default", Enable=True, Default=s)
+        g.configure(i, cfg)
+        c.configure(i, cfg)
+    for step in range(3):
+        m = 150_000
+        src = rng.integers(0, n, m)
+        pk = np.zeros(m, dtype=abi.PKT_DTYPE)
+        pk["src"] = src
+        pk["dst"] = (src + 1 + rng.integers(0, n - 1, m)) % n
+        pk["len"] = rng.integers(40, 1500, m)
+        # bursty ticks: a third of the packets land on 20 ticks
+        tick = rng.integers(0, 2000, m)
+        burst = rng.random(m) < 0.33
+        tick[burst] = rng.choice(rng.integers(0, 2000, 20), burst.sum())
+        pk["tick"] = tick
+        pk["seq"] = rng.permutation(m).astype(np.uint32) + np.uint32(step * m)  # unique, not monotone
+        g.submit(pk)
+        c.submit(pk)
+        g.step(2000)
+        c.step(2000)
+        assert_same(g, c, f"edge shapes step {step}")
+    st = g.stats()
+    assert st["by_verdict"]["queue_full"] > 0 and st["cloned"] > 0
+
+
 def test_mid_run_reconfiguration(make_oracle):
     """C5-style: reshape a subset between steps, including the netem quirks (corrupt persists when
     re-set to 0, correlation state re-randomised) and a re-address (reconnect)."""
