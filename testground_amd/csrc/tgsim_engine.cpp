@@ -418,6 +418,8 @@ int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uin
   return 0;
 }
 
+constexpr uint32_t kOrderMaxSources = 32768;
+
 hipError_t take_event(Eng* E, hipEvent_t* ev) {
   if (!E->ev_pool.empty()) {
     *ev = E->ev_pool.back();
@@ -514,7 +516,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   a.t0_ns = E->now_tick * E->o.tick_ns;
   a.horizon_ns = (E->now_tick + n_ticks) * E->o.tick_ns + E->o.lookahead_ns;
   const uint32_t n_wg = (E->S + kSpw - 1) / kSpw;
-  a.order = (kSpw == 1 && E->order_valid) ? E->d_order.p : nullptr;
+  a.order = (kSpw == 1 && E->order_valid && E->S <= kOrderMaxSources) ? E->d_order.p : nullptr;
   a.stamps = nullptr;
   if (E->stamps_on) {
     HIPCHK(E->d_stamps.ensure(static_cast<size_t>(n_wg) * kStampSlots));
@@ -538,7 +540,9 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.emplace_back(ev0, ev1);
   HIPCHK(hipMemcpyAsync(E->h_err, E->d_stats.p + kStErr, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
-  if (kSpw == 1) {  // heavy-first dispatch order for the next step
+  // heavy-first dispatch order for the next step: it shortens the tail when only a few rounds of
+  // workgroups fit; with many more sources than resident workgroups the dispatcher balances alone
+  if (kSpw == 1 && E->S <= kOrderMaxSources) {
     HIPCHK(E->d_order.ensure(E->S));
     launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
     HIPCHK(hipGetLastError());
@@ -769,12 +773,13 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(E->d_heap.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc heap"))) return bail(rc);
   if ((rc = E->hip(E->d_ring.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc ring"))) return bail(rc);
   if ((rc = E->hip(E->d_gen_seq.ensure(E->S), "alloc gen_seq"))) return bail(rc);
-  if ((rc = E->hip(E->d_stats.ensure(kStSlots), "alloc stats"))) return bail(rc);
+  if ((rc = E->hip(E->d_stats.ensure(kStSlots * kStatCopies), "alloc stats"))) return bail(rc);
   if ((rc = E->hip(E->d_off.ensure(E->S + 1), "alloc off"))) return bail(rc);
   if ((rc = E->hip(E->d_in.ensure(1), "alloc in"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_state.p, 0, sizeof(SrcState) * E->S), "memset"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_gen_seq.p, 0, sizeof(uint32_t) * E->S), "memset"))) return bail(rc);
-  if ((rc = E->hip(hipMemset(E->d_stats.p, 0, sizeof(unsigned long long) * kStSlots), "memset"))) return bail(rc);
+  if ((rc = E->hip(hipMemset(E->d_stats.p, 0, sizeof(unsigned long long) * kStSlots * kStatCopies), "memset")))
+    return bail(rc);
   E->peers_dirty = E->rules_dirty = E->params_dirty = true;
   if ((rc = flush_config(E))) return bail(rc);
   *out = E;
@@ -1152,8 +1157,11 @@ int tgsim_stats(void* e, tgsim_stats_t* out) {
   HIPCHK(hipSetDevice(E->dev));
   int rc = sync_stream(E);
   if (rc) return rc;
-  unsigned long long s[kStSlots];
-  HIPCHK(hipMemcpy(s, E->d_stats.p, sizeof s, hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> all(static_cast<size_t>(kStSlots) * kStatCopies);
+  HIPCHK(hipMemcpy(all.data(), E->d_stats.p, sizeof(unsigned long long) * all.size(), hipMemcpyDeviceToHost));
+  unsigned long long s[kStSlots] = {};
+  for (uint32_t c = 0; c < kStatCopies; ++c)
+    for (uint32_t k = 0; k < kStSlots; ++k) s[k] += all[static_cast<size_t>(c) * kStSlots + k];
   memset(out, 0, sizeof *out);
   out->offered = s[kStOffered];
   out->scheduled = s[kStScheduled];

@@ -69,6 +69,10 @@ enum StatSlot {
   kStOffered = 0, kStScheduled, kStCloned, kStCorrupted, kStVerdict0,  // 4..11 verdicts
   kStBytes = 12, kStErr = 13, kStQueue = 14, kStSlots = 16
 };
+// Counters are spread over kStatCopies copies (workgroup w adds into copy w % kStatCopies) so that
+// a million one-source workgroups do not serialize on 16 addresses; readers sum the copies.  The
+// error word lives in copy 0 only.
+constexpr uint32_t kStatCopies = 64;
 constexpr uint32_t kErrTimeOverflow = 1u;
 
 struct SimArgs {

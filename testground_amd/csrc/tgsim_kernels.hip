@@ -805,14 +805,15 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   const uint64_t qbytes = qbytes_in + 16ull * Q.qn + 8ull * Q.rn;
   const uint64_t err = wave_sum(perr ? 1u : 0u);
   if (lane == 0) {
-    atomicAdd(&a.stats[kStOffered], (unsigned long long)c_off);
-    if (sched) atomicAdd(&a.stats[kStScheduled], (unsigned long long)sched);
-    if (c_clone) atomicAdd(&a.stats[kStCloned], (unsigned long long)c_clone);
-    if (corrupted) atomicAdd(&a.stats[kStCorrupted], (unsigned long long)corrupted);
+    unsigned long long* sc = a.stats + (size_t)(blockIdx.x % kStatCopies) * kStSlots;
+    atomicAdd(&sc[kStOffered], (unsigned long long)c_off);
+    if (sched) atomicAdd(&sc[kStScheduled], (unsigned long long)sched);
+    if (c_clone) atomicAdd(&sc[kStCloned], (unsigned long long)c_clone);
+    if (corrupted) atomicAdd(&sc[kStCorrupted], (unsigned long long)corrupted);
     for (int k = 0; k < 8; ++k)
-      if (c_v[k]) atomicAdd(&a.stats[kStVerdict0 + k], (unsigned long long)c_v[k]);
-    if (bytes) atomicAdd(&a.stats[kStBytes], (unsigned long long)bytes);
-    if (qbytes) atomicAdd(&a.stats[kStQueue], (unsigned long long)qbytes);
+      if (c_v[k]) atomicAdd(&sc[kStVerdict0 + k], (unsigned long long)c_v[k]);
+    if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
+    if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
     if (err) atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
   }
 }
@@ -951,50 +952,50 @@ __global__ void k_gossip_recv(GossipArgs g, const tgsim_delivery* in, uint64_t n
   atomicMin(&g.first[(uint64_t)s * 64 + f], (uint32_t)t);
 }
 
-// Floods due in [win0, win0 + n_ticks) for local peer s, as a bitmask; flags late receipts.
-__device__ __forceinline__ uint64_t gossip_due(const GossipArgs& g, uint32_t s) {
+// Floods due in [win0, win0 + n_ticks) for local peer s: one wavefront per peer, lane f holds
+// flood f's earliest receipt tick (a coalesced 256-B read); late receipts are flagged.
+__device__ __forceinline__ bool gossip_due_lane(const GossipArgs& g, uint32_t s, uint32_t lane, uint32_t& t) {
   const uint64_t done = g.fwd[s];
-  const uint32_t* fs = g.first + (uint64_t)s * 64;
-  uint64_t due = 0;
-  for (uint32_t f = 0; f < g.n_floods; ++f) {
-    const uint32_t t = fs[f];
-    if ((done >> f & 1ull) || t == 0xFFFFFFFFu || (uint64_t)t >= g.win0 + g.n_ticks) continue;
-    if ((uint64_t)t < g.win0) atomicOr(g.err, 1u);
-    due |= 1ull << f;
-  }
+  t = lane < g.n_floods ? g.first[(uint64_t)s * 64 + lane] : 0xFFFFFFFFu;
+  const bool due = lane < g.n_floods && !(done >> lane & 1ull) && t != 0xFFFFFFFFu &&
+                   (uint64_t)t < g.win0 + g.n_ticks;
+  if (due && (uint64_t)t < g.win0) atomicOr(g.err, 1u);
   return due;
 }
 
-__global__ void k_gossip_count(GossipArgs g, uint64_t* counts) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_gossip_count(GossipArgs g, uint64_t* counts) {
+  const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (s >= g.n_src) return;
-  counts[s] = (uint64_t)__popcll(gossip_due(g, s)) * g.degree;
+  uint32_t t;
+  const uint64_t due = __ballot(gossip_due_lane(g, s, lane, t));
+  if (lane == 0) counts[s] = (uint64_t)__popcll(due) * g.degree;
 }
 
-__global__ void k_gossip_write(GossipArgs g, const uint64_t* off, InRec* out) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64_t* off, InRec* out) {
+  const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (s >= g.n_src) return;
-  uint64_t due = gossip_due(g, s);
+  uint32_t t;
+  const bool me = gossip_due_lane(g, s, lane, t);
+  const uint64_t due = __ballot(me);
   if (!due) return;
-  g.fwd[s] |= due;
+  if (lane == 0) g.fwd[s] |= due;
+  // earliest receipt first, ties by flood id (seq order within a tick)
+  uint32_t rank = 0;
+  for (uint64_t m = due; m; m &= m - 1) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(m);
+    const uint32_t tj = readlane32(t, j);
+    rank += (tj < t || (tj == t && j < lane)) ? 1u : 0u;
+  }
+  if (!me) return;
   const uint32_t src = g.shard_begin + s;
-  const uint32_t* fs = g.first + (uint64_t)s * 64;
-  uint64_t o = off[s];
-  while (due) {  // earliest receipt first, ties by flood id (seq order within a tick)
-    uint32_t best = __ffsll((unsigned long long)due) - 1, bt = fs[best];
-    for (uint64_t m = due & (due - 1); m; m &= m - 1) {
-      const uint32_t f = __ffsll((unsigned long long)m) - 1;
-      if (fs[f] < bt) { best = f; bt = fs[f]; }
-    }
-    due &= ~(1ull << best);
-    for (uint32_t k = 0; k < g.degree; ++k) {
-      InRec rec;
-      rec.dst = gossip_neighbour(g, src, k);
-      rec.seq = best * g.degree + k;
-      rec.tick = (uint32_t)(bt - g.win0);
-      rec.len = g.msg_len;
-      out[o++] = rec;
-    }
+  const uint64_t o = off[s] + (uint64_t)rank * g.degree;
+  for (uint32_t k = 0; k < g.degree; ++k) {
+    InRec rec;
+    rec.dst = gossip_neighbour(g, src, k);
+    rec.seq = lane * g.degree + k;
+    rec.tick = (uint32_t)(t - g.win0);
+    rec.len = g.msg_len;
+    out[o + k] = rec;
   }
 }
 
@@ -1342,7 +1343,7 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
     if (n) hipLaunchKernelGGL(k_gossip_recv, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, g, recs, n);
     return;
   }
-  const dim3 grid((g.n_src + 255) / 256), blk(256);
+  const dim3 grid((g.n_src + 3) / 4), blk(256);  // one wavefront per peer
   if (phase == 1) hipLaunchKernelGGL(k_gossip_count, grid, blk, 0, st, g, counts);
   else hipLaunchKernelGGL(k_gossip_write, grid, blk, 0, st, g, off, out);
 }
