@@ -330,6 +330,7 @@ struct SimQueue {
     PROF_T0(i);
     const uint32_t nm = (uint32_t)__popcll(m);
     uint32_t pos = 0, minpos = 0;
+    PROF_T0(q1);
     if (nm <= 8) {
       if (qn) {
         // two-level search, one item at a time: a sample every 16th queued key (one read per
@@ -371,6 +372,7 @@ struct SimQueue {
         }
       }
     }
+    PROF_ADD(14, q1);
     // rank among the new items (equal keys: lane order)
     uint32_t rank = 0;
     if (nm > 1) {
@@ -380,28 +382,70 @@ struct SimQueue {
         rank += (has && (item_lt(o, it) || (!item_lt(it, o) && b < lane))) ? 1u : 0u;
       }
     }
+    PROF_T0(q2);
+    uint32_t kL = 0;  // new items placed by moving the ring and the queue prefix down
     if (nm <= 8) {
-      // queued item r >= minpos moves up by #{new items with pos <= r}; passes of four chunks from
-      // the tail down, all reads of a pass before its writes (no pass reads a slot a previous
-      // pass wrote; within a pass the LDS executes this wave's operations in order)
-      for (int32_t hi = (int32_t)qn; hi > (int32_t)minpos; hi -= 4 * (int32_t)kWave) {
+      if (has) lds.pos[rank] = pos;
+      wave_lds_sync();
+      const uint32_t sp = lane < nm ? lds.pos[lane] : 0u;  // lane r: position of the rank-r item
+      // Two-sided merge.  The first kL items (by key) go in by moving the departure ring and the
+      // queue prefix [0, maxL) down into the free slots before the ring head, the others by
+      // moving the suffix [minR, qn) up; kL minimizes the slots moved.  Items eligible at once
+      // (delay 0, reorder) land at the head and cost only the ring.
+      const uint32_t spm1 = shr1_u32(sp, 0u);
+      const uint32_t cost = lane <= nm ? (lane > 0 ? rn + spm1 : 0u) + (lane < nm ? qn - sp : 0u) : 0xFFFFFFFFu;
+      uint32_t best = readlane32(cost, 0);
+      for (uint32_t k = 1; k <= nm; ++k) {
+        const uint32_t c = readlane32(cost, k);
+        if (c < best) {
+          best = c;
+          kL = k;
+        }
+      }
+      const int32_t maxL = kL ? (int32_t)readlane32(sp, kL - 1) : 0;
+      const int32_t minR = kL < nm ? (int32_t)readlane32(sp, kL) : (int32_t)qn;
+      // suffix up: queue item j >= minR moves by #{rank >= kL with pos <= j}; passes of four
+      // chunks from the tail down, all reads of a pass before its writes
+      for (int32_t hi = (int32_t)qn; hi > minR; hi -= 4 * (int32_t)kWave) {
         uint4 v[4];
         int32_t r[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           r[u] = hi - (u + 1) * (int32_t)kWave + (int32_t)lane;
-          v[u] = r[u] >= (int32_t)minpos ? slot(rn + (uint32_t)r[u]) : make_uint4(0, 0, 0, 0);
+          v[u] = r[u] >= minR ? slot(rn + (uint32_t)r[u]) : make_uint4(0, 0, 0, 0);
         }
         uint32_t sh[4] = {0, 0, 0, 0};
-        for (uint64_t mm = m; mm; mm &= mm - 1) {
-          const int32_t pb = (int32_t)readlane32(pos, (uint32_t)__builtin_ctzll(mm));
+        for (uint32_t k = kL; k < nm; ++k) {
+          const int32_t pb = (int32_t)readlane32(sp, k);
 #pragma unroll
           for (int u = 0; u < 4; ++u) sh[u] += pb <= r[u] ? 1u : 0u;
         }
         __asm__ volatile("" ::: "memory");
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (r[u] >= (int32_t)minpos) slot(rn + (uint32_t)r[u] + sh[u]) = v[u];
+          if (r[u] >= minR) slot(rn + (uint32_t)r[u] + sh[u]) = v[u];
+        PROF_CNT(6, 1);
+      }
+      // ring and prefix down: combined index c < rn + maxL moves by -kL (+ #{rank < kL with
+      // pos <= j} for queue item j = c - rn); passes from the ring head up
+      for (int32_t lo = 0; kL && lo < (int32_t)rn + maxL; lo += 4 * (int32_t)kWave) {
+        uint4 v[4];
+        int32_t c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          c[u] = lo + u * (int32_t)kWave + (int32_t)lane;
+          v[u] = c[u] < (int32_t)rn + maxL ? slot((uint32_t)c[u]) : make_uint4(0, 0, 0, 0);
+        }
+        uint32_t sh[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < kL; ++k) {
+          const int32_t pb = (int32_t)readlane32(sp, k) + (int32_t)rn;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sh[u] += (c[u] >= (int32_t)rn && pb <= c[u]) ? 1u : 0u;
+        }
+        __asm__ volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (c[u] < (int32_t)rn + maxL) slot((uint32_t)(c[u] - (int32_t)kL) + sh[u]) = v[u];
         PROF_CNT(6, 1);
       }
     } else {
@@ -419,8 +463,10 @@ struct SimQueue {
         PROF_CNT(6, 1);
       }
     }
+    PROF_ADD(15, q2);
     __asm__ volatile("" ::: "memory");
-    if (has) slot(rn + pos + rank) = it;
+    if (has) slot(rn - kL + pos + rank) = it;
+    rh = (rh - kL) & kSlotMask;
     qn += nm;
     wave_lds_sync();
     PROF_ADD(4, i);

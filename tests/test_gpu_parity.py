@@ -239,6 +239,7 @@ def test_two_shards_equal_one(make_oracle):
             off = int(cnt[:k].sum()) * 24
             parts.append(buf[off: off + int(cnt[k]) * 24])
         inbound = torch.cat(parts)
+        torch.cuda.current_stream().synchronize()  # torch.cat ran on torch's stream
         s.deliver(inbound.data_ptr(), inbound.numel() // 24)
     d_sh = np.concatenate([s.drain() for s in shards])
     assert len(d_sh) == len(d_ref)
@@ -272,6 +273,7 @@ def test_full_size_storm_properties():
 def _manual_sharded_step(shards, bounds, window):
     """step_sim on every shard, exchange through device buffers, deliver (one GPU, no collective)."""
     outs = []
+    torch.cuda.current_stream().synchronize()  # the engines run on their own streams (shard.py)
     for s in shards:
         buf = torch.empty(max(1, s.sim_capacity()) * 24, dtype=torch.uint8, device="cuda")
         cnt = s.step_sim(window, bounds, buf.data_ptr(), s.sim_capacity())
@@ -279,6 +281,7 @@ def _manual_sharded_step(shards, bounds, window):
     for k, s in enumerate(shards):
         parts = [buf[int(cnt[:k].sum()) * 24: int(cnt[:k + 1].sum()) * 24] for buf, cnt in outs]
         inbound = torch.cat(parts)
+        torch.cuda.current_stream().synchronize()  # torch.cat ran on torch's stream
         s.deliver(inbound.data_ptr(), inbound.numel() // 24)
 
 
