@@ -189,7 +189,11 @@ int tgsim_submit(void* engine, const tgsim_pkt* pkts, size_t n);
  * per source and tick Poisson(lambda) packets to a uniform destination != src, len U{64..1500}. */
 int tgsim_gen_storm(void* engine, double lambda, uint32_t n_ticks);
 /* Advances time by n_ticks: every offered packet of the window goes through filter -> netem ->
- * HTB; deliveries are routed to their destination and sorted.  Single-shard convenience. */
+ * HTB; deliveries are routed to their destination and sorted.  Single-shard convenience.
+ * On an engine that owns every peer the step is asynchronous on the engine's stream (with
+ * TGSIM_OPT_DISCARD_DELIVERIES and no gossip driver it returns without a host round trip); every
+ * call that reads results (drain, verdicts, stats, gossip_reached, sim_kernel_ms) synchronizes
+ * first.  A simulated-time overflow (-EOVERFLOW) is then reported by the next step or reader. */
 int tgsim_step(void* engine, uint32_t n_ticks);
 
 /* Multi-shard form of tgsim_step.  Phase 1 simulates the owned sources and writes the scheduled
@@ -235,7 +239,7 @@ int tgsim_barrier_poll(void* engine, uint32_t state, uint64_t target);
  * with HIP events on the engine's stream. */
 double tgsim_sim_kernel_ms(void* engine, uint64_t* n_launches, int reset);
 void* tgsim_stream(void* engine);
-/* Diagnostics: with TGSIM_STAMPS set at create time, the simulate kernel records 8 words per
+/* Diagnostics: with TGSIM_STAMPS set at create time, the simulate kernel records 24 words per
  * workgroup (s_memrealtime at its phase boundaries, batch count, HW_ID, queue sizes); copies them
  * for the last step and returns the word count (0 when disabled). */
 int64_t tgsim_debug_stamps(void* engine, uint64_t* out, size_t cap);
