@@ -199,12 +199,23 @@ int tgsim_step(void* engine, uint32_t n_ticks);
 /* Multi-shard form of tgsim_step.  Phase 1 simulates the owned sources and writes the scheduled
  * records into d_out (DEVICE memory, caller-owned, capacity out_cap records) grouped by the
  * destination's shard; rank_bounds[0..n_ranks] are the peer boundaries of the shards and
- * rank_counts[0..n_ranks-1] receives the per-shard record counts (host memory). */
+ * rank_counts[0..n_ranks-1] receives the per-shard record counts (host memory).  Returns once
+ * d_out is complete and every earlier delivery (tgsim_deliver_async) has finished. */
 int tgsim_step_sim(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* rank_bounds,
                    void* d_out, size_t out_cap, uint64_t* rank_counts);
 /* Phase 2: sorts the records addressed to this shard (DEVICE memory, n records) into the
  * delivery order and appends them to the drain buffer. */
 int tgsim_deliver(void* engine, const void* d_in, size_t n);
+/* Asynchronous phase 2: enqueues the delivery on the engine's delivery stream and returns.  The
+ * stream first waits for wait_event (a hipEvent_t recorded after the producer of d_in, e.g. the
+ * all-to-all; may be null), so the delivery of one step overlaps the next step's simulation.  d_in
+ * must stay valid until tgsim_sync (or any reader) returns; no count check. */
+int tgsim_deliver_async(void* engine, const void* d_in, size_t n, void* wait_event);
+/* Makes the engine's simulate stream wait for a hipEvent_t of another stream (e.g. the collective
+ * that still reads the d_out buffer the next tgsim_step_sim will overwrite). */
+int tgsim_wait_event(void* engine, void* event);
+/* Waits for all of the engine's device work; reports a pending -EOVERFLOW. */
+int tgsim_sync(void* engine);
 /* Upper bound of records phase 1 can emit for the next step (for sizing d_out). */
 int64_t tgsim_sim_capacity(void* engine);
 

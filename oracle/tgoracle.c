@@ -716,6 +716,19 @@ int tgo_deliver(void* p, const void* in, size_t n) {
     return 0;
 }
 
+/* Host memory, synchronous: the asynchronous forms of the engine are plain calls here. */
+int tgo_deliver_async(void* p, const void* in, size_t n, void* wait_event) {
+    (void)wait_event;
+    return tgo_deliver(p, in, n);
+}
+
+int tgo_wait_event(void* p, void* event) {
+    (void)event;
+    return p ? 0 : -EINVAL;
+}
+
+int tgo_sync(void* p) { return p ? 0 : -EINVAL; }
+
 int64_t tgo_sim_capacity(void* p) {
     oracle* o = (oracle*)p;
     return (int64_t)(2 * o->n_off + 1024ull * o->nsrc);

@@ -37,6 +37,9 @@ int tgo_step(void* o, uint32_t n_ticks);
 int tgo_step_sim(void* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out, size_t cap,
                  uint64_t* counts);
 int tgo_deliver(void* o, const void* in, size_t n);
+int tgo_deliver_async(void* o, const void* in, size_t n, void* wait_event);
+int tgo_wait_event(void* o, void* event);
+int tgo_sync(void* o);
 int64_t tgo_sim_capacity(void* o);
 int64_t tgo_pending_deliveries(void* o);
 int64_t tgo_drain(void* o, tgsim_delivery* out, size_t cap);

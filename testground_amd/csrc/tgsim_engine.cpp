@@ -196,7 +196,10 @@ struct tgsim_engine_s {
   tgsim_opts o{};
   std::string err;
   int dev = 0;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr;      // simulate stream: inputs, k_sim, routing, single-shard delivery
+  hipStream_t dst_st = nullptr;  // delivery stream of inbound records (tgsim_deliver*), overlaps the next k_sim
+  hipEvent_t ev_dst = nullptr;   // recorded after the last delivery on dst_st
+  hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
   // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
   std::vector<hipEvent_t> ev_pool;
@@ -245,7 +248,7 @@ struct tgsim_engine_s {
   // step output
   DevBuf<tgsim_delivery> d_emit;
   DevBuf<uint32_t> d_emit_n;
-  DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts and their scan
+  DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot, d_redges;  // routing: [rank][source] counts, scan, rank edges
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
   uint64_t h_dtot = 0;
@@ -407,14 +410,16 @@ int stage_host_input(Eng* E, uint32_t n_ticks) {
 
 // Device exclusive scan of cnt[0..n) into off[0..n] (off[n] = total); returns total on host.
 int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uint64_t>& blk,
-                DevBuf<uint64_t>& tot, uint64_t n, uint64_t* total, uint64_t* pos = nullptr) {
+                DevBuf<uint64_t>& tot, uint64_t n, uint64_t* total, uint64_t* pos = nullptr,
+                hipStream_t stream = nullptr) {
+  hipStream_t sq = stream ? stream : E->st;
   HIPCHK(off.ensure(n + 1));
   HIPCHK(blk.ensure((n + 1023) / 1024 + 1));
   HIPCHK(tot.ensure(1));
-  launch_scan(cnt.p, off.p, n, blk.p, tot.p, E->st, pos);
+  launch_scan(cnt.p, off.p, n, blk.p, tot.p, sq, pos);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(total, tot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
-  HIPCHK(hipStreamSynchronize(E->st));
+  HIPCHK(hipMemcpyAsync(total, tot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
+  HIPCHK(hipStreamSynchronize(sq));
   return 0;
 }
 
@@ -461,6 +466,7 @@ int check_sim_error(Eng* E) {
 // Every reader of device results goes through here: the step itself does not synchronize.
 int sync_stream(Eng* E) {
   HIPCHK(hipStreamSynchronize(E->st));
+  HIPCHK(hipStreamSynchronize(E->dst_st));
   return harvest_timing(E, true);
 }
 
@@ -583,11 +589,12 @@ int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out,
   HIPCHK(hipGetLastError());
   launch_scan(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, E->st);
   HIPCHK(hipGetLastError());
-  // per-rank totals: pos[r * S] .. pos[(r + 1) * S]
+  // per-rank totals: pos[r * S] .. pos[(r + 1) * S], gathered on the device, one copy
   std::vector<uint64_t> edges(n_ranks + 1);
-  for (uint32_t r = 0; r <= n_ranks; ++r)
-    HIPCHK(hipMemcpyAsync(&edges[r], E->d_rpos.p + static_cast<uint64_t>(r) * E->S, sizeof(uint64_t),
-                          hipMemcpyDeviceToHost, E->st));
+  HIPCHK(E->d_redges.ensure(9));
+  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->d_redges.p, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(edges.data(), E->d_redges.p, sizeof(uint64_t) * (n_ranks + 1), hipMemcpyDeviceToHost, E->st));
   HIPCHK(hipStreamSynchronize(E->st));
   for (uint32_t r = 0; r < n_ranks; ++r) counts[r] = edges[r + 1] - edges[r];
   if (edges[n_ranks] > out_cap)
@@ -619,7 +626,7 @@ GossipArgs gossip_args(Eng* E, uint64_t win0, uint32_t n_ticks) {
 
 // Output of a delivery sort of n records: the drain buffer (grown, undrained tail compacted to the
 // front) or, with TGSIM_OPT_DISCARD_DELIVERIES, a scratch buffer.
-int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out) {
+int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out, hipStream_t sq) {
   if (E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) {
     HIPCHK(E->d_sorted.ensure(n ? n : 1));
     *out = E->d_sorted.p;
@@ -631,8 +638,8 @@ int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out) {
     HIPCHK(nb.ensure(E->drain_n + n));
     if (E->drain_n)
       HIPCHK(hipMemcpyAsync(nb.p, E->d_drain.p + E->drain_head, sizeof(tgsim_delivery) * E->drain_n,
-                            hipMemcpyDeviceToDevice, E->st));
-    HIPCHK(hipStreamSynchronize(E->st));
+                            hipMemcpyDeviceToDevice, sq));
+    HIPCHK(hipStreamSynchronize(sq));
     E->d_drain.release();
     E->d_drain = nb;
     E->drain_head = 0;
@@ -642,34 +649,51 @@ int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out) {
   return 0;
 }
 
-// Records received by this shard (tgsim_deliver, or the routed records of tgsim_step on a
-// partial shard): histogram -> scan -> scatter -> per-destination order.
-int deliver(Eng* E, const tgsim_delivery* in, uint64_t n) {
+// Records received by this shard (tgsim_deliver*, or the routed records of tgsim_step on a
+// partial shard): histogram -> scan -> scatter -> per-destination order, on the delivery stream so
+// that it overlaps the next step's k_sim.  It waits for the simulate stream's work so far (the
+// records may come from it) and for `wait` (the producer of d_in, e.g. the collective's stream).
+// check: read the record count back and reject records addressed to other shards.
+int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool check) {
   const uint32_t nd = E->S;  // destinations owned by this shard
+  hipStream_t sq = E->dst_st;
+  HIPCHK(hipEventRecord(E->ev_sim, E->st));
+  HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+  if (wait) HIPCHK(hipStreamWaitEvent(sq, wait, 0));
   if (E->d_dcnt.cap < nd) {
     HIPCHK(E->d_dcnt.ensure(nd));
-    HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, E->st));
+    HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, sq));
   }
   HIPCHK(E->d_dpos.ensure(nd));
-  launch_dst_hist(in, n, E->o.shard_begin, E->d_dcnt.p, E->st);
+  launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq);
   HIPCHK(hipGetLastError());
-  uint64_t total = 0;
-  int rc = scan_counts(E, E->d_dcnt, E->d_doff, E->d_dblk, E->d_dtot, nd, &total, E->d_dpos.p);
-  if (rc) return rc;
-  if (total != n) return E->fail(-EINVAL, "deliver: %llu of %llu records address other shards",
-                                 static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
+  int rc = 0;
+  if (!check) {  // nothing on the host needs the count
+    HIPCHK(E->d_doff.ensure(nd + 1));
+    HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
+    HIPCHK(E->d_dtot.ensure(1));
+    launch_scan(E->d_dcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
+    HIPCHK(hipGetLastError());
+  } else {
+    uint64_t total = 0;
+    rc = scan_counts(E, E->d_dcnt, E->d_doff, E->d_dblk, E->d_dtot, nd, &total, E->d_dpos.p, sq);
+    if (rc) return rc;
+    if (total != n) return E->fail(-EINVAL, "deliver: %llu of %llu records address other shards",
+                                   static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
+  }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_dst_scatter(in, n, E->o.shard_begin, E->d_dpos.p, E->d_scatter.p, E->st);
+  launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq);
   HIPCHK(hipGetLastError());
   tgsim_delivery* dst = nullptr;
-  rc = delivery_out(E, n, &dst);
+  rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->st);
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq);
   HIPCHK(hipGetLastError());
   if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
-    launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, E->st);
+    launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, sq);
     HIPCHK(hipGetLastError());
   }
+  HIPCHK(hipEventRecord(E->ev_dst, sq));
   return 0;
 }
 
@@ -678,6 +702,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n) {
 // drain bookkeeping (and the gossip receipts) need the record count on the host.
 int deliver_local(Eng* E) {
   const uint32_t nd = E->N;
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // delivery buffers are shared with deliver()
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
@@ -695,7 +720,7 @@ int deliver_local(Eng* E) {
   launch_local_scatter(E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, 0, E->d_dpos.p, E->d_scatter.p, E->st);
   HIPCHK(hipGetLastError());
   tgsim_delivery* dst = nullptr;
-  int rc = delivery_out(E, n, &dst);
+  int rc = delivery_out(E, n, &dst, E->st);
   if (rc) return rc;
   launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->st);
   HIPCHK(hipGetLastError());
@@ -753,6 +778,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   };
   if ((rc = E->hip(hipSetDevice(E->dev), "hipSetDevice"))) return bail(rc);
   if ((rc = E->hip(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking), "stream"))) return bail(rc);
+  if ((rc = E->hip(hipStreamCreateWithFlags(&E->dst_st, hipStreamNonBlocking), "stream"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_dst, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_err), sizeof(uint64_t)), "pinned"))) return bail(rc);
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
@@ -791,12 +820,13 @@ void tgsim_destroy(void* e) {
   if (!E) return;
   (void)hipSetDevice(E->dev);
   if (E->st) (void)hipStreamSynchronize(E->st);
+  if (E->dst_st) (void)hipStreamSynchronize(E->dst_st);
   DevBuf<int> dummy;
   (void)dummy;
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_redges.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
@@ -808,6 +838,9 @@ void tgsim_destroy(void* e) {
   }
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
   if (E->h_err) (void)hipHostFree(E->h_err);
+  if (E->ev_dst) (void)hipEventDestroy(E->ev_dst);
+  if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
+  if (E->dst_st) (void)hipStreamDestroy(E->dst_st);
   if (E->st) (void)hipStreamDestroy(E->st);
   delete E;
 }
@@ -1011,6 +1044,7 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   if (!E || !E->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
   if (!E->staged.empty()) return E->fail(-EBUSY, "host packets already pending for the next step");
   HIPCHK(hipSetDevice(E->dev));
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // receipts are folded on the delivery stream
   const uint64_t win0 = E->now_tick + E->gen_q_ticks;
   const GossipArgs g = gossip_args(E, win0, n_ticks);
   Eng::GenWindow w;
@@ -1076,18 +1110,48 @@ int tgsim_step_sim(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* 
   if (rc) return rc;
   rc = route(E, n_ranks, bounds, static_cast<tgsim_delivery*>(d_out), out_cap, counts);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(E->st));
-  return finish_sim_timing(E);
+  HIPCHK(hipStreamSynchronize(E->st));  // d_out complete for the caller's exchange
+  // and the previous step's asynchronous delivery (it ran beside this k_sim) has released its
+  // input buffer, which the caller's next exchange may overwrite
+  HIPCHK(hipEventSynchronize(E->ev_dst));
+  rc = harvest_timing(E, false);
+  if (rc) return rc;
+  return check_sim_error(E);
 }
 
 int tgsim_deliver(void* e, const void* d_in, size_t n) {
   Eng* E = as_eng(e);
   if (!E || (!d_in && n)) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
-  int rc = deliver(E, static_cast<const tgsim_delivery*>(d_in), n);
+  int rc = deliver(E, static_cast<const tgsim_delivery*>(d_in), n, nullptr,
+                   !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES));
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(E->st));
+  HIPCHK(hipStreamSynchronize(E->dst_st));
   return 0;
+}
+
+int tgsim_deliver_async(void* e, const void* d_in, size_t n, void* wait_event) {
+  Eng* E = as_eng(e);
+  if (!E || (!d_in && n)) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  return deliver(E, static_cast<const tgsim_delivery*>(d_in), n, static_cast<hipEvent_t>(wait_event), false);
+}
+
+int tgsim_wait_event(void* e, void* event) {
+  Eng* E = as_eng(e);
+  if (!E || !event) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  HIPCHK(hipStreamWaitEvent(E->st, static_cast<hipEvent_t>(event), 0));
+  return 0;
+}
+
+int tgsim_sync(void* e) {
+  Eng* E = as_eng(e);
+  if (!E) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
+  return check_sim_error(E);
 }
 
 int tgsim_step(void* e, uint32_t n_ticks) {
@@ -1107,7 +1171,7 @@ int tgsim_step(void* e, uint32_t n_ticks) {
   uint64_t count = 0;
   rc = route(E, 1, bounds, E->d_bucket.p, E->d_bucket.cap, &count);
   if (rc) return rc;
-  rc = deliver(E, E->d_bucket.p, count);
+  rc = deliver(E, E->d_bucket.p, count, nullptr, true);
   if (rc) return rc;
   return finish_sim_timing(E);
 }

@@ -1226,22 +1226,33 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
   }
 }
 
+// Per-rank record ranges of the routed output: edges[r] = pos[r * n_src] (pos[n_ranks * n_src] is
+// the total), gathered so the host reads them with one copy.
+__global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* edges) {
+  const uint32_t r = threadIdx.x;
+  if (r <= n_ranks) edges[r] = pos[(size_t)r * n_src];
+}
+
 // ---------------------------------------------------------------------------------------------
 // Delivery: counting sort by destination (counts -> exclusive scan -> scatter through per-dst
 // cursors), then each destination's records ordered by (t, src, seq, clone first).
-__global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt) {
+// Records addressed outside [dst_begin, dst_begin + n_dst) are skipped (the host reports them as
+// -EINVAL when it reads the count; with discarded deliveries they are dropped).
+__global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[in[i].dst - dst_begin]), 1ull);
+  const uint32_t d = in[i].dst - dst_begin;
+  if (d < n_dst) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[d]), 1ull);
 }
 
 // Flat input (records received from every shard): pos[] starts as the exclusive scan of counts.
-__global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* pos,
-                              tgsim_delivery* out) {
+__global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst,
+                              uint64_t* pos, tgsim_delivery* out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const tgsim_delivery r = in[i];
-  out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[r.dst - dst_begin]), 1ull)] = r;
+  const uint32_t d = r.dst - dst_begin;
+  if (d < n_dst) out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[d]), 1ull)] = r;
 }
 
 // Single shard: straight from k_sim's per-source emit regions (counts were taken by k_sim).
@@ -1412,6 +1423,10 @@ void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_
                      (const uint64_t*)total);
 }
 
+void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* edges, hipStream_t st) {
+  hipLaunchKernelGGL(k_route_edges, dim3(1), dim3(64), 0, st, pos, n_src, n_ranks, edges);
+}
+
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
   RouteArgs a;
   a.emit = h.emit;
@@ -1430,15 +1445,17 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
   else hipLaunchKernelGGL(k_route_scatter, dim3(grid), dim3(256), 0, st, a);
 }
 
-void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt, hipStream_t st) {
+void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
+                     hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, cnt);
+  hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, n_dst, cnt);
 }
 
-void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* pos,
+void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
                         tgsim_delivery* out, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, pos, out);
+  hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, n_dst,
+                     pos, out);
 }
 
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,

@@ -35,8 +35,10 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
                  hipStream_t st, uint64_t* pos = nullptr);
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
-void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* cnt, hipStream_t st);
-void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint64_t* pos,
+void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* edges, hipStream_t st);
+void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
+                     hipStream_t st);
+void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
                         tgsim_delivery* out, hipStream_t st);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st);

@@ -165,6 +165,18 @@ class CABIEngine:
     def deliver(self, d_in: int, n: int) -> None:
         self._check(self._fn("deliver")(self._h, C.c_void_p(d_in), n), "deliver")
 
+    def deliver_async(self, d_in: int, n: int, wait_event: int = 0) -> None:
+        """Delivery enqueued on the engine's delivery stream after `wait_event` (a raw
+        hipEvent_t, e.g. torch.cuda.Event().cuda_event); overlaps the next step_sim."""
+        self._check(self._fn("deliver_async")(self._h, C.c_void_p(d_in), n, C.c_void_p(wait_event or None)),
+                    "deliver_async")
+
+    def wait_event(self, event: int) -> None:
+        self._check(self._fn("wait_event")(self._h, C.c_void_p(event)), "wait_event")
+
+    def sync(self) -> None:
+        self._check(self._fn("sync")(self._h), "sync")
+
     def sim_capacity(self) -> int:
         return self._check(self._fn("sim_capacity")(self._h), "sim_capacity")
 
