@@ -156,7 +156,8 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        from testground_amd.shard import init_rccl
+        init_rccl(torch.device("cuda", local))
     peers_total = a.peers * world
     lo, hi = rank * a.peers, (rank + 1) * a.peers
     kw = dict(lookahead_ns=workloads.GOSSIP_MIN_LAT) if a.workload == "gossip" else {}
@@ -205,8 +206,14 @@ def main():
             one_step()
         for _ in range(a.warmup + a.steps):
             eng.gen_storm(a.lam, a.window)  # inputs resident in HBM before the timed region
-    for _ in range(a.warmup):
-        one_step()
+    def run_steps(n):
+        if stepper is not None and a.workload == "storm":  # pre-generated: simulate one step ahead
+            stepper.run(n, a.window)
+        else:
+            for _ in range(n):
+                one_step()
+
+    run_steps(a.warmup)
     eng.drain()
     s0 = eng.stats()
     eng.sim_kernel_ms(reset=True)
@@ -214,8 +221,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        one_step()
+    run_steps(a.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

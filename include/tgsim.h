@@ -203,6 +203,15 @@ int tgsim_step(void* engine, uint32_t n_ticks);
  * d_out is complete and every earlier delivery (tgsim_deliver_async) has finished. */
 int tgsim_step_sim(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* rank_bounds,
                    void* d_out, size_t out_cap, uint64_t* rank_counts);
+/* tgsim_step_sim in two halves, so a host can start the next step's simulation before it
+ * exchanges this step's records: _launch enqueues the simulation and the routing into d_out and
+ * returns; _finish waits for the oldest launched step (and for earlier asynchronous deliveries)
+ * and fills its counts.  Up to two launched steps may be pending (each with its own d_out), so the
+ * simulate stream always has the next step queued; tgsim_step and tgsim_step_sim refuse (-EBUSY)
+ * while any is.  Records beyond out_cap are dropped and reported as -ENOSPC by _finish. */
+int tgsim_step_sim_launch(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* rank_bounds,
+                          void* d_out, size_t out_cap);
+int tgsim_step_sim_finish(void* engine, uint64_t* rank_counts);
 /* Phase 2: sorts the records addressed to this shard (DEVICE memory, n records) into the
  * delivery order and appends them to the drain buffer. */
 int tgsim_deliver(void* engine, const void* d_in, size_t n);

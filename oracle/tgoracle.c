@@ -200,6 +200,10 @@ typedef struct {
     uint64_t now_tick;
     offered* off;
     size_t n_off, cap_off;
+    /* device-generated windows queued ahead of the steps that consume them (tgsim_gen_*) */
+    struct genwin { offered* pk; size_t n, cap; uint32_t ticks; } *gq;
+    size_t gq_n, gq_cap;
+    uint64_t gq_ticks;
     uint8_t* verdicts;
     size_t n_verdicts;
     tgsim_delivery* out; /* undrained deliveries */
@@ -214,6 +218,9 @@ typedef struct {
     tgsim_gossip g;
     uint32_t* g_first;
     uint64_t* g_fwd;
+    /* split step_sim: counts of a launched, not yet finished step */
+    uint64_t pend_counts[2][8];
+    uint32_t pend_ranks[2], pend_head, pend_n;
 } oracle;
 
 #define HCAP 1024u
@@ -234,6 +241,22 @@ static void* grow(void* p, size_t* cap, size_t need, size_t elem) {
     if (!q) abort();
     *cap = nc;
     return q;
+}
+
+/* Appends a new generated window of n_ticks starting at now_tick + gq_ticks. */
+static struct genwin* gen_window(oracle* o, uint32_t n_ticks) {
+    o->gq = grow(o->gq, &o->gq_cap, o->gq_n + 1, sizeof *o->gq);
+    struct genwin* w = &o->gq[o->gq_n++];
+    memset(w, 0, sizeof *w);
+    w->ticks = n_ticks;
+    return w;
+}
+
+static void gen_push(struct genwin* w, const tgsim_pkt* k) {
+    w->pk = grow(w->pk, &w->cap, w->n + 1, sizeof(offered));
+    w->pk[w->n].p = *k;
+    w->pk[w->n].idx = w->n;
+    w->n++;
 }
 
 static void reset_netem(oracle* o, uint32_t s) {
@@ -295,6 +318,8 @@ void tgo_destroy(void* p) {
         free(o->src[s].ring);
         free(o->src[s].rules);
     }
+    for (size_t i = 0; i < o->gq_n; ++i) free(o->gq[i].pk);
+    free(o->gq);
     free(o->src); free(o->enabled); free(o->ip); free(o->off); free(o->verdicts);
     free(o->out); free(o->step_out); free(o->gen_seq); free(o->g_first); free(o->g_fwd);
     free(o);
@@ -382,6 +407,7 @@ int tgo_configure(void* p, uint32_t peer, const tgsim_config* cfg) {
 int tgo_submit(void* p, const tgsim_pkt* pkts, size_t n) {
     oracle* o = (oracle*)p;
     if (!o || (!pkts && n)) return -EINVAL;
+    if (o->gq_n) return fail(o, -EBUSY, "generated traffic already pending for the next step");
     for (size_t i = 0; i < n; ++i) {
         const tgsim_pkt* k = &pkts[i];
         if (k->src < o->o.shard_begin || k->src >= o->o.shard_end)
@@ -418,11 +444,16 @@ int tgo_gen_storm(void* p, double lambda, uint32_t n_ticks) {
     tgo_poisson_table(lambda, tab);
     uint32_t gk[2] = {o->key[0] ^ 0x9E3779B9u, o->key[1] ^ 0x7F4A7C15u};
     uint32_t N = o->o.n_peers;
+    if (n_ticks == 0) return -EINVAL;
+    if (o->n_off) return fail(o, -EBUSY, "host packets already pending for the next step");
+    const uint64_t base = o->now_tick + o->gq_ticks;
+    struct genwin* w = gen_window(o, n_ticks);
+    o->gq_ticks += n_ticks;
     if (N < 2) return 0;
     for (uint32_t s = 0; s < o->nsrc; ++s) {
         uint32_t src = o->o.shard_begin + s;
         for (uint32_t t = 0; t < n_ticks; ++t) {
-            uint32_t abs_t = (uint32_t)(o->now_tick + t);
+            uint32_t abs_t = (uint32_t)(base + t);
             uint32_t ctr[4] = {src, abs_t, 0x53544F52u, 0}, r[4];
             tgo_philox4x32_10(ctr, gk, r);
             uint32_t cnt = 0;
@@ -435,10 +466,7 @@ int tgo_gen_storm(void* p, double lambda, uint32_t n_ticks) {
                 tgsim_pkt k;
                 k.src = src; k.dst = d; k.seq = o->gen_seq[s]++;
                 k.len = (uint16_t)(64 + q[1] % 1437u); k.tick = (uint16_t)t;
-                o->off = (offered*)grow(o->off, &o->cap_off, o->n_off + 1, sizeof(offered));
-                o->off[o->n_off].p = k;
-                o->off[o->n_off].idx = o->n_off;
-                o->n_off++;
+                gen_push(w, &k);
             }
         }
     }
@@ -447,9 +475,11 @@ int tgo_gen_storm(void* p, double lambda, uint32_t n_ticks) {
 
 int64_t tgo_offered(void* p, tgsim_pkt* out, size_t cap) {
     oracle* o = (oracle*)p;
-    size_t n = o->n_off < cap ? o->n_off : cap;
-    for (size_t i = 0; i < n; ++i) out[i] = o->off[i].p;
-    return (int64_t)o->n_off;
+    const offered* src = o->n_off || !o->gq_n ? o->off : o->gq[0].pk;  /* next step's input */
+    size_t m = o->n_off || !o->gq_n ? o->n_off : o->gq[0].n;
+    size_t n = m < cap ? m : cap;
+    for (size_t i = 0; i < n; ++i) out[i] = src[i].p;
+    return (int64_t)m;
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -634,6 +664,18 @@ static uint64_t queue_bytes(const oracle* o) {
 
 static int step_core(oracle* o, uint32_t n_ticks) {
     if (n_ticks == 0) return -EINVAL;
+    if (o->gq_n) { /* the oldest generated window is this step's input */
+        if (o->n_off) return fail(o, -EBUSY, "host packets and generated traffic in one step");
+        if (o->gq[0].ticks != n_ticks)
+            return fail(o, -EINVAL, "generated window spans %u ticks, step is %u", o->gq[0].ticks, n_ticks);
+        free(o->off);
+        o->off = o->gq[0].pk;
+        o->n_off = o->gq[0].n;
+        o->cap_off = o->gq[0].cap;
+        o->gq_ticks -= n_ticks;
+        memmove(o->gq, o->gq + 1, (o->gq_n - 1) * sizeof *o->gq);
+        o->gq_n--;
+    }
     for (size_t i = 0; i < o->n_off; ++i)
         if (o->off[i].p.tick >= n_ticks)
             return fail(o, -EINVAL, "packet %zu: tick %u beyond step of %u ticks", i, o->off[i].p.tick, n_ticks);
@@ -676,6 +718,7 @@ static void deliver_records(oracle* o, const tgsim_delivery* recs, size_t n) {
 int tgo_step(void* p, uint32_t n_ticks) {
     oracle* o = (oracle*)p;
     if (!o) return -EINVAL;
+    if (o->pend_n) return fail(o, -EBUSY, "launched steps are not finished yet");
     int rc = step_core(o, n_ticks);
     if (rc) return rc;
     deliver_records(o, o->step_out, o->n_step);
@@ -684,9 +727,8 @@ int tgo_step(void* p, uint32_t n_ticks) {
 
 /* Multi-shard form: scheduled records grouped by the destination's shard into `out` (host
  * memory here), counts per shard in `counts`. */
-int tgo_step_sim(void* p, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out,
-                 size_t cap, uint64_t* counts) {
-    oracle* o = (oracle*)p;
+static int step_sim_core(oracle* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out,
+                         size_t cap, uint64_t* counts) {
     if (!o || !n_ranks || n_ranks > 8 || !bounds || !counts) return -EINVAL;
     if (bounds[0] != 0 || bounds[n_ranks] != o->o.n_peers) return fail(o, -EINVAL, "rank bounds must cover [0, n_peers)");
     int rc = step_core(o, n_ticks);
@@ -702,6 +744,38 @@ int tgo_step_sim(void* p, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bo
                 counts[r]++;
             }
     }
+    return 0;
+}
+
+int tgo_step_sim(void* p, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out,
+                 size_t cap, uint64_t* counts) {
+    oracle* o = (oracle*)p;
+    if (o && o->pend_n) return fail(o, -EBUSY, "launched steps are not finished yet");
+    return step_sim_core(o, n_ticks, n_ranks, bounds, out, cap, counts);
+}
+
+/* Split form (up to two launched steps pending): the oracle runs the whole step at launch and
+ * keeps its counts for the matching finish. */
+int tgo_step_sim_launch(void* p, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out,
+                        size_t cap) {
+    oracle* o = (oracle*)p;
+    if (!o) return -EINVAL;
+    if (o->pend_n == 2) return fail(o, -EBUSY, "two launched steps are not finished yet");
+    const uint32_t k = (o->pend_head + o->pend_n) % 2;
+    int rc = step_sim_core(o, n_ticks, n_ranks, bounds, out, cap, o->pend_counts[k]);
+    if (rc) return rc;
+    o->pend_ranks[k] = n_ranks;
+    o->pend_n++;
+    return 0;
+}
+
+int tgo_step_sim_finish(void* p, uint64_t* counts) {
+    oracle* o = (oracle*)p;
+    if (!o || !counts || !o->pend_n) return -EINVAL;
+    const uint32_t k = o->pend_head;
+    o->pend_head = (k + 1) % 2;
+    o->pend_n--;
+    for (uint32_t r = 0; r < o->pend_ranks[k]; ++r) counts[r] = o->pend_counts[k][r];
     return 0;
 }
 
@@ -731,7 +805,8 @@ int tgo_sync(void* p) { return p ? 0 : -EINVAL; }
 
 int64_t tgo_sim_capacity(void* p) {
     oracle* o = (oracle*)p;
-    return (int64_t)(2 * o->n_off + 1024ull * o->nsrc);
+    const size_t n = o->gq_n ? o->gq[0].n : o->n_off;
+    return (int64_t)(2 * n + 1024ull * o->nsrc);
 }
 
 int64_t tgo_pending_deliveries(void* p) {
@@ -827,7 +902,9 @@ static void gossip_receive(oracle* o, const tgsim_delivery* recs, size_t n) {
 int tgo_gen_gossip(void* p, uint32_t n_ticks) {
     oracle* o = (oracle*)p;
     if (!o || !o->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
-    uint64_t A = o->now_tick, B = o->now_tick + n_ticks;
+    if (o->n_off) return fail(o, -EBUSY, "host packets already pending for the next step");
+    uint64_t A = o->now_tick + o->gq_ticks, B = A + n_ticks;
+    struct genwin* w = gen_window(o, n_ticks);
     for (uint32_t s = 0; s < o->nsrc; ++s) {
         uint32_t src = o->o.shard_begin + s;
         for (;;) { /* floods due in the window, earliest receipt first, then by flood id */
@@ -836,8 +913,12 @@ int tgo_gen_gossip(void* p, uint32_t n_ticks) {
                 if (o->g_fwd[s] >> f & 1) continue;
                 uint32_t t = o->g_first[64ull * s + f];
                 if (t >= B) continue;
-                if (t < A) return fail(o, -EINVAL, "gossip: receipt at tick %u precedes the window at %llu", t,
-                                       (unsigned long long)A);
+                if (t < A) { /* the window is not queued */
+                    free(w->pk);
+                    o->gq_n--;
+                    return fail(o, -EINVAL, "gossip: receipt at tick %u precedes the window at %llu", t,
+                                (unsigned long long)A);
+                }
                 if (best < 0 || t < o->g_first[64ull * s + (uint32_t)best]) best = (int)f;
             }
             if (best < 0) break;
@@ -850,13 +931,11 @@ int tgo_gen_gossip(void* p, uint32_t n_ticks) {
                 pk.seq = (uint32_t)best * o->g.degree + k;
                 pk.len = (uint16_t)o->g.msg_len;
                 pk.tick = (uint16_t)(t - A);
-                o->off = (offered*)grow(o->off, &o->cap_off, o->n_off + 1, sizeof(offered));
-                o->off[o->n_off].p = pk;
-                o->off[o->n_off].idx = o->n_off;
-                o->n_off++;
+                gen_push(w, &pk);
             }
         }
     }
+    o->gq_ticks += n_ticks;
     return 0;
 }
 

@@ -36,6 +36,8 @@ int tgo_gen_storm(void* o, double lambda, uint32_t n_ticks);
 int tgo_step(void* o, uint32_t n_ticks);
 int tgo_step_sim(void* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out, size_t cap,
                  uint64_t* counts);
+int tgo_step_sim_launch(void* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out, size_t cap);
+int tgo_step_sim_finish(void* o, uint64_t* counts);
 int tgo_deliver(void* o, const void* in, size_t n);
 int tgo_deliver_async(void* o, const void* in, size_t n, void* wait_event);
 int tgo_wait_event(void* o, void* event);

@@ -12,17 +12,17 @@ import torch.distributed as dist  # noqa: E402
 
 from testground_amd import abi, workloads  # noqa: E402
 from testground_amd.engine import Engine  # noqa: E402
-from testground_amd.shard import ShardedStepper  # noqa: E402
+from testground_amd.shard import ShardedStepper, init_rccl  # noqa: E402
 
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29531")
 torch.cuda.set_device(0)
-dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+init_rccl(torch.device("cuda", 0), rank=0, world_size=1)
 n, win, steps = 10_000, 2000, 10
-for mode in ("local", "sharded"):
+for mode in os.environ.get("MODES", "local,sharded,pipelined").split(","):
     e = Engine(n, flags=abi.OPT_DISCARD_DELIVERIES)
     workloads.configure_storm(e, n)
-    st = ShardedStepper(e, [0, n], device="cuda:0") if mode == "sharded" else None
+    st = ShardedStepper(e, [0, n], device="cuda:0") if mode != "local" else None
     step = e.step if st is None else st.step
     for _ in range(60 + steps):
         e.gen_storm(0.5, win)
@@ -31,8 +31,11 @@ for mode in ("local", "sharded"):
     torch.cuda.synchronize()
     e.sim_kernel_ms(reset=True)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step(win)
+    if mode == "pipelined":
+        st.run(steps, win)
+    else:
+        for _ in range(steps):
+            step(win)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps
     k, _ = e.sim_kernel_ms()

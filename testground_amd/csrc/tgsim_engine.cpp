@@ -16,6 +16,7 @@
 #include <map>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "tgsim_launch.h"
@@ -204,6 +205,17 @@ struct tgsim_engine_s {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
   std::vector<hipEvent_t> ev_pool;
   uint64_t* h_err = nullptr;  // pinned copy of the sticky device error word, refreshed every step
+  // launched, unfinished routed steps (tgsim_step_sim_launch), oldest at route_head: pinned
+  // per-rank record edges behind an event, per slot
+  static constexpr uint32_t kRouteSlots = 2;
+  uint64_t* h_edges = nullptr;  // kRouteSlots x 16 words
+  hipEvent_t ev_route[kRouteSlots] = {};
+  uint32_t route_ranks[kRouteSlots] = {};
+  size_t route_cap[kRouteSlots] = {};
+  uint64_t route_seq[kRouteSlots] = {};
+  uint64_t route_next_seq = 0;
+  uint32_t route_head = 0, route_n = 0;
+  bool st_delivered = false;  // deliver_local wrote delivery buffers on the simulate stream
   uint32_t S = 0, N = 0;
   uint64_t now_tick = 0;
   uint32_t key0 = 0, key1 = 0;
@@ -248,7 +260,7 @@ struct tgsim_engine_s {
   // step output
   DevBuf<tgsim_delivery> d_emit;
   DevBuf<uint32_t> d_emit_n;
-  DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot, d_redges;  // routing: [rank][source] counts, scan, rank edges
+  DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
   uint64_t h_dtot = 0;
@@ -531,6 +543,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   }
   a.dst_cnt = nullptr;
   if (local_hist) {
+    HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // the histogram is shared with deliver()
     if (E->d_dcnt.cap < E->N) {
       HIPCHK(E->d_dcnt.ensure(E->N));
       HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, E->st));
@@ -567,8 +580,10 @@ int finish_sim_timing(Eng* E) {
   return check_sim_error(E);
 }
 
-int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap,
-          uint64_t* counts) {
+// Groups the step's scheduled records by destination shard into `out`, all on the simulate stream:
+// per-(rank, source) counts -> scan -> ordered scatter; the per-rank edges go to pinned host memory
+// behind ev_route, so the host can launch the next step before it reads them (route_finish).
+int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap) {
   RouteArgsHost h;
   memset(&h, 0, sizeof h);
   h.emit = E->d_emit.p;
@@ -585,24 +600,69 @@ int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out,
   h.cnt = E->d_rcnt.p;
   h.pos = E->d_rpos.p;
   h.out = out;
+  h.out_cap = out_cap;
   launch_route(h, 0, E->st);
   HIPCHK(hipGetLastError());
   launch_scan(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, E->st);
   HIPCHK(hipGetLastError());
-  // per-rank totals: pos[r * S] .. pos[(r + 1) * S], gathered on the device, one copy
-  std::vector<uint64_t> edges(n_ranks + 1);
-  HIPCHK(E->d_redges.ensure(9));
-  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->d_redges.p, E->st);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(edges.data(), E->d_redges.p, sizeof(uint64_t) * (n_ranks + 1), hipMemcpyDeviceToHost, E->st));
-  HIPCHK(hipStreamSynchronize(E->st));
-  for (uint32_t r = 0; r < n_ranks; ++r) counts[r] = edges[r + 1] - edges[r];
-  if (edges[n_ranks] > out_cap)
-    return E->fail(-ENOSPC, "route: %llu records exceed capacity %zu",
-                   static_cast<unsigned long long>(edges[n_ranks]), out_cap);
   launch_route(h, 1, E->st);
   HIPCHK(hipGetLastError());
+  // per-rank totals: pos[r * S] .. pos[(r + 1) * S], published to the slot's pinned words
+  const uint32_t k = (E->route_head + E->route_n) % Eng::kRouteSlots;
+  E->route_seq[k] = ++E->route_next_seq;
+  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->h_edges + 16 * k, E->route_seq[k], E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(E->ev_route[k], E->st));
+  E->route_ranks[k] = n_ranks;
+  E->route_cap[k] = out_cap;
+  E->route_n++;
   return 0;
+}
+
+// Spins until the device publishes `want` into the pinned word (kernels release it at system
+// scope); `ev`, recorded after the publishing kernel, tells a fault from a slow step.
+int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev) {
+  for (uint32_t it = 1;; ++it) {
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == want) return 0;
+    if ((it & 255) == 0) {
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == want) return 0;
+        return E->fail(-EIO, "route: step finished without publishing its edges");
+      }
+      if (q != hipErrorNotReady) HIPCHK(q);
+      std::this_thread::yield();
+    }
+  }
+}
+
+// Waits for the oldest launched step's records and edges (and for the asynchronous deliveries
+// enqueued so far, whose input buffers the caller's next exchange may overwrite); per-rank counts
+// into `counts`.
+int route_finish(Eng* E, uint64_t* counts) {
+  if (!E->route_n) return E->fail(-EINVAL, "no routed step pending");
+  const uint32_t k = E->route_head;
+  E->route_head = (k + 1) % Eng::kRouteSlots;
+  E->route_n--;
+  int rc = wait_published(E, &E->h_edges[16 * k + 15], E->route_seq[k], E->ev_route[k]);
+  if (rc) return rc;
+  HIPCHK(hipEventSynchronize(E->ev_dst));
+  const uint32_t n_ranks = E->route_ranks[k];
+  const uint64_t* edges = E->h_edges + 16 * k;
+  for (uint32_t r = 0; r < n_ranks; ++r) counts[r] = edges[r + 1] - edges[r];
+  if (edges[n_ranks] > E->route_cap[k])
+    return E->fail(-ENOSPC, "route: %llu records exceed capacity %zu",
+                   static_cast<unsigned long long>(edges[n_ranks]), E->route_cap[k]);
+  rc = harvest_timing(E, false);
+  if (rc) return rc;
+  return check_sim_error(E);
+}
+
+int route(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap,
+          uint64_t* counts) {
+  int rc = route_launch(E, n_ranks, bounds, out, out_cap);
+  if (rc) return rc;
+  return route_finish(E, counts);
 }
 
 GossipArgs gossip_args(Eng* E, uint64_t win0, uint32_t n_ticks) {
@@ -652,13 +712,17 @@ int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out, hipStream_t sq) {
 // Records received by this shard (tgsim_deliver*, or the routed records of tgsim_step on a
 // partial shard): histogram -> scan -> scatter -> per-destination order, on the delivery stream so
 // that it overlaps the next step's k_sim.  It waits for the simulate stream's work so far (the
-// records may come from it) and for `wait` (the producer of d_in, e.g. the collective's stream).
+// records come from tgsim_step_sim, which completed them before returning) only when a local step
+// last wrote the delivery buffers there, and for `wait` (the producer of d_in, e.g. the collective).
 // check: read the record count back and reject records addressed to other shards.
 int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool check) {
   const uint32_t nd = E->S;  // destinations owned by this shard
   hipStream_t sq = E->dst_st;
-  HIPCHK(hipEventRecord(E->ev_sim, E->st));
-  HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+  if (E->st_delivered) {  // the delivery buffers were last written on the simulate stream
+    HIPCHK(hipEventRecord(E->ev_sim, E->st));
+    HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+    E->st_delivered = false;
+  }
   if (wait) HIPCHK(hipStreamWaitEvent(sq, wait, 0));
   if (E->d_dcnt.cap < nd) {
     HIPCHK(E->d_dcnt.ensure(nd));
@@ -703,6 +767,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
 int deliver_local(Eng* E) {
   const uint32_t nd = E->N;
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // delivery buffers are shared with deliver()
+  E->st_delivered = true;
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
@@ -778,11 +843,23 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   };
   if ((rc = E->hip(hipSetDevice(E->dev), "hipSetDevice"))) return bail(rc);
   if ((rc = E->hip(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking), "stream"))) return bail(rc);
-  if ((rc = E->hip(hipStreamCreateWithFlags(&E->dst_st, hipStreamNonBlocking), "stream"))) return bail(rc);
+  // the delivery stream gets the high priority: ROCclr puts it on a hardware queue of its own, so
+  // the delivery of one step runs beside the next k_sim instead of behind it in one queue
+  int prio_lo = 0, prio_hi = 0;
+  if ((rc = E->hip(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), "stream"))) return bail(rc);
+  if ((rc = E->hip(hipStreamCreateWithPriority(&E->dst_st, hipStreamNonBlocking, prio_hi), "stream")))
+    return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_dst, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_err), sizeof(uint64_t)), "pinned"))) return bail(rc);
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_edges), 16 * Eng::kRouteSlots * sizeof(uint64_t),
+                                 hipHostMallocCoherent | hipHostMallocMapped),
+                   "pinned")))
+    return bail(rc);
+  memset(E->h_edges, 0, 16 * Eng::kRouteSlots * sizeof(uint64_t));
+  for (hipEvent_t& ev : E->ev_route)
+    if ((rc = E->hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return bail(rc);
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
@@ -826,7 +903,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_redges.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
@@ -838,6 +915,9 @@ void tgsim_destroy(void* e) {
   }
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
   if (E->h_err) (void)hipHostFree(E->h_err);
+  if (E->h_edges) (void)hipHostFree(E->h_edges);
+  for (hipEvent_t ev : E->ev_route)
+    if (ev) (void)hipEventDestroy(ev);
   if (E->ev_dst) (void)hipEventDestroy(E->ev_dst);
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->dst_st) (void)hipStreamDestroy(E->dst_st);
@@ -1099,24 +1179,32 @@ int64_t tgsim_sim_capacity(void* e) {
   return static_cast<int64_t>(2 * n + static_cast<uint64_t>(kHeapCap) * E->S);
 }
 
-int tgsim_step_sim(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* d_out,
-                   size_t out_cap, uint64_t* counts) {
+int tgsim_step_sim_launch(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* d_out,
+                          size_t out_cap) {
   Eng* E = as_eng(e);
-  if (!E || n_ticks == 0 || n_ranks == 0 || n_ranks > 8 || !bounds || !counts || (!d_out && out_cap))
-    return -EINVAL;
+  if (!E || n_ticks == 0 || n_ranks == 0 || n_ranks > 8 || !bounds || (!d_out && out_cap)) return -EINVAL;
   if (bounds[0] != 0 || bounds[n_ranks] != E->N) return E->fail(-EINVAL, "rank bounds must cover [0, n_peers)");
+  if (E->route_n == Eng::kRouteSlots) return E->fail(-EBUSY, "two launched steps are not finished yet");
   HIPCHK(hipSetDevice(E->dev));
   int rc = run_sim(E, n_ticks);
   if (rc) return rc;
-  rc = route(E, n_ranks, bounds, static_cast<tgsim_delivery*>(d_out), out_cap, counts);
+  return route_launch(E, n_ranks, bounds, static_cast<tgsim_delivery*>(d_out), out_cap);
+}
+
+int tgsim_step_sim_finish(void* e, uint64_t* counts) {
+  Eng* E = as_eng(e);
+  if (!E || !counts) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  return route_finish(E, counts);
+}
+
+int tgsim_step_sim(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* d_out,
+                   size_t out_cap, uint64_t* counts) {
+  if (!counts) return -EINVAL;
+  if (as_eng(e) && as_eng(e)->route_n) return as_eng(e)->fail(-EBUSY, "launched steps are not finished yet");
+  int rc = tgsim_step_sim_launch(e, n_ticks, n_ranks, bounds, d_out, out_cap);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(E->st));  // d_out complete for the caller's exchange
-  // and the previous step's asynchronous delivery (it ran beside this k_sim) has released its
-  // input buffer, which the caller's next exchange may overwrite
-  HIPCHK(hipEventSynchronize(E->ev_dst));
-  rc = harvest_timing(E, false);
-  if (rc) return rc;
-  return check_sim_error(E);
+  return tgsim_step_sim_finish(e, counts);
 }
 
 int tgsim_deliver(void* e, const void* d_in, size_t n) {
@@ -1157,6 +1245,7 @@ int tgsim_sync(void* e) {
 int tgsim_step(void* e, uint32_t n_ticks) {
   Eng* E = as_eng(e);
   if (!E || n_ticks == 0) return -EINVAL;
+  if (E->route_n) return E->fail(-EBUSY, "launched steps are not finished yet");
   HIPCHK(hipSetDevice(E->dev));
   if (E->S == E->N) {  // whole population on this engine: asynchronous local delivery
     int rc = run_sim(E, n_ticks, true);

@@ -1164,6 +1164,7 @@ struct RouteArgs {
   uint64_t* cnt;                 // [n_ranks][n_src] records per (rank, source)
   const uint64_t* pos;           // exclusive scan of cnt
   tgsim_delivery* out;
+  uint64_t out_cap;              // records beyond it are not written (the host reports -ENOSPC)
 };
 
 __device__ __forceinline__ uint32_t rank_of(const RouteArgs& a, uint32_t dst) {
@@ -1219,7 +1220,10 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
 #pragma unroll
       for (uint32_t q = 0; q < 8; ++q) {
         const uint64_t m = __ballot(rk == q);
-        if (rk == q) a.out[run[q] + __popcll(m & below)] = r;
+        if (rk == q) {
+          const uint64_t p = run[q] + __popcll(m & below);
+          if (p < a.out_cap) a.out[p] = r;
+        }
         run[q] += __popcll(m);
       }
     }
@@ -1228,9 +1232,14 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
 
 // Per-rank record ranges of the routed output: edges[r] = pos[r * n_src] (pos[n_ranks * n_src] is
 // the total), gathered so the host reads them with one copy.
-__global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* edges) {
+// Per-rank record edges straight into the host's pinned slot, then the slot's sequence word
+// (system-scope release): the host polls that word instead of synchronizing on an event, which
+// would also wait for the next step's k_sim queued behind this kernel.
+__global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq) {
   const uint32_t r = threadIdx.x;
-  if (r <= n_ranks) edges[r] = pos[(size_t)r * n_src];
+  if (r <= n_ranks) slot[r] = pos[(size_t)r * n_src];
+  __threadfence_system();
+  if (r == 0) __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1423,8 +1432,9 @@ void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_
                      (const uint64_t*)total);
 }
 
-void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* edges, hipStream_t st) {
-  hipLaunchKernelGGL(k_route_edges, dim3(1), dim3(64), 0, st, pos, n_src, n_ranks, edges);
+void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_route_edges, dim3(1), dim3(64), 0, st, pos, n_src, n_ranks, slot, seq);
 }
 
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
@@ -1438,6 +1448,7 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
   a.cnt = h.cnt;
   a.pos = h.pos;
   a.out = h.out;
+  a.out_cap = h.out_cap;
   uint32_t grid = (h.n_src + 3) / 4;
   if (grid > 4096) grid = 4096;
   if (grid == 0) grid = 1;

@@ -20,6 +20,7 @@ struct RouteArgsHost {
   uint64_t* cnt;        // [n_ranks][n_src]
   const uint64_t* pos;  // exclusive scan of cnt
   tgsim_delivery* out;
+  uint64_t out_cap;
 };
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
@@ -35,7 +36,9 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
                  hipStream_t st, uint64_t* pos = nullptr);
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
-void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* edges, hipStream_t st);
+// edges[0..n_ranks] into slot[0..n_ranks] (pinned host memory), then seq into slot[15].
+void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
+                        hipStream_t st);
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
                      hipStream_t st);
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,

@@ -81,6 +81,7 @@ class CABIEngine:
             exc = EngineUnavailable if rc in (-errno.ENODEV, -errno.EPROTO) else EngineError
             raise exc(rc, f"{prefix}create failed")
         self._h = h
+        self._launched: list = []  # rank counts of launched, unfinished steps (step_sim_launch)
 
     def _fn(self, name):
         return getattr(self._lib, self._p + name)
@@ -160,6 +161,22 @@ class CABIEngine:
         b = (C.c_uint32 * len(bounds))(*bounds)
         counts = (C.c_uint64 * nr)()
         self._check(self._fn("step_sim")(self._h, n_ticks, nr, b, C.c_void_p(d_out), out_cap, counts), "step_sim")
+        return np.array(list(counts), dtype=np.uint64)
+
+    def step_sim_launch(self, n_ticks: int, bounds: Sequence[int], d_out: int, out_cap: int) -> None:
+        """First half of step_sim: the step runs on the engine stream; step_sim_finish waits for
+        it and returns the per-rank counts. The host may enqueue other work (and one more launched
+        step) in between."""
+        nr = len(bounds) - 1
+        b = (C.c_uint32 * len(bounds))(*bounds)
+        self._check(self._fn("step_sim_launch")(self._h, n_ticks, nr, b, C.c_void_p(d_out), out_cap),
+                    "step_sim_launch")
+        self._launched.append(nr)
+
+    def step_sim_finish(self) -> np.ndarray:
+        """Counts of the oldest launched step (up to two may be pending)."""
+        counts = (C.c_uint64 * self._launched.pop(0))()
+        self._check(self._fn("step_sim_finish")(self._h, counts), "step_sim_finish")
         return np.array(list(counts), dtype=np.uint64)
 
     def deliver(self, d_in: int, n: int) -> None:

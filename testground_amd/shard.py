@@ -22,27 +22,41 @@ import torch.distributed as dist
 REC = 24  # sizeof(tgsim_delivery)
 
 
+def init_rccl(device: torch.device, **kw) -> None:
+    """RCCL process group whose collectives run on a high-priority stream.  HIP maps streams onto a
+    few hardware queues; the engine's simulate stream keeps the next steps' k_sim queued, so an
+    exchange placed on the same queue would wait behind them.  High-priority streams (the
+    exchange's, RCCL's and the engine's delivery stream) take a queue of their own."""
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    dist.init_process_group("nccl", pg_options=opts, device_id=device, **kw)
+
+
 def shard_bounds(n_peers: int, world: int) -> List[int]:
     """Contiguous source ranges, as even as possible: rank r owns [b[r], b[r+1])."""
     return [(n_peers * r) // world for r in range(world)] + [n_peers]
 
 
 class ShardedStepper:
-    """One step = step_sim -> exchange -> deliver on every rank.  On GPUs the delivery of step k
-    runs on the engine's delivery stream beside the k_sim of step k+1 (tgsim_deliver_async): the
-    exchange buffers are double-buffered, the engine's simulate stream waits for the collective that
-    still reads the output buffer it is about to overwrite, and step_sim returns only after the
-    previous delivery has released its input buffer."""
+    """One step = step_sim -> exchange -> deliver on every rank; run() pipelines many.  On GPUs the
+    delivery of step k runs on the engine's delivery stream beside the k_sim of the next step
+    (tgsim_deliver_async); the engine's simulate stream waits for the collective that still reads
+    the output buffer it is about to overwrite, and step_sim_finish returns only after the earlier
+    deliveries have released their input buffers."""
 
     def __init__(self, engine, bounds: Sequence[int], device: str = "cuda", group=None):
         self.engine = engine
         self.bounds = list(bounds)
         self.device = torch.device(device)
         self.group = group
-        self._out: List[Optional[torch.Tensor]] = [None, None]
-        self._in: List[Optional[torch.Tensor]] = [None, None]
-        self._ev: List[Optional[torch.cuda.Event]] = [None, None]
+        # records out of step k in _out[k % 3] (two launched steps + the one being exchanged), into
+        # this rank in _in[k % 2]; _ev[j]: the exchange that last read _out[j]
+        self._out: List[Optional[torch.Tensor]] = [None] * 3
+        self._in: List[Optional[torch.Tensor]] = [None] * 2
+        self._ev: List[Optional[torch.cuda.Event]] = [None] * 3
         self._k = 0
+        # the exchange's stream: high priority, off the simulate stream's hardware queue (init_rccl)
+        self._xs = torch.cuda.Stream(self.device, priority=-1) if self.device.type == "cuda" else None
 
     def _buf(self, bufs: list, i: int, n_bytes: int) -> torch.Tensor:
         b = bufs[i]
@@ -51,32 +65,61 @@ class ShardedStepper:
             bufs[i] = b
         return b
 
-    def step(self, n_ticks: int) -> int:
-        """One window on every rank (collective).  Returns the records delivered to this rank."""
-        cuda = self.device.type == "cuda"
-        i = self._k & 1
+    def _launch(self, n_ticks: int):
+        k = self._k
         self._k += 1
-        cap = self.engine.sim_capacity()
-        out = self._buf(self._out, i, cap * REC)
-        if cuda and self._ev[i] is not None:  # the exchange of two steps ago still reads out[i]
-            self.engine.wait_event(self._ev[i].cuda_event)
-        cnt = self.engine.step_sim(n_ticks, self.bounds, out.data_ptr(), out.numel() // REC)
+        j = k % 3
+        out = self._buf(self._out, j, self.engine.sim_capacity() * REC)
+        if self.device.type == "cuda" and self._ev[j] is not None:  # an earlier exchange still reads out[j]
+            self.engine.wait_event(self._ev[j].cuda_event)
+        self.engine.step_sim_launch(n_ticks, self.bounds, out.data_ptr(), out.numel() // REC)
+        return k, out
+
+    def _exchange(self, k: int, out: torch.Tensor, cnt: np.ndarray) -> int:
+        if self._xs is None:
+            return self._exchange_on(k, out, cnt)
+        with torch.cuda.stream(self._xs):
+            return self._exchange_on(k, out, cnt)
+
+    def _exchange_on(self, k: int, out: torch.Tensor, cnt: np.ndarray) -> int:
         send = torch.as_tensor(cnt.astype(np.int64), device=self.device)
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=self.group)
         rcnt = recv.cpu().numpy()
         n_in = int(rcnt.sum())
-        inb = self._buf(self._in, i, n_in * REC)
+        # the previous delivery from _in[k % 2] finished before step_sim_finish returned
+        inb = self._buf(self._in, k % 2, n_in * REC)
         dist.all_to_all_single(inb[: n_in * REC], out[: int(cnt.sum()) * REC],
                                [int(x) * REC for x in rcnt], [int(x) * REC for x in cnt], group=self.group)
-        if cuda:  # the collective runs on torch's stream: the engine's delivery stream waits for it
+        if self.device.type == "cuda":  # the collective runs on torch's stream: the delivery stream waits for it
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
-            self._ev[i] = ev
+            self._ev[k % 3] = ev
             self.engine.deliver_async(inb.data_ptr(), n_in, ev.cuda_event)
         else:
             self.engine.deliver(inb.data_ptr(), n_in)
         return n_in
+
+    def step(self, n_ticks: int) -> int:
+        """One window on every rank (collective).  Returns the records delivered to this rank."""
+        k, out = self._launch(n_ticks)
+        return self._exchange(k, out, self.engine.step_sim_finish())
+
+    def run(self, n_steps: int, n_ticks: int) -> int:
+        """n_steps windows with the simulation two steps ahead of the exchange: while the host
+        exchanges step k, the engine's simulate stream already holds steps k+1 and k+2, so it never
+        idles on the host.  Only for steps with no host-side change between them (pre-generated
+        traffic, no reshaping, no receipts feeding generation); the results are identical to
+        n_steps calls of step()."""
+        total = 0
+        pend = [self._launch(n_ticks) for _ in range(min(2, n_steps))]
+        for s in range(n_steps):
+            k, out = pend.pop(0)
+            cnt = self.engine.step_sim_finish()
+            if s + 2 < n_steps:
+                pend.append(self._launch(n_ticks))
+            total += self._exchange(k, out, cnt)
+        return total
 
     def barrier(self, state: int, target: int) -> bool:
         """Global barrier over the shards' sync counters: the per-rank counts of `state` are summed

@@ -21,7 +21,9 @@ def rccl():
     torch.cuda.init()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from testground_amd.shard import init_rccl
+
+    init_rccl(torch.device("cuda", 0), rank=0, world_size=1)
     yield dist
     dist.destroy_process_group()
 
@@ -63,3 +65,26 @@ def test_stepper_gossip_equals_step(rccl):
         d_sh, d_ref = sh.drain(), ref.drain()
         assert len(d_sh) == len(d_ref) and (d_sh == d_ref).all(), f"window {k}"
     assert (sh.gossip_reached() == ref.gossip_reached()).all()
+
+
+def test_stepper_pipelined_run_equals_step(rccl):
+    """run(): step k+1's k_sim launched before step k's exchange and delivery."""
+    from testground_amd.shard import ShardedStepper
+
+    n, steps = 2000, 8
+    ref, sh = Engine(n), Engine(n)
+    for e in (ref, sh):
+        wl.configure_storm(e, n)
+    for _ in range(steps):
+        sh.gen_storm(0.5, 1000)
+    ShardedStepper(sh, [0, n], device="cuda:0").run(steps, 1000)
+    want = []
+    for _ in range(steps):
+        ref.gen_storm(0.5, 1000)
+        ref.step(1000)
+        want.append(ref.drain())
+    want = np.concatenate(want)
+    got = sh.drain()
+    assert len(got) == len(want) > 10_000 and (got == want).all()
+    s, r = sh.stats(), ref.stats()
+    assert (s["offered"], s["scheduled"], s["by_verdict"]) == (r["offered"], r["scheduled"], r["by_verdict"])

@@ -83,3 +83,46 @@ def test_two_rank_gloo_equals_single_engine(workload, steps, min_pkts):
             total = total + len(v) if k else len(v)
             assert len(dl) == len(dr) and (dl == dr).all(), f"step {k}: deliveries"
         assert total > min_pkts
+
+
+def _rank_pipelined(rank, world, port, outdir, steps):
+    import torch.distributed as dist
+
+    from testground_amd.shard import ShardedStepper, shard_bounds
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = shard_bounds(N, world)
+    eng = _oracle(N, shard=(b[rank], b[rank + 1]))
+    workloads.configure_storm(eng, N)
+    for _ in range(steps):  # every window pre-generated: the stepper simulates one step ahead
+        eng.gen_storm(LAM, WINDOW)
+    ShardedStepper(eng, b, device="cpu").run(steps, WINDOW)
+    np.save(os.path.join(outdir, f"d{rank}.npy"), eng.drain())
+    np.save(os.path.join(outdir, f"s{rank}.npy"), np.array([eng.stats()["offered"], eng.stats()["scheduled"]]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_pipelined_run_equals_single_engine():
+    world, steps = 2, 4
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rank_pipelined, args=(world, 29950 + os.getpid() % 40, d, steps), nprocs=world,
+                           start_method="spawn", join=True)
+        ref = _oracle(N)
+        workloads.configure_storm(ref, N)
+        per_step = []
+        for _ in range(steps):
+            ref.gen_storm(LAM, WINDOW)
+            ref.step(WINDOW)
+            per_step.append(ref.drain())
+        dr = np.concatenate(per_step)
+        s = sum(np.load(os.path.join(d, f"s{r}.npy")) for r in range(world))
+        st = ref.stats()
+        assert list(s) == [st["offered"], st["scheduled"]]
+        # each rank's drain is its destinations' deliveries, step after step
+        lo_hi = [(0, N // 2), (N // 2, N)]
+        for r, (lo, hi) in enumerate(lo_hi):
+            dl = np.load(os.path.join(d, f"d{r}.npy"))
+            want = np.concatenate([x[(x["dst"] >= lo) & (x["dst"] < hi)] for x in per_step])
+            assert len(dl) == len(want) and (dl == want).all(), f"rank {r}"
+        assert len(dr) > 5_000
