@@ -215,7 +215,6 @@ struct tgsim_engine_s {
   uint64_t route_seq[kRouteSlots] = {};
   uint64_t route_next_seq = 0;
   uint32_t route_head = 0, route_n = 0;
-  bool st_delivered = false;  // deliver_local wrote delivery buffers on the simulate stream
   uint32_t S = 0, N = 0;
   uint64_t now_tick = 0;
   uint32_t key0 = 0, key1 = 0;
@@ -258,8 +257,13 @@ struct tgsim_engine_s {
   std::vector<uint64_t> last_perm;
 
   // step output
-  DevBuf<tgsim_delivery> d_emit;
-  DevBuf<uint32_t> d_emit_n;
+  // emit regions and per-destination histogram written by k_sim; a single-shard step reads them
+  // on the delivery stream while the next k_sim writes the other pair (swapped by deliver_local;
+  // ev_local: the delivery that last read the pair)
+  DevBuf<tgsim_delivery> d_emit, d_emit_alt;
+  DevBuf<uint32_t> d_emit_n, d_emit_n_alt;
+  DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (k_dst_sort resets it)
+  hipEvent_t ev_local = nullptr, ev_local_alt = nullptr;
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
@@ -412,6 +416,7 @@ int stage_host_input(Eng* E, uint32_t n_ticks) {
   E->n_in = v.size();
   HIPCHK(E->d_off.ensure(E->S + 1));
   HIPCHK(E->d_in.ensure(E->n_in ? E->n_in : 1));
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // a local delivery may still read d_off
   HIPCHK(hipMemcpyAsync(E->d_off.p, off.data(), sizeof(uint64_t) * (E->S + 1), hipMemcpyHostToDevice, E->st));
   if (E->n_in)
     HIPCHK(hipMemcpyAsync(E->d_in.p, recs.data(), sizeof(InRec) * E->n_in, hipMemcpyHostToDevice, E->st));
@@ -507,6 +512,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   if (rc) return rc;
   const uint64_t emit_cap = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;
   HIPCHK(E->d_verdict.ensure(E->n_in ? E->n_in : 1));
+  if (local_hist)  // the delivery two steps back read this emit pair
+    HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
   HIPCHK(E->d_emit.ensure(emit_cap));
   HIPCHK(E->d_emit_n.ensure(E->S));
   SimArgs a;
@@ -543,12 +550,11 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   }
   a.dst_cnt = nullptr;
   if (local_hist) {
-    HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // the histogram is shared with deliver()
-    if (E->d_dcnt.cap < E->N) {
-      HIPCHK(E->d_dcnt.ensure(E->N));
-      HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, E->st));
+    if (E->d_lcnt.cap < E->N) {
+      HIPCHK(E->d_lcnt.ensure(E->N));
+      HIPCHK(hipMemsetAsync(E->d_lcnt.p, 0, sizeof(uint64_t) * E->d_lcnt.cap, E->st));
     }
-    a.dst_cnt = reinterpret_cast<unsigned long long*>(E->d_dcnt.p);
+    a.dst_cnt = reinterpret_cast<unsigned long long*>(E->d_lcnt.p);
   }
   hipEvent_t ev0, ev1;
   HIPCHK(take_event(E, &ev0));
@@ -712,17 +718,12 @@ int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out, hipStream_t sq) {
 // Records received by this shard (tgsim_deliver*, or the routed records of tgsim_step on a
 // partial shard): histogram -> scan -> scatter -> per-destination order, on the delivery stream so
 // that it overlaps the next step's k_sim.  It waits for the simulate stream's work so far (the
-// records come from tgsim_step_sim, which completed them before returning) only when a local step
-// last wrote the delivery buffers there, and for `wait` (the producer of d_in, e.g. the collective).
+// records come from tgsim_step_sim, which completed them before returning), only for `wait` (the
+// producer of d_in, e.g. the collective).
 // check: read the record count back and reject records addressed to other shards.
 int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool check) {
   const uint32_t nd = E->S;  // destinations owned by this shard
   hipStream_t sq = E->dst_st;
-  if (E->st_delivered) {  // the delivery buffers were last written on the simulate stream
-    HIPCHK(hipEventRecord(E->ev_sim, E->st));
-    HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
-    E->st_delivered = false;
-  }
   if (wait) HIPCHK(hipStreamWaitEvent(sq, wait, 0));
   if (E->d_dcnt.cap < nd) {
     HIPCHK(E->d_dcnt.ensure(nd));
@@ -762,37 +763,45 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
 }
 
 // Single shard: k_sim counted every emitted record per destination, so the step needs no host
-// round trip: scan -> scatter straight from the emit regions -> per-destination order.  Only the
-// drain bookkeeping (and the gossip receipts) need the record count on the host.
+// round trip: scan -> scatter straight from the emit regions -> per-destination order, on the
+// delivery stream beside the next step's k_sim (which writes the other emit pair).  Only the drain
+// bookkeeping (and the gossip receipts) need the record count on the host.
 int deliver_local(Eng* E) {
   const uint32_t nd = E->N;
-  HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // delivery buffers are shared with deliver()
-  E->st_delivered = true;
+  hipStream_t sq = E->dst_st;
+  HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
+  HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
   HIPCHK(E->d_dtot.ensure(1));
-  launch_scan(E->d_dcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, E->st, E->d_dpos.p);
+  launch_scan(E->d_lcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
   HIPCHK(hipGetLastError());
   const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) || E->gossip_on;
   uint64_t n = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;  // upper bound
   if (need_n) {
-    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
-    HIPCHK(hipStreamSynchronize(E->st));
+    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
+    HIPCHK(hipStreamSynchronize(sq));
     n = E->h_dtot;
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_local_scatter(E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, 0, E->d_dpos.p, E->d_scatter.p, E->st);
+  launch_local_scatter(E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq);
   HIPCHK(hipGetLastError());
   tgsim_delivery* dst = nullptr;
-  int rc = delivery_out(E, n, &dst, E->st);
+  int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, E->st);
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_lcnt.p, nd, dst, sq);
   HIPCHK(hipGetLastError());
   if (E->gossip_on) {
-    launch_gossip(gossip_args(E, 0, 0), E->d_scatter.p, n, nullptr, nullptr, nullptr, 0, E->st);
+    launch_gossip(gossip_args(E, 0, 0), E->d_scatter.p, n, nullptr, nullptr, nullptr, 0, sq);
     HIPCHK(hipGetLastError());
   }
+  HIPCHK(hipEventRecord(E->ev_local, sq));
+  HIPCHK(hipEventRecord(E->ev_dst, sq));
+  std::swap(E->d_emit, E->d_emit_alt);
+  std::swap(E->d_emit_n, E->d_emit_n_alt);
+  std::swap(E->d_lcnt, E->d_lcnt_alt);
+  std::swap(E->ev_local, E->ev_local_alt);
   return 0;
 }
 
@@ -852,6 +861,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_dst, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
+  for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt}) {
+    if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
+    if ((rc = E->hip(hipEventRecord(*ev, E->dst_st), "event"))) return bail(rc);
+  }
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_err), sizeof(uint64_t)), "pinned"))) return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_edges), 16 * Eng::kRouteSlots * sizeof(uint64_t),
                                  hipHostMallocCoherent | hipHostMallocMapped),
@@ -903,7 +916,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
@@ -920,6 +933,8 @@ void tgsim_destroy(void* e) {
     if (ev) (void)hipEventDestroy(ev);
   if (E->ev_dst) (void)hipEventDestroy(E->ev_dst);
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
+  if (E->ev_local) (void)hipEventDestroy(E->ev_local);
+  if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);
   if (E->dst_st) (void)hipStreamDestroy(E->dst_st);
   if (E->st) (void)hipStreamDestroy(E->st);
   delete E;
@@ -1067,6 +1082,7 @@ int tgsim_gen_storm(void* e, double lambda, uint32_t n_ticks) {
   g.n_peers = E->N;
   g.n_ticks = n_ticks;
   g.now_tick = E->now_tick + E->gen_q_ticks;  // windows queue up back to back
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // a free window's offsets may still be read by a delivery
   Eng::GenWindow w;
   if (!E->gen_free.empty()) {
     w = std::move(E->gen_free.back());
