@@ -204,7 +204,8 @@ struct tgsim_engine_s {
   // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
   std::vector<hipEvent_t> ev_pool;
-  uint64_t* h_err = nullptr;  // pinned copy of the sticky device error word, refreshed every step
+  uint64_t* h_err = nullptr;    // pinned host word k_sim stores the sticky error bits into
+  uint64_t* d_err_host = nullptr;  // its device address
   // launched, unfinished routed steps (tgsim_step_sim_launch), oldest at route_head: pinned
   // per-rank record edges behind an event, per slot
   static constexpr uint32_t kRouteSlots = 2;
@@ -275,7 +276,7 @@ struct tgsim_engine_s {
   double sim_ms = 0;
   uint64_t sim_launches = 0;
   bool stamps_on = false;
-  DevBuf<uint32_t> d_order;
+  DevBuf<uint32_t> d_order;  // dispatch order of the next k_sim, computed behind this one
   bool order_valid = false;
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
@@ -440,7 +441,7 @@ int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uin
   return 0;
 }
 
-constexpr uint32_t kOrderMaxSources = 32768;
+constexpr uint32_t kOrderMaxSources = 32768;  // = kOrderMax of the order kernel
 
 hipError_t take_event(Eng* E, hipEvent_t* ev) {
   if (!E->ev_pool.empty()) {
@@ -472,8 +473,8 @@ int harvest_timing(Eng* E, bool wait) {
   return 0;
 }
 
-// The sticky error word of k_sim (simulated time past 2^46 ns), as last copied to pinned memory:
-// exact after a stream synchronization, possibly one step late otherwise.
+// The sticky error word of k_sim (simulated time past 2^46 ns), as k_sim stores it into pinned host
+// memory: exact after a stream synchronization, possibly one step late otherwise.
 int check_sim_error(Eng* E) {
   if (E->h_err && (__atomic_load_n(E->h_err, __ATOMIC_RELAXED) & kErrTimeOverflow))
     return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
@@ -541,7 +542,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   a.t0_ns = E->now_tick * E->o.tick_ns;
   a.horizon_ns = (E->now_tick + n_ticks) * E->o.tick_ns + E->o.lookahead_ns;
   const uint32_t n_wg = (E->S + kSpw - 1) / kSpw;
-  a.order = (kSpw == 1 && E->order_valid && E->S <= kOrderMaxSources) ? E->d_order.p : nullptr;
+  const bool ordered = kSpw == 1 && E->S <= kOrderMaxSources;
+  a.order = ordered && E->order_valid ? E->d_order.p : nullptr;
   a.stamps = nullptr;
   if (E->stamps_on) {
     HIPCHK(E->d_stamps.ensure(static_cast<size_t>(n_wg) * kStampSlots));
@@ -549,6 +551,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     E->n_stamp_wg = n_wg;
   }
   a.dst_cnt = nullptr;
+  a.err_host = E->d_err_host;
   if (local_hist) {
     if (E->d_lcnt.cap < E->N) {
       HIPCHK(E->d_lcnt.ensure(E->N));
@@ -564,10 +567,9 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.emplace_back(ev0, ev1);
-  HIPCHK(hipMemcpyAsync(E->h_err, E->d_stats.p + kStErr, sizeof(uint64_t), hipMemcpyDeviceToHost, E->st));
   // heavy-first dispatch order for the next step: it shortens the tail when only a few rounds of
   // workgroups fit; with many more sources than resident workgroups the dispatcher balances alone
-  if (kSpw == 1 && E->S <= kOrderMaxSources) {
+  if (ordered) {
     HIPCHK(E->d_order.ensure(E->S));
     launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
     HIPCHK(hipGetLastError());
@@ -771,6 +773,7 @@ int deliver_local(Eng* E) {
   hipStream_t sq = E->dst_st;
   HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
   HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
@@ -865,7 +868,13 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
     if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
     if ((rc = E->hip(hipEventRecord(*ev, E->dst_st), "event"))) return bail(rc);
   }
-  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_err), sizeof(uint64_t)), "pinned"))) return bail(rc);
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_err), sizeof(uint64_t),
+                                 hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
+    return bail(rc);
+  *E->h_err = 0;
+  if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_err_host), E->h_err, 0), "pinned")))
+    return bail(rc);
+
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_edges), 16 * Eng::kRouteSlots * sizeof(uint64_t),
                                  hipHostMallocCoherent | hipHostMallocMapped),
                    "pinned")))

@@ -15,7 +15,8 @@ constexpr uint32_t kWave = 64;        // lanes per wavefront
 #ifndef TGSIM_SPW
 #define TGSIM_SPW 1
 #endif
-constexpr uint32_t kSpw = TGSIM_SPW;  // sources per simulate wavefront (LDS-resident queues)
+constexpr uint32_t kSpw = TGSIM_SPW;
+ // sources per simulate wavefront (LDS-resident queues)
 constexpr uint32_t kAhead = kWave / kSpw;  // records per source staged per batch
 constexpr uint64_t kEMask = (1ull << 46) - 1;  // eligibility time field of a queued item
 constexpr uint32_t kStates = 1024;    // sync states
@@ -96,6 +97,7 @@ struct SimArgs {
   const uint32_t* order;    // k_sim dispatch order (workgroup -> source), or null for identity
   uint64_t* stamps;         // diagnostics: kStampSlots s_memrealtime stamps per workgroup, or null
   unsigned long long* dst_cnt;  // single shard: per-destination histogram of the emitted records, or null
+  uint64_t* err_host;       // pinned host word: the sticky error bits, or null
 };
 constexpr uint32_t kStampSlots = 24;  // 8 phase stamps + 16 profile counters (TGSIM_PROFILE)
 

@@ -81,7 +81,6 @@ __device__ __forceinline__ bool item_lt(const uint4& a, const uint4& b) {
 // the per-packet path built from the same wave-wide primitives.
 struct SimLds {
   uint4 slot[kHeapCap];     // circular: departure ring, then the sorted eligibility queue
-  uint32_t pos[kWave];      // insertion positions of new items, by rank
 };
 static_assert(sizeof(SimLds) <= 65536, "simulate workgroup LDS");
 
@@ -329,7 +328,7 @@ struct SimQueue {
     if (!m) return;
     PROF_T0(i);
     const uint32_t nm = (uint32_t)__popcll(m);
-    uint32_t pos = 0, minpos = 0;
+    uint32_t pos = 0;
     PROF_T0(q1);
     if (nm <= 8) {
       if (qn) {
@@ -338,7 +337,6 @@ struct SimQueue {
         const uint4 last = slot(rn + qn - 1);
         const bool hs = 16 * lane < qn;
         const uint4 smp = hs ? slot(rn + 16 * lane) : make_uint4(0, 0, 0, 0);
-        minpos = qn;
         for (uint64_t mm = m; mm; mm &= mm - 1) {
           const uint32_t b = (uint32_t)__builtin_ctzll(mm);
           const uint4 k = make_uint4(readlane32(it.x, b), readlane32(it.y, b), readlane32(it.z, b), 0u);
@@ -354,7 +352,6 @@ struct SimQueue {
             }
           }
           if (lane == b) pos = p;
-          minpos = min(minpos, p);
         }
       }
     } else {
@@ -383,11 +380,13 @@ struct SimQueue {
       }
     }
     PROF_T0(q2);
+    // lane r receives the position of the rank-r item through a forward permute (the LDS
+    // crossbar, no LDS allocation); lanes without an item take ranks nm.., so every lane gets one
+    const uint32_t to = has ? rank : nm + (uint32_t)__popcll(~m & ((1ull << lane) - 1));
+    const uint32_t sp_all = (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)(has ? pos : 0xFFFFFFFFu));
     uint32_t kL = 0;  // new items placed by moving the ring and the queue prefix down
     if (nm <= 8) {
-      if (has) lds.pos[rank] = pos;
-      wave_lds_sync();
-      const uint32_t sp = lane < nm ? lds.pos[lane] : 0u;  // lane r: position of the rank-r item
+      const uint32_t sp = lane < nm ? sp_all : 0u;  // lane r: position of the rank-r item
       // Two-sided merge.  The first kL items (by key) go in by moving the departure ring and the
       // queue prefix [0, maxL) down into the free slots before the ring head, the others by
       // moving the suffix [minR, qn) up; kL minimizes the slots moved.  Items eligible at once
@@ -449,17 +448,33 @@ struct SimQueue {
         PROF_CNT(6, 1);
       }
     } else {
-      if (has) lds.pos[rank] = pos;
-      wave_lds_sync();
-      const uint32_t sp = lane < nm ? lds.pos[lane] : 0xFFFFFFFFu;  // ascending
-      const uint32_t mp = readlane32(sp, 0);
-      for (int32_t hi = (int32_t)qn; hi > (int32_t)mp; hi -= (int32_t)kWave) {
-        const int32_t r = hi - (int32_t)kWave + (int32_t)lane;
-        const bool mv = r >= (int32_t)mp;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (mv) v = slot(rn + (uint32_t)r);
-        const uint32_t sh = count_le_sorted_u32(sp, mv ? (uint32_t)r : 0u);
-        if (mv) slot(rn + (uint32_t)r + sh) = v;
+      const uint32_t sp = sp_all;  // ascending, 0xFFFFFFFF beyond nm
+      const int32_t mp = (int32_t)readlane32(sp, 0);
+      const bool mine = lane < nm;
+      // queue item p >= mp moves up by #{new items at or before p}: passes of four chunks from the
+      // tail down, all reads of a pass before its writes
+      for (int32_t hi = (int32_t)qn; hi > mp; hi -= 4 * (int32_t)kWave) {
+        uint4 v[4];
+        int32_t r[4];
+        uint32_t sh[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          r[u] = hi - (u + 1) * (int32_t)kWave + (int32_t)lane;
+          v[u] = r[u] >= mp ? slot(rn + (uint32_t)r[u]) : make_uint4(0, 0, 0, 0);
+        }
+        // the items before the chunk, plus those inside it at or before the lane
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t b = hi - (u + 1) * (int32_t)kWave;
+          uint32_t c = ballot_count(mine && (int32_t)sp < b);
+          for (uint64_t mk = __ballot(mine && (int32_t)sp >= b && (int32_t)sp < b + (int32_t)kWave); mk; mk &= mk - 1)
+            c += (int32_t)lane >= (int32_t)readlane32(sp, (uint32_t)__builtin_ctzll(mk)) - b ? 1u : 0u;
+          sh[u] = c;
+        }
+        __asm__ volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (r[u] >= mp) slot(rn + (uint32_t)r[u] + sh[u]) = v[u];
         PROF_CNT(6, 1);
       }
     }
@@ -860,32 +875,45 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       if (c_v[k]) atomicAdd(&sc[kStVerdict0 + k], (unsigned long long)c_v[k]);
     if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
-    if (err) atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
+    if (err) {
+      atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
+      if (a.err_host)  // the host's pinned copy (sticky; read at its sync points)
+        __hip_atomic_store(a.err_host, (uint64_t)kErrTimeOverflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Longest-processing-time-first dispatch order for the next k_sim: sources bucketed by
-// log2(HTB records emitted this step), heaviest bucket first (one workgroup, LDS counting sort).
-// Only the dispatch order changes; every source's result is independent of it.
-__global__ __launch_bounds__(1024) void k_order(const uint32_t* emit_n, uint32_t n, uint32_t* order) {
-  __shared__ uint32_t cnt[33], base[33];
-  for (uint32_t i = threadIdx.x; i < 33; i += blockDim.x) cnt[i] = 0;
+// Longest-processing-time-first dispatch order: sources bucketed by the HTB records they emitted
+// (8 buckets per octave), heaviest first (one workgroup, LDS counting sort; each weight is read
+// once, so the order is a permutation whatever happens to the weights meanwhile).  Only the
+// dispatch order changes; every source's result is independent of it.
+constexpr uint32_t kOrderMax = 32768;  // sources the one-workgroup order kernel handles
+__device__ __forceinline__ uint32_t weight_bucket(uint32_t c) {  // 0..255, monotone in c
+  const uint32_t v = c | 1u, lz = __clz(v);
+  return (31u - lz) * 8u + ((v << lz) >> 28 & 7u);
+}
+
+__global__ __launch_bounds__(1024) void k_order(const uint32_t* weight, uint32_t n, uint32_t* order) {
+  __shared__ uint32_t cnt[256], base[256];
+  __shared__ uint8_t key[kOrderMax];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) cnt[i] = 0;
   __syncthreads();
-  for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) atomicAdd(&cnt[__clz(emit_n[s])], 1u);
+  for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) {
+    const uint32_t k = 255u - weight_bucket(weight[s]);
+    key[s] = (uint8_t)k;
+    atomicAdd(&cnt[k], 1u);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t acc = 0;
-    for (int b = 0; b < 33; ++b) {
+    for (int b = 0; b < 256; ++b) {
       base[b] = acc;
       acc += cnt[b];
     }
   }
   __syncthreads();
-  for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) {
-    const uint32_t b = __clz(emit_n[s]);
-    order[atomicAdd(&base[b], 1u)] = s;
-  }
+  for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) order[atomicAdd(&base[key[s]], 1u)] = s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1383,8 +1411,9 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
 }
 
-void launch_order(const uint32_t* emit_n, uint32_t n, uint32_t* order, hipStream_t st) {
-  hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, st, emit_n, n, order);
+void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream_t st) {
+  if (n > kOrderMax) return;
+  hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, st, weight, n, order);
 }
 
 void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st) {

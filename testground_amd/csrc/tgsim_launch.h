@@ -24,7 +24,8 @@ struct RouteArgsHost {
 };
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
-void launch_order(const uint32_t* emit_n, uint32_t n, uint32_t* order, hipStream_t st);
+// no-op above kOrderMax (32768) sources
+void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream_t st);
 void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st);
 void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uint32_t* gen_seq,
                 InRec* out, int phase, hipStream_t st);
