@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
 set -o pipefail
-timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/ev/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/ev/pytest_gpu.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/ev/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/ev/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/ev/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/ev/smoke.log
