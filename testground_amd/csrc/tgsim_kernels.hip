@@ -151,6 +151,12 @@ __device__ __forceinline__ uint32_t scan_max_u32(uint32_t v) {
 #undef STEP
   return v;
 }
+__device__ __forceinline__ uint64_t scan_max_u64(uint64_t v) {
+#define STEP(C, R) { const uint64_t p = dpp64<C, R>(0ull, v); v = p > v ? p : v; }
+  TG_SCAN_STEPS(STEP)
+#undef STEP
+  return v;
+}
 __device__ __forceinline__ uint64_t scan_min_u64(uint64_t v) {
 #define STEP(C, R) { const uint64_t p = dpp64<C, R>(~0ull, v); v = p < v ? p : v; }
   TG_SCAN_STEPS(STEP)
@@ -372,7 +378,20 @@ struct SimQueue {
     PROF_ADD(14, q1);
     // rank among the new items (equal keys: lane order)
     uint32_t rank = 0;
-    if (nm > 1) {
+    bool ranked = nm <= 1;
+    if (nm > 2) {
+      // common case (no jitter or reorder: e grows with the offer time): the items are already in
+      // key order across the lanes, checked against each item's predecessor in one pass
+      const uint64_t below = m & ((1ull << lane) - 1);
+      const uint32_t prev = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
+      const uint4 pk = make_uint4((uint32_t)__shfl(it.x, (int)prev, 64), (uint32_t)__shfl(it.y, (int)prev, 64),
+                                  (uint32_t)__shfl(it.z, (int)prev, 64), 0u);
+      if (!__ballot(has && below && !item_lt(pk, it))) {
+        rank = (uint32_t)__popcll(below);
+        ranked = true;
+      }
+    }
+    if (!ranked) {
       for (uint64_t mm = m; mm; mm &= mm - 1) {
         const uint32_t b = (uint32_t)__builtin_ctzll(mm);
         const uint4 o = make_uint4(readlane32(it.x, b), readlane32(it.y, b), readlane32(it.z, b), 0u);
@@ -658,10 +677,24 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
             // with a lookahead the ring need not be sorted across a step boundary)
             const uint64_t stop = __ballot(dep >= T_max);
             const uint32_t nd = stop ? (uint32_t)__builtin_ctzll(stop) : kWave;
-            bool alive = true;
-            for (uint32_t l = 0; l < nd; ++l) {
-              alive = alive && readlane64(dep, l) < T;
-              D += alive ? 1u : 0u;
+            // a lane keeps counting into this chunk only if every earlier entry was before its T
+            const bool carry = D == base;
+            if (nd > 16) {
+              // prefix maxima of the chunk's first nd entries ascend: the lane's departures are
+              // the entries before the first prefix maximum >= T (binary search over the lanes)
+              const uint64_t pm = scan_max_u64(lane < nd ? dep : ~0ull);
+              uint32_t lo = 0;
+#pragma unroll
+              for (uint32_t sb = 32; sb; sb >>= 1)
+                if (shfl64(pm, lo + sb - 1) < T) lo += sb;
+              lo += shfl64(pm, lo) < T ? 1u : 0u;
+              if (carry) D += lo;
+            } else {
+              bool alive = carry;
+              for (uint32_t l = 0; l < nd; ++l) {
+                alive = alive && readlane64(dep, l) < T;
+                D += alive ? 1u : 0u;
+              }
             }
             if (nd < kWave) break;
           }
