@@ -200,10 +200,12 @@ struct tgsim_engine_s {
   hipStream_t st = nullptr;      // simulate stream: inputs, k_sim, routing, single-shard delivery
   hipStream_t dst_st = nullptr;  // delivery stream of inbound records (tgsim_deliver*), overlaps the next k_sim
   hipEvent_t ev_dst = nullptr;   // recorded after the last delivery on dst_st
+  hipEvent_t ev_recv = nullptr;  // recorded after the last delivery's scatter (and gossip receipts)
   hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
   // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
   std::vector<hipEvent_t> ev_pool;
+  uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
   uint64_t* h_err = nullptr;    // pinned host word k_sim stores the sticky error bits into
   uint64_t* d_err_host = nullptr;  // its device address
   // launched, unfinished routed steps (tgsim_step_sim_launch), oldest at route_head: pinned
@@ -751,15 +753,16 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
   launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq);
   HIPCHK(hipGetLastError());
+  if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
+    launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, sq);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(E->ev_recv, sq));  // the next window's generation needs no more than this
   tgsim_delivery* dst = nullptr;
   rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
   launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq);
   HIPCHK(hipGetLastError());
-  if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
-    launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, sq);
-    HIPCHK(hipGetLastError());
-  }
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   return 0;
 }
@@ -767,7 +770,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
 // Single shard: k_sim counted every emitted record per destination, so the step needs no host
 // round trip: scan -> scatter straight from the emit regions -> per-destination order, on the
 // delivery stream beside the next step's k_sim (which writes the other emit pair).  Only the drain
-// bookkeeping (and the gossip receipts) need the record count on the host.
+// bookkeeping needs the record count on the host.
 int deliver_local(Eng* E) {
   const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
@@ -780,7 +783,7 @@ int deliver_local(Eng* E) {
   HIPCHK(E->d_dtot.ensure(1));
   launch_scan(E->d_lcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
   HIPCHK(hipGetLastError());
-  const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) || E->gossip_on;
+  const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
   uint64_t n = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;  // upper bound
   if (need_n) {
     HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
@@ -790,15 +793,18 @@ int deliver_local(Eng* E) {
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
   launch_local_scatter(E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq);
   HIPCHK(hipGetLastError());
+  if (E->gossip_on) {  // receipts (before the sort, which may reuse the scatter buffer), the count
+                       // read on the device when the host never needed it
+    if (need_n) launch_gossip(gossip_args(E, 0, 0), E->d_scatter.p, n, nullptr, nullptr, nullptr, 0, sq);
+    else launch_gossip_recv_dev(gossip_args(E, 0, 0), E->d_scatter.p, E->d_dtot.p, sq);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(E->ev_recv, sq));  // the next window's generation needs no more than this
   tgsim_delivery* dst = nullptr;
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
   launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_lcnt.p, nd, dst, sq);
   HIPCHK(hipGetLastError());
-  if (E->gossip_on) {
-    launch_gossip(gossip_args(E, 0, 0), E->d_scatter.p, n, nullptr, nullptr, nullptr, 0, sq);
-    HIPCHK(hipGetLastError());
-  }
   HIPCHK(hipEventRecord(E->ev_local, sq));
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   std::swap(E->d_emit, E->d_emit_alt);
@@ -864,6 +870,8 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_dst, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventRecord(E->ev_recv, E->dst_st), "event"))) return bail(rc);
   for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt}) {
     if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
     if ((rc = E->hip(hipEventRecord(*ev, E->dst_st), "event"))) return bail(rc);
@@ -872,6 +880,8 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
                                  hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
     return bail(rc);
   *E->h_err = 0;
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_gerr), sizeof(uint32_t)), "pinned"))) return bail(rc);
+  *E->h_gerr = 0;
   if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_err_host), E->h_err, 0), "pinned")))
     return bail(rc);
 
@@ -937,10 +947,12 @@ void tgsim_destroy(void* e) {
   }
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
   if (E->h_err) (void)hipHostFree(E->h_err);
+  if (E->h_gerr) (void)hipHostFree(E->h_gerr);
   if (E->h_edges) (void)hipHostFree(E->h_edges);
   for (hipEvent_t ev : E->ev_route)
     if (ev) (void)hipEventDestroy(ev);
   if (E->ev_dst) (void)hipEventDestroy(E->ev_dst);
+  if (E->ev_recv) (void)hipEventDestroy(E->ev_recv);
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->ev_local) (void)hipEventDestroy(E->ev_local);
   if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);
@@ -1149,7 +1161,8 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   if (!E || !E->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
   if (!E->staged.empty()) return E->fail(-EBUSY, "host packets already pending for the next step");
   HIPCHK(hipSetDevice(E->dev));
-  HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // receipts are folded on the delivery stream
+  // receipts are folded on the delivery stream (the sort of the same delivery may still run)
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_recv, 0));
   const uint64_t win0 = E->now_tick + E->gen_q_ticks;
   const GossipArgs g = gossip_args(E, win0, n_ticks);
   Eng::GenWindow w;
@@ -1160,20 +1173,18 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   HIPCHK(E->d_cnt.ensure(E->S));
   launch_gossip(g, nullptr, 0, E->d_cnt.p, nullptr, nullptr, 1, E->st);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(E->h_gerr, E->d_gerr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
   uint64_t total = 0;
-  int rc = scan_counts(E, E->d_cnt, w.off, E->d_blk, E->d_tot, E->S, &total);
+  int rc = scan_counts(E, E->d_cnt, w.off, E->d_blk, E->d_tot, E->S, &total);  // synchronizes the stream
   if (rc) return rc;
-  uint32_t errw = 0;
-  HIPCHK(hipMemcpy(&errw, E->d_gerr.p, sizeof errw, hipMemcpyDeviceToHost));
-  if (errw) {
+  if (*E->h_gerr) {
     E->gen_free.push_back(std::move(w));
     return E->fail(-EINVAL, "gossip: a receipt precedes the window at tick %llu (lookahead shorter than the window)",
                    static_cast<unsigned long long>(win0));
   }
   HIPCHK(w.in.ensure(total ? total : 1));
-  launch_gossip(g, nullptr, 0, nullptr, w.off.p, w.in.p, 2, E->st);
+  launch_gossip(g, nullptr, 0, nullptr, w.off.p, w.in.p, 2, E->st);  // the step runs behind it on E->st
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(E->st));
   w.n = total;
   w.ticks = n_ticks;
   E->gen_q_ticks += n_ticks;

@@ -1046,10 +1046,7 @@ __device__ __forceinline__ uint32_t gossip_neighbour(const GossipArgs& g, uint32
   return d + (d >= peer);
 }
 
-__global__ void k_gossip_recv(GossipArgs g, const tgsim_delivery* in, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const tgsim_delivery r = in[i];
+__device__ __forceinline__ void gossip_recv_one(const GossipArgs& g, const tgsim_delivery& r) {
   const uint32_t f = r.seq / g.degree;
   if (f >= g.n_floods || (r.flags & TGSIM_FLAG_CORRUPT)) return;
   const uint32_t s = r.dst - g.shard_begin;
@@ -1057,6 +1054,18 @@ __global__ void k_gossip_recv(GossipArgs g, const tgsim_delivery* in, uint64_t n
   uint64_t t = r.t_ns / g.tick_ns + 1;
   if (t > 0xFFFFFFFEull) t = 0xFFFFFFFEull;
   atomicMin(&g.first[(uint64_t)s * 64 + f], (uint32_t)t);
+}
+
+__global__ void k_gossip_recv(GossipArgs g, const tgsim_delivery* in, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) gossip_recv_one(g, in[i]);
+}
+
+// Same, with the record count on the device (a delivery whose size the host never reads).
+__global__ __launch_bounds__(256) void k_gossip_recv_dev(GossipArgs g, const tgsim_delivery* in, const uint64_t* n_dev) {
+  const uint64_t n = *n_dev;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    gossip_recv_one(g, in[i]);
 }
 
 // Floods due in [win0, win0 + n_ticks) for local peer s: one wavefront per peer, lane f holds
@@ -1463,6 +1472,10 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
   const dim3 wgrid((h.n_src + 3) / 4), wblk(256);  // one wavefront per source
   if (phase == 0) hipLaunchKernelGGL(k_gen_count, wgrid, wblk, 0, st, g, counts);
   else hipLaunchKernelGGL(k_gen_write, wgrid, wblk, 0, st, g, off, gen_seq, out);
+}
+
+void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st) {
+  hipLaunchKernelGGL(k_gossip_recv_dev, dim3(2048), dim3(256), 0, st, g, recs, n_dev);
 }
 
 void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,

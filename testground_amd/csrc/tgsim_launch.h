@@ -32,6 +32,8 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
 // phase 0: fold delivered records into receipts; 1: per-source counts; 2: write the window.
 void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
                    const uint64_t* off, InRec* out, int phase, hipStream_t st);
+// Receipts of n_dev[0] records (count read on the device).
+void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st);
 // Exclusive scan of in[0..n) into out[0..n] (out[n] = total, also stored at *total when non-null);
 // pos (optional) receives a copy of out[0..n), the scatter cursors.
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
