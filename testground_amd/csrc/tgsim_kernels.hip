@@ -565,7 +565,22 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   const bool corr = (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0;
   const uint32_t lim = a.queue_limit;
   uint32_t last_dup = st.last_dup, last_cor = st.last_cor, last_reo = st.last_reo;
-  uint64_t c_off = 0, c_clone = 0, c_v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // per-lane verdict counts, reduced over the wave once at the end (no wave-uniform counters held
+  // in SGPRs through the loop): 16-bit fields, verdicts 0..3 in vc_lo and 4..7 in vc_hi, emptied
+  // into the statistics every 2^14 batches (at most 2 counts per lane and batch), before a field
+  // can overflow
+  unsigned long long* const sc = a.stats + (size_t)(blockIdx.x % kStatCopies) * kStSlots;
+  uint64_t vc_lo = 0, vc_hi = 0;
+  uint32_t n_clone = 0;
+  auto flush_verdicts = [&]() {
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t f = (uint32_t)(((k < 4 ? vc_lo : vc_hi) >> (16u * (k & 3u))) & 0xFFFFu);
+      const uint32_t tot = readlane32((uint32_t)scan_sum_i32((int32_t)f), kWave - 1);
+      if (lane == 0 && tot) atomicAdd(&sc[kStVerdict0 + k], (unsigned long long)tot);
+    }
+    vc_lo = vc_hi = 0;
+  };
   uint32_t perr = 0;
   wave_lds_sync();
   stamp(a, lane, 1, __builtin_amdgcn_s_memrealtime());
@@ -854,14 +869,17 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         if (lane == j) vout = vj;
       }
     }
-    if (staged) a.verdict[my_idx] = (uint8_t)vout;
-    // statistics from the verdict bytes (wave-uniform ballot counts)
-    const uint32_t v = staged ? vout : 0xFFu;
-    c_off += ballot_count(staged);
-    c_clone += ballot_count(staged && (v >> 4) != TGSIM_V_NONE);
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k)
-      c_v[k] += ballot_count(staged && (v & 15u) == k) + ballot_count(staged && (v >> 4) == k);
+    if (staged) {
+      a.verdict[my_idx] = (uint8_t)vout;
+      const uint32_t vo = vout & 15u, vc = vout >> 4;  // original 0..7, clone 0..7 or NONE
+      const uint64_t uo = 1ull << (16u * (vo & 3u)), uc = 1ull << (16u * (vc & 3u));
+      if (vo < 4) vc_lo += uo;
+      else vc_hi += uo;
+      if (vc < 4) vc_lo += uc;
+      else if (vc < 8) vc_hi += uc;
+      n_clone += vc != TGSIM_V_NONE ? 1u : 0u;
+    }
+    if ((b & 0x3FFFu) == 0x3FFFu) flush_verdicts();
   }
   stamp(a, lane, 2, __builtin_amdgcn_s_memrealtime());
   PROF_T0(e);
@@ -898,14 +916,13 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   const uint64_t bytes = wave_sum(Q.bytes);
   const uint64_t qbytes = qbytes_in + 16ull * Q.qn + 8ull * Q.rn;
   const uint64_t err = wave_sum(perr ? 1u : 0u);
+  const uint32_t c_clone = readlane32((uint32_t)scan_sum_i32((int32_t)n_clone), kWave - 1);
+  flush_verdicts();
   if (lane == 0) {
-    unsigned long long* sc = a.stats + (size_t)(blockIdx.x % kStatCopies) * kStSlots;
-    atomicAdd(&sc[kStOffered], (unsigned long long)c_off);
+    if (send > sbeg) atomicAdd(&sc[kStOffered], (unsigned long long)(send - sbeg));
     if (sched) atomicAdd(&sc[kStScheduled], (unsigned long long)sched);
     if (c_clone) atomicAdd(&sc[kStCloned], (unsigned long long)c_clone);
     if (corrupted) atomicAdd(&sc[kStCorrupted], (unsigned long long)corrupted);
-    for (int k = 0; k < 8; ++k)
-      if (c_v[k]) atomicAdd(&sc[kStVerdict0 + k], (unsigned long long)c_v[k]);
     if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
     if (err) {
