@@ -521,7 +521,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   if (s >= a.n_src) return;
   stamp(a, lane, 0, __builtin_amdgcn_s_memrealtime());
   const SrcParams pp = a.params[s];
-  SrcState st = a.state[s];
+  const SrcState st = a.state[s];  // dead after the set-up: the end writes a fresh state
   SimQueue Q{lds, pp, lane};
   Q.rh = 0;
   Q.rn = st.ring_n;
@@ -559,7 +559,6 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       if (k < qn) lds.slot[(rn + k) & kSlotMask] = qv[u];
     }
   }
-  const uint64_t qbytes_in = 16ull * Q.qn + 8ull * Q.rn;
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const bool src_on = a.enabled[Q.src] != 0;
   const bool corr = (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0;
@@ -570,6 +569,8 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   // into the statistics every 2^14 batches (at most 2 counts per lane and batch), before a field
   // can overflow
   unsigned long long* const sc = a.stats + (size_t)(blockIdx.x % kStatCopies) * kStSlots;
+  if (lane == 0 && (Q.qn | Q.rn))  // the queue state loaded (the stored part is added at the end)
+    atomicAdd(&sc[kStQueue], (unsigned long long)(16ull * Q.qn + 8ull * Q.rn));
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
   auto flush_verdicts = [&]() {
@@ -895,14 +896,15 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     for (uint32_t k = lane; k < Q.qn; k += kWave) gh[k] = Q.slot(Q.rn + k);
   }
   if (lane == 0) {
-    st.tat = Q.tat;
-    st.heap_n = Q.qn;
-    st.ring_n = Q.rn;
-    st.ring_head = 0;
-    st.last_dup = last_dup;
-    st.last_cor = last_cor;
-    st.last_reo = last_reo;
-    a.state[s] = st;
+    SrcState ns;
+    ns.tat = Q.tat;
+    ns.heap_n = Q.qn;
+    ns.ring_head = 0;
+    ns.ring_n = Q.rn;
+    ns.last_dup = last_dup;
+    ns.last_cor = last_cor;
+    ns.last_reo = last_reo;
+    a.state[s] = ns;
   }
   stamp(a, lane, 4, __builtin_amdgcn_s_memrealtime());
   stamp(a, lane, 5, ((uint64_t)s << 32) | n_batches);
@@ -911,11 +913,11 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
 #ifdef TGSIM_PROFILE
   for (int k = 0; k < 16; ++k) stamp(a, lane, 8 + k, Q.pf[k]);
 #endif
-  const uint64_t sched = wave_sum(Q.sched);
-  const uint64_t corrupted = wave_sum(Q.corrupted);
+  const uint32_t sched = readlane32((uint32_t)scan_sum_i32((int32_t)Q.sched), kWave - 1);
+  const uint32_t corrupted = readlane32((uint32_t)scan_sum_i32((int32_t)Q.corrupted), kWave - 1);
   const uint64_t bytes = wave_sum(Q.bytes);
-  const uint64_t qbytes = qbytes_in + 16ull * Q.qn + 8ull * Q.rn;
-  const uint64_t err = wave_sum(perr ? 1u : 0u);
+  const uint64_t qbytes = 16ull * Q.qn + 8ull * Q.rn;
+  const bool err = __ballot(perr != 0) != 0;
   const uint32_t c_clone = readlane32((uint32_t)scan_sum_i32((int32_t)n_clone), kWave - 1);
   flush_verdicts();
   if (lane == 0) {
