@@ -20,6 +20,9 @@ namespace tgsim {
 // Philox4x32-10 (Random123 constants).
 __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                        uint32_t k0, uint32_t k1, uint32_t r[4]) {
+  // the round keys are derived from the key at every call (2 SALU per round): hoisted out of the
+  // simulate loop they held 20 SGPRs and came back as spill reloads (v_readlane) at every draw
+  __asm__ volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     // one v_mad_u64_u32 per product instead of a v_mul_hi_u32 + v_mul_lo_u32 pair
