@@ -564,6 +564,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   }
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const bool src_on = a.enabled[Q.src] != 0;
+  // no rules and every peer connected (the storm and gossip runs): the filter reduces to the
+  // external-destination check, and the FIB/peer tables stay out of the loop's registers
+  const bool plain = src_on && !a.any_disabled && pp.rule_n == 0;
+  const uint32_t ext_v = (pp.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE;
   const bool corr = (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0;
   const uint32_t lim = a.queue_limit;
   uint32_t last_dup = st.last_dup, last_cor = st.last_cor, last_reo = st.last_reo;
@@ -604,7 +608,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     if (idx + kWave < send) rec2 = a.in[idx + kWave];  // in flight two batches ahead
     const uint64_t T = a.t0_ns + (uint64_t)r.tick * a.tick_ns;
     const uint32_t len = r.len & 0xFFFFu;
-    const uint32_t fv = staged ? filter(a, pp, src_on, r.dst) : 0u;
+    uint32_t fv = 0u;
+    if (plain) fv = r.dst == TGSIM_EXTERNAL ? ext_v : kFvPass;
+    else if (staged) fv = filter(a, pp, src_on, r.dst);
+    if (!staged) fv = 0u;
     uint32_t vout = 0xF0u | fv;  // verdict byte (final for filtered packets)
     if (!corr) {
       // ---------- parallel phase: every decision that does not depend on queue state
