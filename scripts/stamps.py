@@ -83,3 +83,19 @@ for i in np.argsort(-tot)[:a.top]:
         line += (f"  L {s.Latency / 1e6:6.2f} J {s.Jitter / 1e6:5.2f} bw {s.Bandwidth / 1e6:5.0f} "
                  f"reo {s.Reorder:.2f}")
     print(line)
+# Launch tail: which workgroups finish last, when they started, and how duration depends on the
+# dispatch position (workgroup id = dispatch order).
+span = end.max()
+tail = end > 0.85 * span
+print(f"  tail (end > 85 % of span): {tail.sum()} wgs, start mean {start[tail].mean():.1f} us, "
+      f"duration mean {tot[tail].mean():.1f} us, max {tot[tail].max():.1f}")
+dec = np.array_split(np.arange(len(st)), 10)
+print("  duration by dispatch decile (mean us):", [round(float(tot[d].mean()), 1) for d in dec])
+print("  start by dispatch decile (mean us):   ", [round(float(start[d].mean()), 1) for d in dec])
+print("  end by dispatch decile (max us):      ", [round(float(end[d].max()), 1) for d in dec])
+if shapes:
+    lat = np.array([shapes[i].Latency for i in src_of]) / 1e6
+    jit = np.array([shapes[i].Jitter for i in src_of]) / 1e6
+    bw = np.array([shapes[i].Bandwidth for i in src_of]) / 1e6
+    print(f"  tail sources: L {lat[tail].mean():.1f} ms, J {jit[tail].mean():.1f} ms, "
+          f"bw mix {dict(zip(*np.unique(bw[tail], return_counts=True)))}")
