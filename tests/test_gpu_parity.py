@@ -344,3 +344,25 @@ def test_epochs_reshaping_and_barriers(make_oracle):
         v, _ = assert_same(g, c, f"epoch {k}")
         assert len(v) > 300_000
     assert g.barrier_poll(wl.epoch_state(5)[0], n) and not g.barrier_poll(wl.epoch_state(6)[0], 1)
+
+
+def test_full_size_storm_rates():
+    """C3 at full size: the netem event rates the engine produced match the configured shapes
+    (loss, duplicate within +-0.5 pp of the offered-weighted mean of the per-instance rates)."""
+    n = 10_000
+    e = Engine(n)
+    wl.configure_storm(e, n)
+    e.gen_storm(0.5, 2000)
+    e.step(2000)
+    v = e.verdicts()
+    shapes = wl.storm_shape_arrays(n)
+    s = e.stats()
+    offered = s["offered"]
+    # every instance offers Poisson(0.5) per tick: weights equal in expectation
+    loss_exp = float(np.mean(shapes["loss"])) / 100
+    dup_exp = float(np.mean(shapes["duplicate"])) / 100
+    lost_orig = int(((v & 15) == abi.V_LOSS).sum())
+    cloned = int(((v >> 4) != abi.V_NONE).sum())
+    # loss on an original happens only without a duplicate event: P = loss * (1 - dup)
+    assert abs(lost_orig / offered - loss_exp * (1 - dup_exp)) <= 0.005
+    assert abs(cloned / offered - dup_exp * (1 - loss_exp)) <= 0.005

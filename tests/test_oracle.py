@@ -197,3 +197,59 @@ def test_configure_batch_equals_sequential(make_oracle):
     recs["network"][1] = ctypes.addressof(bogus)
     with pytest.raises(Exception, match="peer 7.*unsupported network: bogus"):
         b.configure_batch([3, 7], recs)
+
+
+@pytest.mark.parametrize("bw,gap_ticks", [(1 << 20, 5000), (10 ** 7, 500), (10 ** 8, 50)])
+def test_htb_rate(make_oracle, bw, gap_ticks):
+    """Bandwidth (link.go:156-167 -> HTB class rate = Bandwidth/8 B/s): a source offered about
+    twice its rate delivers at the configured rate, within 0.5 %, once its burst is spent."""
+    e = make_oracle(2)
+    e.configure(0, nw.Config(Network="default", Enable=True,
+                             Default=nw.LinkShape(Latency=1 * nw.Millisecond, Bandwidth=bw)))
+    length = 1250
+    step_ticks = 50_000  # 50 ms per step, 12 steps
+    per = step_ticks // gap_ticks
+    for k in range(12):
+        pk = np.zeros(per, dtype=abi.PKT_DTYPE)
+        pk["src"], pk["dst"], pk["len"] = 0, 1, length
+        pk["seq"] = np.arange(per) + k * per
+        pk["tick"] = np.arange(per) * gap_ticks
+        e.submit(pk)
+        e.step(step_ticks)
+    d = e.drain()
+    t = np.sort(d["t_ns"].astype(np.int64))
+    t = t[t >= 200_000_000]  # steady state: the queue backlog has absorbed the burst
+    rate = (len(t) - 1) * length * 8 / ((t[-1] - t[0]) * 1e-9)
+    assert abs(rate / bw - 1) <= 0.005, (bw, rate)
+
+
+def test_netem_event_rates(make_oracle):
+    """Duplicate, corrupt and reorder rates within +-0.5 pp of the configured percentages
+    (link.go:169-179: the only netem attributes the sidecar sets besides delay and loss)."""
+    n_pk, per, gap = 60_000, 1000, 65
+    e = make_oracle(2, queue_limit=1000)
+    shape = nw.LinkShape(Latency=10 * nw.Millisecond, Duplicate=4.0, Corrupt=6.0, Reorder=8.0)
+    e.configure(0, nw.Config(Network="default", Enable=True, Default=shape))
+    clones = 0
+    for chunk in range(n_pk // per):
+        pk = np.zeros(per, dtype=abi.PKT_DTYPE)
+        pk["src"], pk["dst"], pk["len"] = 0, 1, 100
+        pk["seq"] = np.arange(per) + chunk * per
+        pk["tick"] = np.arange(per) * gap
+        e.submit(pk)
+        e.step(per * gap)
+        v = e.verdicts()
+        assert not ((v & 15) == abi.V_QUEUE_FULL).any()
+        clones += int(((v >> 4) != abi.V_NONE).sum())
+    e.step(20_000)
+    d = e.drain()
+    orig = d[(d["flags"] & abi.FLAG_DUP) == 0]
+    assert len(orig) == n_pk
+    assert abs(clones / n_pk - 0.04) <= 0.005
+    assert abs(float((d["flags"] & abi.FLAG_CORRUPT != 0).mean()) - 0.06) <= 0.005
+    delay = orig["t_ns"].astype(np.int64) - orig["seq"].astype(np.int64) * gap * 1000
+    # reordered (sent at once) or delayed by L, plus at most the HTB serialisation behind items
+    # served at the same instant (100 B at the unlimited class rate of 2^32-1 B/s: 23 ns each)
+    now = delay < 1000
+    assert (now | ((delay >= 10_000_000) & (delay < 10_001_000))).all(), np.unique(delay)
+    assert abs(float(now.mean()) - 0.08) <= 0.005
