@@ -594,6 +594,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   stamp(a, lane, 1, __builtin_amdgcn_s_memrealtime());
 
   const uint32_t n_batches = (uint32_t)((send - sbeg + kWave - 1) / kWave);
+  // open queue: even if every offered packet and its clone were admitted the queue would stay
+  // below the netem limit (sparse sources: gossip, ping-pong, splitbrain)
+  const bool open_q = !corr && (uint64_t)Q.rn + Q.qn + 2 * (send - sbeg) < lim;
+  uint64_t T_enq = 0;  // open queue: offer time of the last packet that reached the netem enqueue
   uint64_t idx = sbeg + lane;
   InRec rec = {}, rec2 = {};  // records of batches b and b + 1 (two batches in flight)
   if (idx < send) rec = a.in[idx];
@@ -644,8 +648,31 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       }
       PROF_ADD(0, b);
       PROF_T0(w);
+      if (open_q) {
+        // ---------- the netem limit cannot be reached in this step: every candidate is admitted,
+        // and HTB serves in key order whatever the interleaving, so the items are merged now and
+        // served once the batches are done
+        uint64_t eo = reo_o ? T : T + pp.lat_ns;
+        const bool need1 = cand && !reo_o && pp.sigma != 0;
+        if (__ballot(need1)) {
+          if (need1) {
+            uint32_t r1[4];
+            philox(Q.src, r.dst, r.seq, 1, a.key0, a.key1, r1);
+            eo = delayed(pp, T, r1[0]);
+          }
+        }
+        if (cand && eo > kEMask) { perr = 1; eo = kEMask; }
+        if (cand) {
+          const uint32_t cv = cst == 0 ? TGSIM_V_NONE : cst == 1 ? TGSIM_V_LOSS : TGSIM_V_SCHEDULED;
+          vout = (cv << 4) | TGSIM_V_SCHEDULED;
+        }
+        Q.insert(cand, make_item(eo, len, flo, r.seq, r.dst));
+        Q.insert(cand && cst == 2, make_item(ec, len, flc, r.seq, r.dst));
+        const uint64_t mc = __ballot(cand);
+        if (mc) T_enq = readlane64(T, 63u - (uint32_t)__builtin_clzll(mc));
+      }
       // ---------- windows
-      uint64_t pend = __ballot(cand);
+      uint64_t pend = open_q ? 0ull : __ballot(cand);
       while (pend) {
         PROF_CNT(3, 1);
         if (Q.rn + Q.qn >= lim) {
@@ -893,6 +920,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     if ((b & 0x3FFFu) == 0x3FFFu) flush_verdicts();
   }
   stamp(a, lane, 2, __builtin_amdgcn_s_memrealtime());
+  if (open_q && T_enq) {  // what the last enqueue saw: service before its offer time, then departures
+    Q.serve_until(T_enq);
+    Q.depart_before(T_enq);
+  }
   PROF_T0(e);
   Q.serve_until(a.horizon_ns);
   PROF_ADD(13, e);
