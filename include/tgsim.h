@@ -72,6 +72,7 @@ enum tgsim_verdict {
 /* Engine flags (tgsim_opts.flags). */
 #define TGSIM_OPT_KEEP_DELIVERIES 0x1u /* keep delivered records for tgsim_drain (default on via 0) */
 #define TGSIM_OPT_DISCARD_DELIVERIES 0x2u /* bench: sort deliveries but do not accumulate them  */
+#define TGSIM_OPT_METRICS 0x4u            /* per-instance counters and histograms (tgsim_metrics) */
 
 typedef struct {
     uint32_t abi_version;  /* = TGSIM_ABI_VERSION                                          */
@@ -253,6 +254,22 @@ int64_t tgsim_gossip_reached(void* engine, uint64_t* out, size_t cap);
 int64_t tgsim_signal(void* engine, uint32_t state, uint32_t n);
 /* Returns 1 when the state's count >= target, 0 otherwise. */
 int tgsim_barrier_poll(void* engine, uint32_t state, uint64_t target);
+
+/* ---- metrics (the plans' runenv counters/histograms, pkg/metrics viewer.go:46) ---- */
+/* With TGSIM_OPT_METRICS, every step folds per-instance counters and log2 histograms on the
+ * device (accumulated since create).  tgsim_metrics copies one table and returns its word count:
+ *   TGSIM_METRICS_SRC  [instance of this shard][12]: offered packets, offered bytes, verdict
+ *                      counts 0..7 (originals + clones), HTB records served, bytes served;
+ *   TGSIM_METRICS_DST  [instance of this shard][2]: records and bytes delivered to it;
+ *   TGSIM_METRICS_HIST [2][64]: per step, instances by netem backlog at the step end (ring +
+ *                      queue), and by records delivered to them; bin b = floor(log2 x) + 1
+ *                      (bin 0: none).
+ * -ENODATA when the engine was created without TGSIM_OPT_METRICS. */
+enum tgsim_metrics_kind { TGSIM_METRICS_SRC = 0, TGSIM_METRICS_DST = 1, TGSIM_METRICS_HIST = 2 };
+#define TGSIM_METRICS_SRC_WORDS 12u
+#define TGSIM_METRICS_DST_WORDS 2u
+#define TGSIM_METRICS_BINS 64u
+int64_t tgsim_metrics(void* engine, uint32_t kind, uint64_t* out, size_t cap);
 
 /* ---- device timing (bench instrumentation) ------------------------------------------------ */
 /* Average device time (ms) of the simulate kernel over the steps since the last reset, measured

@@ -218,6 +218,11 @@ typedef struct {
     tgsim_gossip g;
     uint32_t* g_first;
     uint64_t* g_fwd;
+    /* K8 metrics (TGSIM_OPT_METRICS): per-instance tables and the two log2 histograms */
+    int metrics_on;
+    uint64_t* m_src; /* [nsrc][TGSIM_METRICS_SRC_WORDS] */
+    uint64_t* m_dst; /* [nsrc][TGSIM_METRICS_DST_WORDS] */
+    uint64_t m_hist[2 * TGSIM_METRICS_BINS];
     /* split step_sim: counts of a launched, not yet finished step */
     uint64_t pend_counts[2][8];
     uint32_t pend_ranks[2], pend_head, pend_n;
@@ -301,6 +306,11 @@ int tgo_create(const tgsim_opts* opts, void** out) {
     o->ip = (uint32_t*)malloc(sizeof(uint32_t) * o->o.n_peers);
     for (uint32_t i = 0; i < o->o.n_peers; ++i) o->ip[i] = o->o.subnet_base + 2 + i;
     o->gen_seq = (uint32_t*)calloc(o->nsrc, sizeof(uint32_t));
+    o->metrics_on = (o->o.flags & TGSIM_OPT_METRICS) != 0;
+    if (o->metrics_on) {
+        o->m_src = (uint64_t*)calloc((size_t)o->nsrc * TGSIM_METRICS_SRC_WORDS, sizeof(uint64_t));
+        o->m_dst = (uint64_t*)calloc((size_t)o->nsrc * TGSIM_METRICS_DST_WORDS, sizeof(uint64_t));
+    }
     for (uint32_t s = 0; s < o->nsrc; ++s) {
         o->src[s].heap = (item*)malloc(sizeof(item) * HCAP);
         o->src[s].ring = (uint64_t*)malloc(sizeof(uint64_t) * HCAP);
@@ -322,6 +332,7 @@ void tgo_destroy(void* p) {
     free(o->gq);
     free(o->src); free(o->enabled); free(o->ip); free(o->off); free(o->verdicts);
     free(o->out); free(o->step_out); free(o->gen_seq); free(o->g_first); free(o->g_fwd);
+    free(o->m_src); free(o->m_dst);
     free(o);
 }
 
@@ -662,6 +673,45 @@ static uint64_t queue_bytes(const oracle* o) {
     return b;
 }
 
+/* Histogram bin of x: 0 for none, b for 2^(b-1) <= x < 2^b (include/tgsim.h TGSIM_METRICS_HIST). */
+static uint32_t log2_bin(uint64_t x) {
+    uint32_t b = 0;
+    while (x) { b++; x >>= 1; }
+    return b < TGSIM_METRICS_BINS ? b : TGSIM_METRICS_BINS - 1;
+}
+
+/* Per source after a step: offered packets/bytes and verdicts of the step's input, the HTB
+ * records it served, and the backlog histogram (K8 metrics, include/tgsim.h). */
+static void metrics_step(oracle* o) {
+    for (size_t i = 0; i < o->n_off; ++i) {
+        const tgsim_pkt* k = &o->off[i].p;
+        uint64_t* row = o->m_src + (size_t)(k->src - o->o.shard_begin) * TGSIM_METRICS_SRC_WORDS;
+        uint8_t v = o->verdicts[o->off[i].idx];
+        row[0]++;
+        row[1] += k->len;
+        row[2 + (v & 15)]++;
+        if ((v >> 4) < 8) row[2 + (v >> 4)]++;
+    }
+    for (size_t i = 0; i < o->n_step; ++i) {
+        uint64_t* row = o->m_src + (size_t)(o->step_out[i].src - o->o.shard_begin) * TGSIM_METRICS_SRC_WORDS;
+        row[10]++;
+        row[11] += o->step_out[i].len;
+    }
+    for (uint32_t s = 0; s < o->nsrc; ++s) o->m_hist[log2_bin((uint64_t)o->src[s].heap_n + o->src[s].ring_n)]++;
+}
+
+int64_t tgo_metrics(void* p, uint32_t kind, uint64_t* out, size_t cap) {
+    oracle* o = (oracle*)p;
+    if (!o || (!out && cap) || kind > TGSIM_METRICS_HIST) return -EINVAL;
+    if (!o->metrics_on) return fail(o, -ENODATA, "engine created without TGSIM_OPT_METRICS");
+    const uint64_t* b = kind == TGSIM_METRICS_SRC ? o->m_src : kind == TGSIM_METRICS_DST ? o->m_dst : o->m_hist;
+    size_t n = kind == TGSIM_METRICS_SRC   ? (size_t)o->nsrc * TGSIM_METRICS_SRC_WORDS
+               : kind == TGSIM_METRICS_DST ? (size_t)o->nsrc * TGSIM_METRICS_DST_WORDS
+                                           : 2 * TGSIM_METRICS_BINS;
+    memcpy(out, b, sizeof(uint64_t) * (cap < n ? cap : n));
+    return (int64_t)n;
+}
+
 static int step_core(oracle* o, uint32_t n_ticks) {
     if (n_ticks == 0) return -EINVAL;
     if (o->gq_n) { /* the oldest generated window is this step's input */
@@ -698,6 +748,7 @@ static int step_core(oracle* o, uint32_t n_ticks) {
     uint64_t T1 = (o->now_tick + n_ticks) * o->o.tick_ns;
     for (uint32_t s = 0; s < o->nsrc; ++s) htb_until(o, s, T1 + o->o.lookahead_ns);
     o->st.queue_state_bytes += queue_bytes(o);
+    if (o->metrics_on) metrics_step(o);
     o->n_off = 0;
     o->now_tick += n_ticks;
     o->st.now_tick = o->now_tick;
@@ -709,6 +760,19 @@ static void gossip_receive(oracle* o, const tgsim_delivery* recs, size_t n);
 
 static void deliver_records(oracle* o, const tgsim_delivery* recs, size_t n) {
     if (o->gossip_on) gossip_receive(o, recs, n);
+    if (o->metrics_on) { /* per destination of this shard: records and bytes, histogram of counts */
+        uint64_t* cnt = (uint64_t*)calloc(o->nsrc, sizeof(uint64_t));
+        for (size_t i = 0; i < n; ++i) {
+            uint32_t d = recs[i].dst - o->o.shard_begin;
+            cnt[d]++;
+            o->m_dst[(size_t)d * TGSIM_METRICS_DST_WORDS + 1] += recs[i].len;
+        }
+        for (uint32_t d = 0; d < o->nsrc; ++d) {
+            o->m_dst[(size_t)d * TGSIM_METRICS_DST_WORDS] += cnt[d];
+            o->m_hist[TGSIM_METRICS_BINS + log2_bin(cnt[d])]++;
+        }
+        free(cnt);
+    }
     o->out = (tgsim_delivery*)grow(o->out, &o->cap_out, o->n_out + n, sizeof(tgsim_delivery));
     memcpy(o->out + o->n_out, recs, n * sizeof(tgsim_delivery));
     qsort(o->out + o->n_out, n, sizeof(tgsim_delivery), cmp_del);

@@ -52,6 +52,7 @@ int tgo_barrier_poll(void* o, uint32_t state, uint64_t target);
 int tgo_gossip_init(void* o, const tgsim_gossip* g);
 int tgo_gen_gossip(void* o, uint32_t n_ticks);
 int64_t tgo_gossip_reached(void* o, uint64_t* out, size_t cap);
+int64_t tgo_metrics(void* o, uint32_t kind, uint64_t* out, size_t cap);
 
 /* Building blocks exposed for known-answer tests. */
 void tgo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

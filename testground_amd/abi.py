@@ -18,6 +18,11 @@ FLAG_DUP = 0x1
 FLAG_CORRUPT = 0x2
 
 OPT_DISCARD_DELIVERIES = 0x2
+OPT_METRICS = 0x4
+METRICS_SRC, METRICS_DST, METRICS_HIST = 0, 1, 2
+METRICS_SRC_WORDS, METRICS_DST_WORDS, METRICS_BINS = 12, 2, 64
+# columns of the per-instance source table (include/tgsim.h TGSIM_METRICS_SRC)
+METRICS_SRC_COLUMNS = ["offered", "offered_bytes"] + [f"verdict_{i}" for i in range(8)] + ["served", "served_bytes"]
 
 
 class Opts(C.Structure):
@@ -116,7 +121,7 @@ EXPORTS = [
     "tgsim_deliver_async", "tgsim_wait_event", "tgsim_sync", "tgsim_step_sim_launch", "tgsim_step_sim_finish",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_barrier_poll", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
-    "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached",
+    "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
 ]
 
 
@@ -162,3 +167,4 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("gen_gossip", C.c_int, vp, C.c_uint32)
     f("gossip_reached", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("offered", C.c_int64, vp, C.c_void_p, C.c_size_t)
+    f("metrics", C.c_int64, vp, C.c_uint32, C.c_void_p, C.c_size_t)

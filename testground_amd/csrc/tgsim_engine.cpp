@@ -283,6 +283,10 @@ struct tgsim_engine_s {
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
 
+  // K8 metrics (TGSIM_OPT_METRICS): per-source and per-destination tables, two histograms
+  bool metrics_on = false;
+  DevBuf<unsigned long long> d_msrc, d_mdst, d_mhist;
+
   // gossip workload (C4)
   bool gossip_on = false;
   tgsim_gossip gossip{};
@@ -569,6 +573,20 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.emplace_back(ev0, ev1);
+  if (E->metrics_on) {
+    MetricsArgs m;
+    m.off = E->d_off.p;
+    m.in = E->d_in.p;
+    m.verdict = E->d_verdict.p;
+    m.emit = E->d_emit.p;
+    m.emit_n = E->d_emit_n.p;
+    m.state = E->d_state.p;
+    m.n_src = E->S;
+    m.src = E->d_msrc.p;
+    m.hist = E->d_mhist.p;
+    launch_metrics_src(m, E->st);
+    HIPCHK(hipGetLastError());
+  }
   // heavy-first dispatch order for the next step: it shortens the tail when only a few rounds of
   // workgroups fit; with many more sources than resident workgroups the dispatcher balances alone
   if (ordered) {
@@ -763,6 +781,10 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   if (rc) return rc;
   launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq);
   HIPCHK(hipGetLastError());
+  if (E->metrics_on) {
+    launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   return 0;
 }
@@ -805,6 +827,10 @@ int deliver_local(Eng* E) {
   if (rc) return rc;
   launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_lcnt.p, nd, dst, sq);
   HIPCHK(hipGetLastError());
+  if (E->metrics_on) {
+    launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipEventRecord(E->ev_local, sq));
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   std::swap(E->d_emit, E->d_emit_alt);
@@ -918,6 +944,17 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipMemset(E->d_gen_seq.p, 0, sizeof(uint32_t) * E->S), "memset"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_stats.p, 0, sizeof(unsigned long long) * kStSlots * kStatCopies), "memset")))
     return bail(rc);
+  E->metrics_on = (E->o.flags & TGSIM_OPT_METRICS) != 0;
+  if (E->metrics_on) {
+    const size_t ns = static_cast<size_t>(E->S) * kMetricSrcWords, nd = static_cast<size_t>(E->S) * kMetricDstWords;
+    if ((rc = E->hip(E->d_msrc.ensure(ns), "alloc metrics"))) return bail(rc);
+    if ((rc = E->hip(E->d_mdst.ensure(nd), "alloc metrics"))) return bail(rc);
+    if ((rc = E->hip(E->d_mhist.ensure(2 * kMetricBins), "alloc metrics"))) return bail(rc);
+    if ((rc = E->hip(hipMemset(E->d_msrc.p, 0, sizeof(unsigned long long) * ns), "memset"))) return bail(rc);
+    if ((rc = E->hip(hipMemset(E->d_mdst.p, 0, sizeof(unsigned long long) * nd), "memset"))) return bail(rc);
+    if ((rc = E->hip(hipMemset(E->d_mhist.p, 0, sizeof(unsigned long long) * 2 * kMetricBins), "memset")))
+      return bail(rc);
+  }
   E->peers_dirty = E->rules_dirty = E->params_dirty = true;
   if ((rc = flush_config(E))) return bail(rc);
   *out = E;
@@ -939,6 +976,7 @@ void tgsim_destroy(void* e) {
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
+  E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
   for (auto& pr : E->ev_pending) {
@@ -1368,6 +1406,21 @@ int64_t tgsim_signal(void* e, uint32_t state, uint32_t n) {
   if (!E || state >= kStates) return -EINVAL;
   E->counters64[state] += n;
   return static_cast<int64_t>(E->counters64[state]);
+}
+
+int64_t tgsim_metrics(void* e, uint32_t kind, uint64_t* out, size_t cap) {
+  Eng* E = as_eng(e);
+  if (!E || (!out && cap) || kind > TGSIM_METRICS_HIST) return -EINVAL;
+  if (!E->metrics_on) return E->fail(-ENODATA, "engine created without TGSIM_OPT_METRICS");
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
+  const DevBuf<unsigned long long>& b = kind == TGSIM_METRICS_SRC ? E->d_msrc : kind == TGSIM_METRICS_DST ? E->d_mdst : E->d_mhist;
+  const size_t n = kind == TGSIM_METRICS_SRC   ? static_cast<size_t>(E->S) * kMetricSrcWords
+                   : kind == TGSIM_METRICS_DST ? static_cast<size_t>(E->S) * kMetricDstWords
+                                               : 2 * kMetricBins;
+  if (cap) HIPCHK(hipMemcpy(out, b.p, sizeof(uint64_t) * (cap < n ? cap : n), hipMemcpyDeviceToHost));
+  return static_cast<int64_t>(n);
 }
 
 int tgsim_barrier_poll(void* e, uint32_t state, uint64_t target) {

@@ -101,6 +101,21 @@ struct SimArgs {
 };
 constexpr uint32_t kStampSlots = 24;  // 8 phase stamps + 16 profile counters (TGSIM_PROFILE)
 
+// K8 metrics tables (include/tgsim.h TGSIM_METRICS_*).
+constexpr uint32_t kMetricSrcWords = TGSIM_METRICS_SRC_WORDS, kMetricDstWords = TGSIM_METRICS_DST_WORDS;
+constexpr uint32_t kMetricBins = TGSIM_METRICS_BINS;
+struct MetricsArgs {
+  const uint64_t* off;          // the step's CSR offsets (S+1)
+  const InRec* in;
+  const uint8_t* verdict;
+  const tgsim_delivery* emit;   // per-source emit regions, base 2*off[s] + kHeapCap*s
+  const uint32_t* emit_n;
+  const SrcState* state;
+  uint32_t n_src;
+  unsigned long long* src;      // [S][kMetricSrcWords]
+  unsigned long long* hist;     // [2][kMetricBins]
+};
+
 // Gossip workload state (C4) of one shard.
 struct GossipArgs {
   uint32_t* first;          // [s][64] earliest receipt tick (0xFFFFFFFF: none)

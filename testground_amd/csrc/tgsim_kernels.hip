@@ -1508,6 +1508,70 @@ __global__ __launch_bounds__(256) void k_dst_sort(tgsim_delivery* in, const uint
 }
 
 // ---------------------------------------------------------------------------------------------
+// K8 metrics (opt-in): per-instance counters and log2 histograms folded after each step, one
+// wavefront per instance, no atomics on the counters (an instance is one wavefront's).
+__device__ __forceinline__ uint32_t log2_bin(uint64_t x) {  // 0: none, b: 2^(b-1) <= x < 2^b
+  const uint32_t b = x ? 64u - (uint32_t)__builtin_clzll(x) : 0u;
+  return b < kMetricBins ? b : kMetricBins - 1;
+}
+
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+  return readlane32((uint32_t)scan_sum_i32((int32_t)v), kWave - 1);
+}
+
+// Per source: offered packets and bytes, verdict counts (originals + clones), HTB records served
+// and their bytes (the step's emit region), and the backlog histogram at the step end.
+__global__ __launch_bounds__(256) void k_metrics_src(MetricsArgs m) {
+  const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (s >= m.n_src) return;
+  const uint64_t b0 = m.off[s], b1 = m.off[s + 1];
+  uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t bytes = 0;
+  for (uint64_t i = b0 + lane; i < b1; i += kWave) {
+    const uint32_t vb = m.verdict[i], vo = vb & 15u, vc = vb >> 4;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) v[k] += (vo == k ? 1u : 0u) + (vc == k ? 1u : 0u);
+    bytes += m.in[i].len & 0xFFFFu;
+  }
+  const uint32_t n_emit = m.emit_n[s];
+  const tgsim_delivery* e = m.emit + 2 * b0 + (uint64_t)kHeapCap * s;
+  uint64_t sbytes = 0;
+  for (uint32_t i = lane; i < n_emit; i += kWave) sbytes += e[i].len;
+  unsigned long long* row = m.src + (size_t)s * kMetricSrcWords;
+  uint32_t tv[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) tv[k] = wave_total(v[k]);
+  const uint64_t tb = wave_sum(bytes), ts = wave_sum(sbytes);
+  if (lane == 0) {
+    row[0] += b1 - b0;
+    row[1] += tb;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) row[2 + k] += tv[k];
+    row[10] += n_emit;
+    row[11] += ts;
+    const SrcState st = m.state[s];
+    atomicAdd(&m.hist[log2_bin((uint64_t)st.heap_n + st.ring_n)], 1ull);
+  }
+}
+
+// Per destination of this shard: the records delivered to it in this step (its segment of the
+// delivery-ordered output) and their bytes; histogram of the per-destination record counts.
+__global__ __launch_bounds__(256) void k_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_t n_dst,
+                                                     unsigned long long* dst, unsigned long long* hist) {
+  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (d >= n_dst) return;
+  const uint64_t b0 = off[d], b1 = off[d + 1];
+  uint64_t bytes = 0;
+  for (uint64_t i = b0 + lane; i < b1; i += kWave) bytes += recs[i].len;
+  const uint64_t tb = wave_sum(bytes);
+  if (lane == 0) {
+    dst[(size_t)d * kMetricDstWords] += b1 - b0;
+    dst[(size_t)d * kMetricDstWords + 1] += tb;
+    atomicAdd(&hist[kMetricBins + log2_bin(b1 - b0)], 1ull);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Host-side launchers.
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
@@ -1532,6 +1596,15 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
   const dim3 wgrid((h.n_src + 3) / 4), wblk(256);  // one wavefront per source
   if (phase == 0) hipLaunchKernelGGL(k_gen_count, wgrid, wblk, 0, st, g, counts);
   else hipLaunchKernelGGL(k_gen_write, wgrid, wblk, 0, st, g, off, gen_seq, out);
+}
+
+void launch_metrics_src(const MetricsArgs& m, hipStream_t st) {
+  if (m.n_src) hipLaunchKernelGGL(k_metrics_src, dim3((m.n_src + 3) / 4), dim3(256), 0, st, m);
+}
+
+void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_t n_dst, unsigned long long* dst,
+                        unsigned long long* hist, hipStream_t st) {
+  if (n_dst) hipLaunchKernelGGL(k_metrics_dst, dim3((n_dst + 3) / 4), dim3(256), 0, st, recs, off, n_dst, dst, hist);
 }
 
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st) {

@@ -32,6 +32,10 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
 // phase 0: fold delivered records into receipts; 1: per-source counts; 2: write the window.
 void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
                    const uint64_t* off, InRec* out, int phase, hipStream_t st);
+// K8 metrics folds (opt-in): per source after k_sim, per destination after the delivery sort.
+void launch_metrics_src(const MetricsArgs& m, hipStream_t st);
+void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_t n_dst, unsigned long long* dst,
+                        unsigned long long* hist, hipStream_t st);
 // Receipts of n_dev[0] records (count read on the device).
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st);
 // Exclusive scan of in[0..n) into out[0..n] (out[n] = total, also stored at *total when non-null);

@@ -217,6 +217,21 @@ class CABIEngine:
             self._check(self._fn("verdicts")(self._h, out.ctypes.data, n), "verdicts")
         return out
 
+    def metrics(self) -> dict:
+        """K8 metrics tables accumulated since create (engine flag abi.OPT_METRICS): `src`
+        [instances of this shard, 12] (columns abi.METRICS_SRC_COLUMNS), `dst` [instances, 2]
+        (records, bytes delivered), `hist` [2, 64] (log2 bins of the per-step netem backlog and of
+        the per-step records delivered, per instance)."""
+        out = {}
+        for kind, key, shape in ((abi.METRICS_SRC, "src", (-1, abi.METRICS_SRC_WORDS)),
+                                 (abi.METRICS_DST, "dst", (-1, abi.METRICS_DST_WORDS)),
+                                 (abi.METRICS_HIST, "hist", (2, abi.METRICS_BINS))):
+            n = self._check(self._fn("metrics")(self._h, kind, None, 0), "metrics")
+            a = np.zeros(n, dtype=np.uint64)
+            self._check(self._fn("metrics")(self._h, kind, a.ctypes.data, n), "metrics")
+            out[key] = a.reshape(shape)
+        return out
+
     def stats(self) -> dict:
         s = abi.Stats()
         self._check(self._fn("stats")(self._h, C.byref(s)), "stats")
