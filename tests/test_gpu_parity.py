@@ -366,3 +366,59 @@ def test_full_size_storm_rates():
     # loss on an original happens only without a duplicate event: P = loss * (1 - dup)
     assert abs(lost_orig / offered - loss_exp * (1 - dup_exp)) <= 0.005
     assert abs(cloned / offered - dup_exp * (1 - loss_exp)) <= 0.005
+
+
+def test_edge_inputs(make_oracle):
+    """Empty and ragged inputs, extreme values: steps with no packets at all, one peer sending
+    everything, the last tick of a window, zero- and maximum-length packets, the maximum netem
+    limit (1024) filled from empty in one burst, external traffic from a disconnected source,
+    a latency past the 2^32 us clamp (link.go:143-151), and 1-tick steps."""
+    n = 50
+    g, c = both(make_oracle, n, queue_limit=1024)
+    shapes = [nw.LinkShape(), nw.LinkShape(Latency=5 * nw.Millisecond, Bandwidth=1 << 20),
+              nw.LinkShape(Latency=(1 << 33) * nw.Microsecond), nw.LinkShape(Jitter=3 * nw.Millisecond),
+              nw.LinkShape(Latency=1, Loss=100.0), nw.LinkShape(Duplicate=100.0, Reorder=100.0)]
+    for i in range(n):
+        cfg = nw.Config(Network="default", Enable=(i != 7), Default=shapes[i % len(shapes)],
+                        RoutingPolicy=nw.RoutingPolicyType.AllowAll if i % 2 else nw.RoutingPolicyType.DenyAll)
+        g.configure(i, cfg)
+        c.configure(i, cfg)
+    seq = np.zeros(n, dtype=np.uint32)
+
+    def run(pk, ticks, what):
+        if pk is not None:
+            g.submit(pk)
+            c.submit(pk)
+        g.step(ticks)
+        c.step(ticks)
+        assert_same(g, c, what)
+
+    run(None, 1000, "empty step")
+    run(None, 1, "empty 1-tick step")
+    # one source, 3000 packets in one tick: the 1024 queue fills, the rest are QUEUE_FULL
+    m = 3000
+    pk = np.zeros(m, dtype=abi.PKT_DTYPE)
+    pk["src"], pk["dst"], pk["len"], pk["tick"] = 1, 2, 1500, 999
+    pk["seq"] = np.arange(m)
+    run(pk, 1000, "burst into the max limit")
+    # ragged: every source a different count, lengths 0 and 65535, externals, disconnected source
+    rng = np.random.default_rng(21)
+    parts = []
+    for s in range(n):
+        k = int(s * 3 % 17)
+        if not k:
+            continue
+        p = np.zeros(k, dtype=abi.PKT_DTYPE)
+        p["src"] = s
+        p["dst"] = np.where(rng.random(k) < 0.2, abi.EXTERNAL, (s + 1 + rng.integers(0, n - 1, k)) % n)
+        p["len"] = rng.choice([0, 1, 65535], k)
+        p["tick"] = np.sort(rng.integers(0, 5, k))
+        p["seq"] = seq[s] + np.arange(k) + 10_000
+        seq[s] += k
+        parts.append(p)
+    run(np.concatenate(parts), 5, "ragged 5-tick step")
+    for w in (1, 7, 1):
+        run(None, w, f"empty {w}-tick step after traffic")
+    st = g.stats()
+    bv = st["by_verdict"]
+    assert bv["queue_full"] > 0 and bv["disconnected"] > 0 and bv["external"] > 0 and bv["no_route"] > 0
