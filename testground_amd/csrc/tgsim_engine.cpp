@@ -779,7 +779,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   tgsim_delivery* dst = nullptr;
   rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq);
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq, n);
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
@@ -825,7 +825,7 @@ int deliver_local(Eng* E) {
   tgsim_delivery* dst = nullptr;
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_lcnt.p, nd, dst, sq);
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_lcnt.p, nd, dst, sq, need_n ? n : E->n_in);
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);

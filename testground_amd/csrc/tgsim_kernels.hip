@@ -1439,14 +1439,7 @@ __device__ __forceinline__ uint32_t wave_rank(const RecKey& k, uint32_t n, uint3
 // buffer and the output (each element's place = its index in its run + its rank in the other
 // run, a binary search), so no scratch memory is needed.  The destination's count is reset to
 // zero for the next step's histogram.
-__global__ __launch_bounds__(256) void k_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
-                                                  uint32_t n_dst, tgsim_delivery* out) {
-  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63u;
-  if (d >= n_dst) return;
-  const uint32_t n = (uint32_t)cnt[d];
-  if (n == 0) return;
-  const uint64_t b = off[d];
+__device__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_delivery* out, uint32_t lane) {
   if (n <= kWave) {
     tgsim_delivery r;
     RecKey k{~0ull, ~0ull, 1u};
@@ -1504,7 +1497,51 @@ __global__ __launch_bounds__(256) void k_dst_sort(tgsim_delivery* in, const uint
       for (uint32_t i = lane; i < n; i += kWave) out[b + i] = src[i];
     }
   }
+}
+
+// One destination per wavefront (segments of tens of records and more: storm).
+__global__ __launch_bounds__(256) void k_dst_sort_wide(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
+                                                       uint32_t n_dst, tgsim_delivery* out) {
+  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (d >= n_dst) return;
+  const uint32_t n = (uint32_t)cnt[d];
+  if (n == 0) return;
+  sort_segment(in, off[d], n, out, lane);
   if (lane == 0) cnt[d] = 0;
+}
+
+// Eight destinations per wavefront (a few records each: gossip): a destination with at most 8
+// records is ordered by its lane group of 8 (ranks from in-group shuffles); longer segments take
+// the whole wavefront in turn.
+__global__ __launch_bounds__(256) void k_dst_sort_narrow(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
+                                                  uint32_t n_dst, tgsim_delivery* out) {
+  const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u, g = lane >> 3, j = lane & 7u, d = w * 8 + g;
+  if (w * 8 >= n_dst) return;
+  const uint32_t n = d < n_dst ? (uint32_t)cnt[d] : 0u;
+  const uint64_t b = d < n_dst ? off[d] : 0ull;
+  const bool have = n <= 8 && j < n;
+  tgsim_delivery r;
+  RecKey k{~0ull, ~0ull, 1u};
+  if (have) {
+    r = in[b + j];
+    k = rec_key(r);
+  }
+  uint32_t rank = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) {  // ties: input order, as wave_rank
+    const uint32_t from = (g << 3) | q;
+    const uint64_t t = shfl64(k.t, from), sq = shfl64(k.sq, from);
+    const uint32_t c = (uint32_t)__shfl((int)k.c, (int)from, 64);
+    rank += (q < n && (rec_lt(t, sq, c, k.t, k.sq, k.c) || (!rec_lt(k.t, k.sq, k.c, t, sq, c) && q < j))) ? 1u : 0u;
+  }
+  if (have) out[b + rank] = r;
+  for (uint64_t big = __ballot(j == 0 && n > 8); big; big &= big - 1) {
+    const uint32_t gl = (uint32_t)__builtin_ctzll(big);
+    sort_segment(in, readlane64(b, gl), readlane32(n, gl), out, lane);
+  }
+  if (j == 0 && n) cnt[d] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1685,9 +1722,12 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
 }
 
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, hipStream_t st) {
+                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
   if (!n_dst) return;
-  hipLaunchKernelGGL(k_dst_sort, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
+  if (n_hint <= 8ull * n_dst)
+    hipLaunchKernelGGL(k_dst_sort_narrow, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
+  else
+    hipLaunchKernelGGL(k_dst_sort_wide, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
 }
 
 

@@ -54,7 +54,8 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st);
 // Orders each destination's records; resets cnt[] to zero for the next histogram.
 // (in, the scatter buffer, is overwritten for segments longer than 64.)
+// n_hint: about how many records (picks one wavefront per destination or eight).
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, hipStream_t st);
+                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint);
 
 }  // namespace tgsim
