@@ -100,6 +100,56 @@ class SyncClient:
         pass
 
 
+class EngineSyncClient(SyncClient):
+    """Sync client whose signal and barrier counters are the engine's sync counters
+    (tgsim_signal / tgsim_barrier_poll, K7): the states the handler signals
+    (`network-initialized`, sidecar_handler.go:40-44; callback states, :75-80) and the plans'
+    barriers live beside the simulated network instead of in a Redis-backed sync service.
+    Pub/sub topics stay in memory (the handler's `network:<hostname>` subscription, :49).
+
+    State names map to the engine's 1024 state slots in first-use order, so every process of a
+    sharded run must touch its states in the same order; `reduce`, when given, sums a state's
+    count over the shards (ShardedStepper.barrier does it with an RCCL all-reduce)."""
+
+    def __init__(self, engine, lock: Optional[threading.Lock] = None,
+                 reduce: Optional[Callable[[int, int], bool]] = None):
+        super().__init__()
+        self.engine = engine
+        self.lock = lock or threading.Lock()
+        self.reduce = reduce
+        self._ids: Dict[str, int] = {}
+
+    def state_id(self, state: str) -> int:
+        with self._cv:
+            if state not in self._ids:
+                if len(self._ids) >= 1024:
+                    raise RuntimeError("engine sync counters: more than 1024 states")
+                self._ids[state] = len(self._ids)
+            return self._ids[state]
+
+    def SignalEntry(self, ctx: Context, state: str) -> int:
+        sid = self.state_id(state)
+        with self.lock:
+            seq = self.engine.signal(sid, 1)
+        with self._cv:
+            self._cv.notify_all()
+        return seq
+
+    def _reached(self, state: str, target: int) -> bool:
+        sid = self.state_id(state)
+        if self.reduce is not None:
+            return self.reduce(sid, target)
+        with self.lock:
+            return self.engine.barrier_poll(sid, target)
+
+    def Barrier(self, ctx: Context, state: str, target: int) -> None:
+        while not self._reached(state, target):
+            if ctx.done():
+                raise TimeoutError(f"barrier {state!r}: {ctx.err()}")
+            with self._cv:
+                self._cv.wait(timeout=0.01)
+
+
 @dataclasses.dataclass
 class RunEnv:
     TestInstanceCount: int = 1
@@ -260,9 +310,9 @@ class SimReactor(Reactor):
     def __init__(self, engine, n_instances: int, client: Optional[SyncClient] = None):
         self.engine = engine
         self.n = n_instances
-        self.Client = client or SyncClient()
-        self.RunEnv = RunEnv(TestInstanceCount=n_instances)
         self.lock = threading.Lock()
+        self.Client = client if client is not None else EngineSyncClient(engine, self.lock)
+        self.RunEnv = RunEnv(TestInstanceCount=n_instances)
         self.threads: List[threading.Thread] = []
         self.errors: List[BaseException] = []
         self.networks = [SimNetwork(engine, p, self.lock) for p in range(n_instances)]

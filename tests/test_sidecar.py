@@ -77,6 +77,11 @@ def _sim_flow(engine, n=3):
                                          nw.Config(Network="bogus", Enable=True, CallbackState="never"))
     ctx.cancel()
     r.Close()
+    # the handler's states went through the engine's sync counters (K7)
+    assert isinstance(r.Client, sc.EngineSyncClient)
+    assert engine.barrier_poll(r.Client.state_id(sc.NET_INIT_STATE), n)
+    assert not engine.barrier_poll(r.Client.state_id(sc.NET_INIT_STATE), n + 1)
+    assert engine.barrier_poll(r.Client.state_id("rules-installed"), 1)
     assert any("failed to update network bogus: " in str(e) and "unsupported network: bogus" in str(e)
                for e in r.errors), r.errors
     engine.submit(np.array([(0, 1, 0, 100, 0), (0, 2, 1, 100, 0)], dtype=abi.PKT_DTYPE))
