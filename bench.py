@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--queue-limit", type=int, default=0, help="netem limit (0 = netlink default 1000)")
     p.add_argument("--shapes", default="storm", choices=["storm", "fixed"],
                    help="storm: C3 heterogeneous shapes; fixed: L=5 ms, no jitter/loss/reorder (probe)")
+    p.add_argument("--sharded", action="store_true",
+                   help="use the peer-sharded step (RCCL exchange) even at one rank, to time the N>1 path")
     a = p.parse_args()
     if not a.peers:
         a.peers = {"storm": 10_000, "gossip": 125_000, "epochs": 100_000}[a.workload]
@@ -167,6 +169,11 @@ WORKLOAD_NAMES = {
 
 def main():
     a = parse()
+    # the one JSON line goes to the original stdout; everything else (RCCL's version banner, library
+    # chatter) is sent to stderr so that the line stays the only thing on stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -179,7 +186,12 @@ def main():
 
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    sharded = world > 1 or a.sharded
+    if sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         import torch.distributed as dist
         from testground_amd.shard import init_rccl
         init_rccl(torch.device("cuda", local))
@@ -196,7 +208,7 @@ def main():
         eng.configure_batch(np.arange(peers_total), configs_array(np.full(peers_total, 5_000_000), routing_policy=2))
     bounds = [r * a.peers for r in range(world)] + [peers_total]
     stepper = None
-    if world > 1:
+    if sharded:
         from testground_amd.shard import ShardedStepper
         stepper = ShardedStepper(eng, bounds, device=f"cuda:{local}")
     step = eng.step if stepper is None else stepper.step
@@ -308,7 +320,7 @@ def main():
     if world == 1 and not a.no_cpu:
         res["cpu_baseline"] = cpu_baseline(a, peers_total)
         res["cpu_baseline"]["gpu_over_cpu"] = res["value"] / res["cpu_baseline"]["value"]
-    print(json.dumps(res))
+    os.write(json_fd, (json.dumps(res) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 

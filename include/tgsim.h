@@ -213,6 +213,10 @@ int tgsim_step_sim(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint3
 int tgsim_step_sim_launch(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* rank_bounds,
                           void* d_out, size_t out_cap);
 int tgsim_step_sim_finish(void* engine, uint64_t* rank_counts);
+/* tgsim_step_sim_finish without the wait for earlier asynchronous deliveries: the caller orders
+ * the reuse of a delivery's input buffer on the device instead (tgsim_delivery_event), so the host
+ * never blocks on the delivery stream. */
+int tgsim_step_sim_counts(void* engine, uint64_t* rank_counts);
 /* Phase 2: sorts the records addressed to this shard (DEVICE memory, n records) into the
  * delivery order and appends them to the drain buffer. */
 int tgsim_deliver(void* engine, const void* d_in, size_t n);
@@ -224,6 +228,9 @@ int tgsim_deliver_async(void* engine, const void* d_in, size_t n, void* wait_eve
 /* Makes the engine's simulate stream wait for a hipEvent_t of another stream (e.g. the collective
  * that still reads the d_out buffer the next tgsim_step_sim will overwrite). */
 int tgsim_wait_event(void* engine, void* event);
+/* Records a hipEvent_t on the engine's delivery stream after every delivery enqueued so far (a
+ * stream about to overwrite a delivery's input buffer waits for it). */
+int tgsim_delivery_event(void* engine, void* event);
 /* Waits for all of the engine's device work; reports a pending -EOVERFLOW. */
 int tgsim_sync(void* engine);
 /* Upper bound of records phase 1 can emit for the next step (for sizing d_out). */

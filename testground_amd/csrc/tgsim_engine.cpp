@@ -197,8 +197,11 @@ struct tgsim_engine_s {
   tgsim_opts o{};
   std::string err;
   int dev = 0;
-  hipStream_t st = nullptr;      // simulate stream: inputs, k_sim, routing, single-shard delivery
+  hipStream_t st = nullptr;      // simulate stream: inputs, k_sim, dispatch order
   hipStream_t dst_st = nullptr;  // delivery stream of inbound records (tgsim_deliver*), overlaps the next k_sim
+  hipStream_t rt_st = nullptr;   // routing stream: a sharded step's records grouped by destination shard
+                                 // beside the next k_sim (which writes the other emit pair)
+  hipEvent_t ev_rt = nullptr;    // recorded after the last routing on rt_st (it reads d_off)
   hipEvent_t ev_dst = nullptr;   // recorded after the last delivery on dst_st
   hipEvent_t ev_recv = nullptr;  // recorded after the last delivery's scatter (and gossip receipts)
   hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
@@ -424,6 +427,7 @@ int stage_host_input(Eng* E, uint32_t n_ticks) {
   HIPCHK(E->d_off.ensure(E->S + 1));
   HIPCHK(E->d_in.ensure(E->n_in ? E->n_in : 1));
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // a local delivery may still read d_off
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));   // and so may a routing
   HIPCHK(hipMemcpyAsync(E->d_off.p, off.data(), sizeof(uint64_t) * (E->S + 1), hipMemcpyHostToDevice, E->st));
   if (E->n_in)
     HIPCHK(hipMemcpyAsync(E->d_in.p, recs.data(), sizeof(InRec) * E->n_in, hipMemcpyHostToDevice, E->st));
@@ -490,6 +494,7 @@ int check_sim_error(Eng* E) {
 // Every reader of device results goes through here: the step itself does not synchronize.
 int sync_stream(Eng* E) {
   HIPCHK(hipStreamSynchronize(E->st));
+  HIPCHK(hipStreamSynchronize(E->rt_st));
   HIPCHK(hipStreamSynchronize(E->dst_st));
   return harvest_timing(E, true);
 }
@@ -519,8 +524,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   if (rc) return rc;
   const uint64_t emit_cap = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;
   HIPCHK(E->d_verdict.ensure(E->n_in ? E->n_in : 1));
-  if (local_hist)  // the delivery two steps back read this emit pair
-    HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
+  // the local delivery or routing two steps back read this emit pair
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
   HIPCHK(E->d_emit.ensure(emit_cap));
   HIPCHK(E->d_emit_n.ensure(E->S));
   SimArgs a;
@@ -608,10 +613,14 @@ int finish_sim_timing(Eng* E) {
   return check_sim_error(E);
 }
 
-// Groups the step's scheduled records by destination shard into `out`, all on the simulate stream:
-// per-(rank, source) counts -> scan -> ordered scatter; the per-rank edges go to pinned host memory
-// behind ev_route, so the host can launch the next step before it reads them (route_finish).
+// Groups the step's scheduled records by destination shard into `out` on the routing stream, after
+// the step's k_sim and beside the next one (which writes the other emit pair): per-(rank, source)
+// counts -> scan -> ordered scatter; the per-rank edges go to pinned host memory behind ev_route, so
+// the host can launch the next step before it reads them (route_finish).
 int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap) {
+  hipStream_t rs = E->rt_st;
+  HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
+  HIPCHK(hipStreamWaitEvent(rs, E->ev_sim, 0));
   RouteArgsHost h;
   memset(&h, 0, sizeof h);
   h.emit = E->d_emit.p;
@@ -629,18 +638,24 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
   h.pos = E->d_rpos.p;
   h.out = out;
   h.out_cap = out_cap;
-  launch_route(h, 0, E->st);
+  launch_route(h, 0, rs);
   HIPCHK(hipGetLastError());
-  launch_scan(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, E->st);
+  launch_scan(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, rs);
   HIPCHK(hipGetLastError());
-  launch_route(h, 1, E->st);
+  launch_route(h, 1, rs);
   HIPCHK(hipGetLastError());
   // per-rank totals: pos[r * S] .. pos[(r + 1) * S], published to the slot's pinned words
   const uint32_t k = (E->route_head + E->route_n) % Eng::kRouteSlots;
   E->route_seq[k] = ++E->route_next_seq;
-  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->h_edges + 16 * k, E->route_seq[k], E->st);
+  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->h_edges + 16 * k, E->route_seq[k], rs);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(E->ev_route[k], E->st));
+  HIPCHK(hipEventRecord(E->ev_route[k], rs));
+  HIPCHK(hipEventRecord(E->ev_rt, rs));
+  HIPCHK(hipEventRecord(E->ev_local, rs));  // the last reader of this emit pair
+  std::swap(E->d_emit, E->d_emit_alt);
+  std::swap(E->d_emit_n, E->d_emit_n_alt);
+  std::swap(E->d_lcnt, E->d_lcnt_alt);
+  std::swap(E->ev_local, E->ev_local_alt);
   E->route_ranks[k] = n_ranks;
   E->route_cap[k] = out_cap;
   E->route_n++;
@@ -664,17 +679,17 @@ int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev) {
   }
 }
 
-// Waits for the oldest launched step's records and edges (and for the asynchronous deliveries
-// enqueued so far, whose input buffers the caller's next exchange may overwrite); per-rank counts
-// into `counts`.
-int route_finish(Eng* E, uint64_t* counts) {
+// Waits for the oldest launched step's records and edges (and, with wait_deliveries, for the
+// asynchronous deliveries enqueued so far, whose input buffers the caller's next exchange may
+// overwrite); per-rank counts into `counts`.
+int route_finish(Eng* E, uint64_t* counts, bool wait_deliveries = true) {
   if (!E->route_n) return E->fail(-EINVAL, "no routed step pending");
   const uint32_t k = E->route_head;
   E->route_head = (k + 1) % Eng::kRouteSlots;
   E->route_n--;
   int rc = wait_published(E, &E->h_edges[16 * k + 15], E->route_seq[k], E->ev_route[k]);
   if (rc) return rc;
-  HIPCHK(hipEventSynchronize(E->ev_dst));
+  if (wait_deliveries) HIPCHK(hipEventSynchronize(E->ev_dst));
   const uint32_t n_ranks = E->route_ranks[k];
   const uint64_t* edges = E->h_edges + 16 * k;
   for (uint32_t r = 0; r < n_ranks; ++r) counts[r] = edges[r + 1] - edges[r];
@@ -893,6 +908,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), "stream"))) return bail(rc);
   if ((rc = E->hip(hipStreamCreateWithPriority(&E->dst_st, hipStreamNonBlocking, prio_hi), "stream")))
     return bail(rc);
+  if ((rc = E->hip(hipStreamCreateWithPriority(&E->rt_st, hipStreamNonBlocking, prio_hi), "stream")))
+    return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_rt, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventRecord(E->ev_rt, E->rt_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_dst, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
@@ -967,6 +986,7 @@ void tgsim_destroy(void* e) {
   (void)hipSetDevice(E->dev);
   if (E->st) (void)hipStreamSynchronize(E->st);
   if (E->dst_st) (void)hipStreamSynchronize(E->dst_st);
+  if (E->rt_st) (void)hipStreamSynchronize(E->rt_st);
   DevBuf<int> dummy;
   (void)dummy;
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
@@ -990,11 +1010,13 @@ void tgsim_destroy(void* e) {
   for (hipEvent_t ev : E->ev_route)
     if (ev) (void)hipEventDestroy(ev);
   if (E->ev_dst) (void)hipEventDestroy(E->ev_dst);
+  if (E->ev_rt) (void)hipEventDestroy(E->ev_rt);
   if (E->ev_recv) (void)hipEventDestroy(E->ev_recv);
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->ev_local) (void)hipEventDestroy(E->ev_local);
   if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);
   if (E->dst_st) (void)hipStreamDestroy(E->dst_st);
+  if (E->rt_st) (void)hipStreamDestroy(E->rt_st);
   if (E->st) (void)hipStreamDestroy(E->st);
   delete E;
 }
@@ -1142,6 +1164,7 @@ int tgsim_gen_storm(void* e, double lambda, uint32_t n_ticks) {
   g.n_ticks = n_ticks;
   g.now_tick = E->now_tick + E->gen_q_ticks;  // windows queue up back to back
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // a free window's offsets may still be read by a delivery
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));   // or a routing
   Eng::GenWindow w;
   if (!E->gen_free.empty()) {
     w = std::move(E->gen_free.back());
@@ -1201,6 +1224,7 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   HIPCHK(hipSetDevice(E->dev));
   // receipts are folded on the delivery stream (the sort of the same delivery may still run)
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_recv, 0));
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));  // a free window's offsets may still be read by a routing
   const uint64_t win0 = E->now_tick + E->gen_q_ticks;
   const GossipArgs g = gossip_args(E, win0, n_ticks);
   Eng::GenWindow w;
@@ -1272,6 +1296,21 @@ int tgsim_step_sim_finish(void* e, uint64_t* counts) {
   return route_finish(E, counts);
 }
 
+int tgsim_step_sim_counts(void* e, uint64_t* counts) {
+  Eng* E = as_eng(e);
+  if (!E || !counts) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  return route_finish(E, counts, false);
+}
+
+int tgsim_delivery_event(void* e, void* event) {
+  Eng* E = as_eng(e);
+  if (!E || !event) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  HIPCHK(hipEventRecord(static_cast<hipEvent_t>(event), E->dst_st));
+  return 0;
+}
+
 int tgsim_step_sim(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* d_out,
                    size_t out_cap, uint64_t* counts) {
   if (!counts) return -EINVAL;
@@ -1304,6 +1343,7 @@ int tgsim_wait_event(void* e, void* event) {
   if (!E || !event) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
   HIPCHK(hipStreamWaitEvent(E->st, static_cast<hipEvent_t>(event), 0));
+  HIPCHK(hipStreamWaitEvent(E->rt_st, static_cast<hipEvent_t>(event), 0));  // routing writes the caller's buffer
   return 0;
 }
 

@@ -179,6 +179,17 @@ class CABIEngine:
         self._check(self._fn("step_sim_finish")(self._h, counts), "step_sim_finish")
         return np.array(list(counts), dtype=np.uint64)
 
+    def step_sim_counts(self) -> np.ndarray:
+        """step_sim_finish without waiting for earlier asynchronous deliveries (the caller orders
+        the reuse of their input buffers with delivery_event)."""
+        counts = (C.c_uint64 * self._launched.pop(0))()
+        self._check(self._fn("step_sim_counts")(self._h, counts), "step_sim_counts")
+        return np.array(list(counts), dtype=np.uint64)
+
+    def delivery_event(self, event: int) -> None:
+        """Records a raw hipEvent_t on the delivery stream after the deliveries enqueued so far."""
+        self._check(self._fn("delivery_event")(self._h, C.c_void_p(event)), "delivery_event")
+
     def deliver(self, d_in: int, n: int) -> None:
         self._check(self._fn("deliver")(self._h, C.c_void_p(d_in), n), "deliver")
 

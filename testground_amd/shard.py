@@ -40,9 +40,12 @@ def shard_bounds(n_peers: int, world: int) -> List[int]:
 class ShardedStepper:
     """One step = step_sim -> exchange -> deliver on every rank; run() pipelines many.  On GPUs the
     delivery of step k runs on the engine's delivery stream beside the k_sim of the next step
-    (tgsim_deliver_async); the engine's simulate stream waits for the collective that still reads
-    the output buffer it is about to overwrite, and step_sim_finish returns only after the earlier
-    deliveries have released their input buffers."""
+    (tgsim_deliver_async).  The host never blocks on device work except for the step's per-rank
+    record counts: the engine's simulate stream waits for the collective that still reads the
+    output buffer it is about to overwrite, and the exchange stream waits for the delivery that
+    still reads the input buffer it is about to overwrite (events, not host synchronization).  The
+    counts themselves are host values (pinned edges), so they are exchanged over a CPU (gloo)
+    group: a device collective would queue behind the running k_sim for a CU."""
 
     def __init__(self, engine, bounds: Sequence[int], device: str = "cuda", group=None):
         self.engine = engine
@@ -54,9 +57,13 @@ class ShardedStepper:
         self._out: List[Optional[torch.Tensor]] = [None] * 3
         self._in: List[Optional[torch.Tensor]] = [None] * 2
         self._ev: List[Optional[torch.cuda.Event]] = [None] * 3
+        self._dev: List[Optional[torch.cuda.Event]] = [None] * 2  # _dev[i]: the delivery that last read _in[i]
         self._k = 0
         # the exchange's stream: high priority, off the simulate stream's hardware queue (init_rccl)
         self._xs = torch.cuda.Stream(self.device, priority=-1) if self.device.type == "cuda" else None
+        # host-side count exchange (collective: every rank constructs its stepper)
+        ranks = dist.get_process_group_ranks(group) if group is not None else None
+        self._cpu_group = dist.new_group(ranks=ranks, backend="gloo") if self.device.type == "cuda" else group
 
     def _buf(self, bufs: list, i: int, n_bytes: int) -> torch.Tensor:
         b = bufs[i]
@@ -82,20 +89,32 @@ class ShardedStepper:
             return self._exchange_on(k, out, cnt)
 
     def _exchange_on(self, k: int, out: torch.Tensor, cnt: np.ndarray) -> int:
-        send = torch.as_tensor(cnt.astype(np.int64), device=self.device)
+        cuda = self.device.type == "cuda"
+        send = torch.as_tensor(cnt.astype(np.int64))
         recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group)
-        rcnt = recv.cpu().numpy()
+        dist.all_to_all_single(recv, send, group=self._cpu_group)
+        rcnt = recv.numpy()
         n_in = int(rcnt.sum())
-        # the previous delivery from _in[k % 2] finished before step_sim_finish returned
-        inb = self._buf(self._in, k % 2, n_in * REC)
+        i = k % 2
+        if cuda:
+            if self._dev[i] is not None:  # the delivery of step k - 2 still reads _in[i]
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(self._dev[i])
+                if self._in[i] is not None and self._in[i].numel() < n_in * REC:
+                    self._dev[i].synchronize()  # growing: the old block returns to the allocator
+        inb = self._buf(self._in, i, n_in * REC)
         dist.all_to_all_single(inb[: n_in * REC], out[: int(cnt.sum()) * REC],
                                [int(x) * REC for x in rcnt], [int(x) * REC for x in cnt], group=self.group)
-        if self.device.type == "cuda":  # the collective runs on torch's stream: the delivery stream waits for it
+        if cuda:  # the collective runs on torch's stream: the delivery stream waits for it
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
             self._ev[k % 3] = ev
             self.engine.deliver_async(inb.data_ptr(), n_in, ev.cuda_event)
+            dv = self._dev[i] or torch.cuda.Event()
+            if self._dev[i] is None:
+                dv.record(torch.cuda.current_stream(self.device))  # creates the event
+            self.engine.delivery_event(dv.cuda_event)
+            self._dev[i] = dv
         else:
             self.engine.deliver(inb.data_ptr(), n_in)
         return n_in
@@ -103,7 +122,12 @@ class ShardedStepper:
     def step(self, n_ticks: int) -> int:
         """One window on every rank (collective).  Returns the records delivered to this rank."""
         k, out = self._launch(n_ticks)
-        return self._exchange(k, out, self.engine.step_sim_finish())
+        return self._exchange(k, out, self._finish())
+
+    def _finish(self) -> np.ndarray:
+        if self.device.type == "cuda":
+            return self.engine.step_sim_counts()
+        return self.engine.step_sim_finish()
 
     def run(self, n_steps: int, n_ticks: int) -> int:
         """n_steps windows with the simulation two steps ahead of the exchange: while the host
@@ -115,7 +139,7 @@ class ShardedStepper:
         pend = [self._launch(n_ticks) for _ in range(min(2, n_steps))]
         for s in range(n_steps):
             k, out = pend.pop(0)
-            cnt = self.engine.step_sim_finish()
+            cnt = self._finish()
             if s + 2 < n_steps:
                 pend.append(self._launch(n_ticks))
             total += self._exchange(k, out, cnt)
