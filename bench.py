@@ -221,9 +221,15 @@ def main():
             step(a.window)
         elif a.workload == "epochs":  # traffic pre-generated; reshape + epoch + barrier
             k = epoch[0]
-            if k:
-                workloads.epoch_reshape(eng, peers_total, k)
-            step(a.window)
+            if stepper is None:
+                if k:
+                    workloads.epoch_reshape(eng, peers_total, k)
+                step(a.window)  # asynchronous: the next reshape's host work overlaps this k_sim
+            else:
+                # the sharded step waits for its records, so epoch k+1's ConfigureNetwork calls
+                # are staged on the host while epoch k simulates (epoch k's were staged during
+                # epoch k-1); staged configs take effect at the next launch, after the barrier below
+                stepper.step(a.window, between=lambda: workloads.epoch_reshape(eng, peers_total, k + 1))
             state, rnd = workloads.epoch_state(k)
             eng.signal(state, a.peers)
             ok = barrier(state, rnd * peers_total) if barrier else eng.barrier_poll(state, rnd * peers_total)

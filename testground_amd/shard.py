@@ -13,7 +13,7 @@ tests, CPU-oracle shards with CPU buffers over `gloo`.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -119,9 +119,13 @@ class ShardedStepper:
             self.engine.deliver(inb.data_ptr(), n_in)
         return n_in
 
-    def step(self, n_ticks: int) -> int:
-        """One window on every rank (collective).  Returns the records delivered to this rank."""
+    def step(self, n_ticks: int, between: Optional[Callable[[], object]] = None) -> int:
+        """One window on every rank (collective).  Returns the records delivered to this rank.
+        `between` runs on the host while the window simulates (e.g. staging the next epoch's
+        ConfigureNetwork calls, which take effect at the next launch)."""
         k, out = self._launch(n_ticks)
+        if between is not None:
+            between()
         return self._exchange(k, out, self._finish())
 
     def _finish(self) -> np.ndarray:
@@ -147,8 +151,10 @@ class ShardedStepper:
 
     def barrier(self, state: int, target: int) -> bool:
         """Global barrier over the shards' sync counters: the per-rank counts of `state` are summed
-        with an all-reduce (RCCL on GPUs) and compared with target (SignalAndWait semantics)."""
+        with an all-reduce and compared with target (SignalAndWait semantics).  The counters are
+        host values (tgsim_signal), so the sum runs on the host group: a device all-reduce would
+        wait for a CU behind the running k_sim only to be copied back."""
         local = self.engine.signal(state, 0)
-        t = torch.tensor([local], dtype=torch.int64, device=self.device)
-        dist.all_reduce(t, group=self.group)
+        t = torch.tensor([local], dtype=torch.int64)
+        dist.all_reduce(t, group=self._cpu_group)
         return int(t.item()) >= target

@@ -88,3 +88,31 @@ def test_stepper_pipelined_run_equals_step(rccl):
     assert len(got) == len(want) > 10_000 and (got == want).all()
     s, r = sh.stats(), ref.stats()
     assert (s["offered"], s["scheduled"], s["by_verdict"]) == (r["offered"], r["scheduled"], r["by_verdict"])
+
+
+def test_stepper_epochs_staged_reshape_equals_step(rccl):
+    """C5 through the stepper as bench.py runs it: epoch k+1's reshape staged on the host while
+    epoch k simulates (between=), the barrier summed on the host group; the same verdicts,
+    deliveries and barrier releases as reshaping before each single-engine step."""
+    from testground_amd.shard import ShardedStepper
+
+    n, ticks = 3000, 800
+    ref, sh = Engine(n), Engine(n)
+    for e in (ref, sh):
+        wl.configure_storm(e, n)
+    st = ShardedStepper(sh, [0, n], device="cuda:0")
+    for k in range(5):
+        if k:
+            wl.epoch_reshape(ref, n, k)
+        ref.gen_storm(0.2, ticks)
+        sh.gen_storm(0.2, ticks)
+        ref.step(ticks)
+        st.step(ticks, between=lambda: wl.epoch_reshape(sh, n, k + 1))
+        state, rnd = wl.epoch_state(k)
+        ref.signal(state, n)
+        sh.signal(state, n)
+        assert ref.barrier_poll(state, rnd * n) and st.barrier(state, rnd * n)
+        assert not st.barrier(state, rnd * n + 1)
+        assert (sh.verdicts() == ref.verdicts()).all(), f"epoch {k}"
+        d_sh, d_ref = sh.drain(), ref.drain()
+        assert len(d_sh) == len(d_ref) > 0 and (d_sh == d_ref).all(), f"epoch {k}"
