@@ -316,7 +316,7 @@ def main():
                         "tick_ns": 1000, "window_ticks": a.window, "settle_sim_ms": settle * a.window / 1000,
                         "shapes": a.shapes if a.workload == "storm" else a.workload,
                         "queue_limit": a.queue_limit or 1000, "packets_per_step": offered_all / a.steps,
-                        "parallelism": f"peer-sharded x{world}"}, **extra),
+                        "parallelism": f"peer-sharded x{world}" + (" (RCCL exchange path)" if sharded else "")}, **extra),
         "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": load_pmc(a), "algorithmic_bytes_per_launch": per_launch,

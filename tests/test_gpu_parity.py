@@ -422,3 +422,56 @@ def test_edge_inputs(make_oracle):
     st = g.stats()
     bv = st["by_verdict"]
     assert bv["queue_full"] > 0 and bv["disconnected"] > 0 and bv["external"] > 0 and bv["no_route"] > 0
+
+
+def _ks_uniform(x, lo, hi):
+    x = np.sort((np.asarray(x, dtype=np.float64) - lo) / (hi - lo))
+    cdf = np.arange(1, len(x) + 1) / len(x)
+    return max(np.max(cdf - x), np.max(x - (cdf - 1 / len(x))))
+
+
+def test_full_size_latency_distribution():
+    """Statistical parity on the GPU at scale (north_star: KS <= 0.02 on latency, loss +-0.5 pp):
+    1,000 instances in four LinkShape groups, 100 packets each, sparse enough that the netem limit
+    is never reached and unlimited bandwidth (HTB passes at e).  Each group's delays follow
+    netem's uniform U[L-J, L+J) (no distribution table, link.go:169-179) and its loss rate is the
+    configured percentage."""
+    n, per, gap = 1000, 100, 700
+    groups = [(20, 5, 1.0), (50, 10, 3.0), (5, 0, 0.0), (80, 20, 2.0)]  # L ms, J ms, loss %
+    e = Engine(n)
+    for i in range(n):
+        L, J, loss = groups[i % 4]
+        e.configure(i, nw.Config(Network="default", Enable=True, Default=nw.LinkShape(
+            Latency=L * nw.Millisecond, Jitter=J * nw.Millisecond, Loss=loss)))
+    half = per // 2  # ticks are u16 within a step: two steps of 50 packets per instance
+    src = np.repeat(np.arange(n, dtype=np.uint32), half)
+    vs = []
+    for c in range(2):
+        idx = np.tile(np.arange(half, dtype=np.uint32), n)
+        pk = np.zeros(n * half, dtype=abi.PKT_DTYPE)
+        pk["src"], pk["seq"], pk["len"] = src, idx + c * half, 200
+        pk["dst"] = (src + 1 + ((idx + c * half) * 7919) % (n - 1)) % n
+        pk["tick"] = idx * gap
+        e.submit(pk)
+        e.step(half * gap)
+        vs.append(e.verdicts() & 15)
+    v = np.concatenate(vs)
+    src = np.concatenate([src, src])
+    assert not (v == abi.V_QUEUE_FULL).any()
+    for _ in range(2):
+        e.step(60_000)  # past the largest L + J
+    d = e.drain()
+    d = d[(d["flags"] & abi.FLAG_DUP) == 0]
+    delays = d["t_ns"].astype(np.int64) - d["seq"].astype(np.int64) * gap * 1000
+    for g, (L, J, loss) in enumerate(groups):
+        mine = (d["src"] % 4) == g
+        x = delays[mine]
+        lo, hi = (L - J) * 1e6, (L + J) * 1e6
+        if J == 0:
+            assert (x == L * 1_000_000).all()
+        else:
+            assert x.min() >= lo and x.max() < hi
+            assert _ks_uniform(x, lo, hi) <= 0.02, f"group {g}"
+        sent = np.asarray(src % 4 == g)
+        lost = int((v[sent] == abi.V_LOSS).sum())
+        assert abs(lost / int(sent.sum()) - loss / 100) <= 0.005, f"group {g}"
