@@ -42,7 +42,7 @@ B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 24, 148
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=None, help="timed steps (default: 10; gossip: 70 windows)")
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default: 30; gossip: 70 windows)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; gossip: 0)")
     p.add_argument("--workload", default="storm", choices=["storm", "gossip", "epochs"])
     p.add_argument("--peers", type=int, default=0,
@@ -63,6 +63,8 @@ def parse():
                    help="storm: C3 heterogeneous shapes; fixed: L=5 ms, no jitter/loss/reorder (probe)")
     p.add_argument("--sharded", action="store_true",
                    help="use the peer-sharded step (RCCL exchange) even at one rank, to time the N>1 path")
+    p.add_argument("--exact-exchange", action="store_true",
+                   help="sharded storm: exchange exact record counts every step instead of fixed-size chunks")
     a = p.parse_args()
     if not a.peers:
         a.peers = {"storm": 10_000, "gossip": 125_000, "epochs": 100_000}[a.workload]
@@ -71,7 +73,7 @@ def parse():
     if a.workload == "gossip":
         a.window = 5000
     if a.steps is None:
-        a.steps = 70 if a.workload == "gossip" else 10
+        a.steps = 70 if a.workload == "gossip" else 30  # enough to amortize the pipeline fill and drain
     if a.warmup is None:
         a.warmup = 0 if a.workload == "gossip" else 3
     return a
@@ -256,6 +258,12 @@ def main():
             for _ in range(n):
                 one_step()
 
+    if stepper is not None and a.workload == "storm" and not a.exact_exchange:
+        # fixed-size exchange for the pipelined run: per-rank chunks sized from the largest count
+        # the settle steps exchanged (max over ranks) plus a margin; an overflow fails the run
+        m = torch.tensor([stepper.max_count], dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        stepper.slot_cap = int(int(m.item()) * 1.25) + 4096
     run_steps(a.warmup)
     eng.drain()
     s0 = eng.stats()
@@ -316,7 +324,9 @@ def main():
                         "tick_ns": 1000, "window_ticks": a.window, "settle_sim_ms": settle * a.window / 1000,
                         "shapes": a.shapes if a.workload == "storm" else a.workload,
                         "queue_limit": a.queue_limit or 1000, "packets_per_step": offered_all / a.steps,
-                        "parallelism": f"peer-sharded x{world}" + (" (RCCL exchange path)" if sharded else "")}, **extra),
+                        "parallelism": f"peer-sharded x{world}" + (" (RCCL exchange path)" if sharded else ""),
+                        **({"exchange": "slotted" if stepper.slot_cap else "exact",
+                            "slot_cap_records": stepper.slot_cap} if stepper is not None else {})}, **extra),
         "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": load_pmc(a), "algorithmic_bytes_per_launch": per_launch,

@@ -217,6 +217,16 @@ int tgsim_step_sim_finish(void* engine, uint64_t* rank_counts);
  * the reuse of a delivery's input buffer on the device instead (tgsim_delivery_event), so the host
  * never blocks on the delivery stream. */
 int tgsim_step_sim_counts(void* engine, uint64_t* rank_counts);
+/* Slotted form of the pipelined step, for an exchange with fixed per-rank sizes (no count
+ * exchange, so the host never waits for the device): d_out holds n_ranks chunks of
+ * (slot_cap + 1) records; chunk r starts with a header record whose t_ns is the number of records
+ * for rank r that follow it.  routed_event (a hipEvent_t, may be null) is recorded when d_out is
+ * complete; the exchange waits for it on the device.  A rank whose records exceed slot_cap sets a
+ * sticky error: the next step launch, release or reader fails with -ENOSPC.  _release retires the
+ * oldest launched step without waiting for it. */
+int tgsim_step_sim_launch_slotted(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* rank_bounds,
+                                  void* d_out, uint64_t slot_cap, void* routed_event);
+int tgsim_step_sim_release(void* engine);
 /* Phase 2: sorts the records addressed to this shard (DEVICE memory, n records) into the
  * delivery order and appends them to the drain buffer. */
 int tgsim_deliver(void* engine, const void* d_in, size_t n);
@@ -225,6 +235,9 @@ int tgsim_deliver(void* engine, const void* d_in, size_t n);
  * all-to-all; may be null), so the delivery of one step overlaps the next step's simulation.  d_in
  * must stay valid until tgsim_sync (or any reader) returns; no count check. */
 int tgsim_deliver_async(void* engine, const void* d_in, size_t n, void* wait_event);
+/* tgsim_deliver_async of a slotted exchange's output: n_ranks chunks of (slot_cap + 1) records,
+ * each a count header and the records (the layout tgsim_step_sim_launch_slotted writes). */
+int tgsim_deliver_slotted_async(void* engine, const void* d_in, uint32_t n_ranks, uint64_t slot_cap, void* wait_event);
 /* Makes the engine's simulate stream wait for a hipEvent_t of another stream (e.g. the collective
  * that still reads the d_out buffer the next tgsim_step_sim will overwrite). */
 int tgsim_wait_event(void* engine, void* event);

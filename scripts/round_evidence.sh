@@ -14,7 +14,7 @@ tail -c 600 gpurun_out/ev/bench.json
 rm -rf gpurun_out/ev/trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ev/trace -o run -- python3 bench.py --no-cpu > gpurun_out/ev/trace.log 2>&1 || { tail gpurun_out/ev/trace.log; exit 1; }
 echo trace ok
-python scripts/trace_summary.py gpurun_out/ev/trace/run_kernel_trace.csv k_sim 10 > gpurun_out/ev/k_sim_timed.json && cat gpurun_out/ev/k_sim_timed.json
+python scripts/trace_summary.py gpurun_out/ev/trace/run_kernel_trace.csv k_sim 30 > gpurun_out/ev/k_sim_timed.json && cat gpurun_out/ev/k_sim_timed.json
 rm -rf gpurun_out/ev/pmc && mkdir -p gpurun_out/ev/pmc
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY"; do

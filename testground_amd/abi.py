@@ -119,7 +119,8 @@ EXPORTS = [
     "tgsim_configure_batch",
     "tgsim_submit", "tgsim_gen_storm", "tgsim_step", "tgsim_step_sim", "tgsim_deliver",
     "tgsim_deliver_async", "tgsim_wait_event", "tgsim_sync", "tgsim_step_sim_launch", "tgsim_step_sim_finish",
-    "tgsim_step_sim_counts", "tgsim_delivery_event",
+    "tgsim_step_sim_counts", "tgsim_delivery_event", "tgsim_step_sim_launch_slotted", "tgsim_step_sim_release",
+    "tgsim_deliver_slotted_async",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_barrier_poll", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
@@ -151,6 +152,9 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("step_sim_finish", C.c_int, vp, C.POINTER(C.c_uint64))
     f("step_sim_counts", C.c_int, vp, C.POINTER(C.c_uint64))
     f("delivery_event", C.c_int, vp, vp)
+    f("step_sim_launch_slotted", C.c_int, vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), vp, C.c_uint64, vp)
+    f("step_sim_release", C.c_int, vp)
+    f("deliver_slotted_async", C.c_int, vp, vp, C.c_uint32, C.c_uint64, vp)
     f("deliver", C.c_int, vp, vp, C.c_size_t)
     f("deliver_async", C.c_int, vp, vp, C.c_size_t, vp)
     f("wait_event", C.c_int, vp, vp)

@@ -211,6 +211,8 @@ struct tgsim_engine_s {
   uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
   uint64_t* h_err = nullptr;    // pinned host word k_sim stores the sticky error bits into
   uint64_t* d_err_host = nullptr;  // its device address
+  uint32_t* h_xerr = nullptr;   // pinned sticky flag: a slotted exchange chunk overflowed (k_route_edges)
+  uint32_t* d_xerr = nullptr;   // its device address
   // launched, unfinished routed steps (tgsim_step_sim_launch), oldest at route_head: pinned
   // per-rank record edges behind an event, per slot
   static constexpr uint32_t kRouteSlots = 2;
@@ -488,6 +490,8 @@ int harvest_timing(Eng* E, bool wait) {
 int check_sim_error(Eng* E) {
   if (E->h_err && (__atomic_load_n(E->h_err, __ATOMIC_RELAXED) & kErrTimeOverflow))
     return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
+  if (E->h_xerr && __atomic_load_n(E->h_xerr, __ATOMIC_RELAXED))
+    return E->fail(-ENOSPC, "exchange: a step's records for one rank exceed the slot capacity");
   return 0;
 }
 
@@ -617,7 +621,8 @@ int finish_sim_timing(Eng* E) {
 // the step's k_sim and beside the next one (which writes the other emit pair): per-(rank, source)
 // counts -> scan -> ordered scatter; the per-rank edges go to pinned host memory behind ev_route, so
 // the host can launch the next step before it reads them (route_finish).
-int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap) {
+int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap,
+                 uint64_t slot_cap = 0, hipEvent_t routed = nullptr) {
   hipStream_t rs = E->rt_st;
   HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
   HIPCHK(hipStreamWaitEvent(rs, E->ev_sim, 0));
@@ -638,6 +643,7 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
   h.pos = E->d_rpos.p;
   h.out = out;
   h.out_cap = out_cap;
+  h.slot_cap = slot_cap;
   launch_route(h, 0, rs);
   HIPCHK(hipGetLastError());
   launch_scan(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, rs);
@@ -647,8 +653,9 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
   // per-rank totals: pos[r * S] .. pos[(r + 1) * S], published to the slot's pinned words
   const uint32_t k = (E->route_head + E->route_n) % Eng::kRouteSlots;
   E->route_seq[k] = ++E->route_next_seq;
-  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->h_edges + 16 * k, E->route_seq[k], rs);
+  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->h_edges + 16 * k, E->route_seq[k], rs, out, slot_cap, E->d_xerr);
   HIPCHK(hipGetLastError());
+  if (routed) HIPCHK(hipEventRecord(routed, rs));
   HIPCHK(hipEventRecord(E->ev_route[k], rs));
   HIPCHK(hipEventRecord(E->ev_rt, rs));
   HIPCHK(hipEventRecord(E->ev_local, rs));  // the last reader of this emit pair
@@ -758,7 +765,7 @@ int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out, hipStream_t sq) {
 // records come from tgsim_step_sim, which completed them before returning), only for `wait` (the
 // producer of d_in, e.g. the collective).
 // check: read the record count back and reject records addressed to other shards.
-int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool check) {
+int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool check, uint64_t slot = 0) {
   const uint32_t nd = E->S;  // destinations owned by this shard
   hipStream_t sq = E->dst_st;
   if (wait) HIPCHK(hipStreamWaitEvent(sq, wait, 0));
@@ -767,7 +774,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
     HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, sq));
   }
   HIPCHK(E->d_dpos.ensure(nd));
-  launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq);
+  launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq, slot);
   HIPCHK(hipGetLastError());
   int rc = 0;
   if (!check) {  // nothing on the host needs the count
@@ -784,11 +791,17 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
                                    static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq);
+  launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq, slot);
   HIPCHK(hipGetLastError());
   if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
-    launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, sq);
+    if (slot) launch_gossip_recv_dev(gossip_args(E, 0, 0), E->d_scatter.p, E->d_dtot.p, sq);
+    else launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, sq);
     HIPCHK(hipGetLastError());
+  }
+  if (slot && !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES)) {  // the drain needs the record count
+    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
+    HIPCHK(hipStreamSynchronize(sq));
+    n = E->h_dtot;
   }
   HIPCHK(hipEventRecord(E->ev_recv, sq));  // the next window's generation needs no more than this
   tgsim_delivery* dst = nullptr;
@@ -925,6 +938,12 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
                                  hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
     return bail(rc);
   *E->h_err = 0;
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_xerr), sizeof(uint32_t),
+                                 hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
+    return bail(rc);
+  *E->h_xerr = 0;
+  if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_xerr), E->h_xerr, 0), "pinned")))
+    return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_gerr), sizeof(uint32_t)), "pinned"))) return bail(rc);
   *E->h_gerr = 0;
   if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_err_host), E->h_err, 0), "pinned")))
@@ -1005,6 +1024,7 @@ void tgsim_destroy(void* e) {
   }
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
   if (E->h_err) (void)hipHostFree(E->h_err);
+  if (E->h_xerr) (void)hipHostFree(E->h_xerr);
   if (E->h_gerr) (void)hipHostFree(E->h_gerr);
   if (E->h_edges) (void)hipHostFree(E->h_edges);
   for (hipEvent_t ev : E->ev_route)
@@ -1301,6 +1321,39 @@ int tgsim_step_sim_counts(void* e, uint64_t* counts) {
   if (!E || !counts) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
   return route_finish(E, counts, false);
+}
+
+int tgsim_step_sim_launch_slotted(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* d_out,
+                                  uint64_t slot_cap, void* routed_event) {
+  Eng* E = as_eng(e);
+  if (!E || n_ticks == 0 || n_ranks == 0 || n_ranks > 8 || !bounds || !d_out || slot_cap == 0) return -EINVAL;
+  if (bounds[0] != 0 || bounds[n_ranks] != E->N) return E->fail(-EINVAL, "rank bounds must cover [0, n_peers)");
+  if (E->route_n == Eng::kRouteSlots) return E->fail(-EBUSY, "two launched steps are not released yet");
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = run_sim(E, n_ticks);
+  if (rc) return rc;
+  return route_launch(E, n_ranks, bounds, static_cast<tgsim_delivery*>(d_out), n_ranks * (slot_cap + 1), slot_cap,
+                      static_cast<hipEvent_t>(routed_event));
+}
+
+int tgsim_step_sim_release(void* e) {
+  Eng* E = as_eng(e);
+  if (!E) return -EINVAL;
+  if (!E->route_n) return E->fail(-EINVAL, "no routed step pending");
+  HIPCHK(hipSetDevice(E->dev));
+  E->route_head = (E->route_head + 1) % Eng::kRouteSlots;
+  E->route_n--;
+  int rc = harvest_timing(E, false);
+  if (rc) return rc;
+  return check_sim_error(E);
+}
+
+int tgsim_deliver_slotted_async(void* e, const void* d_in, uint32_t n_ranks, uint64_t slot_cap, void* wait_event) {
+  Eng* E = as_eng(e);
+  if (!E || !d_in || n_ranks == 0 || n_ranks > 8 || slot_cap == 0) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  return deliver(E, static_cast<const tgsim_delivery*>(d_in), n_ranks * (slot_cap + 1),
+                 static_cast<hipEvent_t>(wait_event), false, slot_cap);
 }
 
 int tgsim_delivery_event(void* e, void* event) {

@@ -1295,6 +1295,7 @@ struct RouteArgs {
   const uint64_t* pos;           // exclusive scan of cnt
   tgsim_delivery* out;
   uint64_t out_cap;              // records beyond it are not written (the host reports -ENOSPC)
+  uint64_t slot_cap;             // 0: flat, rank-major; else rank r's records at out[r * (slot_cap + 1) + 1 ..]
 };
 
 __device__ __forceinline__ uint32_t rank_of(const RouteArgs& a, uint32_t dst) {
@@ -1335,9 +1336,12 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
   for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < a.n_src; s += nw) {
     const uint32_t n = a.emit_n[s];
     const tgsim_delivery* base = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
-    uint64_t run[8];
+    uint64_t run[8], edge[8];
 #pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) run[q] = q < a.n_ranks ? a.pos[(size_t)q * a.n_src + s] : 0;
+    for (uint32_t q = 0; q < 8; ++q) {
+      run[q] = q < a.n_ranks ? a.pos[(size_t)q * a.n_src + s] : 0;
+      edge[q] = (a.slot_cap && q < a.n_ranks) ? a.pos[(size_t)q * a.n_src] : 0;
+    }
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
       const uint32_t i = i0 + lane;
       tgsim_delivery r;
@@ -1352,7 +1356,12 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
         const uint64_t m = __ballot(rk == q);
         if (rk == q) {
           const uint64_t p = run[q] + __popcll(m & below);
-          if (p < a.out_cap) a.out[p] = r;
+          if (a.slot_cap) {
+            const uint64_t j = p - edge[q];
+            if (j < a.slot_cap) a.out[q * (a.slot_cap + 1) + 1 + j] = r;
+          } else if (p < a.out_cap) {
+            a.out[p] = r;
+          }
         }
         run[q] += __popcll(m);
       }
@@ -1365,9 +1374,17 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
 // Per-rank record edges straight into the host's pinned slot, then the slot's sequence word
 // (system-scope release): the host polls that word instead of synchronizing on an event, which
 // would also wait for the next step's k_sim queued behind this kernel.
-__global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq) {
+__global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
+                              tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow) {
   const uint32_t r = threadIdx.x;
   if (r <= n_ranks) slot[r] = pos[(size_t)r * n_src];
+  if (slot_cap && r < n_ranks) {  // slotted output: each rank's chunk starts with its record count
+    const uint64_t c = pos[(size_t)(r + 1) * n_src] - pos[(size_t)r * n_src];
+    tgsim_delivery h = {};
+    h.t_ns = c < slot_cap ? c : slot_cap;
+    out[r * (slot_cap + 1)] = h;
+    if (c > slot_cap) *overflow = 1u;  // sticky, in pinned host memory: the host fails with -ENOSPC
+  }
   __threadfence_system();
   if (r == 0) __hip_atomic_store(&slot[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1377,18 +1394,27 @@ __global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ra
 // cursors), then each destination's records ordered by (t, src, seq, clone first).
 // Records addressed outside [dst_begin, dst_begin + n_dst) are skipped (the host reports them as
 // -EINVAL when it reads the count; with discarded deliveries they are dropped).
-__global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt) {
+// Slotted input (slot != 0): n = ranks * (slot + 1) records, each rank's chunk a count header then
+// up to `slot` records; the slots past the count are skipped.
+__device__ __forceinline__ bool slot_empty(const tgsim_delivery* in, uint64_t i, uint64_t slot) {
+  if (!slot) return false;
+  const uint64_t r = i / (slot + 1), j = i - r * (slot + 1);
+  return j == 0 || j > in[r * (slot + 1)].t_ns;
+}
+
+__global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
+                           uint64_t slot) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || slot_empty(in, i, slot)) return;
   const uint32_t d = in[i].dst - dst_begin;
   if (d < n_dst) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[d]), 1ull);
 }
 
 // Flat input (records received from every shard): pos[] starts as the exclusive scan of counts.
 __global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst,
-                              uint64_t* pos, tgsim_delivery* out) {
+                              uint64_t* pos, tgsim_delivery* out, uint64_t slot) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || slot_empty(in, i, slot)) return;
   const tgsim_delivery r = in[i];
   const uint32_t d = r.dst - dst_begin;
   if (d < n_dst) out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[d]), 1ull)] = r;
@@ -1678,8 +1704,9 @@ void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_
 }
 
 void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
-                        hipStream_t st) {
-  hipLaunchKernelGGL(k_route_edges, dim3(1), dim3(64), 0, st, pos, n_src, n_ranks, slot, seq);
+                        hipStream_t st, tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow) {
+  hipLaunchKernelGGL(k_route_edges, dim3(1), dim3(64), 0, st, pos, n_src, n_ranks, slot, seq, out, slot_cap,
+                     overflow);
 }
 
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
@@ -1694,6 +1721,7 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
   a.pos = h.pos;
   a.out = h.out;
   a.out_cap = h.out_cap;
+  a.slot_cap = h.slot_cap;
   uint32_t grid = (h.n_src + 3) / 4;
   if (grid > 4096) grid = 4096;
   if (grid == 0) grid = 1;
@@ -1702,16 +1730,17 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
 }
 
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
-                     hipStream_t st) {
+                     hipStream_t st, uint64_t slot) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, n_dst, cnt);
+  hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, n_dst, cnt,
+                     slot);
 }
 
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
-                        tgsim_delivery* out, hipStream_t st) {
+                        tgsim_delivery* out, hipStream_t st, uint64_t slot) {
   if (!n) return;
   hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, n_dst,
-                     pos, out);
+                     pos, out, slot);
 }
 
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,

@@ -21,6 +21,7 @@ struct RouteArgsHost {
   const uint64_t* pos;  // exclusive scan of cnt
   tgsim_delivery* out;
   uint64_t out_cap;
+  uint64_t slot_cap;  // 0: flat; else per-rank chunks of a count header + slot_cap records
 };
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
@@ -44,12 +45,16 @@ void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_
                  hipStream_t st, uint64_t* pos = nullptr);
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
 // edges[0..n_ranks] into slot[0..n_ranks] (pinned host memory), then seq into slot[15].
+// slotted output (slot_cap != 0): also each rank chunk's count header in out, and *overflow = 1
+// when a rank's count exceeds slot_cap.
 void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
-                        hipStream_t st);
+                        hipStream_t st, tgsim_delivery* out = nullptr, uint64_t slot_cap = 0,
+                        uint32_t* overflow = nullptr);
+// slot != 0: slotted input of n = ranks * (slot + 1) records (see launch_route_edges)
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
-                     hipStream_t st);
+                     hipStream_t st, uint64_t slot = 0);
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
-                        tgsim_delivery* out, hipStream_t st);
+                        tgsim_delivery* out, hipStream_t st, uint64_t slot = 0);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st);
 // Orders each destination's records; resets cnt[] to zero for the next histogram.

@@ -186,6 +186,23 @@ class CABIEngine:
         self._check(self._fn("step_sim_counts")(self._h, counts), "step_sim_counts")
         return np.array(list(counts), dtype=np.uint64)
 
+    def step_sim_launch_slotted(self, n_ticks: int, bounds: Sequence[int], d_out: int, slot_cap: int,
+                                routed_event: int = 0) -> None:
+        """Slotted pipelined step: records for rank r go to chunk r of (slot_cap + 1) records in
+        d_out, after a count header; routed_event is recorded when d_out is complete."""
+        b = (C.c_uint32 * len(bounds))(*bounds)
+        self._check(self._fn("step_sim_launch_slotted")(self._h, n_ticks, len(bounds) - 1, b, C.c_void_p(d_out),
+                                                         slot_cap, C.c_void_p(routed_event or None)),
+                    "step_sim_launch_slotted")
+
+    def step_sim_release(self) -> None:
+        """Retires the oldest launched slotted step without waiting for it."""
+        self._check(self._fn("step_sim_release")(self._h), "step_sim_release")
+
+    def deliver_slotted_async(self, d_in: int, n_ranks: int, slot_cap: int, wait_event: int = 0) -> None:
+        self._check(self._fn("deliver_slotted_async")(self._h, C.c_void_p(d_in), n_ranks, slot_cap,
+                                                       C.c_void_p(wait_event or None)), "deliver_slotted_async")
+
     def delivery_event(self, event: int) -> None:
         """Records a raw hipEvent_t on the delivery stream after the deliveries enqueued so far."""
         self._check(self._fn("delivery_event")(self._h, C.c_void_p(event)), "delivery_event")

@@ -40,14 +40,19 @@ def shard_bounds(n_peers: int, world: int) -> List[int]:
 class ShardedStepper:
     """One step = step_sim -> exchange -> deliver on every rank; run() pipelines many.  On GPUs the
     delivery of step k runs on the engine's delivery stream beside the k_sim of the next step
-    (tgsim_deliver_async).  The host never blocks on device work except for the step's per-rank
-    record counts: the engine's simulate stream waits for the collective that still reads the
-    output buffer it is about to overwrite, and the exchange stream waits for the delivery that
-    still reads the input buffer it is about to overwrite (events, not host synchronization).  The
-    counts themselves are host values (pinned edges), so they are exchanged over a CPU (gloo)
-    group: a device collective would queue behind the running k_sim for a CU."""
+    (tgsim_deliver_async).  The engine's simulate stream waits for the collective that still reads
+    the output buffer it is about to overwrite, and the exchange stream waits for the delivery that
+    still reads the input buffer it is about to overwrite (events, not host synchronization).
 
-    def __init__(self, engine, bounds: Sequence[int], device: str = "cuda", group=None):
+    Exact mode (step(), and run() without slot_cap): the per-rank record counts are exchanged
+    first (an all-to-all of the count vector), so the host waits for each step's routing and for
+    that collective.  Slotted mode (run() with slot_cap, on GPUs): every rank sends every rank a
+    fixed chunk of slot_cap records behind a count header, so nothing the host needs comes from the
+    device and the host only enqueues; a chunk that would overflow fails the run with -ENOSPC.
+    max_count (the largest per-rank count an exact step saw) sizes slot_cap."""
+
+    def __init__(self, engine, bounds: Sequence[int], device: str = "cuda", group=None,
+                 slot_cap: Optional[int] = None):
         self.engine = engine
         self.bounds = list(bounds)
         self.device = torch.device(device)
@@ -61,9 +66,9 @@ class ShardedStepper:
         self._k = 0
         # the exchange's stream: high priority, off the simulate stream's hardware queue (init_rccl)
         self._xs = torch.cuda.Stream(self.device, priority=-1) if self.device.type == "cuda" else None
-        # host-side count exchange (collective: every rank constructs its stepper)
-        ranks = dist.get_process_group_ranks(group) if group is not None else None
-        self._cpu_group = dist.new_group(ranks=ranks, backend="gloo") if self.device.type == "cuda" else group
+        self.slot_cap = slot_cap
+        self.max_count = 0
+        self._routed: List[Optional[torch.cuda.Event]] = [None] * 3  # slotted: out[j] complete
 
     def _buf(self, bufs: list, i: int, n_bytes: int) -> torch.Tensor:
         b = bufs[i]
@@ -90,10 +95,11 @@ class ShardedStepper:
 
     def _exchange_on(self, k: int, out: torch.Tensor, cnt: np.ndarray) -> int:
         cuda = self.device.type == "cuda"
-        send = torch.as_tensor(cnt.astype(np.int64))
+        self.max_count = max(self.max_count, int(cnt.max()) if len(cnt) else 0)
+        send = torch.as_tensor(cnt.astype(np.int64), device=self.device)
         recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self._cpu_group)
-        rcnt = recv.numpy()
+        dist.all_to_all_single(recv, send, group=self.group)
+        rcnt = recv.cpu().numpy()
         n_in = int(rcnt.sum())
         i = k % 2
         if cuda:
@@ -106,18 +112,62 @@ class ShardedStepper:
         dist.all_to_all_single(inb[: n_in * REC], out[: int(cnt.sum()) * REC],
                                [int(x) * REC for x in rcnt], [int(x) * REC for x in cnt], group=self.group)
         if cuda:  # the collective runs on torch's stream: the delivery stream waits for it
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
-            self._ev[k % 3] = ev
-            self.engine.deliver_async(inb.data_ptr(), n_in, ev.cuda_event)
-            dv = self._dev[i] or torch.cuda.Event()
-            if self._dev[i] is None:
-                dv.record(torch.cuda.current_stream(self.device))  # creates the event
-            self.engine.delivery_event(dv.cuda_event)
-            self._dev[i] = dv
+            self.engine.deliver_async(inb.data_ptr(), n_in, self._exchanged(k))
+            self._mark_delivery(i)
         else:
             self.engine.deliver(inb.data_ptr(), n_in)
         return n_in
+
+    def _exchanged(self, k: int) -> int:
+        """Event after the exchange of step k on the current (exchange) stream."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._ev[k % 3] = ev
+        return ev.cuda_event
+
+    def _mark_delivery(self, i: int) -> None:
+        """_dev[i]: recorded on the delivery stream after the delivery just enqueued (from _in[i])."""
+        dv = self._dev[i] or torch.cuda.Event()
+        if self._dev[i] is None:
+            dv.record(torch.cuda.current_stream(self.device))  # creates the event
+        self.engine.delivery_event(dv.cuda_event)
+        self._dev[i] = dv
+
+    def _event(self, evs: list, j: int) -> torch.cuda.Event:
+        ev = evs[j]
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))  # creates the event
+            evs[j] = ev
+        return ev
+
+    def _launch_slotted(self, n_ticks: int):
+        k = self._k
+        self._k += 1
+        j = k % 3
+        n_r = len(self.bounds) - 1
+        out = self._buf(self._out, j, n_r * (self.slot_cap + 1) * REC)
+        if self._ev[j] is not None:  # an earlier exchange still reads out[j]
+            self.engine.wait_event(self._ev[j].cuda_event)
+        routed = self._event(self._routed, j)
+        self.engine.step_sim_launch_slotted(n_ticks, self.bounds, out.data_ptr(), self.slot_cap, routed.cuda_event)
+        return k, out
+
+    def _exchange_slotted(self, k: int, out: torch.Tensor) -> None:
+        n_r = len(self.bounds) - 1
+        size = n_r * (self.slot_cap + 1) * REC
+        i = k % 2
+        with torch.cuda.stream(self._xs):
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(self._routed[k % 3])  # the routing of step k filled out
+            if self._dev[i] is not None:  # the delivery of step k - 2 still reads _in[i]
+                cur.wait_event(self._dev[i])
+            if self._in[i] is not None and self._in[i].numel() < size and self._dev[i] is not None:
+                self._dev[i].synchronize()  # growing: the old block returns to the allocator
+            inb = self._buf(self._in, i, size)
+            dist.all_to_all_single(inb[:size], out[:size], group=self.group)
+            self.engine.deliver_slotted_async(inb.data_ptr(), n_r, self.slot_cap, self._exchanged(k))
+            self._mark_delivery(i)
 
     def step(self, n_ticks: int, between: Optional[Callable[[], object]] = None) -> int:
         """One window on every rank (collective).  Returns the records delivered to this rank.
@@ -138,7 +188,17 @@ class ShardedStepper:
         exchanges step k, the engine's simulate stream already holds steps k+1 and k+2, so it never
         idles on the host.  Only for steps with no host-side change between them (pre-generated
         traffic, no reshaping, no receipts feeding generation); the results are identical to
-        n_steps calls of step()."""
+        n_steps calls of step().  Returns the records delivered to this rank, or -1 in slotted
+        mode (the host never reads a count there)."""
+        if self.slot_cap and self.device.type == "cuda":
+            pend = [self._launch_slotted(n_ticks) for _ in range(min(2, n_steps))]
+            for s in range(n_steps):
+                k, out = pend.pop(0)
+                self.engine.step_sim_release()
+                if s + 2 < n_steps:
+                    pend.append(self._launch_slotted(n_ticks))
+                self._exchange_slotted(k, out)
+            return -1  # the host never read a count
         total = 0
         pend = [self._launch(n_ticks) for _ in range(min(2, n_steps))]
         for s in range(n_steps):
@@ -151,10 +211,8 @@ class ShardedStepper:
 
     def barrier(self, state: int, target: int) -> bool:
         """Global barrier over the shards' sync counters: the per-rank counts of `state` are summed
-        with an all-reduce and compared with target (SignalAndWait semantics).  The counters are
-        host values (tgsim_signal), so the sum runs on the host group: a device all-reduce would
-        wait for a CU behind the running k_sim only to be copied back."""
+        with an all-reduce (RCCL on GPUs) and compared with target (SignalAndWait semantics)."""
         local = self.engine.signal(state, 0)
-        t = torch.tensor([local], dtype=torch.int64)
-        dist.all_reduce(t, group=self._cpu_group)
+        t = torch.tensor([local], dtype=torch.int64, device=self.device)
+        dist.all_reduce(t, group=self.group)
         return int(t.item()) >= target

@@ -116,3 +116,43 @@ def test_stepper_epochs_staged_reshape_equals_step(rccl):
         assert (sh.verdicts() == ref.verdicts()).all(), f"epoch {k}"
         d_sh, d_ref = sh.drain(), ref.drain()
         assert len(d_sh) == len(d_ref) > 0 and (d_sh == d_ref).all(), f"epoch {k}"
+
+
+def test_stepper_slotted_run_equals_step(rccl):
+    """run() with fixed-size exchange chunks (slot_cap): the host only enqueues, never reads a count;
+    the same deliveries and statistics as the single-engine steps."""
+    from testground_amd.shard import ShardedStepper
+
+    n, steps = 2000, 8
+    ref, sh = Engine(n), Engine(n)
+    for e in (ref, sh):
+        wl.configure_storm(e, n)
+    for _ in range(steps):
+        sh.gen_storm(0.5, 1000)
+    st = ShardedStepper(sh, [0, n], device="cuda:0", slot_cap=400_000)
+    assert st.run(steps, 1000) == -1
+    want = []
+    for _ in range(steps):
+        ref.gen_storm(0.5, 1000)
+        ref.step(1000)
+        want.append(ref.drain())
+    want = np.concatenate(want)
+    got = sh.drain()
+    assert len(got) == len(want) > 10_000 and (got == want).all()
+    s, r = sh.stats(), ref.stats()
+    assert (s["offered"], s["scheduled"], s["by_verdict"]) == (r["offered"], r["scheduled"], r["by_verdict"])
+
+
+def test_stepper_slotted_overflow_fails(rccl):
+    """A chunk too small for a step's records is an error (-ENOSPC), never a silent loss."""
+    from testground_amd.engine import EngineError
+    from testground_amd.shard import ShardedStepper
+
+    n = 500
+    sh = Engine(n)
+    wl.configure_storm(sh, n)
+    for _ in range(3):
+        sh.gen_storm(0.5, 1000)
+    with pytest.raises(EngineError, match="slot capacity"):
+        ShardedStepper(sh, [0, n], device="cuda:0", slot_cap=16).run(3, 1000)
+        sh.sync()
