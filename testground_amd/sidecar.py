@@ -109,7 +109,7 @@ class EngineSyncClient(SyncClient):
 
     State names map to the engine's 1024 state slots in first-use order, so every process of a
     sharded run must touch its states in the same order; `reduce`, when given, sums a state's
-    count over the shards (ShardedStepper.barrier sums them with an all-reduce over the ranks)."""
+    count over the shards (ShardedStepper.barrier does it with an RCCL all-reduce)."""
 
     def __init__(self, engine, lock: Optional[threading.Lock] = None,
                  reduce: Optional[Callable[[int, int], bool]] = None):
