@@ -42,7 +42,7 @@ B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 24, 148
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=None, help="timed steps (default: 30; gossip: 70 windows)")
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default: storm 30, epochs 10, gossip 70 windows)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; gossip: 0)")
     p.add_argument("--workload", default="storm", choices=["storm", "gossip", "epochs"])
     p.add_argument("--peers", type=int, default=0,
@@ -73,7 +73,7 @@ def parse():
     if a.workload == "gossip":
         a.window = 5000
     if a.steps is None:
-        a.steps = 70 if a.workload == "gossip" else 30  # enough to amortize the pipeline fill and drain
+        a.steps = {"gossip": 70, "epochs": 10}.get(a.workload, 30)  # storm: amortizes the pipeline fill and drain
     if a.warmup is None:
         a.warmup = 0 if a.workload == "gossip" else 3
     return a
@@ -242,7 +242,12 @@ def main():
             step(a.window)
 
     if a.workload == "gossip":
-        eng.gossip_init(n_floods=a.floods, degree=8, msg_len=1024, start_gap_ticks=a.flood_gap, start_tick=0)
+        # two empty windows, untimed: the step's buffers (two emit regions, sized for a full netem
+        # queue per source: ~64 GB at 1M peers) are allocated and first touched here, not in the
+        # timed flood; the floods start at the next window
+        for _ in range(2):
+            step(a.window)
+        eng.gossip_init(n_floods=a.floods, degree=8, msg_len=1024, start_gap_ticks=a.flood_gap)
         settle = 0  # a flood is a transient by nature: the timed windows cover it from the start
     else:
         settle = int(a.settle_ms * 1000 / a.window + 0.999)
