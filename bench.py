@@ -341,6 +341,11 @@ def main():
     if world == 1 and not a.no_cpu:
         res["cpu_baseline"] = cpu_baseline(a, peers_total)
         res["cpu_baseline"]["gpu_over_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+        import shutil
+        missing = [t for t in ("docker", "tc") if shutil.which(t) is None]
+        # the reference's local:docker sidecar + netem path is timed only where it runs
+        res["cpu_baseline"]["reference_docker_netem"] = (
+            f"not available on this host ({', '.join(missing)} absent)" if missing else "present, not timed by bench.py")
     os.write(json_fd, (json.dumps(res) + "\n").encode())
     if dist:
         dist.destroy_process_group()
