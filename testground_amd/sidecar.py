@@ -64,6 +64,10 @@ class SyncClient:
             self._cv.notify_all()
             return self._counts[state]
 
+    def _reached(self, state: str, target: int) -> bool:
+        with self._cv:
+            return self._counts.get(state, 0) >= target
+
     def Barrier(self, ctx: Context, state: str, target: int) -> None:
         with self._cv:
             while self._counts.get(state, 0) < target:

@@ -1,0 +1,142 @@
+"""`local:mi355x-sim` runner (testground_amd/runner.py): plans run as simulated instances of one
+engine.  CPU tests drive the runner over the CPU oracle (the checker) through the runner's
+engine_factory; the GPU test runs the same plan on the HIP engine and compares the results."""
+import io
+import tarfile
+
+import pytest
+
+from testground_amd import network as nw
+from testground_amd import runner as rn
+from testground_amd import workloads as wl
+from testground_amd.sidecar import Context
+
+
+def pingpong_plan(env: rn.PlanEnv) -> None:
+    """plans/network/pingpong.go:23-187 on the simulated data plane: configure 100 ms latency and
+    1 Mibit/s (callback "network-configured"), ping-pong with RTT in [200, 215] ms
+    (pingpong.go:185), reconfigure to 10 ms (callback "latency-reduced", :191-194), RTT in
+    [20, 35] ms (:195).  Round-trip times go to rtt.txt in the instance's outputs dir."""
+    env.net.WaitNetworkInitialized(env.ctx)
+    peer = 1 - env.seq
+    rtts = []
+
+    def ping_pong(lo_ms, hi_ms):
+        env.sync.SignalAndWait(env.ctx, f"ready-{lo_ms}", env.runenv.TestInstanceCount)
+        t0 = env.data.now_ns()
+        env.data.send(peer, bytes([env.seq]))
+        got_own = got_other = False
+        while not (got_own and got_other):
+            for t_ns, src, data, _f in env.data.recv(timeout_ns=10 * 10**9):
+                if data[0] == env.seq:
+                    rtt = t_ns - t0
+                    rtts.append(rtt)
+                    if not lo_ms * nw.Millisecond <= rtt <= hi_ms * nw.Millisecond:
+                        raise AssertionError(f"expected an RTT between {lo_ms} and {hi_ms} ms, got {rtt} ns")
+                    got_own = True
+                else:
+                    env.data.send(src, data, at_ns=t_ns)  # echo at the arrival time
+                    got_other = True
+        env.sync.SignalAndWait(env.ctx, f"done-{lo_ms}", env.runenv.TestInstanceCount)
+
+    cfg = wl.pingpong_config(100 * nw.Millisecond)
+    env.net.ConfigureNetwork(env.ctx, cfg)
+    ping_pong(200, 215)
+    cfg.Default.Latency = 10 * nw.Millisecond
+    cfg.CallbackState = "latency-reduced"
+    env.net.ConfigureNetwork(env.ctx, cfg)
+    ping_pong(20, 35)
+    with open(f"{env.runenv.TestOutputsPath}/rtt.txt", "w") as f:
+        f.write(" ".join(map(str, rtts)))
+
+
+def failing_plan(env: rn.PlanEnv) -> None:
+    if env.group_seq == 1:
+        raise RuntimeError("boom")
+
+
+def sleeper_plan(env: rn.PlanEnv) -> None:
+    env.data.sleep(int(env.runenv.TestInstanceParams["sleep_ms"]) * nw.Millisecond)
+
+
+def _job(run_id, groups, cfg):
+    return rn.RunInput(RunID=run_id, TestPlan="network", TestCase="ping-pong",
+                       TotalInstances=sum(g.Instances for g in groups), Groups=groups, RunnerConfig=cfg)
+
+
+def _cfg(tmp_path, factory, **kw):
+    return rn.LocalSimRunnerCfg(outputs_dir=str(tmp_path), engine_factory=factory, run_timeout_s=60, **kw)
+
+
+def _rtts(tmp_path, run_id):
+    return [open(tmp_path / "network" / run_id / "single" / str(i) / "rtt.txt").read() for i in (0, 1)]
+
+
+def test_runner_surface():
+    r = rn.LocalSimRunner()
+    assert r.ID() == "local:mi355x-sim"
+    assert r.ConfigType() is rn.LocalSimRunnerCfg
+    assert r.CompatibleBuilders() == ["exec:py"]
+    res = rn.Result(Outcome=rn.OUTCOME_SUCCESS, Outcomes={"a": rn.GroupOutcome(2, 3)})
+    assert str(res) == "outcome = success (a:2/3)"
+
+
+def test_runner_rejects_bad_input(tmp_path, make_oracle):
+    r = rn.LocalSimRunner()
+    g = [rn.RunGroup("single", 2, pingpong_plan)]
+    job = _job("bad", g, _cfg(tmp_path, make_oracle))
+    job.TotalInstances = 3
+    with pytest.raises(ValueError, match="TotalInstances"):
+        r.Run(Context(), job)
+    with pytest.raises(ValueError, match="artifact"):
+        r.Run(Context(), _job("bad2", [rn.RunGroup("single", 2, "not a plan")], _cfg(tmp_path, make_oracle)))
+
+
+def test_runner_pingpong_over_oracle(tmp_path, make_oracle):
+    """The reference's ping-pong test case as a plan: two instances, sidecar-applied shapes,
+    both RTT windows met; the run is reproducible and its outputs can be collected."""
+    r = rn.LocalSimRunner()
+    outs = []
+    for run_id in ("r1", "r2"):
+        out = r.Run(Context(), _job(run_id, [rn.RunGroup("single", 2, pingpong_plan)], _cfg(tmp_path, make_oracle)))
+        assert out.Result.Outcome == rn.OUTCOME_SUCCESS, out.Result.Errors
+        assert str(out.Result.Outcomes["single"]) == "2/2"
+        outs.append(_rtts(tmp_path, run_id))
+    assert outs[0] == outs[1]  # conservative clock: same simulated times every run
+    buf = io.BytesIO()
+    r.CollectOutputs(Context(), rn.CollectionInput("r1", "network"), buf, _cfg(tmp_path, make_oracle))
+    names = tarfile.open(fileobj=io.BytesIO(buf.getvalue()), mode="r:gz").getnames()
+    assert "r1/single/0/rtt.txt" in names and "r1/run.json" in names
+
+
+def test_runner_outcomes_per_group(tmp_path, make_oracle):
+    """cluster_k8s.go:1235-1245: the run fails unless every group has ok == total."""
+    r = rn.LocalSimRunner()
+    g = [rn.RunGroup("good", 2, sleeper_plan, {"sleep_ms": "5"}), rn.RunGroup("bad", 2, failing_plan)]
+    out = r.Run(Context(), _job("mixed", g, _cfg(tmp_path, make_oracle)))
+    assert out.Result.Outcome == rn.OUTCOME_FAILURE
+    assert str(out.Result.Outcomes["good"]) == "2/2" and str(out.Result.Outcomes["bad"]) == "1/2"
+    assert "boom" in out.Result.Errors["bad[001]"]
+    assert out.Result.SimulatedNs >= 5 * nw.Millisecond
+
+
+def test_runner_sim_time_cap(tmp_path, make_oracle):
+    r = rn.LocalSimRunner()
+    cfg = _cfg(tmp_path, make_oracle, max_sim_ns=20 * nw.Millisecond)
+    out = r.Run(Context(), _job("cap", [rn.RunGroup("g", 1, sleeper_plan, {"sleep_ms": "100"})], cfg))
+    assert out.Result.Outcome != rn.OUTCOME_SUCCESS
+    assert "simulation stopped" in out.Result.Errors["g[000]"]
+
+
+@pytest.mark.gpu
+def test_runner_pingpong_gpu_equals_oracle(tmp_path, make_oracle):
+    """The ping-pong plan on the HIP engine (the runner's default engine): success, and the same
+    round-trip times as over the oracle."""
+    import torch
+    assert torch.cuda.is_available()
+    r = rn.LocalSimRunner()
+    gpu = r.Run(Context(), _job("gpu", [rn.RunGroup("single", 2, pingpong_plan)], _cfg(tmp_path, None)))
+    assert gpu.Result.Outcome == rn.OUTCOME_SUCCESS, gpu.Result.Errors
+    cpu = r.Run(Context(), _job("cpu", [rn.RunGroup("single", 2, pingpong_plan)], _cfg(tmp_path, make_oracle)))
+    assert cpu.Result.Outcome == rn.OUTCOME_SUCCESS, cpu.Result.Errors
+    assert _rtts(tmp_path, "gpu") == _rtts(tmp_path, "cpu")
