@@ -211,10 +211,13 @@ class DataPlane:
         return self._c.now_ns()
 
     def send(self, dst: int, data: bytes, at_ns: Optional[int] = None) -> int:
-        """Sends one datagram at at_ns (default: now_ns()); returns its sequence number."""
+        """Sends one datagram at at_ns (default: now_ns()); returns its sequence number.  A time
+        already simulated (a reply to a delivery that arrived less than one window after it was
+        sent, on a link shorter than the window) leaves at now_ns(): the clock cannot go back, so
+        links shorter than `window_ticks` see their replies rounded up to the next window."""
         b = self._c.bridge
-        at = None if at_ns is None else -(-int(at_ns) // b.tick_ns)
         with self._c.lock:
+            at = None if at_ns is None else max(-(-int(at_ns) // b.tick_ns), b.now_tick)
             return b.send(self.peer, dst, data, at_tick=at)
 
     def recv(self, timeout_ns: Optional[int] = None) -> List[Tuple[int, int, bytes, int]]:

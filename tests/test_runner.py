@@ -2,6 +2,7 @@
 engine.  CPU tests drive the runner over the CPU oracle (the checker) through the runner's
 engine_factory; the GPU test runs the same plan on the HIP engine and compares the results."""
 import io
+import ipaddress
 import tarfile
 
 import pytest
@@ -140,3 +141,75 @@ def test_runner_pingpong_gpu_equals_oracle(tmp_path, make_oracle):
     cpu = r.Run(Context(), _job("cpu", [rn.RunGroup("single", 2, pingpong_plan)], _cfg(tmp_path, make_oracle)))
     assert cpu.Result.Outcome == rn.OUTCOME_SUCCESS, cpu.Result.Errors
     assert _rtts(tmp_path, "gpu") == _rtts(tmp_path, "cpu")
+
+
+def splitbrain_plan(case: str, ok: dict):
+    """plans/splitbrain/main.go:61-180 as a plan: sequence numbers from SignalEntry give the
+    region (seq % 3, :84-87); region-A instances install one /32 rule per region-B instance with
+    the case's action through ConfigureNetwork (callback "reconfigured<seq>", target 1,
+    :101-140); then every instance contacts every other one and answers every request it gets.
+    ok[(i, j)] = instance i got j's answer; the expectation is expectErrors (:50-58)."""
+    def plan(env: rn.PlanEnv) -> None:
+        n = env.runenv.TestInstanceCount
+        env.net.WaitNetworkInitialized(env.ctx)
+        seq = env.sync.SignalEntry(env.ctx, "ip-allocation")
+        env.sync.Publish(env.ctx, "nodes", (env.seq, seq % 3))
+        env.sync.SignalAndWait(env.ctx, "published", n)
+        q = env.sync.Subscribe(env.ctx, "nodes")
+        region = dict(q.get_nowait() for _ in range(n))
+        if region[env.seq] == wl.REGION_A:
+            action = {"drop": nw.FilterAction.Drop, "reject": nw.FilterAction.Reject,
+                      "accept": nw.FilterAction.Accept}[case]
+            rules = [nw.LinkRule(Subnet=(str(ipaddress.IPv4Address(wl.peer_ip(p))), 32),
+                                 LinkShape=nw.LinkShape(Filter=action))
+                     for p, r in sorted(region.items()) if r == wl.REGION_B]
+            env.net.ConfigureNetwork(env.ctx, nw.Config(
+                Network="default", Enable=True, Default=nw.LinkShape(Latency=nw.Millisecond),
+                Rules=rules, CallbackState=f"reconfigured{seq}", CallbackTarget=1))
+        env.sync.SignalAndWait(env.ctx, "configured", n)
+        for p in range(n):
+            if p != env.seq:
+                env.data.send(p, b"Q")
+        deadline = env.data.now_ns() + 50 * nw.Millisecond
+        while env.data.now_ns() < deadline:
+            for t_ns, src, data, _f in env.data.recv(timeout_ns=deadline - env.data.now_ns()):
+                if data == b"Q":
+                    env.data.send(src, b"A", at_ns=t_ns)
+                else:
+                    ok[(env.seq, src)] = region
+    return plan
+
+
+@pytest.mark.parametrize("case", ["accept", "reject", "drop"])
+def test_runner_splitbrain_over_oracle(tmp_path, make_oracle, case):
+    n = 9
+    ok = {}
+    r = rn.LocalSimRunner()
+    out = r.Run(Context(), _job(f"sb-{case}", [rn.RunGroup("all", n, splitbrain_plan(case, ok))],
+                                _cfg(tmp_path, make_oracle)))
+    assert out.Result.Outcome == rn.OUTCOME_SUCCESS, out.Result.Errors
+    region = next(iter(ok.values()))
+    for i in range(n):
+        for j in range(n):
+            if i != j:
+                reachable = not wl.expect_errors(case, region[i], region[j])
+                assert ((i, j) in ok) == reachable, (case, i, j, region[i], region[j])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["reject", "drop"])
+def test_runner_splitbrain_gpu(tmp_path, case):
+    """The splitbrain plan on the HIP engine: rules applied by the sidecar handler on the device
+    filter exactly the region A <-> B pairs."""
+    import torch
+    assert torch.cuda.is_available()
+    n = 9
+    ok = {}
+    out = rn.LocalSimRunner().Run(Context(), _job(f"sbg-{case}", [rn.RunGroup("all", n, splitbrain_plan(case, ok))],
+                                                  _cfg(tmp_path, None)))
+    assert out.Result.Outcome == rn.OUTCOME_SUCCESS, out.Result.Errors
+    region = next(iter(ok.values()))
+    for i in range(n):
+        for j in range(n):
+            if i != j:
+                assert ((i, j) in ok) == (not wl.expect_errors(case, region[i], region[j])), (i, j)
