@@ -285,8 +285,33 @@ def _resolve(artifact) -> Callable[[PlanEnv], None]:
     raise ValueError(f"artifact {artifact!r} is not a plan callable or 'module:function'")
 
 
+HEALTH_OK = "ok"                 # pkg/api/healthcheck.go:20-35
+HEALTH_FAILED = "failed"
+HEALTH_ABORTED = "aborted"
+HEALTH_OMITTED = "omitted"
+HEALTH_UNNECESSARY = "unnecessary"
+
+
+@dataclasses.dataclass
+class HealthcheckItem:
+    """api.HealthcheckItem (healthcheck.go:39-47)."""
+    Name: str
+    Status: str
+    Message: str = ""
+
+
+@dataclasses.dataclass
+class HealthcheckReport:
+    """api.HealthcheckReport (healthcheck.go:49-56)."""
+    Checks: List[HealthcheckItem] = dataclasses.field(default_factory=list)
+    Fixes: List[HealthcheckItem] = dataclasses.field(default_factory=list)
+
+    def ChecksSucceeded(self) -> bool:
+        return all(c.Status == HEALTH_OK for c in self.Checks)
+
+
 class LocalSimRunner:
-    """api.Runner for `local:mi355x-sim`."""
+    """api.Runner (and api.Healthchecker) for `local:mi355x-sim`."""
 
     def __init__(self):
         self._lk = threading.Lock()
@@ -407,6 +432,63 @@ class LocalSimRunner:
             raise FileNotFoundError(f"no outputs for run {inp.RunID} under {run_dir}")
         with tarfile.open(fileobj=ow, mode="w:gz") as tar:
             tar.add(run_dir, arcname=inp.RunID)
+
+    def Healthcheck(self, ctx: Context, fix: bool = False, cfg: Optional[LocalSimRunnerCfg] = None,
+                    ow=None) -> HealthcheckReport:
+        """api.Healthchecker (healthcheck.go:13-15).  Checks, as the local runners' helper does
+        (Enlist check + fix, local_exec.go:49-72): the outputs directory (fixed by creating it),
+        the engine library and an engine on a GPU (both need manual fixing: build the extension,
+        run on a box with an MI355X)."""
+        cfg = cfg or LocalSimRunnerCfg()
+        rep = HealthcheckReport()
+
+        def outputs():
+            d = self._outputs_dir(cfg)
+            return (HEALTH_OK, d) if os.path.isdir(d) else (HEALTH_FAILED, f"{d} does not exist")
+
+        def library():
+            from .engine import load_library
+            try:
+                load_library()
+                return HEALTH_OK, "libtgsim.so loaded"
+            except (OSError, RuntimeError) as e:  # EngineUnavailable is a RuntimeError
+                return HEALTH_FAILED, str(e)
+
+        def engine():
+            try:
+                if cfg.engine_factory is None:
+                    from .engine import Engine
+                    e = Engine(1, tick_ns=cfg.tick_ns)
+                else:
+                    e = cfg.engine_factory(1, tick_ns=cfg.tick_ns)
+                e.close()
+                return HEALTH_OK, "engine created"
+            except Exception as e:  # noqa: BLE001 - reported in the check
+                return HEALTH_FAILED, str(e)
+
+        def fix_outputs():
+            os.makedirs(self._outputs_dir(cfg), exist_ok=True)
+
+        for name, check, fixer in (("outputs-dir", outputs, fix_outputs), ("engine-library", library, None),
+                                   ("engine-device", engine, None)):
+            status, msg = check()
+            rep.Checks.append(HealthcheckItem(name, status, msg))
+            if not fix:
+                continue
+            if status == HEALTH_OK:
+                rep.Fixes.append(HealthcheckItem(name, HEALTH_UNNECESSARY))
+            elif fixer is None:
+                rep.Fixes.append(HealthcheckItem(name, HEALTH_FAILED, "requires manual fixing"))
+            else:
+                try:
+                    fixer()
+                    rep.Fixes.append(HealthcheckItem(name, HEALTH_OK))
+                except OSError as e:
+                    rep.Fixes.append(HealthcheckItem(name, HEALTH_FAILED, str(e)))
+        if ow is not None:
+            for c in rep.Checks:
+                ow.write(f"check {c.Name}: {c.Status} {c.Message}\n")
+        return rep
 
     def TerminateAll(self, ctx: Context, ow=None) -> None:
         with self._lk:

@@ -213,3 +213,17 @@ def test_runner_splitbrain_gpu(tmp_path, case):
         for j in range(n):
             if i != j:
                 assert ((i, j) in ok) == (not wl.expect_errors(case, region[i], region[j])), (i, j)
+
+
+def test_runner_healthcheck(tmp_path, make_oracle):
+    """healthcheck.go:13-56: the outputs dir check is fixed by creating it; checks that pass
+    report their fix as unnecessary; the engine checks pass with a working engine."""
+    r = rn.LocalSimRunner()
+    cfg = rn.LocalSimRunnerCfg(outputs_dir=str(tmp_path / "out"), engine_factory=make_oracle)
+    rep = r.Healthcheck(Context(), fix=False, cfg=cfg)
+    st = {c.Name: c.Status for c in rep.Checks}
+    assert st == {"outputs-dir": rn.HEALTH_FAILED, "engine-library": rn.HEALTH_OK, "engine-device": rn.HEALTH_OK}
+    assert not rep.ChecksSucceeded() and rep.Fixes == []
+    rep = r.Healthcheck(Context(), fix=True, cfg=cfg)
+    assert [f.Status for f in rep.Fixes] == [rn.HEALTH_OK, rn.HEALTH_UNNECESSARY, rn.HEALTH_UNNECESSARY]
+    assert r.Healthcheck(Context(), cfg=cfg).ChecksSucceeded()
