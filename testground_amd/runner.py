@@ -147,7 +147,9 @@ class _Clock:
         self.lock = lock
         self.ctx = ctx
         self.max_sim_ns = max_sim_ns
-        self.cv = threading.Condition()
+        self._mu = threading.Lock()
+        self.cv = threading.Condition(self._mu)                            # the clock waits here
+        self.pcv = [threading.Condition(self._mu) for _ in range(n)]       # instance p waits here
         self.live = set(range(n))
         self.waiting: Dict[int, Callable[[], bool]] = {}
         self.inbox: List[List[Tuple[int, int, bytes, int]]] = [[] for _ in range(n)]
@@ -166,9 +168,16 @@ class _Clock:
                         raise RuntimeError(f"simulation stopped: {self.error}")
                     if self.ctx.done():
                         raise TimeoutError(f"instance {peer}: {self.ctx.err()}")
-                    self.cv.wait(timeout=0.05)
+                    self.pcv[peer].wait(timeout=0.05)
             finally:
                 del self.waiting[peer]
+
+    def kick(self) -> None:
+        """Wakes every blocked instance to re-check (after a sync signal)."""
+        with self.cv:
+            for c in self.pcv:
+                c.notify()
+            self.cv.notify_all()
 
     def finish(self, peer: int) -> None:
         with self.cv:
@@ -184,7 +193,8 @@ class _Clock:
                     continue
                 if self.now_ns() >= self.max_sim_ns:
                     self.error = TimeoutError(f"simulated time reached {self.max_sim_ns} ns")
-                    self.cv.notify_all()
+                    for c in self.pcv:
+                        c.notify()
                     return
                 try:
                     with self.lock:
@@ -194,9 +204,12 @@ class _Clock:
                                 self.inbox[p].append((t_ns, src, data, flags))
                 except BaseException as e:  # noqa: BLE001 - surfaced to every instance
                     self.error = e
-                    self.cv.notify_all()
+                    for c in self.pcv:
+                        c.notify()
                     return
-                self.cv.notify_all()
+                for p, r in self.waiting.items():  # wake only the instances that can go on
+                    if r():
+                        self.pcv[p].notify()
 
 
 class DataPlane:
@@ -245,7 +258,9 @@ class ClockedSync:
         self.peer = peer
 
     def SignalEntry(self, ctx: Context, state: str) -> int:
-        return self.inner.SignalEntry(ctx, state)
+        seq = self.inner.SignalEntry(ctx, state)
+        self._c.kick()
+        return seq
 
     def Barrier(self, ctx: Context, state: str, target: int) -> None:
         self._c.block(self.peer, lambda: self.inner._reached(state, target))
