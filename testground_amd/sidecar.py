@@ -177,7 +177,10 @@ class NetClient:
         if not config.CallbackState:  # pinned by sidecar_test.go:59
             raise ValueError("failed to configure network; no callback state provided")
         target = config.CallbackTarget or self.runenv.TestInstanceCount
-        self.sync.PublishAndWait(ctx, "network:" + self.hostname, config, config.CallbackState, target)
+        # sdk-go serialises the config onto the topic, so the sidecar gets a copy and the caller
+        # may change its own object afterwards (plans/network/pingpong.go:191-194 does)
+        self.sync.PublishAndWait(ctx, "network:" + self.hostname, copy.deepcopy(config),
+                                 config.CallbackState, target)
 
 
 class Network:
