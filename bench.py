@@ -5,22 +5,29 @@ over 10,000 instances per GPU, heterogeneous LinkShape (latency/jitter/loss/dup/
 bandwidth), Poisson(0.5) packets per instance per 1 µs tick.  One step = one pass of the hot path
 over one window of `--window` ticks of offered traffic that is already resident in HBM (generated
 on the device before the timed region): filter -> netem -> HTB (k_sim), routing by destination
-shard, RCCL all-to-all (N > 1), per-destination delivery sort.
+shard, RCCL all-to-all (N > 1), per-destination delivery sort.  The same line carries an
+`at_1M_peers` object: the C4 gossip flood over 1,000,000 peers in total (split over the N GPUs),
+so both halves of BASELINE.json's metric ("at 10k & 1M peers") are measured in one run.
 
 `--workload gossip` (C4, BASELINE.json configs[3]): flood of 64 messages over --peers instances per
-GPU (125,000 per GPU = 1M at 8 GPUs), degree 8, 1 KiB, L~U[5,50] ms, loss 1 %.  A step is one 5 ms
-window: forwards of the previous window's receipts generated on the device, then the hot path.
+GPU, degree 8, 1 KiB, L~U[5,50] ms, loss 1 %.  A step is one 5 ms window: forwards of the previous
+window's receipts generated on the device, then the hot path.
 `--workload epochs` (C5, configs[4]): 100,000 instances per GPU, C3 shapes and traffic at
 lambda 0.2, 1,000-tick epochs; a step reshapes 10 % of the instances (batched ConfigureNetwork),
-runs the epoch and passes the `epoch-k` barrier (counters summed over ranks).
+runs the epoch and passes the `epoch-k` barrier (counters summed over ranks on the device).
 
-N = 1 runs directly; N > 1 is launched by torch.distributed.run, one rank per GPU, each rank owning
---peers instances (weak scaling), cross-shard deliveries exchanged with all_to_all_single (RCCL).
+Launch: N = 1 runs directly.  `--gpus N` with N > 1 and no WORLD_SIZE in the environment starts N
+ranks itself (torch.distributed.run, one process per GPU) from this parent, which never touches
+the GPU; under an external launcher WORLD_SIZE must equal --gpus.  Every rank owns --peers
+instances (weak scaling); cross-shard deliveries are exchanged with all_to_all_single (RCCL).
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -37,9 +44,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # across steps (16 B per queued item, 8 B per departing item, loaded at step start and stored at
 # step end: the engine's queue_state_bytes counter).
 B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 24, 148
+REC = 24  # sizeof(tgsim_delivery), the record an exchange moves
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None, help="timed steps (default: storm 30, epochs 10, gossip 70 windows)")
@@ -65,7 +73,13 @@ def parse():
                    help="use the peer-sharded step (RCCL exchange) even at one rank, to time the N>1 path")
     p.add_argument("--exact-exchange", action="store_true",
                    help="sharded storm: exchange exact record counts every step instead of fixed-size chunks")
-    a = p.parse_args()
+    p.add_argument("--no-1m", action="store_true",
+                   help="storm: skip the at_1M_peers gossip run that accompanies the headline line")
+    p.add_argument("--gossip-1m-peers", type=int, default=1_000_000,
+                   help="total peers of the at_1M_peers run (split over the ranks)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="launcher self-test: every rank reports RANK/WORLD_SIZE and exits before any GPU call")
+    a = p.parse_args(argv)
     if not a.peers:
         a.peers = {"storm": 10_000, "gossip": 125_000, "epochs": 100_000}[a.workload]
     if a.workload == "epochs":
@@ -79,9 +93,46 @@ def parse():
     return a
 
 
-def cpu_baseline(a, peers_total):
-    """The CPU oracle (a 'port' of the reference semantics) timed on this host, single thread, on a
-    bounded sample of the same workload."""
+# ------------------------------------------------------------------------------------------------
+# Launcher: the driver may call `bench.py --gpus N` bare; ranks are then started from here, before
+# anything initializes HIP in this process (a GPU-initialized process must never exec).
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(n: int, argv, port: int):
+    """torch.distributed.run command that starts n ranks of this script with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *argv]
+
+
+def launch_decision(gpus: int, env) -> str:
+    """'run' (this process is a rank), 'spawn' (start gpus ranks) or an error message."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        return f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}; launch one rank per GPU (--nproc-per-node {gpus})"
+    return "run"
+
+
+def spawn_ranks(n: int, argv) -> int:
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["TGSIM_BENCH_LAUNCHED"] = "1"
+    return subprocess.run(launch_command(n, argv, free_port()), env=env).returncode
+
+
+# ------------------------------------------------------------------------------------------------
+def kernel_sha16() -> str:
+    return hashlib.sha256((ROOT / "testground_amd" / "csrc" / "tgsim_kernels.hip").read_bytes()).hexdigest()[:16]
+
+
+def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds):
+    """The CPU oracle (a 'port' of the reference semantics) timed on this host, on a bounded sample
+    of the same workload: single thread, plus (storm/epochs) one oracle shard per thread."""
     from testground_amd import abi, workloads
     from testground_amd.build import build_oracle
     from testground_amd.engine import CABIEngine
@@ -89,76 +140,83 @@ def cpu_baseline(a, peers_total):
     lib = ctypes.CDLL(str(build_oracle()))
     abi.declare(lib, "tgo_")
     busy, steps = 0.0, 0
-    if a.workload == "gossip":  # closed loop: needs every peer, so the sample is a smaller flood
+    if workload == "gossip":  # closed loop: needs every peer, so the sample is a smaller flood
         n = min(peers_total, 20_000)
         e = CABIEngine(lib, "tgo_", n, lookahead_ns=workloads.GOSSIP_MIN_LAT)
         workloads.configure_gossip(e, n)
         e.gossip_init(n_floods=a.floods, degree=8, msg_len=1024, start_gap_ticks=a.flood_gap, start_tick=0)
-        while busy < a.cpu_seconds and steps < 400:
+        while busy < cpu_seconds and steps < 400:
             t0 = time.perf_counter()
-            e.gen_gossip(a.window)
-            e.step(a.window)
+            e.gen_gossip(window)
+            e.step(window)
             busy += time.perf_counter() - t0
             steps += 1
             e.drain()
         pkts = e.stats()["offered"]
         sample = (f"oracle/tgoracle.c, the same flood over {n} instances ({a.floods} floods, degree 8), "
-                  f"{steps} windows of {a.window} ticks incl. forward generation, {pkts} packets, {busy:.1f} s")
-    else:
-        sample_src = min(1000, peers_total)
+                  f"{steps} windows of {window} ticks incl. forward generation, {pkts} packets, {busy:.1f} s")
+        return {"value": pkts / busy, "unit": "packets/s", "cores": 1, "kind": "port", "sample": sample}
+    sample_src = min(1000, peers_total)
 
-        def leg(lo, hi, seconds):
-            """One oracle shard [lo, hi) of the same workload stepped for ~seconds of step time."""
-            e = CABIEngine(lib, "tgo_", peers_total, shard=(lo, hi))
-            workloads.configure_storm(e, peers_total)
-            busy, steps = 0.0, 0
-            while busy < seconds:
-                if a.workload == "epochs" and steps:
-                    r0 = time.perf_counter()
-                    workloads.epoch_reshape(e, peers_total, steps)
-                    busy += time.perf_counter() - r0
-                e.gen_storm(a.lam, a.window)
-                t0 = time.perf_counter()
-                e.step(a.window)
-                busy += time.perf_counter() - t0
-                steps += 1
-                e.drain()
-            return e.stats()["offered"], busy, steps
+    def leg(lo, hi, seconds):
+        """One oracle shard [lo, hi) of the same workload stepped for ~seconds of step time."""
+        e = CABIEngine(lib, "tgo_", peers_total, shard=(lo, hi))
+        workloads.configure_storm(e, peers_total)
+        busy, steps = 0.0, 0
+        while busy < seconds:
+            if workload == "epochs" and steps:
+                r0 = time.perf_counter()
+                workloads.epoch_reshape(e, peers_total, steps)
+                busy += time.perf_counter() - r0
+            e.gen_storm(lam, window)
+            t0 = time.perf_counter()
+            e.step(window)
+            busy += time.perf_counter() - t0
+            steps += 1
+            e.drain()
+        return e.stats()["offered"], busy, steps
 
-        pkts, busy, steps = leg(0, sample_src, a.cpu_seconds)
-        sample = (f"oracle/tgoracle.c, sources 0..{sample_src - 1} of the {peers_total}-instance {a.workload} "
-                  f"workload, lambda={a.lam}, {steps} windows of {a.window} ticks, {pkts} packets, {busy:.1f} s")
-        if a.cpu_threads > 1:  # all-core leg: one oracle shard per thread (ctypes drops the GIL)
-            from concurrent.futures import ThreadPoolExecutor
+    pkts, busy, steps = leg(0, sample_src, cpu_seconds)
+    sample = (f"oracle/tgoracle.c, sources 0..{sample_src - 1} of the {peers_total}-instance {workload} "
+              f"workload, lambda={lam}, {steps} windows of {window} ticks, {pkts} packets, {busy:.1f} s")
+    if a.cpu_threads > 1:  # all-core leg: one oracle shard per thread (ctypes drops the GIL)
+        from concurrent.futures import ThreadPoolExecutor
 
-            t = a.cpu_threads
-            per = max(1, min(sample_src, peers_total // t))
-            w0 = time.perf_counter()
-            with ThreadPoolExecutor(t) as ex:
-                res = list(ex.map(lambda k: leg(k * per, (k + 1) * per, a.cpu_seconds / 2), range(t)))
-            wall = time.perf_counter() - w0
-            # each thread's packets over its own stepping time; the sum is the all-core rate
-            rate = sum(p / b for p, b, _ in res)
-            return {"value": rate, "unit": "packets/s", "cores": t, "kind": "port",
-                    "sample": (f"oracle/tgoracle.c, {t} threads, thread k steps sources "
-                               f"[{per}k, {per}(k+1)) of the {peers_total}-instance {a.workload} workload "
-                               f"(lambda={a.lam}, windows of {a.window} ticks) for ~{a.cpu_seconds / 2:.0f} s; "
-                               f"{sum(p for p, _, _ in res)} packets, {wall:.1f} s wall"),
-                    "single_thread": {"value": pkts / busy, "cores": 1, "sample": sample}}
+        t = a.cpu_threads
+        per = max(1, min(sample_src, peers_total // t))
+        w0 = time.perf_counter()
+        with ThreadPoolExecutor(t) as ex:
+            res = list(ex.map(lambda k: leg(k * per, (k + 1) * per, cpu_seconds / 2), range(t)))
+        wall = time.perf_counter() - w0
+        # each thread's packets over its own stepping time; the sum is the all-core rate
+        rate = sum(p / b for p, b, _ in res)
+        return {"value": rate, "unit": "packets/s", "cores": t, "kind": "port",
+                "sample": (f"oracle/tgoracle.c, {t} threads, thread k steps sources "
+                           f"[{per}k, {per}(k+1)) of the {peers_total}-instance {workload} workload "
+                           f"(lambda={lam}, windows of {window} ticks) for ~{cpu_seconds / 2:.0f} s; "
+                           f"{sum(p for p, _, _ in res)} packets, {wall:.1f} s wall"),
+                "single_thread": {"value": pkts / busy, "cores": 1, "sample": sample}}
     return {"value": pkts / busy, "unit": "packets/s", "cores": 1, "kind": "port", "sample": sample}
 
 
-def load_pmc(a):
-    f = ROOT / "profiles" / ("pmc_k_sim.json" if a.workload == "storm" else f"pmc_k_sim_{a.workload}.json")
+def load_pmc(workload, window, peers, lam):
+    """HBM traffic of k_sim from the committed PMC passes (rocprofv3 cannot run inside the bench).
+    Reported only when the file was collected on the same k_sim source (sha of tgsim_kernels.hip)
+    and the same workload configuration; the line names the file and its provenance either way."""
+    f = ROOT / "profiles" / ("pmc_k_sim.json" if workload == "storm" else f"pmc_k_sim_{workload}.json")
+    src = {"file": str(f.relative_to(ROOT)), "kernel_sha16_now": kernel_sha16()}
     if not f.exists():
-        return None
+        return None, dict(src, status="absent")
     try:
         pmc = json.loads(f.read_text())
     except Exception:
-        return None
-    if pmc.get("window") == a.window and pmc.get("peers") == a.peers and pmc.get("lam", a.lam) == a.lam:
-        return pmc.get("hbm_bytes_per_launch")
-    return None
+        return None, dict(src, status="unreadable")
+    src.update({k: pmc.get(k) for k in ("kernel_sha16", "commit", "peers", "lam", "window")})
+    if pmc.get("kernel_sha16") != src["kernel_sha16_now"]:
+        return None, dict(src, status="stale: collected on another k_sim source")
+    if pmc.get("window") != window or pmc.get("peers") != peers or pmc.get("lam", lam) != lam:
+        return None, dict(src, status="other configuration")
+    return pmc.get("hbm_bytes_per_launch"), dict(src, status="matches this kernel and configuration")
 
 
 WORKLOAD_NAMES = {
@@ -169,16 +227,10 @@ WORKLOAD_NAMES = {
 }
 
 
-def main():
-    a = parse()
-    # the one JSON line goes to the original stdout; everything else (RCCL's version banner, library
-    # chatter) is sent to stderr so that the line stays the only thing on stdout
-    sys.stdout.flush()
-    json_fd = os.dup(1)
-    os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, local, dist, want_cpu):
+    """Builds one engine shard of `peers` sources on this rank, brings the workload to its timed
+    state, times `steps` steps (barrier + synchronize on both sides, max over ranks) and returns the
+    rank-0 result object (None on the other ranks)."""
     import numpy as np
     import torch
 
@@ -186,98 +238,90 @@ def main():
     from testground_amd.engine import Engine
     from testground_amd.network import configs_array
 
-    torch.cuda.set_device(local)
-    dist = None
-    sharded = world > 1 or a.sharded
-    if sharded:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
-        import torch.distributed as dist
-        from testground_amd.shard import init_rccl
-        init_rccl(torch.device("cuda", local))
-    peers_total = a.peers * world
-    lo, hi = rank * a.peers, (rank + 1) * a.peers
-    kw = dict(lookahead_ns=workloads.GOSSIP_MIN_LAT) if a.workload == "gossip" else {}
+    sharded = dist is not None
+    peers_total = peers * world
+    lo, hi = rank * peers, (rank + 1) * peers
+    kw = dict(lookahead_ns=workloads.GOSSIP_MIN_LAT) if workload == "gossip" else {}
     eng = Engine(peers_total, shard=(lo, hi), device=local, flags=abi.OPT_DISCARD_DELIVERIES,
                  queue_limit=a.queue_limit, **kw)
-    if a.workload == "gossip":
+    t_setup = time.perf_counter()
+    if workload == "gossip":
         workloads.configure_gossip(eng, peers_total)
     elif a.shapes == "storm":
         workloads.configure_storm(eng, peers_total)
     else:
         eng.configure_batch(np.arange(peers_total), configs_array(np.full(peers_total, 5_000_000), routing_policy=2))
-    bounds = [r * a.peers for r in range(world)] + [peers_total]
+    bounds = [r * peers for r in range(world)] + [peers_total]
     stepper = None
     if sharded:
         from testground_amd.shard import ShardedStepper
         stepper = ShardedStepper(eng, bounds, device=f"cuda:{local}")
     step = eng.step if stepper is None else stepper.step
-    barrier = None if stepper is None else stepper.barrier
     epoch = [0]
 
     def one_step():
-        if a.workload == "gossip":
-            eng.gen_gossip(a.window)
-            step(a.window)
-        elif a.workload == "epochs":  # traffic pre-generated; reshape + epoch + barrier
+        if workload == "gossip":
+            eng.gen_gossip(window)
+            step(window)
+        elif workload == "epochs":  # traffic pre-generated; reshape + epoch + barrier
             k = epoch[0]
             if stepper is None:
                 if k:
                     workloads.epoch_reshape(eng, peers_total, k)
-                step(a.window)  # asynchronous: the next reshape's host work overlaps this k_sim
+                step(window)  # asynchronous: the next reshape's host work overlaps this k_sim
             else:
                 # the sharded step waits for its records, so epoch k+1's ConfigureNetwork calls
                 # are staged on the host while epoch k simulates (epoch k's were staged during
                 # epoch k-1); staged configs take effect at the next launch, after the barrier below
-                stepper.step(a.window, between=lambda: workloads.epoch_reshape(eng, peers_total, k + 1))
+                stepper.step(window, between=lambda: workloads.epoch_reshape(eng, peers_total, k + 1))
             state, rnd = workloads.epoch_state(k)
-            eng.signal(state, a.peers)
-            ok = barrier(state, rnd * peers_total) if barrier else eng.barrier_poll(state, rnd * peers_total)
+            eng.signal_async(state, peers)  # K7: the count stays on the device
+            ok = stepper.barrier(state, rnd * peers_total) if stepper else eng.barrier_poll(state, rnd * peers_total)
             if not ok:
                 raise RuntimeError(f"barrier epoch-{k} did not release")
             epoch[0] += 1
         else:
-            step(a.window)
+            step(window)
 
-    if a.workload == "gossip":
-        # two empty windows, untimed: the step's buffers (two emit regions, sized for a full netem
-        # queue per source: ~64 GB at 1M peers) are allocated and first touched here, not in the
-        # timed flood; the floods start at the next window
+    if workload == "gossip":
+        # two empty windows, untimed: the step's buffers are allocated and first touched here, not
+        # in the timed flood; the floods start at the next window
         for _ in range(2):
-            step(a.window)
+            step(window)
         eng.gossip_init(n_floods=a.floods, degree=8, msg_len=1024, start_gap_ticks=a.flood_gap)
         settle = 0  # a flood is a transient by nature: the timed windows cover it from the start
     else:
-        settle = int(a.settle_ms * 1000 / a.window + 0.999)
+        settle = int(a.settle_ms * 1000 / window + 0.999)
         for _ in range(settle):  # untimed: bring every netem queue to its sustained state
-            eng.gen_storm(a.lam, a.window)
+            eng.gen_storm(lam, window)
             one_step()
-        for _ in range(a.warmup + a.steps):
-            eng.gen_storm(a.lam, a.window)  # inputs resident in HBM before the timed region
+        for _ in range(warmup + steps):
+            eng.gen_storm(lam, window)  # inputs resident in HBM before the timed region
+
     def run_steps(n):
-        if stepper is not None and a.workload == "storm":  # pre-generated: simulate one step ahead
-            stepper.run(n, a.window)
+        if stepper is not None and workload == "storm":  # pre-generated: simulate one step ahead
+            stepper.run(n, window)
         else:
             for _ in range(n):
                 one_step()
 
-    if stepper is not None and a.workload == "storm" and not a.exact_exchange:
+    if stepper is not None and workload == "storm" and not a.exact_exchange:
         # fixed-size exchange for the pipelined run: per-rank chunks sized from the largest count
         # the settle steps exchanged (max over ranks) plus a margin; an overflow fails the run
         m = torch.tensor([stepper.max_count], dtype=torch.int64, device=f"cuda:{local}")
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
         stepper.slot_cap = int(int(m.item()) * 1.25) + 4096
-    run_steps(a.warmup)
+    run_steps(warmup)
     eng.drain()
+    setup_s = time.perf_counter() - t_setup
     s0 = eng.stats()
+    x0 = stepper.exchanged_records if stepper is not None else 0
     eng.sim_kernel_ms(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(a.steps)
+    run_steps(steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -285,68 +329,131 @@ def main():
     s1 = eng.stats()
     offered = s1["offered"] - s0["offered"]
     scheduled = s1["scheduled"] - s0["scheduled"]
+    verd = np.array([s1["by_verdict"][k] - s0["by_verdict"][k] for k in abi.VERDICT_NAMES], dtype=np.float64)
+    exch = (stepper.exchanged_records - x0) if stepper is not None else 0
     sim_ms, n_launch = eng.sim_kernel_ms()
     if dist:
-        t = torch.tensor([el, float(offered)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el, float(offered), float(scheduled), float(exch), *verd], dtype=torch.float64,
+                         device=f"cuda:{local}")
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         el = float(mx[0])
-        offered_all = float(t[1])
+        offered_all, scheduled_all, exch_all = float(t[1]), float(t[2]), float(t[3])
+        verd_all = t[4:].cpu().numpy()
     else:
-        offered_all = float(offered)
+        offered_all, scheduled_all, exch_all, verd_all = float(offered), float(scheduled), 0.0, verd
     extra = {}
-    if a.workload == "gossip":
+    if workload == "gossip":
         reached = eng.gossip_reached()
         if dist:
-            r = torch.as_tensor(reached.astype(np.int64), device="cuda")
+            r = torch.as_tensor(reached.astype(np.int64), device=f"cuda:{local}")
             dist.all_reduce(r)
             reached = r.cpu().numpy()
         extra = {"floods": a.floods, "flood_gap_ticks": a.flood_gap,
                  "reached_min_frac": float(reached.min()) / peers_total,
-                 "sim_ms_covered": (a.warmup + a.steps) * a.window / 1000}
-    if rank != 0:
-        dist.destroy_process_group()
-        return
+                 "sim_ms_covered": (warmup + steps) * window / 1000}
     qbytes = s1["queue_state_bytes"] - s0["queue_state_bytes"]
-    per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled + qbytes) / max(1, a.steps) + B_SOURCE * a.peers
+    slot_cap = stepper.slot_cap if stepper is not None else None
+    eng.close()
+    del eng, stepper
+    if rank != 0:
+        return None
+    per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled + qbytes) / max(1, steps) + B_SOURCE * peers
     achieved = per_launch / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else None
+    traffic, traffic_src = load_pmc(workload, window, peers, lam)
+    tot_v = max(1.0, float(verd_all.sum()))
     res = {
         "metric": METRIC,
         "value": offered_all / el,
         "unit": "packets/s",
         "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": el * 1e3 / a.steps,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": el * 1e3 / steps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
-        "data": f"synthetic (device-generated {a.workload} traffic, Philox-keyed)",
-        "config": dict({"workload": WORKLOAD_NAMES[a.workload],
-                        "peers_per_gpu": a.peers, "peers_total": peers_total, "lambda_per_tick": a.lam,
-                        "tick_ns": 1000, "window_ticks": a.window, "settle_sim_ms": settle * a.window / 1000,
-                        "shapes": a.shapes if a.workload == "storm" else a.workload,
-                        "queue_limit": a.queue_limit or 1000, "packets_per_step": offered_all / a.steps,
+        "data": f"synthetic (device-generated {workload} traffic, Philox-keyed)",
+        "config": dict({"workload": WORKLOAD_NAMES[workload],
+                        "peers_per_gpu": peers, "peers_total": peers_total, "lambda_per_tick": lam,
+                        "tick_ns": 1000, "window_ticks": window, "settle_sim_ms": settle * window / 1000,
+                        "shapes": a.shapes if workload == "storm" else workload,
+                        "queue_limit": a.queue_limit or 1000, "packets_per_step": offered_all / steps,
                         "parallelism": f"peer-sharded x{world}" + (" (RCCL exchange path)" if sharded else ""),
-                        **({"exchange": "slotted" if stepper.slot_cap else "exact",
-                            "slot_cap_records": stepper.slot_cap} if stepper is not None else {})}, **extra),
+                        **({"exchange": "slotted" if slot_cap else "exact", "slot_cap_records_per_rank": slot_cap,
+                            "exchanged_bytes_per_step": (exch_all * REC / steps)} if sharded else {})}, **extra),
+        # what the packets/s hides: the verdict mix of the timed offered packets (originals + clones)
+        # and the rate of records that went through netem + HTB and were given a delivery time
+        "scheduled_per_s": scheduled_all / el,
+        "verdict_mix": {k: float(v) / tot_v for k, v in zip(abi.VERDICT_NAMES, verd_all)},
+        "setup_s": setup_s,
         "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": load_pmc(a), "algorithmic_bytes_per_launch": per_launch,
-                     "kernel_ms_avg": sim_ms, "launches": n_launch},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": per_launch, "kernel_ms_avg": sim_ms, "launches": n_launch},
         "cpu_baseline": None,
     }
-    if world == 1 and not a.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(a, peers_total)
+    if world == 1 and want_cpu:
+        res["cpu_baseline"] = cpu_baseline(a, workload, peers_total, lam, window,
+                                           a.cpu_seconds if workload != "gossip" else a.cpu_seconds / 2)
         res["cpu_baseline"]["gpu_over_cpu"] = res["value"] / res["cpu_baseline"]["value"]
         import shutil
         missing = [t for t in ("docker", "tc") if shutil.which(t) is None]
         # the reference's local:docker sidecar + netem path is timed only where it runs
         res["cpu_baseline"]["reference_docker_netem"] = (
             f"not available on this host ({', '.join(missing)} absent)" if missing else "present, not timed by bench.py")
-    os.write(json_fd, (json.dumps(res) + "\n").encode())
+    return res
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    decision = launch_decision(a.gpus, os.environ)
+    if decision == "spawn":
+        sys.exit(spawn_ranks(a.gpus, argv))
+    if decision != "run":
+        print(decision, file=sys.stderr)
+        sys.exit(2)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.launch_check:
+        line = json.dumps({"rank": rank, "world": world, "local_rank": local, "gpus": a.gpus,
+                           "launched_by_bench": os.environ.get("TGSIM_BENCH_LAUNCHED") == "1"})
+        os.write(1, (line + "\n").encode())  # one write: the ranks share the pipe
+        return
+    # the one JSON line goes to the original stdout; everything else (RCCL's version banner, library
+    # chatter) is sent to stderr so that the line stays the only thing on stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+    import torch
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1 or a.sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        import torch.distributed as dist
+        from testground_amd.shard import init_rccl
+        init_rccl(torch.device("cuda", local))
+    res = run_workload(a, a.workload, a.peers, a.steps, a.warmup, a.window, a.lam, world, rank, local, dist,
+                       want_cpu=not a.no_cpu)
+    if a.workload == "storm" and not a.no_1m:
+        # the 1M-peer half of the metric: C4 gossip over 1M peers in total, split over the ranks
+        g = run_workload(a, "gossip", a.gossip_1m_peers // world, 70, 0, 5000, a.lam, world, rank, local, dist,
+                         want_cpu=not a.no_cpu)
+        if res is not None:
+            res["at_1M_peers"] = {k: g[k] for k in ("value", "unit", "ms_per_step", "steps", "config",
+                                                    "scheduled_per_s", "verdict_mix", "setup_s", "roofline",
+                                                    "cpu_baseline")}
+            res["at_1M_peers"]["scaling"] = "strong (1M peers in total, split over the GPUs)"
+    if res is not None:
+        os.write(json_fd, (json.dumps(res) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 

@@ -16,7 +16,10 @@
  *   tgsim_drain       <- veth -> docker bridge -> peer delivery (pkg/runner/local_docker.go:706-721)
  *   tgsim_signal/
  *   tgsim_barrier     <- sync-service SignalEntry / SignalAndWait used by the handler
- *                        (pkg/sidecar/sidecar_handler.go:40-44, :75-80)
+ *                        (pkg/sidecar/sidecar_handler.go:40-44, :75-80); the counters live in
+ *                        device memory (K7), mirrored to pinned host memory for polling
+ *   TGSIM_OPT_K8S     <- K8sNetwork.ConfigureNetwork instead of DockerNetwork's
+ *                        (pkg/sidecar/k8s_network.go:114-256)
  *
  * A Go maintainer binds these with cgo.  Rules of the ABI:
  *   - plain C structs, caller-owned buffers, no exceptions across the boundary;
@@ -40,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TGSIM_ABI_VERSION 1u
+#define TGSIM_ABI_VERSION 2u
 
 /* Reserved destination id: traffic leaving the data network (the "external" routes that
  * RoutingPolicy AllowAll/DenyAll adds or removes, route.go:68-117). */
@@ -73,6 +76,12 @@ enum tgsim_verdict {
 #define TGSIM_OPT_KEEP_DELIVERIES 0x1u /* keep delivered records for tgsim_drain (default on via 0) */
 #define TGSIM_OPT_DISCARD_DELIVERIES 0x2u /* bench: sort deliveries but do not accumulate them  */
 #define TGSIM_OPT_METRICS 0x4u            /* per-instance counters and histograms (tgsim_metrics) */
+/* K8sNetwork semantics (k8s_network.go:114-256) instead of DockerNetwork's (docker_network.go:51-148):
+ * only network "default" (else "configured network is not `default`"); the first call re-creates
+ * the data link (InitializeNetwork, :85-112); Shape -> AddRules -> routing policy, the policy only
+ * on an enabled network (:246-254); connecting with an IPv6 address fails "ipv6 not supported"
+ * (:161-163), after an address change has already disconnected the instance (:142-155). */
+#define TGSIM_OPT_K8S 0x8u
 
 typedef struct {
     uint32_t abi_version;  /* = TGSIM_ABI_VERSION                                          */
@@ -106,18 +115,24 @@ typedef struct {
     uint32_t _pad;
 } tgsim_shape;
 
-/* network.Config flattened (sdk-go; fields used at docker_network.go:52-143). */
+/* network.Config flattened (sdk-go; fields used at docker_network.go:52-143, k8s_network.go:114-254).
+ * cfg.IPv4 / cfg.IPv6 are pointers in sdk-go (nil = keep the current address); has_ipv4 /
+ * has_ipv6 carry that.  A changed address (docker_network.go:77-78) disconnects and reconnects the
+ * instance: its netem/HTB qdiscs are re-created empty and packets still queued towards it at any
+ * sender are lost (they leave the sender and find no port).  LinkRule subnets are IPv4 only: an
+ * IPv6 rule subnet must be rejected by the binding, never truncated. */
 typedef struct {
     const char* network;    /* must be "default" (else "unsupported network: %s") */
     uint8_t enable;
     uint8_t routing_policy; /* enum tgsim_policy */
     uint8_t has_ipv4;
-    uint8_t _pad;
+    uint8_t has_ipv6;
     uint32_t ipv4;          /* host order; used when has_ipv4 */
     tgsim_shape shape;      /* cfg.Default */
     const tgsim_rule* rules;
     uint32_t n_rules;
     uint32_t _pad2;
+    uint8_t ipv6[16];       /* network order; used when has_ipv6 */
 } tgsim_config;
 
 /* Offered packet, host -> engine (16 B). tick is relative to the engine's current time and must
@@ -152,6 +167,11 @@ typedef struct {
     uint64_t queue_state_bytes; /* netem queue state carried across steps: 16 B per
                                    queued item + 8 B per departing item, summed at
                                    every step start and end (the HBM round trip)   */
+    uint64_t flushed;         /* queued/departing items lost when their sender's data
+                                 link was removed (disconnect, re-addressing)       */
+    uint64_t lost_in_flight;  /* records served by HTB whose destination had been
+                                 disconnected or re-addressed after they were
+                                 queued (no delivery)                               */
 } tgsim_stats_t;
 
 /* Closed-loop gossip flood workload, generated and consumed on the device.
@@ -270,10 +290,21 @@ int tgsim_gen_gossip(void* engine, uint32_t n_ticks);
 int64_t tgsim_gossip_reached(void* engine, uint64_t* out, size_t cap);
 
 /* ---- sync counters (sync-service SignalEntry / Barrier) ------------------------------------ */
-/* Increments state `state` (0..1023) by n and returns the new value (1-based sequence). */
+/* K7: TGSIM_SYNC_STATES u64 counters in device memory, incremented by a kernel on the engine's sync
+ * stream (never behind a queued simulation) that also writes the new value into a pinned host
+ * mirror, so polling a barrier reads host memory and never calls the device. */
+#define TGSIM_SYNC_STATES 65536u
+/* Increments state `state` by n and returns the new value (1-based sequence, SignalEntry). */
 int64_t tgsim_signal(void* engine, uint32_t state, uint32_t n);
-/* Returns 1 when the state's count >= target, 0 otherwise. */
+/* tgsim_signal without waiting for (or returning) the new value: bulk signals such as n instances
+ * entering a barrier at once.  0 on success. */
+int tgsim_signal_async(void* engine, uint32_t state, uint32_t n);
+/* Returns 1 when the state's count >= target, 0 otherwise (after every signal issued so far). */
 int tgsim_barrier_poll(void* engine, uint32_t state, uint64_t target);
+/* The device counter table (TGSIM_SYNC_STATES u64, device memory) for a collective over the
+ * shards (the sum over ranks is the global count); `event` (a hipEvent_t, may be null) is recorded
+ * on the sync stream after every signal issued so far, for the collective's stream to wait on. */
+int tgsim_sync_counters(void* engine, void** d_table, uint32_t* n_states, void* event);
 
 /* ---- metrics (the plans' runenv counters/histograms, pkg/metrics viewer.go:46) ---- */
 /* With TGSIM_OPT_METRICS, every step folds per-instance counters and log2 histograms on the

@@ -10,7 +10,10 @@
  *   rule semantics       link.go:187-217 (Accept deletes, Reject=prohibit, Drop=blackhole,
  *                        cumulative across configs, rule LinkShape ignored)
  *   routing policy       route.go:102-117 (AllowAll enables external routes, anything else denies)
- *   order of operations  docker_network.go:51-148
+ *   order of operations  docker_network.go:51-148 (docker), k8s_network.go:114-256 (TGSIM_OPT_K8S)
+ *   link removal         NetworkDisconnect / CNI DelNetworkList drop the link with its qdiscs
+ *                        (docker_network.go:65-75, :84-87; k8s_network.go:134, :151): queued
+ *                        items are lost, packets queued towards the instance find no port
  *   per-packet enqueue   Linux sch_netem.c netem_enqueue (dup -> loss -> clone -> corrupt ->
  *                        limit -> reorder/delay), tabledist uniform branch, get_crandom [ext]
  *   token bucket         Linux sch_htb.c class tokens + psched_ratecfg_precompute/l2t_ns [ext]
@@ -196,6 +199,9 @@ typedef struct {
     source* src;
     uint8_t* enabled;
     uint32_t* ip;
+    uint8_t* ip6_set;   /* the link carries an IPv6 address (cfg.IPv6 was given at connect) */
+    uint8_t (*ip6)[16];
+    uint8_t* k8s_init;  /* K8sNetwork.initialized, per instance (k8s_network.go:119-125) */
     uint32_t key[2];
     uint64_t now_tick;
     offered* off;
@@ -211,7 +217,7 @@ typedef struct {
     tgsim_delivery* step_out;
     size_t n_step, cap_step;
     tgsim_stats_t st;
-    uint64_t counters[1024];
+    uint64_t counters[TGSIM_SYNC_STATES];
     uint32_t* gen_seq;
     /* gossip workload (C4): receipt tick per (local peer, flood), forwarded-flood bitmask */
     int gossip_on;
@@ -304,6 +310,9 @@ int tgo_create(const tgsim_opts* opts, void** out) {
     o->enabled = (uint8_t*)malloc(o->o.n_peers);
     memset(o->enabled, 1, o->o.n_peers); /* containers start attached (local_docker.go:459) */
     o->ip = (uint32_t*)malloc(sizeof(uint32_t) * o->o.n_peers);
+    o->ip6_set = (uint8_t*)calloc(o->o.n_peers, 1);
+    o->ip6 = calloc(o->o.n_peers, 16);
+    o->k8s_init = (uint8_t*)calloc(o->o.n_peers, 1);
     for (uint32_t i = 0; i < o->o.n_peers; ++i) o->ip[i] = o->o.subnet_base + 2 + i;
     o->gen_seq = (uint32_t*)calloc(o->nsrc, sizeof(uint32_t));
     o->metrics_on = (o->o.flags & TGSIM_OPT_METRICS) != 0;
@@ -331,6 +340,7 @@ void tgo_destroy(void* p) {
     for (size_t i = 0; i < o->gq_n; ++i) free(o->gq[i].pk);
     free(o->gq);
     free(o->src); free(o->enabled); free(o->ip); free(o->off); free(o->verdicts);
+    free(o->ip6_set); free(o->ip6); free(o->k8s_init);
     free(o->out); free(o->step_out); free(o->gen_seq); free(o->g_first); free(o->g_fwd);
     free(o->m_src); free(o->m_dst);
     free(o);
@@ -375,28 +385,47 @@ static int add_rules(oracle* o, source* S, const tgsim_rule* rules, uint32_t n) 
     return 0;
 }
 
-int tgo_configure(void* p, uint32_t peer, const tgsim_config* cfg) {
-    oracle* o = (oracle*)p;
-    if (!o || !cfg) return -EINVAL;
-    if (peer >= o->o.n_peers) return fail(o, -EINVAL, "peer %u out of range", peer);
-    const char* net = cfg->network ? cfg->network : "";
-    if (strcmp(net, "default") != 0) return fail(o, -EINVAL, "unsupported network: %s", net);
-    int owned = peer >= o->o.shard_begin && peer < o->o.shard_end;
-    source* S = owned ? &o->src[peer - o->o.shard_begin] : NULL;
-    if (S) S->allow_ext = cfg->routing_policy == TGSIM_ALLOW_ALL; /* route.go:102-117 */
-    if (!cfg->enable) {                                         /* docker_network.go:65-75 */
-        o->enabled[peer] = 0;
-        return 0;
+#define DEAD_DST 0xFFFFFFFFu /* queued item whose destination link went away (never a real queued dst) */
+
+/* The instance's data link is removed: its HTB/netem qdiscs die with what they hold, and every
+ * packet still waiting in some sender's netem queue towards it will leave into a missing port. */
+static void link_down(oracle* o, uint32_t peer) {
+    o->enabled[peer] = 0;
+    if (peer >= o->o.shard_begin && peer < o->o.shard_end) {
+        source* S = &o->src[peer - o->o.shard_begin];
+        o->st.flushed += S->heap_n + S->ring_n;
+        S->heap_n = 0;
+        S->ring_n = 0;
+        S->ring_head = 0;
     }
-    int reconnect = !o->enabled[peer] || (cfg->has_ipv4 && cfg->ipv4 != o->ip[peer]);
-    if (cfg->has_ipv4) o->ip[peer] = cfg->ipv4;
+    for (uint32_t s = 0; s < o->nsrc; ++s)
+        for (uint32_t k = 0; k < o->src[s].heap_n; ++k)
+            if (o->src[s].heap[k].dst == peer) o->src[s].heap[k].dst = DEAD_DST;
+}
+
+/* A new data link: NetworkConnect / CNI AddNetworkList with the requested addresses, then
+ * NewNetlinkLink's fresh HTB class and netem qdisc. */
+static void link_up(oracle* o, uint32_t peer, const tgsim_config* cfg) {
     o->enabled[peer] = 1;
-    if (!S) return 0;
-    uint32_t s = peer - o->o.shard_begin;
-    if (reconnect) reset_netem(o, s); /* NewNetlinkLink: fresh HTB class + netem qdisc */
-    /* link.Shape (docker_network.go:139) */
+    if (cfg->has_ipv4) o->ip[peer] = cfg->ipv4;
+    o->ip6_set[peer] = cfg->has_ipv6 != 0;
+    if (cfg->has_ipv6) memcpy(o->ip6[peer], cfg->ipv6, 16);
+    if (peer >= o->o.shard_begin && peer < o->o.shard_end) {
+        uint32_t s = peer - o->o.shard_begin;
+        source* S = &o->src[s];
+        o->st.flushed += S->heap_n + S->ring_n;
+        S->heap_n = 0;
+        S->ring_n = 0;
+        S->ring_head = 0;
+        reset_netem(o, s);
+    }
+}
+
+/* link.Shape (link.go:155-183) with netem_change's handling of absent attributes. */
+static void shape_link(oracle* o, uint32_t peer, const tgsim_shape* shape) {
+    source* S = &o->src[peer - o->o.shard_begin];
     cshape c;
-    compile_shape(&cfg->shape, &c);
+    compile_shape(shape, &c);
     S->shape_epoch++;
     uint32_t ctr[4] = {peer, 0xFFFFFFFEu, S->shape_epoch, 3}, rnd[4]; /* init_crandom: last = random */
     tgo_philox4x32_10(ctr, o->key, rnd);
@@ -411,8 +440,69 @@ int tgo_configure(void* p, uint32_t peer, const tgsim_config* cfg) {
     S->mult = c.mult;
     S->shift = c.shift;
     S->burst_ns = c.burst_ns;
-    /* link.AddRules (docker_network.go:143) */
-    return add_rules(o, S, cfg->rules, cfg->n_rules);
+}
+
+static int owned_peer(const oracle* o, uint32_t peer) { return peer >= o->o.shard_begin && peer < o->o.shard_end; }
+
+static void routing_policy(oracle* o, uint32_t peer, uint8_t policy) { /* route.go:102-117 */
+    if (owned_peer(o, peer)) o->src[peer - o->o.shard_begin].allow_ext = policy == TGSIM_ALLOW_ALL;
+}
+
+static int ipv4_differs(const oracle* o, uint32_t peer, const tgsim_config* cfg) {
+    return cfg->has_ipv4 && cfg->ipv4 != o->ip[peer];
+}
+
+int tgo_configure(void* p, uint32_t peer, const tgsim_config* cfg) {
+    oracle* o = (oracle*)p;
+    if (!o || !cfg) return -EINVAL;
+    if (peer >= o->o.n_peers) return fail(o, -EINVAL, "peer %u out of range", peer);
+    const char* net = cfg->network ? cfg->network : "";
+    int online;
+    if (!(o->o.flags & TGSIM_OPT_K8S)) {
+        /* DockerNetwork.ConfigureNetwork, docker_network.go:51-148 */
+        if (strcmp(net, "default") != 0) return fail(o, -EINVAL, "unsupported network: %s", net);
+        routing_policy(o, peer, cfg->routing_policy); /* :57 */
+        online = o->enabled[peer];
+        if (!cfg->enable) { /* :65-75 */
+            if (online) link_down(o, peer);
+            return 0;
+        }
+        int v6 = cfg->has_ipv6 && (!o->ip6_set[peer] || memcmp(o->ip6[peer], cfg->ipv6, 16) != 0);
+        if (online && (v6 || ipv4_differs(o, peer, cfg))) { /* :77-88 */
+            link_down(o, peer);
+            online = 0;
+        }
+        if (!online) link_up(o, peer, cfg); /* :90-137 */
+        if (!owned_peer(o, peer)) return 0;
+        shape_link(o, peer, &cfg->shape);                                                /* :139 */
+        return add_rules(o, &o->src[peer - o->o.shard_begin], cfg->rules, cfg->n_rules); /* :143 */
+    }
+    /* K8sNetwork.ConfigureNetwork, k8s_network.go:114-256 */
+    if (strcmp(net, "default") != 0) return fail(o, -EINVAL, "configured network is not `default`");
+    if (!o->k8s_init[peer]) { /* :119-125, InitializeNetwork removes the pod's original address */
+        o->k8s_init[peer] = 1;
+        if (o->enabled[peer]) link_down(o, peer);
+    }
+    online = o->enabled[peer];
+    if (!cfg->enable) { /* :130-140 */
+        if (online) link_down(o, peer);
+        return 0;
+    }
+    if (online && (cfg->has_ipv6 || ipv4_differs(o, peer, cfg))) { /* :142-155, links hold no IPv6 */
+        link_down(o, peer);
+        online = 0;
+    }
+    if (!online) {
+        if (cfg->has_ipv6) return fail(o, -EAFNOSUPPORT, "ipv6 not supported"); /* :161-163 */
+        link_up(o, peer, cfg);
+    }
+    if (owned_peer(o, peer)) {
+        shape_link(o, peer, &cfg->shape); /* :246-248 */
+        int rc = add_rules(o, &o->src[peer - o->o.shard_begin], cfg->rules, cfg->n_rules); /* :249-251 */
+        if (rc) return rc;
+    }
+    routing_policy(o, peer, cfg->routing_policy); /* :252-254 */
+    return 0;
 }
 
 int tgo_submit(void* p, const tgsim_pkt* pkts, size_t n) {
@@ -538,6 +628,10 @@ static void htb_until(oracle* o, uint32_t s, uint64_t horizon) {
         S->tat = base + (((uint64_t)it.len * S->mult) >> S->shift);
         S->ring[(S->ring_head + S->ring_n) % HCAP] = d;
         S->ring_n++;
+        if (it.dst == DEAD_DST) { /* leaves the sender, finds no port */
+            o->st.lost_in_flight++;
+            continue;
+        }
         o->step_out = (tgsim_delivery*)grow(o->step_out, &o->cap_step, o->n_step + 1, sizeof(tgsim_delivery));
         tgsim_delivery* r = &o->step_out[o->n_step++];
         r->t_ns = d;
@@ -902,15 +996,30 @@ int tgo_stats(void* p, tgsim_stats_t* out) {
 
 int64_t tgo_signal(void* p, uint32_t state, uint32_t n) {
     oracle* o = (oracle*)p;
-    if (state >= 1024) return -EINVAL;
+    if (!o || state >= TGSIM_SYNC_STATES) return -EINVAL;
     o->counters[state] += n;
     return (int64_t)o->counters[state];
 }
 
+int tgo_signal_async(void* p, uint32_t state, uint32_t n) {
+    int64_t v = tgo_signal(p, state, n);
+    return v < 0 ? (int)v : 0;
+}
+
 int tgo_barrier_poll(void* p, uint32_t state, uint64_t target) {
     oracle* o = (oracle*)p;
-    if (state >= 1024) return -EINVAL;
+    if (!o || state >= TGSIM_SYNC_STATES) return -EINVAL;
     return o->counters[state] >= target;
+}
+
+/* Host memory here: the table the sharded barrier sums over the ranks. */
+int tgo_sync_counters(void* p, void** table, uint32_t* n_states, void* event) {
+    oracle* o = (oracle*)p;
+    (void)event;
+    if (!o || !table || !n_states) return -EINVAL;
+    *table = o->counters;
+    *n_states = TGSIM_SYNC_STATES;
+    return 0;
 }
 
 /* ------------------------------------------------------------------------------------------ */

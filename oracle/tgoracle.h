@@ -49,6 +49,8 @@ int64_t tgo_verdicts(void* o, uint8_t* out, size_t cap);
 int tgo_stats(void* o, tgsim_stats_t* out);
 int64_t tgo_signal(void* o, uint32_t state, uint32_t n);
 int tgo_barrier_poll(void* o, uint32_t state, uint64_t target);
+int tgo_signal_async(void* o, uint32_t state, uint32_t n);
+int tgo_sync_counters(void* o, void** table, uint32_t* n_states, void* event);
 int tgo_gossip_init(void* o, const tgsim_gossip* g);
 int tgo_gen_gossip(void* o, uint32_t n_ticks);
 int64_t tgo_gossip_reached(void* o, uint64_t* out, size_t cap);

@@ -11,7 +11,7 @@ ok() { # rc 0 = pass, 1 = test failures (keep going), anything else = stop
 }
 STEPS="${STEPS:-all}"
 if [[ "$STEPS" == *test* || "$STEPS" == all ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
   ok $? pytest; tail -30 gpurun_out/pytest_gpu.log
 fi
 if [[ "$STEPS" == *smoke* || "$STEPS" == all ]]; then

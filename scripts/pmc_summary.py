@@ -6,8 +6,13 @@ read).  Only the last `steps` k_sim dispatches (the bench's timed steps) are ave
 import csv
 import glob
 import json
+import hashlib
+import subprocess
 import sys
 from collections import defaultdict
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
 
 root, steps = sys.argv[1], int(sys.argv[2])
 vals = defaultdict(dict)
@@ -25,5 +30,9 @@ out = {"kernel": "tgsim::k_sim", "counters_avg_per_launch": avg,
        "hbm_bytes_per_launch": (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)) * 1024
        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg else None,
        "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 64 B per 128 B request)",
-       "peers": int(sys.argv[3]), "lam": float(sys.argv[4]), "window": int(sys.argv[5])}
+       "peers": int(sys.argv[3]), "lam": float(sys.argv[4]), "window": int(sys.argv[5]),
+       # provenance: bench.py reports this traffic only for the same k_sim source and configuration
+       "kernel_sha16": hashlib.sha256((REPO / "testground_amd/csrc/tgsim_kernels.hip").read_bytes()).hexdigest()[:16],
+       "commit": subprocess.run(["git", "-C", str(REPO), "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                text=True).stdout.strip() or None}
 print(json.dumps(out, indent=1))

@@ -5,7 +5,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 EXTERNAL = 0xFFFFFFFF
 
 # enum tgsim_verdict
@@ -19,6 +19,8 @@ FLAG_CORRUPT = 0x2
 
 OPT_DISCARD_DELIVERIES = 0x2
 OPT_METRICS = 0x4
+OPT_K8S = 0x8           # K8sNetwork.ConfigureNetwork semantics (k8s_network.go:114-256)
+SYNC_STATES = 65536     # K7 device sync counters
 METRICS_SRC, METRICS_DST, METRICS_HIST = 0, 1, 2
 METRICS_SRC_WORDS, METRICS_DST_WORDS, METRICS_BINS = 12, 2, 64
 # columns of the per-instance source table (include/tgsim.h TGSIM_METRICS_SRC)
@@ -67,12 +69,13 @@ class Config(C.Structure):
         ("enable", C.c_uint8),
         ("routing_policy", C.c_uint8),
         ("has_ipv4", C.c_uint8),
-        ("_pad", C.c_uint8),
+        ("has_ipv6", C.c_uint8),
         ("ipv4", C.c_uint32),
         ("shape", Shape),
         ("rules", C.POINTER(Rule)),
         ("n_rules", C.c_uint32),
         ("_pad2", C.c_uint32),
+        ("ipv6", C.c_uint8 * 16),
     ]
 
 
@@ -86,6 +89,8 @@ class Stats(C.Structure):
         ("bytes_scheduled", C.c_uint64),
         ("now_tick", C.c_uint64),
         ("queue_state_bytes", C.c_uint64),
+        ("flushed", C.c_uint64),
+        ("lost_in_flight", C.c_uint64),
     ]
 
 
@@ -107,11 +112,11 @@ SHAPE_DTYPE = np.dtype([("latency_ns", "<i8"), ("jitter_ns", "<i8"), ("bandwidth
                         ("corrupt", "<f4"), ("corrupt_corr", "<f4"), ("reorder", "<f4"), ("reorder_corr", "<f4"),
                         ("duplicate", "<f4"), ("duplicate_corr", "<f4"), ("_pad", "<u4")])
 CONFIG_DTYPE = np.dtype([("network", "<u8"), ("enable", "u1"), ("routing_policy", "u1"), ("has_ipv4", "u1"),
-                         ("_pad", "u1"), ("ipv4", "<u4"), ("shape", SHAPE_DTYPE), ("rules", "<u8"),
-                         ("n_rules", "<u4"), ("_pad2", "<u4")])
-assert SHAPE_DTYPE.itemsize == 56 and CONFIG_DTYPE.itemsize == 88
+                         ("has_ipv6", "u1"), ("ipv4", "<u4"), ("shape", SHAPE_DTYPE), ("rules", "<u8"),
+                         ("n_rules", "<u4"), ("_pad2", "<u4"), ("ipv6", "u1", (16,))])
+assert SHAPE_DTYPE.itemsize == 56 and CONFIG_DTYPE.itemsize == 104
 assert PKT_DTYPE.itemsize == 16 and DELIVERY_DTYPE.itemsize == 24
-assert C.sizeof(Gossip) == 24 and C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56 and C.sizeof(Config) == 88
+assert C.sizeof(Gossip) == 24 and C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56 and C.sizeof(Config) == 104
 
 # Every symbol include/tgsim.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -122,7 +127,7 @@ EXPORTS = [
     "tgsim_step_sim_counts", "tgsim_delivery_event", "tgsim_step_sim_launch_slotted", "tgsim_step_sim_release",
     "tgsim_deliver_slotted_async",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
-    "tgsim_signal", "tgsim_barrier_poll", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
+    "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
 ]
 
@@ -166,6 +171,8 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("stats", C.c_int, vp, C.POINTER(Stats))
     f("signal", C.c_int64, vp, C.c_uint32, C.c_uint32)
     f("barrier_poll", C.c_int, vp, C.c_uint32, C.c_uint64)
+    f("signal_async", C.c_int, vp, C.c_uint32, C.c_uint32)
+    f("sync_counters", C.c_int, vp, C.POINTER(vp), C.POINTER(C.c_uint32), vp)
     f("sim_kernel_ms", C.c_double, vp, C.POINTER(C.c_uint64), C.c_int)
     f("stream", vp, vp)
     f("debug_stamps", C.c_int64, vp, C.c_void_p, C.c_size_t)

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <map>
 #include <numeric>
@@ -230,10 +231,23 @@ struct tgsim_engine_s {
   std::vector<uint8_t> enabled;
   uint32_t n_disabled = 0;  // peers with Enable=false (0 lets k_sim skip the enabled[dst] gather)
   std::vector<uint32_t> ip;
+  std::vector<uint8_t> ip6_set;                 // an IPv6 address was assigned (cfg.IPv6 != nil)
+  std::vector<std::array<uint8_t, 16>> ip6;
+  std::vector<uint8_t> k8s_init;                // K8sNetwork.initialized (k8s_network.go:119-125)
+  std::vector<uint8_t> gone;                    // link removed since the last step (purge pending)
+  bool any_gone = false;
+  DevBuf<uint8_t> d_gone;
   std::vector<HostSrc> src;
   bool peers_dirty = true, rules_dirty = true, any_patch = false, params_dirty = true;
-  std::vector<uint32_t> counters = std::vector<uint32_t>(kStates, 0);
-  std::vector<uint64_t> counters64 = std::vector<uint64_t>(kStates, 0);
+  // K7 sync counters: device table, pinned host mirror, pinned result/marker words, own stream
+  hipStream_t sy_st = nullptr;
+  hipEvent_t ev_sig = nullptr;  // after the last issued signal
+  DevBuf<unsigned long long> d_sync;
+  uint64_t* h_mirror = nullptr;
+  uint64_t* dm_mirror = nullptr;
+  uint64_t* h_sig = nullptr;    // [0] result of the last signal, [1] marker
+  uint64_t* dm_sig = nullptr;
+  uint64_t sig_seq = 0;
 
   DevBuf<SrcParams> d_params;
   DevBuf<SrcState> d_state;
@@ -334,13 +348,194 @@ void reset_source(Eng* E, uint32_t s) {
   h.p.rule_n = keep_n;
   h.p.thr_cor = 0;
   h.p.rho_dup = h.p.rho_cor = h.p.rho_reo = 0;
-  h.patch_mask |= 1u | 2u | 4u | 8u;
+  h.patch_mask |= 1u | 2u | 4u | 8u | 16u;
   h.last[0] = h.last[1] = h.last[2] = 0;
   h.dirty = true;
   E->any_patch = true;
 }
 
+bool owns(const Eng* E, uint32_t peer) { return peer >= E->o.shard_begin && peer < E->o.shard_end; }
+
+// The instance's data link goes away (NetworkDisconnect, docker_network.go:65-75 and :84-87; CNI
+// DelNetworkList, k8s_network.go:134 and :151): its qdiscs die with whatever they held (flushed at
+// the next step), and packets still queued towards it at any sender will find no port (k_purge at
+// the next step marks them dead).  Every shard applies this to its replicated peer tables.
+void link_down(Eng* E, uint32_t peer) {
+  if (E->enabled[peer]) {
+    E->enabled[peer] = 0;
+    E->n_disabled++;
+    E->peers_dirty = true;
+  }
+  E->gone[peer] = 1;
+  E->any_gone = true;
+  if (owns(E, peer)) {
+    HostSrc& h = E->src[peer - E->o.shard_begin];
+    h.patch_mask |= 16u;
+    h.dirty = true;
+    E->any_patch = true;
+  }
+}
+
+// A new data link (NetworkConnect + NewNetlinkLink, docker_network.go:90-137; CNI AddNetworkList,
+// k8s_network.go:158-244): fresh HTB class and netem qdisc, the requested addresses.
+void link_up(Eng* E, uint32_t peer, const tgsim_config* cfg) {
+  if (!E->enabled[peer]) {
+    E->enabled[peer] = 1;
+    E->n_disabled--;
+    E->peers_dirty = true;
+  }
+  if (cfg->has_ipv4 && cfg->ipv4 != E->ip[peer]) {
+    E->ip[peer] = cfg->ipv4;
+    E->peers_dirty = true;
+  }
+  E->ip6_set[peer] = cfg->has_ipv6 ? 1 : 0;  // IPAMConfig.IPv6Address only when cfg.IPv6 != nil
+  if (cfg->has_ipv6) memcpy(E->ip6[peer].data(), cfg->ipv6, 16);
+  if (owns(E, peer)) reset_source(E, peer - E->o.shard_begin);
+}
+
+// link.Shape (link.go:155-183): HTB ClassChange + netem QdiscChange (netem_change semantics).
+void apply_shape(Eng* E, uint32_t peer, const tgsim_shape& shape) {
+  HostSrc& h = E->src[peer - E->o.shard_begin];
+  const Compiled c = compile_shape(shape);
+  h.shape_epoch++;
+  uint32_t rnd[4];
+  philox_host(peer, 0xFFFFFFFEu, h.shape_epoch, 3, E->key0, E->key1, rnd);  // init_crandom()
+  h.p.lat_ns = c.p.lat_ns;
+  h.p.sigma = c.p.sigma;
+  h.p.thr_loss = c.p.thr_loss;
+  h.p.thr_dup = c.p.thr_dup;
+  h.p.thr_reo = c.p.thr_reo;
+  h.p.burst_ns = c.p.burst_ns;
+  h.p.mult = c.p.mult;
+  h.p.shift_ext = c.p.shift_ext;
+  if (c.corr_attr) {
+    h.p.rho_dup = c.rho_dup_new;
+    h.last[0] = rnd[0];
+    h.patch_mask |= 1u;
+  }
+  if (c.corrupt_attr) {  // absent attribute: q->corrupt and its correlation persist
+    h.p.thr_cor = c.thr_cor_new;
+    h.p.rho_cor = c.rho_cor_new;
+    h.last[1] = rnd[1];
+    h.patch_mask |= 2u;
+  }
+  if (c.reorder_attr) {
+    h.p.rho_reo = c.rho_reo_new;
+    h.last[2] = rnd[2];
+    h.patch_mask |= 4u;
+  }
+  h.dirty = true;
+  E->any_patch = true;
+}
+
+// link.AddRules (link.go:187-217): cumulative; Accept deletes; host bits -> EINVAL.
+int add_rules(Eng* E, uint32_t peer, const tgsim_config* cfg) {
+  HostSrc& h = E->src[peer - E->o.shard_begin];
+  for (uint32_t i = 0; i < cfg->n_rules; ++i) {
+    const tgsim_rule& r = cfg->rules[i];
+    const bool bad_len = r.len > 32;
+    const uint32_t mask = (!bad_len && r.len) ? (0xFFFFFFFFu << (32 - r.len)) : 0u;
+    const bool bad = bad_len || (r.prefix & ~mask) != 0;
+    const uint64_t key = (static_cast<uint64_t>(r.prefix) << 8) | r.len;
+    if (r.action == TGSIM_ACCEPT) {
+      if (!bad && h.rules.erase(key)) E->rules_dirty = true;
+      continue;
+    }
+    if (r.action != TGSIM_REJECT && r.action != TGSIM_DROP)
+      return E->fail(-EINVAL, "invalid filter action %u", r.action);
+    if (bad) return E->fail(-EINVAL, "invalid argument");
+    auto it = h.rules.find(key);
+    if (it == h.rules.end() || it->second != r.action) {
+      h.rules[key] = r.action;
+      E->rules_dirty = true;
+    }
+  }
+  return 0;
+}
+
+// handleRoutingPolicy (route.go:102-117): AllowAll enables the external routes, anything else
+// (DenyAll, empty, unknown: the default case :110-112) removes them.
+void apply_policy(Eng* E, uint32_t peer, uint8_t policy) {
+  if (!owns(E, peer)) return;
+  HostSrc& h = E->src[peer - E->o.shard_begin];
+  const bool allow = policy == TGSIM_ALLOW_ALL;
+  if (allow != h.allow_ext) {
+    h.allow_ext = allow;
+    h.dirty = true;
+    E->any_patch = true;
+  }
+}
+
+bool ip_changed(const Eng* E, uint32_t peer, const tgsim_config* cfg) {
+  return cfg->has_ipv4 && cfg->ipv4 != E->ip[peer];
+}
+bool ip6_changed(const Eng* E, uint32_t peer, const tgsim_config* cfg) {
+  // a link without an IPv6 address differs from any requested one (the reference dereferences
+  // link.IPv6.IP there, docker_network.go:77)
+  return cfg->has_ipv6 && (!E->ip6_set[peer] || memcmp(E->ip6[peer].data(), cfg->ipv6, 16) != 0);
+}
+
+// DockerNetwork.ConfigureNetwork (docker_network.go:51-148).
+int configure_docker(Eng* E, uint32_t peer, const tgsim_config* cfg) {
+  const char* net = cfg->network ? cfg->network : "";
+  if (strcmp(net, "default") != 0) return E->fail(-EINVAL, "unsupported network: %s", net);
+  apply_policy(E, peer, cfg->routing_policy);  // :57, before anything else
+  bool online = E->enabled[peer] != 0;
+  if (!cfg->enable) {  // :65-75
+    if (online) link_down(E, peer);
+    return 0;
+  }
+  if (online && (ip6_changed(E, peer, cfg) || ip_changed(E, peer, cfg))) {  // :77-88
+    link_down(E, peer);
+    online = false;
+  }
+  if (!online) link_up(E, peer, cfg);  // :90-137
+  if (!owns(E, peer)) return 0;
+  apply_shape(E, peer, cfg->shape);  // :139
+  return add_rules(E, peer, cfg);    // :143
+}
+
+// K8sNetwork.ConfigureNetwork (k8s_network.go:114-256).
+int configure_k8s(Eng* E, uint32_t peer, const tgsim_config* cfg) {
+  const char* net = cfg->network ? cfg->network : "";
+  if (strcmp(net, "default") != 0) return E->fail(-EINVAL, "configured network is not `default`");  // :115-117
+  if (!E->k8s_init[peer]) {  // :119-125: InitializeNetwork deletes the address the pod came with
+    E->k8s_init[peer] = 1;
+    if (E->enabled[peer]) link_down(E, peer);
+  }
+  bool online = E->enabled[peer] != 0;
+  if (!cfg->enable) {  // :130-140 (the routing policy is left as it is)
+    if (online) link_down(E, peer);
+    return 0;
+  }
+  // :142-155; k8s links carry no IPv6 address (:238), so any requested one is a change
+  if (online && (cfg->has_ipv6 || ip_changed(E, peer, cfg))) {
+    link_down(E, peer);
+    online = false;
+  }
+  if (!online) {
+    if (cfg->has_ipv6) return E->fail(-EAFNOSUPPORT, "ipv6 not supported");  // :161-163, already disconnected
+    link_up(E, peer, cfg);
+  }
+  if (owns(E, peer)) {
+    apply_shape(E, peer, cfg->shape);           // :246-248
+    const int rc = add_rules(E, peer, cfg);     // :249-251
+    if (rc) return rc;
+  }
+  apply_policy(E, peer, cfg->routing_policy);  // :252-254, last
+  return 0;
+}
+
 int flush_config(Eng* E) {
+  if (E->any_gone) {  // packets queued towards a removed link: marked dead in every sender's queue
+    HIPCHK(E->d_gone.ensure(E->N));
+    HIPCHK(hipMemcpyAsync(E->d_gone.p, E->gone.data(), E->N, hipMemcpyHostToDevice, E->st));
+    launch_purge(E->d_heap.p, E->d_state.p, E->S, E->d_gone.p, E->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(E->st));
+    std::fill(E->gone.begin(), E->gone.end(), 0);
+    E->any_gone = false;
+  }
   if (E->peers_dirty) {
     HIPCHK(hipMemcpyAsync(E->d_enabled.p, E->enabled.data(), E->N, hipMemcpyHostToDevice, E->st));
     HIPCHK(hipMemcpyAsync(E->d_ip.p, E->ip.data(), sizeof(uint32_t) * E->N, hipMemcpyHostToDevice, E->st));
@@ -393,7 +588,8 @@ int flush_config(Eng* E) {
       HIPCHK(E->d_patch.ensure(patches.size()));
       HIPCHK(hipMemcpyAsync(E->d_patch.p, patches.data(), sizeof(CfgPatch) * patches.size(),
                             hipMemcpyHostToDevice, E->st));
-      launch_apply_cfg(E->d_patch.p, static_cast<uint32_t>(patches.size()), E->d_params.p, E->d_state.p, E->st);
+      launch_apply_cfg(E->d_patch.p, static_cast<uint32_t>(patches.size()), E->d_params.p, E->d_state.p,
+                       E->d_stats.p, E->st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(E->st));
     }
@@ -959,6 +1155,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
+  E->ip6_set.assign(E->N, 0);
+  E->ip6.resize(E->N);
+  E->k8s_init.assign(E->N, 0);
+  E->gone.assign(E->N, 0);
   E->ip.resize(E->N);
   for (uint32_t i = 0; i < E->N; ++i) E->ip[i] = E->o.subnet_base + 2 + i;
   E->src.resize(E->S);
@@ -976,6 +1176,25 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(E->d_ring.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc ring"))) return bail(rc);
   if ((rc = E->hip(E->d_gen_seq.ensure(E->S), "alloc gen_seq"))) return bail(rc);
   if ((rc = E->hip(E->d_stats.ensure(kStSlots * kStatCopies), "alloc stats"))) return bail(rc);
+  // K7 sync counters: device table, pinned mirror and result/marker words, their own stream
+  if ((rc = E->hip(hipStreamCreateWithPriority(&E->sy_st, hipStreamNonBlocking, prio_hi), "stream")))
+    return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sig, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventRecord(E->ev_sig, E->sy_st), "event"))) return bail(rc);
+  if ((rc = E->hip(E->d_sync.ensure(kStates), "alloc sync"))) return bail(rc);
+  if ((rc = E->hip(hipMemset(E->d_sync.p, 0, sizeof(unsigned long long) * kStates), "memset"))) return bail(rc);
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_mirror), sizeof(uint64_t) * kStates,
+                                 hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
+    return bail(rc);
+  memset(E->h_mirror, 0, sizeof(uint64_t) * kStates);
+  if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->dm_mirror), E->h_mirror, 0), "pinned")))
+    return bail(rc);
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_sig), 2 * sizeof(uint64_t),
+                                 hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
+    return bail(rc);
+  E->h_sig[0] = E->h_sig[1] = 0;
+  if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->dm_sig), E->h_sig, 0), "pinned")))
+    return bail(rc);
   if ((rc = E->hip(E->d_off.ensure(E->S + 1), "alloc off"))) return bail(rc);
   if ((rc = E->hip(E->d_in.ensure(1), "alloc in"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_state.p, 0, sizeof(SrcState) * E->S), "memset"))) return bail(rc);
@@ -1006,6 +1225,12 @@ void tgsim_destroy(void* e) {
   if (E->st) (void)hipStreamSynchronize(E->st);
   if (E->dst_st) (void)hipStreamSynchronize(E->dst_st);
   if (E->rt_st) (void)hipStreamSynchronize(E->rt_st);
+  if (E->sy_st) (void)hipStreamSynchronize(E->sy_st);
+  E->d_sync.release(); E->d_gone.release();
+  if (E->h_mirror) (void)hipHostFree(E->h_mirror);
+  if (E->h_sig) (void)hipHostFree(E->h_sig);
+  if (E->ev_sig) (void)hipEventDestroy(E->ev_sig);
+  if (E->sy_st) (void)hipStreamDestroy(E->sy_st);
   DevBuf<int> dummy;
   (void)dummy;
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
@@ -1045,96 +1270,13 @@ const char* tgsim_last_error(const void* e) {
   return e ? static_cast<const Eng*>(e)->err.c_str() : "null engine";
 }
 
-// DockerNetwork.ConfigureNetwork (docker_network.go:51-148), netlink replaced by staged state.
+// ConfigureNetwork with netlink replaced by staged state (applied at the next step): the docker
+// sidecar's order of operations and errors, or the k8s one with TGSIM_OPT_K8S.
 int tgsim_configure(void* e, uint32_t peer, const tgsim_config* cfg) {
   Eng* E = as_eng(e);
   if (!E || !cfg) return -EINVAL;
   if (peer >= E->N) return E->fail(-EINVAL, "peer %u out of range", peer);
-  const char* net = cfg->network ? cfg->network : "";
-  if (strcmp(net, "default") != 0) return E->fail(-EINVAL, "unsupported network: %s", net);
-  const bool owned = peer >= E->o.shard_begin && peer < E->o.shard_end;
-  const uint32_t s = peer - E->o.shard_begin;
-  if (owned) {  // handleRoutingPolicy (route.go:102-117): AllowAll enables, anything else disables
-    const bool allow = cfg->routing_policy == TGSIM_ALLOW_ALL;
-    if (allow != E->src[s].allow_ext) {
-      E->src[s].allow_ext = allow;
-      E->src[s].dirty = true;
-      E->any_patch = true;
-    }
-  }
-  if (!cfg->enable) {  // NetworkDisconnect; shape and rules untouched
-    if (E->enabled[peer]) {
-      E->enabled[peer] = 0;
-      E->n_disabled++;
-      E->peers_dirty = true;
-    }
-    return 0;
-  }
-  const bool reconnect = !E->enabled[peer] || (cfg->has_ipv4 && cfg->ipv4 != E->ip[peer]);
-  if (cfg->has_ipv4 && cfg->ipv4 != E->ip[peer]) {
-    E->ip[peer] = cfg->ipv4;
-    E->peers_dirty = true;
-  }
-  if (!E->enabled[peer]) {
-    E->enabled[peer] = 1;
-    E->n_disabled--;
-    E->peers_dirty = true;
-  }
-  if (!owned) return 0;
-  HostSrc& h = E->src[s];
-  if (reconnect) reset_source(E, s);  // NewNetlinkLink: fresh HTB class and netem qdisc
-  // link.Shape (link.go:155-183): HTB ClassChange + netem QdiscChange (netem_change semantics)
-  const Compiled c = compile_shape(cfg->shape);
-  h.shape_epoch++;
-  uint32_t rnd[4];
-  philox_host(peer, 0xFFFFFFFEu, h.shape_epoch, 3, E->key0, E->key1, rnd);  // init_crandom()
-  h.p.lat_ns = c.p.lat_ns;
-  h.p.sigma = c.p.sigma;
-  h.p.thr_loss = c.p.thr_loss;
-  h.p.thr_dup = c.p.thr_dup;
-  h.p.thr_reo = c.p.thr_reo;
-  h.p.burst_ns = c.p.burst_ns;
-  h.p.mult = c.p.mult;
-  h.p.shift_ext = c.p.shift_ext;
-  if (c.corr_attr) {
-    h.p.rho_dup = c.rho_dup_new;
-    h.last[0] = rnd[0];
-    h.patch_mask |= 1u;
-  }
-  if (c.corrupt_attr) {  // absent attribute: q->corrupt and its correlation persist
-    h.p.thr_cor = c.thr_cor_new;
-    h.p.rho_cor = c.rho_cor_new;
-    h.last[1] = rnd[1];
-    h.patch_mask |= 2u;
-  }
-  if (c.reorder_attr) {
-    h.p.rho_reo = c.rho_reo_new;
-    h.last[2] = rnd[2];
-    h.patch_mask |= 4u;
-  }
-  h.dirty = true;
-  E->any_patch = true;
-  // link.AddRules (link.go:187-217): cumulative; Accept deletes; host bits -> EINVAL
-  for (uint32_t i = 0; i < cfg->n_rules; ++i) {
-    const tgsim_rule& r = cfg->rules[i];
-    const bool bad_len = r.len > 32;
-    const uint32_t mask = (!bad_len && r.len) ? (0xFFFFFFFFu << (32 - r.len)) : 0u;
-    const bool bad = bad_len || (r.prefix & ~mask) != 0;
-    const uint64_t key = (static_cast<uint64_t>(r.prefix) << 8) | r.len;
-    if (r.action == TGSIM_ACCEPT) {
-      if (!bad && h.rules.erase(key)) E->rules_dirty = true;
-      continue;
-    }
-    if (r.action != TGSIM_REJECT && r.action != TGSIM_DROP)
-      return E->fail(-EINVAL, "invalid filter action %u", r.action);
-    if (bad) return E->fail(-EINVAL, "invalid argument");
-    auto it = h.rules.find(key);
-    if (it == h.rules.end() || it->second != r.action) {
-      h.rules[key] = r.action;
-      E->rules_dirty = true;
-    }
-  }
-  return 0;
+  return (E->o.flags & TGSIM_OPT_K8S) ? configure_k8s(E, peer, cfg) : configure_docker(E, peer, cfg);
 }
 
 int64_t tgsim_configure_batch(void* e, const uint32_t* peers, const tgsim_config* cfgs, size_t n, int32_t* rcs) {
@@ -1491,14 +1633,45 @@ int tgsim_stats(void* e, tgsim_stats_t* out) {
   out->bytes_scheduled = s[kStBytes];
   out->now_tick = E->now_tick;
   out->queue_state_bytes = s[kStQueue];
+  out->flushed = s[kStFlushed];
+  out->lost_in_flight = s[kStLost];
   return 0;
+}
+
+// K7: SignalEntry on the device counter table (sync stream; see include/tgsim.h).
+int tgsim_signal_async(void* e, uint32_t state, uint32_t n) {
+  Eng* E = as_eng(e);
+  if (!E || state >= kStates) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  launch_signal(E->d_sync.p, E->dm_mirror, state, n, E->dm_sig, E->dm_sig + 1, ++E->sig_seq, E->sy_st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(E->ev_sig, E->sy_st));
+  return 0;
+}
+
+// Waits until every signal issued so far has landed in the pinned words (no device call).
+static int signals_landed(Eng* E) {
+  if (!E->sig_seq) return 0;
+  return wait_published(E, &E->h_sig[1], E->sig_seq, E->ev_sig);
 }
 
 int64_t tgsim_signal(void* e, uint32_t state, uint32_t n) {
   Eng* E = as_eng(e);
-  if (!E || state >= kStates) return -EINVAL;
-  E->counters64[state] += n;
-  return static_cast<int64_t>(E->counters64[state]);
+  int rc = tgsim_signal_async(e, state, n);
+  if (rc) return rc;
+  rc = signals_landed(E);
+  if (rc) return rc;
+  return static_cast<int64_t>(__atomic_load_n(&E->h_sig[0], __ATOMIC_ACQUIRE));
+}
+
+int tgsim_sync_counters(void* e, void** d_table, uint32_t* n_states, void* event) {
+  Eng* E = as_eng(e);
+  if (!E || !d_table || !n_states) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  *d_table = E->d_sync.p;
+  *n_states = kStates;
+  if (event) HIPCHK(hipEventRecord(static_cast<hipEvent_t>(event), E->sy_st));
+  return 0;
 }
 
 int64_t tgsim_metrics(void* e, uint32_t kind, uint64_t* out, size_t cap) {
@@ -1519,7 +1692,9 @@ int64_t tgsim_metrics(void* e, uint32_t kind, uint64_t* out, size_t cap) {
 int tgsim_barrier_poll(void* e, uint32_t state, uint64_t target) {
   Eng* E = as_eng(e);
   if (!E || state >= kStates) return -EINVAL;
-  return E->counters64[state] >= target ? 1 : 0;
+  const int rc = signals_landed(E);
+  if (rc) return rc;
+  return __atomic_load_n(&E->h_mirror[state], __ATOMIC_ACQUIRE) >= target ? 1 : 0;
 }
 
 double tgsim_sim_kernel_ms(void* e, uint64_t* n, int reset) {

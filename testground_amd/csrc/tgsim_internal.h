@@ -19,7 +19,11 @@ constexpr uint32_t kSpw = TGSIM_SPW;
  // sources per simulate wavefront (LDS-resident queues)
 constexpr uint32_t kAhead = kWave / kSpw;  // records per source staged per batch
 constexpr uint64_t kEMask = (1ull << 46) - 1;  // eligibility time field of a queued item
-constexpr uint32_t kStates = 1024;    // sync states
+constexpr uint32_t kStates = TGSIM_SYNC_STATES;  // sync states (K7 device counters)
+// dst of a queued item whose destination disconnected or was re-addressed after it was queued
+// (k_purge): HTB still serves it (it leaves the sender), nothing is delivered.  Never a real queued
+// dst: TGSIM_EXTERNAL packets are filtered before the netem queue.
+constexpr uint32_t kDeadDst = 0xFFFFFFFFu;
 
 // Compiled netem + HTB parameters of one source (64 B, read once per step).
 struct alignas(16) SrcParams {
@@ -61,14 +65,15 @@ struct Interval {
 // Configuration delta scattered by the config-apply kernel (K9).
 struct CfgPatch {
   uint32_t s;          // shard-local source
-  uint32_t mask;       // bit0 last_dup, bit1 last_cor, bit2 last_reo, bit3 reset tat
+  uint32_t mask;       // bit0 last_dup, bit1 last_cor, bit2 last_reo, bit3 reset tat,
+                       // bit4 flush the netem queue and departure ring (link removed)
   uint32_t last_dup, last_cor, last_reo, _pad;
   SrcParams p;
 };
 
 enum StatSlot {
   kStOffered = 0, kStScheduled, kStCloned, kStCorrupted, kStVerdict0,  // 4..11 verdicts
-  kStBytes = 12, kStErr = 13, kStQueue = 14, kStSlots = 16
+  kStBytes = 12, kStErr = 13, kStQueue = 14, kStLost = 15, kStFlushed = 16, kStSlots = 20
 };
 // Counters are spread over kStatCopies copies (workgroup w adds into copy w % kStatCopies) so that
 // a million one-source workgroups do not serialize on 16 addresses; readers sum the copies.  The

@@ -255,7 +255,7 @@ struct SimQueue {
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
-  uint32_t sched, corrupted;
+  uint32_t sched, corrupted, lost;
   uint64_t bytes;
 #ifdef TGSIM_PROFILE
   uint64_t pf[16];
@@ -281,23 +281,31 @@ struct SimQueue {
   }
 
   // Commits the HTB service of the first n queue items (lanes < n): slot -> ring entry, record.
+  // An item whose destination went away while it was queued (kDeadDst, k_purge) still takes its
+  // HTB turn and its place in the ring (it leaves the sender) but emits no record.
   __device__ __forceinline__ void commit(bool c, uint32_t n, const uint4& qi, uint64_t d, uint64_t tat_after) {
+    const bool live = c && qi.w != kDeadDst;
+    const uint64_t lm = __ballot(live);
     if (c) {
       *reinterpret_cast<uint2*>(&slot(rn + lane)) = make_uint2((uint32_t)d, (uint32_t)(d >> 32));
-      const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
-      uint64_t* rw = reinterpret_cast<uint64_t*>(emit + n_emit + lane);
-      rw[0] = d;
-      rw[1] = ((uint64_t)qi.w << 32) | src;
-      rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
-      if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
-      sched++;
-      bytes += len;
-      corrupted += (flags >> 1) & 1u;
+      if (live) {
+        const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
+        uint64_t* rw = reinterpret_cast<uint64_t*>(emit + n_emit + __popcll(lm & ((1ull << lane) - 1)));
+        rw[0] = d;
+        rw[1] = ((uint64_t)qi.w << 32) | src;
+        rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
+        if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
+        sched++;
+        bytes += len;
+        corrupted += (flags >> 1) & 1u;
+      } else {
+        lost++;
+      }
     }
     tat = readlane64(tat_after, n - 1);
     rn += n;
     qn -= n;
-    n_emit += n;
+    n_emit += (uint32_t)__popcll(lm);
     wave_lds_sync();
   }
 
@@ -534,7 +542,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
-  Q.sched = Q.corrupted = 0;
+  Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
 #ifdef TGSIM_PROFILE
   for (int k = 0; k < 16; ++k) Q.pf[k] = 0;
@@ -956,6 +964,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
 #endif
   const uint32_t sched = readlane32((uint32_t)scan_sum_i32((int32_t)Q.sched), kWave - 1);
   const uint32_t corrupted = readlane32((uint32_t)scan_sum_i32((int32_t)Q.corrupted), kWave - 1);
+  const uint32_t lost = readlane32((uint32_t)scan_sum_i32((int32_t)Q.lost), kWave - 1);
   const uint64_t bytes = wave_sum(Q.bytes);
   const uint64_t qbytes = 16ull * Q.qn + 8ull * Q.rn;
   const bool err = __ballot(perr != 0) != 0;
@@ -966,6 +975,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     if (sched) atomicAdd(&sc[kStScheduled], (unsigned long long)sched);
     if (c_clone) atomicAdd(&sc[kStCloned], (unsigned long long)c_clone);
     if (corrupted) atomicAdd(&sc[kStCorrupted], (unsigned long long)corrupted);
+    if (lost) atomicAdd(&sc[kStLost], (unsigned long long)lost);
     if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
     if (err) {
@@ -1010,9 +1020,11 @@ __global__ __launch_bounds__(1024) void k_order(const uint32_t* weight, uint32_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// K9: configuration apply.
+// K9: configuration apply.  A removed data link (disconnect, re-addressing: docker_network.go:65-75,
+// :84-87) takes its qdiscs with it: the netem queue and the departure ring are emptied (mask bit 4)
+// and their items counted as flushed.
 __global__ void k_apply_cfg(const CfgPatch* __restrict__ patches, uint32_t n, SrcParams* params,
-                            SrcState* state) {
+                            SrcState* state, unsigned long long* stats) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const CfgPatch c = patches[i];
@@ -1022,7 +1034,39 @@ __global__ void k_apply_cfg(const CfgPatch* __restrict__ patches, uint32_t n, Sr
   if (c.mask & 2u) st.last_cor = c.last_cor;
   if (c.mask & 4u) st.last_reo = c.last_reo;
   if (c.mask & 8u) st.tat = 0;
+  if (c.mask & 16u) {
+    const uint32_t k = st.heap_n + st.ring_n;
+    if (k) atomicAdd(&stats[(size_t)(i % kStatCopies) * kStSlots + kStFlushed], (unsigned long long)k);
+    st.heap_n = st.ring_n = st.ring_head = 0;
+  }
   state[c.s] = st;
+}
+
+// Packets still queued (not yet served by HTB) towards a destination whose link went away at this
+// step boundary: they will leave the sender and find no port (or an address no longer in use), so
+// they are marked dead in place; the queue order and occupancy are unchanged.  One wavefront per
+// source, gone[] is per global peer.
+__global__ __launch_bounds__(256) void k_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone) {
+  const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (s >= n_src) return;
+  const uint32_t qn = state[s].heap_n;
+  uint4* q = heap + (size_t)s * kHeapCap;
+  for (uint32_t k = lane; k < qn; k += kWave) {
+    const uint32_t d = q[k].w;
+    if (d != kDeadDst && gone[d]) q[k].w = kDeadDst;
+  }
+}
+
+// K7 sync counters: table[state] += n on the device; the new value also goes to the pinned host
+// mirror (barrier polls read it there) and to the pinned result word, then the pinned marker word
+// is released with the call's sequence number (the host spins on it instead of synchronizing).
+__global__ void k_signal(unsigned long long* table, uint64_t* mirror, uint32_t state, uint32_t n, uint64_t* result,
+                         uint64_t* marker, uint64_t seq) {
+  const unsigned long long v = atomicAdd(&table[state], (unsigned long long)n) + n;
+  __hip_atomic_store(&mirror[state], (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(result, (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __hip_atomic_store(marker, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1645,9 +1689,19 @@ void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream
   hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, st, weight, n, order);
 }
 
-void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st) {
+void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state,
+                      unsigned long long* stats, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_apply_cfg, dim3((n + 255) / 256), dim3(256), 0, st, p, n, params, state);
+  hipLaunchKernelGGL(k_apply_cfg, dim3((n + 255) / 256), dim3(256), 0, st, p, n, params, state, stats);
+}
+
+void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone, hipStream_t st) {
+  if (n_src) hipLaunchKernelGGL(k_purge, dim3((n_src + 3) / 4), dim3(256), 0, st, heap, state, n_src, gone);
+}
+
+void launch_signal(unsigned long long* table, uint64_t* mirror, uint32_t state, uint32_t n, uint64_t* result,
+                   uint64_t* marker, uint64_t seq, hipStream_t st) {
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, st, table, mirror, state, n, result, marker, seq);
 }
 
 void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uint32_t* gen_seq,

@@ -27,7 +27,13 @@ struct RouteArgsHost {
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
 // no-op above kOrderMax (32768) sources
 void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream_t st);
-void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state, hipStream_t st);
+void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state,
+                      unsigned long long* stats, hipStream_t st);
+// marks queued items towards gone[dst] != 0 dead (kDeadDst)
+void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone, hipStream_t st);
+// K7: table[state] += n; new value -> mirror[state] and *result (pinned), then *marker = seq
+void launch_signal(unsigned long long* table, uint64_t* mirror, uint32_t state, uint32_t n, uint64_t* result,
+                   uint64_t* marker, uint64_t seq, hipStream_t st);
 void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uint32_t* gen_seq,
                 InRec* out, int phase, hipStream_t st);
 // phase 0: fold delivered records into receipts; 1: per-source counts; 2: write the window.

@@ -264,7 +264,7 @@ class CABIEngine:
         s = abi.Stats()
         self._check(self._fn("stats")(self._h, C.byref(s)), "stats")
         d = {k: getattr(s, k) for k in ("offered", "scheduled", "cloned", "corrupted", "bytes_scheduled", "now_tick",
-                                   "queue_state_bytes")}
+                                   "queue_state_bytes", "flushed", "lost_in_flight")}
         d["by_verdict"] = {abi.VERDICT_NAMES[i]: s.by_verdict[i] for i in range(8)}
         return d
 
@@ -272,8 +272,20 @@ class CABIEngine:
     def signal(self, state: int, n: int = 1) -> int:
         return self._check(self._fn("signal")(self._h, state, n), "signal")
 
+    def signal_async(self, state: int, n: int = 1) -> None:
+        """signal() without waiting for the new value (K7 counters stay on the device)."""
+        self._check(self._fn("signal_async")(self._h, state, n), "signal_async")
+
     def barrier_poll(self, state: int, target: int) -> bool:
         return bool(self._check(self._fn("barrier_poll")(self._h, state, target), "barrier_poll"))
+
+    def sync_counters(self, event: int = 0) -> Tuple[int, int]:
+        """(address, states) of the sync counter table (device memory on the HIP engine, host
+        memory on the oracle); `event` (a raw hipEvent_t) is recorded after every issued signal."""
+        ptr, n = C.c_void_p(), C.c_uint32()
+        self._check(self._fn("sync_counters")(self._h, C.byref(ptr), C.byref(n), C.c_void_p(event or None)),
+                    "sync_counters")
+        return int(ptr.value or 0), int(n.value)
 
     # -- instrumentation -----------------------------------------------------------------------
     def sim_kernel_ms(self, reset: bool = False) -> Tuple[float, int]:

@@ -56,14 +56,29 @@ IPNetLike = Union[str, ipaddress.IPv4Interface, ipaddress.IPv4Network, tuple]
 
 def _ipnet(x: IPNetLike) -> tuple:
     """Returns (address as int, prefix length) without masking host bits (the kernel rejects
-    routes whose prefix carries host bits; the engine reproduces that error)."""
+    routes whose prefix carries host bits; the engine reproduces that error).  IPv4 only: the
+    engine's rules are IPv4 prefixes, and an IPv6 subnet is refused here rather than truncated."""
     if isinstance(x, tuple):
         ip, plen = x
-        return int(ipaddress.IPv4Address(ip)), int(plen)
-    if isinstance(x, ipaddress.IPv4Network):
+        a = ipaddress.ip_address(ip)
+        if a.version != 4:
+            raise ValueError(f"IPv6 subnet {ip}/{plen}: link rules are IPv4 only")
+        return int(a), int(plen)
+    if isinstance(x, (ipaddress.IPv4Network, ipaddress.IPv6Network)):
+        if x.version != 4:
+            raise ValueError(f"IPv6 subnet {x}: link rules are IPv4 only")
         return int(x.network_address), x.prefixlen
-    iface = ipaddress.IPv4Interface(x)
+    iface = ipaddress.ip_interface(x)
+    if iface.version != 4:
+        raise ValueError(f"IPv6 subnet {x}: link rules are IPv4 only")
     return int(iface.ip), iface.network.prefixlen
+
+
+def _ipv6(x) -> bytes:
+    """cfg.IPv6 (an address or interface string, or an IPv6Address/Interface) -> 16 bytes."""
+    if isinstance(x, (ipaddress.IPv6Address, ipaddress.IPv6Interface)):
+        return (x.ip if isinstance(x, ipaddress.IPv6Interface) else x).packed
+    return ipaddress.IPv6Interface(x).ip.packed
 
 
 @dataclasses.dataclass
@@ -76,7 +91,7 @@ class LinkRule:
 class Config:
     Network: str = ""
     IPv4: Optional[IPNetLike] = None
-    IPv6: Optional[str] = None
+    IPv6: Optional[Union[str, ipaddress.IPv6Interface, ipaddress.IPv6Address]] = None
     Enable: bool = False
     Default: LinkShape = dataclasses.field(default_factory=LinkShape)
     Rules: List[LinkRule] = dataclasses.field(default_factory=list)
@@ -99,6 +114,9 @@ def to_c(cfg: Config):
         ip, _ = _ipnet(cfg.IPv4)
         c.has_ipv4 = 1
         c.ipv4 = ip
+    if cfg.IPv6 is not None:
+        c.has_ipv6 = 1
+        c.ipv6[:] = list(_ipv6(cfg.IPv6))
     s = cfg.Default
     c.shape.latency_ns = int(s.Latency)
     c.shape.jitter_ns = int(s.Jitter)

@@ -31,6 +31,7 @@ import dataclasses
 import io
 import json
 import os
+import queue
 import tarfile
 import tempfile
 import threading
@@ -184,32 +185,34 @@ class _Clock:
             self.live.discard(peer)
             self.cv.notify_all()
 
+    def _fail(self, e: BaseException) -> None:
+        """Stops the clock with `e`, surfaced to every instance (called with the lock held)."""
+        self.error = e
+        for c in self.pcv:
+            c.notify()
+
     def run(self) -> None:
         with self.cv:
             while self.live and not self.ctx.done():
-                if (len(self.waiting) < len(self.live)
-                        or any(r() for r in self.waiting.values())):
-                    self.cv.wait(timeout=0.005)
-                    continue
-                if self.now_ns() >= self.max_sim_ns:
-                    self.error = TimeoutError(f"simulated time reached {self.max_sim_ns} ns")
-                    for c in self.pcv:
-                        c.notify()
-                    return
-                try:
+                try:  # readiness checks call into the engine (barrier polls) and may raise too
+                    if (len(self.waiting) < len(self.live)
+                            or any(r() for r in self.waiting.values())):
+                        self.cv.wait(timeout=0.005)
+                        continue
+                    if self.now_ns() >= self.max_sim_ns:
+                        self._fail(TimeoutError(f"simulated time reached {self.max_sim_ns} ns"))
+                        return
                     with self.lock:
                         self.bridge.step()
                         for p in range(self.bridge.n):
                             for t_ns, src, _seq, data, flags in self.bridge.recv(p):
                                 self.inbox[p].append((t_ns, src, data, flags))
+                    for p, r in self.waiting.items():  # wake only the instances that can go on
+                        if r():
+                            self.pcv[p].notify()
                 except BaseException as e:  # noqa: BLE001 - surfaced to every instance
-                    self.error = e
-                    for c in self.pcv:
-                        c.notify()
+                    self._fail(e)
                     return
-                for p, r in self.waiting.items():  # wake only the instances that can go on
-                    if r():
-                        self.pcv[p].notify()
 
 
 class DataPlane:
@@ -273,8 +276,37 @@ class ClockedSync:
     def Publish(self, ctx: Context, topic: str, payload) -> int:
         return self.inner.Publish(ctx, topic, payload)
 
-    def Subscribe(self, ctx: Context, topic: str):
-        return self.inner.Subscribe(ctx, topic)
+    def Subscribe(self, ctx: Context, topic: str) -> "ClockedSubscription":
+        return ClockedSubscription(self.inner.Subscribe(ctx, topic), self._c, self.peer)
+
+    def PublishSubscribe(self, ctx: Context, topic: str, payload) -> "ClockedSubscription":
+        """sdk-go PublishSubscribe (pingpong.go:225): publish, then subscribe from the start."""
+        self.Publish(ctx, topic, payload)
+        return self.Subscribe(ctx, topic)
+
+
+class ClockedSubscription:
+    """A topic subscription whose blocking get() waits through the clock (so simulated time can
+    advance, and the run's context cancels it) instead of blocking a thread the clock cannot see."""
+
+    def __init__(self, q: "queue.Queue", clock: "_Clock", peer: int):
+        self._q = q
+        self._c = clock
+        self._peer = peer
+
+    def get(self, block: bool = True, timeout: Optional[float] = None):
+        if block:
+            self._c.block(self._peer, lambda: not self._q.empty())
+        return self._q.get_nowait()
+
+    def get_nowait(self):
+        return self._q.get_nowait()
+
+    def empty(self) -> bool:
+        return self._q.empty()
+
+    def qsize(self) -> int:
+        return self._q.qsize()
 
 
 @dataclasses.dataclass
@@ -322,7 +354,7 @@ class HealthcheckReport:
     Fixes: List[HealthcheckItem] = dataclasses.field(default_factory=list)
 
     def ChecksSucceeded(self) -> bool:
-        return all(c.Status == HEALTH_OK for c in self.Checks)
+        return all(c.Status in (HEALTH_OK, HEALTH_OMITTED) for c in self.Checks)
 
 
 class LocalSimRunner:
@@ -407,8 +439,9 @@ class LocalSimRunner:
             for t in threads:
                 t.start()
             clock_t.start()
+            deadline = time.monotonic() + max(0.0, cfg.run_timeout_s)  # one deadline for the whole run
             for t in threads:
-                t.join(max(0.0, cfg.run_timeout_s))
+                t.join(max(0.0, deadline - time.monotonic()))
             canceled = run_ctx.done() or any(t.is_alive() for t in threads)
             run_ctx.cancel()
             clock_t.join(timeout=5)
@@ -462,6 +495,8 @@ class LocalSimRunner:
             return (HEALTH_OK, d) if os.path.isdir(d) else (HEALTH_FAILED, f"{d} does not exist")
 
         def library():
+            if cfg.engine_factory is not None:  # the run will not load libtgsim.so
+                return HEALTH_OMITTED, "engine_factory configured"
             from .engine import load_library
             try:
                 load_library()
@@ -490,7 +525,7 @@ class LocalSimRunner:
             rep.Checks.append(HealthcheckItem(name, status, msg))
             if not fix:
                 continue
-            if status == HEALTH_OK:
+            if status in (HEALTH_OK, HEALTH_OMITTED):
                 rep.Fixes.append(HealthcheckItem(name, HEALTH_UNNECESSARY))
             elif fixer is None:
                 rep.Fixes.append(HealthcheckItem(name, HEALTH_FAILED, "requires manual fixing"))

@@ -32,6 +32,19 @@ def init_rccl(device: torch.device, **kw) -> None:
     dist.init_process_group("nccl", pg_options=opts, device_id=device, **kw)
 
 
+class _DevArray:
+    """__cuda_array_interface__ view of engine-owned device memory (zero copy)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False), "version": 2}
+
+
+def device_table(ptr: int, n: int, device: torch.device) -> torch.Tensor:
+    """The engine's K7 counter table (n u64 in device memory) as an int64 tensor, without a copy."""
+    with torch.cuda.device(device):
+        return torch.as_tensor(_DevArray(ptr, n), device=device)
+
+
 def shard_bounds(n_peers: int, world: int) -> List[int]:
     """Contiguous source ranges, as even as possible: rank r owns [b[r], b[r+1])."""
     return [(n_peers * r) // world for r in range(world)] + [n_peers]
@@ -68,7 +81,9 @@ class ShardedStepper:
         self._xs = torch.cuda.Stream(self.device, priority=-1) if self.device.type == "cuda" else None
         self.slot_cap = slot_cap
         self.max_count = 0
+        self.exchanged_records = 0  # records (slotted: record slots) this rank has sent, all steps
         self._routed: List[Optional[torch.cuda.Event]] = [None] * 3  # slotted: out[j] complete
+        self._sig_ev: Optional[torch.cuda.Event] = None  # after the engine's issued signals
 
     def _buf(self, bufs: list, i: int, n_bytes: int) -> torch.Tensor:
         b = bufs[i]
@@ -96,6 +111,7 @@ class ShardedStepper:
     def _exchange_on(self, k: int, out: torch.Tensor, cnt: np.ndarray) -> int:
         cuda = self.device.type == "cuda"
         self.max_count = max(self.max_count, int(cnt.max()) if len(cnt) else 0)
+        self.exchanged_records += int(cnt.sum())
         send = torch.as_tensor(cnt.astype(np.int64), device=self.device)
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=self.group)
@@ -165,6 +181,7 @@ class ShardedStepper:
             if self._in[i] is not None and self._in[i].numel() < size and self._dev[i] is not None:
                 self._dev[i].synchronize()  # growing: the old block returns to the allocator
             inb = self._buf(self._in, i, size)
+            self.exchanged_records += n_r * (self.slot_cap + 1)
             dist.all_to_all_single(inb[:size], out[:size], group=self.group)
             self.engine.deliver_slotted_async(inb.data_ptr(), n_r, self.slot_cap, self._exchanged(k))
             self._mark_delivery(i)
@@ -210,9 +227,24 @@ class ShardedStepper:
         return total
 
     def barrier(self, state: int, target: int) -> bool:
-        """Global barrier over the shards' sync counters: the per-rank counts of `state` are summed
-        with an all-reduce (RCCL on GPUs) and compared with target (SignalAndWait semantics)."""
-        local = self.engine.signal(state, 0)
-        t = torch.tensor([local], dtype=torch.int64, device=self.device)
-        dist.all_reduce(t, group=self.group)
-        return int(t.item()) >= target
+        """Global barrier over the shards' sync counters (K7): the per-rank counts of `state` are
+        summed with an all-reduce and compared with target (SignalAndWait semantics).  On GPUs the
+        counter is read straight from the engine's device table on the exchange stream, behind an
+        event recorded after every signal the engine issued (no host copy before the collective;
+        the comparison itself is the barrier's one host read).  On CPU (oracle shards, gloo) the
+        table is host memory."""
+        if self.device.type != "cuda":
+            t = torch.tensor([self.engine.signal(state, 0)], dtype=torch.int64)
+            dist.all_reduce(t, group=self.group)
+            return int(t.item()) >= target
+        ev = self._sig_ev or torch.cuda.Event()
+        if self._sig_ev is None:
+            ev.record(torch.cuda.current_stream(self.device))  # creates the event
+            self._sig_ev = ev
+        ptr, n = self.engine.sync_counters(ev.cuda_event)
+        table = device_table(ptr, n, self.device)
+        with torch.cuda.stream(self._xs):
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            t = table[state:state + 1].clone()
+            dist.all_reduce(t, group=self.group)
+            return int(t.item()) >= target

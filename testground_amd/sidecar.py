@@ -23,6 +23,7 @@ import threading
 import time
 from typing import Callable, Dict, List, Optional
 
+from .abi import SYNC_STATES
 from .engine import EngineError
 from .network import Config
 
@@ -81,6 +82,9 @@ class SyncClient:
         return seq
 
     def Publish(self, ctx: Context, topic: str, payload) -> int:
+        # sdk-go serialises the payload onto the topic: subscribers get a copy, and the publisher
+        # may change its own object afterwards (pingpong.go:190-192 reuses its Config)
+        payload = copy.deepcopy(payload)
         with self._cv:
             self._topics.setdefault(topic, []).append(payload)
             for q in self._subs.get(topic, []):
@@ -111,28 +115,39 @@ class EngineSyncClient(SyncClient):
     barriers live beside the simulated network instead of in a Redis-backed sync service.
     Pub/sub topics stay in memory (the handler's `network:<hostname>` subscription, :49).
 
-    State names map to the engine's 1024 state slots in first-use order, so every process of a
-    sharded run must touch its states in the same order; `reduce`, when given, sums a state's
-    count over the shards (ShardedStepper.barrier does it with an RCCL all-reduce)."""
+    State names map to the engine's device counters (abi.SYNC_STATES of them) in first-use order,
+    so every process of a sharded run must touch its states in the same order; `reduce`, when
+    given, sums a state's count over the shards (ShardedStepper.barrier does it with an RCCL
+    all-reduce).  The reference's sync service has no state limit, so a run that names more states
+    than the engine holds (e.g. one callback state per instance, splitbrain/main.go:113, at more
+    than 65,536 instances) keeps the rest in this client's in-memory counters; that works for a
+    single engine, while a sharded run (`reduce`) refuses the extra state with a clear error."""
 
     def __init__(self, engine, lock: Optional[threading.Lock] = None,
-                 reduce: Optional[Callable[[int, int], bool]] = None):
+                 reduce: Optional[Callable[[int, int], bool]] = None, n_slots: Optional[int] = None):
         super().__init__()
         self.engine = engine
         self.lock = lock or threading.Lock()
         self.reduce = reduce
+        self.n_slots = n_slots if n_slots is not None else SYNC_STATES
         self._ids: Dict[str, int] = {}
 
-    def state_id(self, state: str) -> int:
+    def state_id(self, state: str) -> Optional[int]:
+        """The engine counter of `state`, or None when it lives in the in-memory counters."""
         with self._cv:
             if state not in self._ids:
-                if len(self._ids) >= 1024:
-                    raise RuntimeError("engine sync counters: more than 1024 states")
+                if len(self._ids) >= self.n_slots:
+                    if self.reduce is not None:
+                        raise RuntimeError(f"sync state {state!r}: all {self.n_slots} engine sync counters are "
+                                           "in use and a sharded run cannot sum in-memory counters")
+                    return None
                 self._ids[state] = len(self._ids)
             return self._ids[state]
 
     def SignalEntry(self, ctx: Context, state: str) -> int:
         sid = self.state_id(state)
+        if sid is None:
+            return super().SignalEntry(ctx, state)
         with self.lock:
             seq = self.engine.signal(sid, 1)
         with self._cv:
@@ -141,6 +156,8 @@ class EngineSyncClient(SyncClient):
 
     def _reached(self, state: str, target: int) -> bool:
         sid = self.state_id(state)
+        if sid is None:
+            return super()._reached(state, target)
         if self.reduce is not None:
             return self.reduce(sid, target)
         with self.lock:
@@ -165,10 +182,17 @@ class RunEnv:
 class NetClient:
     """sdk-go network.Client as used by the plans (pingpong.go:21-22, splitbrain/main.go:73-74)."""
 
-    def __init__(self, sync_client: SyncClient, runenv: RunEnv, hostname: str):
+    def __init__(self, sync_client: SyncClient, runenv: RunEnv, hostname: str, ip: Optional[str] = None):
         self.sync = sync_client
         self.runenv = runenv
         self.hostname = hostname
+        self._ip = ip  # the data-network address (sdk-go reads it from the interface)
+
+    def GetDataNetworkIP(self) -> str:
+        """MustGetDataNetworkIP (pingpong.go:83): the instance's current data-network address."""
+        if self._ip is None:
+            raise RuntimeError("no data network address")
+        return self._ip
 
     def WaitNetworkInitialized(self, ctx: Context) -> None:
         self.sync.Barrier(ctx, NET_INIT_STATE, self.runenv.TestInstanceCount)
@@ -181,6 +205,10 @@ class NetClient:
         # may change its own object afterwards (plans/network/pingpong.go:191-194 does)
         self.sync.PublishAndWait(ctx, "network:" + self.hostname, copy.deepcopy(config),
                                  config.CallbackState, target)
+        if config.IPv4 is not None and config.Enable:
+            from .network import _ipnet
+            import ipaddress
+            self._ip = str(ipaddress.IPv4Address(_ipnet(config.IPv4)[0]))
 
 
 class Network:
@@ -340,7 +368,9 @@ class SimReactor(Reactor):
             self.threads.append(t)
 
     def net_client(self, peer: int) -> NetClient:
-        return NetClient(self.Client, self.RunEnv, self.hostname(peer))
+        import ipaddress
+        base = int(getattr(self.engine, "subnet_base", 0) or (16 << 24))
+        return NetClient(self.Client, self.RunEnv, self.hostname(peer), str(ipaddress.IPv4Address(base + 2 + peer)))
 
     def Close(self) -> None:
         for t in self.threads:

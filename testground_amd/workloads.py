@@ -240,7 +240,8 @@ def epoch_reshape(eng, n_peers: int, epoch: int, seed: int = SEED) -> int:
 
 
 def epoch_state(epoch: int) -> Tuple[int, int]:
-    """Sync state id of barrier `epoch-k` and the round of that id (states are 1024 counters)."""
+    """Sync state id of barrier `epoch-k` and the round of that id (epochs cycle over 1024 of the
+    engine's sync counters, so a long run keeps reusing the same few)."""
     return epoch % 1024, epoch // 1024 + 1
 
 
@@ -253,7 +254,7 @@ def run_epoch(eng, n_peers: int, epoch: int, n_local: int, step=None, barrier=No
     eng.gen_storm(lam, ticks)
     (step or eng.step)(ticks)
     state, rnd = epoch_state(epoch)
-    eng.signal(state, n_local)
+    eng.signal_async(state, n_local)
     ok = barrier(state, rnd * n_peers) if barrier else eng.barrier_poll(state, rnd * n_peers)
     if not ok:
         raise RuntimeError(f"barrier epoch-{epoch} did not release")

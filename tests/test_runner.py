@@ -15,7 +15,9 @@ from testground_amd.sidecar import Context
 
 def pingpong_plan(env: rn.PlanEnv) -> None:
     """plans/network/pingpong.go:23-187 on the simulated data plane: configure 100 ms latency and
-    1 Mibit/s (callback "network-configured"), ping-pong with RTT in [200, 215] ms
+    1 Mibit/s (callback "network-configured"), re-address to subnet.a.b.((seq>>8)+1).seq/12
+    (callback "ip-changed", :54-81; the sidecar reconnects the instance) and exchange the new
+    addresses over the "peers" topic (:204-244), ping-pong with RTT in [200, 215] ms
     (pingpong.go:185), reconfigure to 10 ms (callback "latency-reduced", :191-194), RTT in
     [20, 35] ms (:195).  Round-trip times go to rtt.txt in the instance's outputs dir."""
     env.net.WaitNetworkInitialized(env.ctx)
@@ -42,6 +44,20 @@ def pingpong_plan(env: rn.PlanEnv) -> None:
 
     cfg = wl.pingpong_config(100 * nw.Millisecond)
     env.net.ConfigureNetwork(env.ctx, cfg)
+    n = env.runenv.TestInstanceCount
+    seq = env.sync.SignalAndWait(env.ctx, "ip-allocation", n)
+    net = ipaddress.IPv4Network(env.runenv.TestSubnet, strict=False).network_address.packed
+    ip = ipaddress.IPv4Address(bytes([net[0], net[1], (seq >> 8) + 1, seq & 0xFF]))
+    cfg.IPv4 = (str(ip), 12)
+    cfg.CallbackState = "ip-changed"
+    env.net.ConfigureNetwork(env.ctx, cfg)
+    own = env.net.GetDataNetworkIP()
+    assert own == str(ip), (own, ip)
+    env.sync.SignalAndWait(env.ctx, "listening", n)
+    q = env.sync.PublishSubscribe(env.ctx, "peers", own)
+    addrs = [q.get() for _ in range(n)]
+    assert len(set(addrs)) == n and own in addrs
+    env.sync.SignalAndWait(env.ctx, "got-other-addrs", n)
     ping_pong(200, 215)
     cfg.Default.Latency = 10 * nw.Millisecond
     cfg.CallbackState = "latency-reduced"
@@ -222,8 +238,52 @@ def test_runner_healthcheck(tmp_path, make_oracle):
     cfg = rn.LocalSimRunnerCfg(outputs_dir=str(tmp_path / "out"), engine_factory=make_oracle)
     rep = r.Healthcheck(Context(), fix=False, cfg=cfg)
     st = {c.Name: c.Status for c in rep.Checks}
-    assert st == {"outputs-dir": rn.HEALTH_FAILED, "engine-library": rn.HEALTH_OK, "engine-device": rn.HEALTH_OK}
+    # the run would not load libtgsim.so with an engine_factory: that check is omitted
+    assert st == {"outputs-dir": rn.HEALTH_FAILED, "engine-library": rn.HEALTH_OMITTED,
+                  "engine-device": rn.HEALTH_OK}
     assert not rep.ChecksSucceeded() and rep.Fixes == []
     rep = r.Healthcheck(Context(), fix=True, cfg=cfg)
     assert [f.Status for f in rep.Fixes] == [rn.HEALTH_OK, rn.HEALTH_UNNECESSARY, rn.HEALTH_UNNECESSARY]
     assert r.Healthcheck(Context(), cfg=cfg).ChecksSucceeded()
+
+
+def subscriber_plan(env: rn.PlanEnv) -> None:
+    """One instance publishes after sleeping in simulated time; the other blocks in a topic get(),
+    which waits through the clock (so the publisher's sleep can advance time)."""
+    if env.seq == 0:
+        env.data.sleep(3 * nw.Millisecond)
+        env.sync.Publish(env.ctx, "t", {"at": env.data.now_ns()})
+    else:
+        got = env.sync.Subscribe(env.ctx, "t").get()
+        assert got["at"] >= 3 * nw.Millisecond
+
+
+def test_runner_clocked_subscription(tmp_path, make_oracle):
+    r = rn.LocalSimRunner()
+    out = r.Run(Context(), _job("sub", [rn.RunGroup("g", 2, subscriber_plan)], _cfg(tmp_path, make_oracle)))
+    assert out.Result.Outcome == rn.OUTCOME_SUCCESS, out.Result.Errors
+
+
+def test_runner_clock_readiness_error_fails_fast(tmp_path, make_oracle):
+    """A readiness check that raises (here: a barrier poll on a broken engine) stops the run with
+    the cause instead of leaving every instance waiting for run_timeout."""
+    import time
+
+    def broken(n, **kw):
+        e = make_oracle(n, **kw)
+
+        def boom(*a, **k):
+            raise RuntimeError("barrier poll exploded")
+        e.barrier_poll = boom
+        return e
+
+    def plan(env):
+        env.sync.Barrier(env.ctx, "never", 5)
+
+    cfg = _cfg(tmp_path, broken)
+    cfg.run_timeout_s = 30
+    t0 = time.monotonic()
+    out = rn.LocalSimRunner().Run(Context(), _job("boom", [rn.RunGroup("g", 2, plan)], cfg))
+    assert out.Result.Outcome != rn.OUTCOME_SUCCESS
+    assert time.monotonic() - t0 < 20
+    assert any("exploded" in e for e in out.Result.Errors.values()), out.Result.Errors

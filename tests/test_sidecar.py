@@ -100,3 +100,58 @@ def test_sim_network_over_oracle(make_oracle):
 def test_sim_network_over_engine():
     from testground_amd.engine import Engine
     _sim_flow(Engine(3))
+
+
+def test_publish_delivers_a_copy():
+    """sdk-go serialises published payloads: a publisher changing its object afterwards does not
+    change what subscribers (or the sidecar, via ConfigureNetwork) see."""
+    from testground_amd import network as nw
+    from testground_amd.sidecar import Context, SyncClient
+
+    c = SyncClient()
+    cfg = nw.Config(Network="default", Enable=True, Default=nw.LinkShape(Latency=5))
+    c.Publish(Context(), "t", cfg)
+    cfg.Default.Latency = 99
+    assert c.Subscribe(Context(), "t").get_nowait().Default.Latency == 5
+
+
+def test_configure_network_passes_a_copy_to_the_sidecar():
+    import threading
+
+    from testground_amd import network as nw
+    from testground_amd.sidecar import Context, MockReactor, NetClient, handler
+
+    r = MockReactor()
+    ctx = Context(timeout=10)
+    t = threading.Thread(target=r.Handle, args=(ctx, handler), daemon=True)
+    t.start()
+    nc = NetClient(r.Client, r.RunEnv, r.Hostname)
+    nc.WaitNetworkInitialized(ctx)
+    cfg = nw.Config(Network="default", Enable=True, Default=nw.LinkShape(Latency=7), CallbackState="a")
+    nc.ConfigureNetwork(ctx, cfg)
+    cfg.Default.Latency = 1234
+    assert r.Network.Active["default"].Default.Latency == 7
+    ctx.cancel()
+    t.join(5)
+
+
+def test_engine_sync_client_beyond_engine_slots(make_oracle):
+    """More distinct states than the engine holds (one callback state per instance): the extra
+    states live in the client's in-memory counters; a sharded client refuses them clearly."""
+    import pytest
+
+    from testground_amd.sidecar import Context, EngineSyncClient
+
+    e = make_oracle(2)
+    c = EngineSyncClient(e, n_slots=1024)
+    ctx = Context()
+    for i in range(1100):
+        assert c.SignalEntry(ctx, f"reconfigured{i}") == 1
+    assert c.SignalEntry(ctx, "reconfigured1099") == 2
+    c.Barrier(ctx, "reconfigured1099", 2)
+    assert c._reached("reconfigured5", 1) and not c._reached("reconfigured5", 2)
+    sharded = EngineSyncClient(e, n_slots=2, reduce=lambda sid, t: True)
+    sharded.SignalEntry(ctx, "a")
+    sharded.SignalEntry(ctx, "b")
+    with pytest.raises(RuntimeError, match="engine sync counters"):
+        sharded.SignalEntry(ctx, "c")
