@@ -42,8 +42,8 @@ static_assert(sizeof(SrcParams) == 64, "SrcParams must stay 64 B");
 // Mutable per-source state carried across steps (32 B).
 struct alignas(16) SrcState {
   uint64_t tat;        // HTB theoretical arrival time (tokens >= 0 once now >= tat)
-  uint32_t heap_n;     // queued, not yet eligible items
-  uint32_t ring_head;  // departure ring of items given a departure time
+  uint32_t heap_n;     // queued, not yet eligible items (near + pool)
+  uint32_t near_n;     // the first near_n of them: the sorted near region (the rest: the pool)
   uint32_t ring_n;
   uint32_t last_dup, last_cor, last_reo;  // get_crandom() correlation state
 };

@@ -63,10 +63,15 @@ __device__ __forceinline__ bool item_lt(const uint4& a, const uint4& b) {
 // k_sim: one wavefront owns one source's netem queue for the whole step.
 //
 // The queue lives in LDS as ONE circular buffer of kHeapCap 16-B slots: the departure ring (items
-// already given a departure time by HTB, d in .x/.y, oldest first) immediately followed by the
-// eligibility queue (items waiting for their netem time e, kept SORTED by (e, seq, clone first)).
-// HTB serves the eligibility queue from its head, so serving an item turns the slot at the
-// boundary into the ring's newest entry in place; the netem limit bounds ring + queue <= 1024.
+// already given a departure time by HTB, d in .x/.y, oldest first), immediately followed by the
+// eligibility queue (items waiting for their netem time e) in two regions: the NEAR region, kept
+// SORTED by (e, seq, clone first), holds every item with e < B; the POOL behind it holds the items
+// with e >= B in no order.  HTB serves the near region from its head, so serving an item turns the
+// slot at the boundary into the ring's newest entry in place; the netem limit bounds
+// ring + near + pool <= 1024.  A new item whose e >= B is appended to the pool (no search, no
+// shift: with jitter or a long latency most items are far in the future); before anything needs
+// the items eligible before h, `refill` raises B past h, moving the pool items below the new B
+// into the near region (chosen so that at most 64 move at a time).
 //
 // The sequential recurrence of netem_enqueue (limit check) + HTB is resolved a WINDOW of offered
 // packets at a time, wave-parallel:
@@ -249,7 +254,8 @@ struct SimQueue {
   SimLds& lds;
   const SrcParams& p;
   uint32_t lane;
-  uint32_t rh, rn, qn;      // ring head slot, ring length, eligibility-queue length
+  uint32_t rh, rn, qn, pn;  // ring head slot, ring length, near-region length, pool length
+  uint64_t B;               // near/pool boundary: near items have e < B, pool items e >= B
   uint64_t tat;             // HTB theoretical arrival time
   tgsim_delivery* emit;
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
@@ -310,7 +316,8 @@ struct SimQueue {
   }
 
   // HTB serves every queued item eligible before h (e < h), in (e, seq, clone first) order.
-  __device__ void serve_until(uint64_t h) {
+  __device__ __forceinline__ void serve_until(uint64_t h) {
+    refill(h);
     for (;;) {
       const bool hq = lane < qn;
       const uint4 qi = hq ? slot(rn + lane) : make_uint4(0, 0, 0, 0);
@@ -326,7 +333,7 @@ struct SimQueue {
   }
 
   // Items whose departure time is before T leave the netem queue.
-  __device__ void depart_before(uint64_t T) {
+  __device__ __forceinline__ void depart_before(uint64_t T) {
     for (;;) {
       const uint64_t dep = lane < rn ? ring_d(lane) : ~0ull;
       const uint64_t stop = __ballot(dep >= T);  // released from the head while head < T
@@ -337,10 +344,116 @@ struct SimQueue {
     }
   }
 
-  // Merges the lanes' new items (has) into the sorted eligibility queue: each item's position
-  // among the queued items (lower bound of its key), its rank among the new items, then the
-  // queued items from the first position on move up by the number of new items before them.
-  __device__ void insert(bool has, const uint4& it) {
+  // New items of the lanes (has): into the near region when eligible before B, else appended to
+  // the pool.
+  __device__ __forceinline__ void insert(bool has, const uint4& it) {
+    const bool far = has && (w0_of(it) & kEMask) >= B;
+    insert_near(has && !far, it, true);
+    const uint64_t m = __ballot(far);
+    if (!m) return;
+    if (far) slot(rn + qn + pn + (uint32_t)__popcll(m & ((1ull << lane) - 1))) = it;
+    pn += (uint32_t)__popcll(m);
+    wave_lds_sync();
+  }
+
+  // The near region grows by k at its end: the first min(k, pn) pool items move behind the pool
+  // (the pool has no order), so the near suffix can shift up into their slots.
+  __device__ __forceinline__ void relocate_pool(uint32_t k) {
+    const uint32_t mv = k < pn ? k : pn, off = k > pn ? k : pn;
+    if (!mv) return;
+    const bool l = lane < mv;
+    const uint4 v = l ? slot(rn + qn + lane) : make_uint4(0, 0, 0, 0);
+    __asm__ volatile("" ::: "memory");
+    if (l) slot(rn + qn + off + lane) = v;
+    __asm__ volatile("" ::: "memory");
+  }
+
+  // Raises B to at least h: every pool item eligible before h joins the near region.  The new B
+  // is the largest candidate h + d_c whose pool items number at most 64 (one count pass, eleven
+  // thresholds); those are taken out of the pool (the pool's first slots refill the holes they
+  // leave, so the pool then starts right behind them) and merged into the near region, where they
+  // land at its end: every pool item is >= B > every near item.  More than 64 pool items below h
+  // itself take several rounds.
+  __device__ __forceinline__ void refill(uint64_t h) {
+    while (pn && B < h) {
+      constexpr int kCand = 11;
+      uint32_t cnt[kCand];
+#pragma unroll
+      for (int c = 0; c < kCand; ++c) cnt[c] = 0;
+      for (uint32_t base = 0; base < pn; base += kWave) {
+        const uint32_t k = base + lane;
+        const uint64_t e = k < pn ? (ring_d(rn + qn + k) & kEMask) : ~0ull;
+#pragma unroll
+        for (int c = 0; c < kCand; ++c) cnt[c] += ballot_count(e < h + (c ? (4096ull << c) : 0ull));
+      }
+      uint64_t Bp = h;
+      uint32_t total = cnt[0];
+#pragma unroll
+      for (int c = 1; c < kCand; ++c)
+        if (cnt[c] <= kWave) {  // counts grow with c: the last that fits
+          Bp = h + (4096ull << c);
+          total = cnt[c];
+        }
+      if (!total) {
+        B = Bp;
+        break;
+      }
+      const uint32_t nx = total < kWave ? total : kWave;
+      const uint64_t below = (1ull << lane) - 1;
+      uint4 xv = make_uint4(0, 0, 0, 0), av = make_uint4(0, 0, 0, 0);
+      uint32_t gx = 0, gh = 0;  // items taken so far, holes refilled so far
+      for (uint32_t base = 0; gx < nx; base += kWave) {
+        const uint32_t k = base + lane;
+        const bool in = k < pn;
+        const uint4 v = in ? slot(rn + qn + k) : make_uint4(0, 0, 0, 0);
+        const bool ex0 = in && (w0_of(v) & kEMask) < Bp;
+        const uint32_t rx = gx + (uint32_t)__popcll(__ballot(ex0) & below);
+        const bool ex = ex0 && rx < nx;  // the first nx by position
+        const uint64_t mex = __ballot(ex);
+        const uint32_t cx = (uint32_t)__popcll(mex);
+        {  // taken items to lanes [gx, gx + cx) (forward permute; the others fill the rest)
+          const uint32_t to = (ex ? rx : gx + cx + (uint32_t)__popcll(~mex & below)) & (kWave - 1);
+          const uint4 pv = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.x),
+                                      (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.y),
+                                      (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.z),
+                                      (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.w));
+          if (lane >= gx && lane < gx + cx) xv = pv;
+        }
+        if (base == 0) {  // the items that stay but sit in the first nx slots, ranked, to lanes
+          const bool st = in && k < nx && !ex;
+          const uint64_t ma = __ballot(st);
+          const uint32_t to = (st ? (uint32_t)__popcll(ma & below)
+                                  : (uint32_t)__popcll(ma) + (uint32_t)__popcll(~ma & below)) & (kWave - 1);
+          av = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.x),
+                          (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.y),
+                          (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.z),
+                          (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.w));
+        }
+        // slots the taken items leave behind the first nx receive those items, in rank order
+        const bool hole = ex && k >= nx;
+        const uint64_t mh = __ballot(hole);
+        const uint32_t src = (gh + (uint32_t)__popcll(mh & below)) & (kWave - 1);
+        const uint4 fill = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)av.x),
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)av.y),
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)av.z),
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)av.w));
+        if (hole) slot(rn + qn + k) = fill;
+        gh += (uint32_t)__popcll(mh);
+        gx += cx;
+      }
+      wave_lds_sync();
+      pn -= nx;  // the pool now starts nx slots further; those slots are free
+      insert_near(lane < nx, xv, false);
+      if (total <= kWave) B = Bp;
+    }
+  }
+
+  // Merges the lanes' new items (has) into the sorted near region: each item's position among
+  // the queued items (lower bound of its key), its rank among the new items, then the queued items
+  // from the first position on move up by the number of new items before them (after the pool
+  // has made room behind the near region, when reloc; without it the slots behind the near region
+  // are free).
+  __device__ __forceinline__ void insert_near(bool has, const uint4& it, bool reloc) {
     const uint64_t m = __ballot(has);
     if (!m) return;
     PROF_T0(i);
@@ -422,7 +535,8 @@ struct SimQueue {
       // moving the suffix [minR, qn) up; kL minimizes the slots moved.  Items eligible at once
       // (delay 0, reorder) land at the head and cost only the ring.
       const uint32_t spm1 = shr1_u32(sp, 0u);
-      const uint32_t cost = lane <= nm ? (lane > 0 ? rn + spm1 : 0u) + (lane < nm ? qn - sp : 0u) : 0xFFFFFFFFu;
+      const uint32_t pmv = reloc ? (nm - lane < pn ? nm - lane : pn) : 0u;  // pool items moved aside
+      const uint32_t cost = lane <= nm ? (lane > 0 ? rn + spm1 : 0u) + (lane < nm ? qn - sp + pmv : 0u) : 0xFFFFFFFFu;
       uint32_t best = readlane32(cost, 0);
       for (uint32_t k = 1; k <= nm; ++k) {
         const uint32_t c = readlane32(cost, k);
@@ -433,6 +547,7 @@ struct SimQueue {
       }
       const int32_t maxL = kL ? (int32_t)readlane32(sp, kL - 1) : 0;
       const int32_t minR = kL < nm ? (int32_t)readlane32(sp, kL) : (int32_t)qn;
+      if (reloc) relocate_pool(nm - kL);
       // suffix up: queue item j >= minR moves by #{rank >= kL with pos <= j}; passes of four
       // chunks from the tail down, all reads of a pass before its writes
       for (int32_t hi = (int32_t)qn; hi > minR; hi -= 4 * (int32_t)kWave) {
@@ -481,6 +596,7 @@ struct SimQueue {
       const uint32_t sp = sp_all;  // ascending, 0xFFFFFFFF beyond nm
       const int32_t mp = (int32_t)readlane32(sp, 0);
       const bool mine = lane < nm;
+      if (reloc) relocate_pool(nm);
       // queue item p >= mp moves up by #{new items at or before p}: passes of four chunks from the
       // tail down, all reads of a pass before its writes
       for (int32_t hi = (int32_t)qn; hi > mp; hi -= 4 * (int32_t)kWave) {
@@ -536,7 +652,8 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   SimQueue Q{lds, pp, lane};
   Q.rh = 0;
   Q.rn = st.ring_n;
-  Q.qn = st.heap_n;
+  Q.qn = st.near_n;
+  Q.pn = st.heap_n - st.near_n;
   Q.tat = st.tat;
   Q.src = a.shard_begin + s;
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
@@ -552,7 +669,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   {
     const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     const uint4* gh = a.heap + (size_t)s * kHeapCap;
-    const uint32_t rn = Q.rn, qn = Q.qn;
+    const uint32_t rn = Q.rn, qn = Q.qn + Q.pn;
     // every load of the ring and the queue in flight before the first LDS write (one HBM
     // latency instead of one per 256 slots)
     uint64_t rv[kHeapCap / kWave];
@@ -584,8 +701,8 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   // into the statistics every 2^14 batches (at most 2 counts per lane and batch), before a field
   // can overflow
   unsigned long long* const sc = a.stats + (size_t)(blockIdx.x % kStatCopies) * kStSlots;
-  if (lane == 0 && (Q.qn | Q.rn))  // the queue state loaded (the stored part is added at the end)
-    atomicAdd(&sc[kStQueue], (unsigned long long)(16ull * Q.qn + 8ull * Q.rn));
+  if (lane == 0 && (Q.qn | Q.pn | Q.rn))  // the queue state loaded (the stored part is added at the end)
+    atomicAdd(&sc[kStQueue], (unsigned long long)(16ull * (Q.qn + Q.pn) + 8ull * Q.rn));
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
   auto flush_verdicts = [&]() {
@@ -599,12 +716,15 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   };
   uint32_t perr = 0;
   wave_lds_sync();
+  // every pool item is >= the B of the previous step > every near item, so both of these are
+  // valid boundaries; with an empty near region every new item starts in the pool
+  Q.B = Q.qn ? (w0_of(Q.slot(Q.rn + Q.qn - 1)) & kEMask) + 1 : a.t0_ns;
   stamp(a, lane, 1, __builtin_amdgcn_s_memrealtime());
 
   const uint32_t n_batches = (uint32_t)((send - sbeg + kWave - 1) / kWave);
   // open queue: even if every offered packet and its clone were admitted the queue would stay
   // below the netem limit (sparse sources: gossip, ping-pong, splitbrain)
-  const bool open_q = !corr && (uint64_t)Q.rn + Q.qn + 2 * (send - sbeg) < lim;
+  const bool open_q = !corr && (uint64_t)Q.rn + Q.qn + Q.pn + 2 * (send - sbeg) < lim;
   uint64_t T_enq = 0;  // open queue: offer time of the last packet that reached the netem enqueue
   uint64_t idx = sbeg + lane;
   InRec rec = {}, rec2 = {};  // records of batches b and b + 1 (two batches in flight)
@@ -683,10 +803,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       uint64_t pend = open_q ? 0ull : __ballot(cand);
       while (pend) {
         PROF_CNT(3, 1);
-        if (Q.rn + Q.qn >= lim) {
+        if (Q.rn + Q.qn + Q.pn >= lim) {
           // full queue: nothing changes before the next eligibility or departure time, so every
-          // packet offered up to then is a QUEUE_FULL drop
-          const uint64_t qh = Q.qn ? (w0_of(Q.slot(Q.rn)) & kEMask) : ~0ull;
+          // packet offered up to then is a QUEUE_FULL drop (B bounds the pool's earliest e)
+          const uint64_t qh = Q.qn ? (w0_of(Q.slot(Q.rn)) & kEMask) : (Q.pn ? Q.B : ~0ull);
           const uint64_t dh = Q.rn ? Q.ring_d(0) : ~0ull;
           const uint64_t t_ev = qh < dh ? qh : dh;
           const uint64_t mf = __ballot(((pend >> lane) & 1ull) && T <= t_ev);
@@ -703,6 +823,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         const uint32_t w0 = (uint32_t)__builtin_ctzll(pend);
         const uint32_t wl = 63u - (uint32_t)__builtin_clzll(pend);
         const uint64_t T_last = readlane64(T, wl);
+        Q.refill(T_last);  // every item eligible before the window's last packet in the near region
         PROF_T0(s1);
         // (1) queue-head items eligible before the last pending packet, served optimistically
         const bool hq = lane < Q.qn;
@@ -768,7 +889,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         const int32_t cnt = inw ? 1 + (cst == 2) : 0;
         const int32_t P = scan_sum_i32(cnt - delta);
         const int32_t M = scan_max_i32(P);
-        const int32_t x0 = (int32_t)(Q.rn + Q.qn), ilim = (int32_t)lim;
+        const int32_t x0 = (int32_t)(Q.rn + Q.qn + Q.pn), ilim = (int32_t)lim;
         const int32_t Pex = (int32_t)shr1_u32((uint32_t)P, 0u);
         const int32_t Mex = (int32_t)shr1_u32((uint32_t)M, 0u);  // lane 0: 0 = identity here
         const int32_t xb = Pex + min(x0, ilim - Mex);
@@ -888,7 +1009,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
           auto enq = [&](uint32_t reo_raw, uint32_t delay_raw, uint32_t fl) -> uint32_t {
             Q.serve_until(Tj);
             Q.depart_before(Tj);
-            if (Q.rn + Q.qn >= lim) return TGSIM_V_QUEUE_FULL;
+            if (Q.rn + Q.qn + Q.pn >= lim) return TGSIM_V_QUEUE_FULL;
             bool reordered = false;
             if (pp.thr_reo) reordered = !(pp.thr_reo < crand(reo_raw, pp.rho_reo, last_reo));
             uint64_t e = reordered ? Tj : delayed(pp, Tj, delay_raw);
@@ -942,13 +1063,13 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     uint4* gh = a.heap + (size_t)s * kHeapCap;
     for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
-    for (uint32_t k = lane; k < Q.qn; k += kWave) gh[k] = Q.slot(Q.rn + k);
+    for (uint32_t k = lane; k < Q.qn + Q.pn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
   }
   if (lane == 0) {
     SrcState ns;
     ns.tat = Q.tat;
-    ns.heap_n = Q.qn;
-    ns.ring_head = 0;
+    ns.heap_n = Q.qn + Q.pn;
+    ns.near_n = Q.qn;
     ns.ring_n = Q.rn;
     ns.last_dup = last_dup;
     ns.last_cor = last_cor;
@@ -958,7 +1079,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   stamp(a, lane, 4, __builtin_amdgcn_s_memrealtime());
   stamp(a, lane, 5, ((uint64_t)s << 32) | n_batches);
   stamp(a, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
-  stamp(a, lane, 7, ((uint64_t)Q.qn << 32) | Q.rn);
+  stamp(a, lane, 7, ((uint64_t)(Q.qn + Q.pn) << 32) | Q.rn);
 #ifdef TGSIM_PROFILE
   for (int k = 0; k < 16; ++k) stamp(a, lane, 8 + k, Q.pf[k]);
 #endif
@@ -966,7 +1087,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   const uint32_t corrupted = readlane32((uint32_t)scan_sum_i32((int32_t)Q.corrupted), kWave - 1);
   const uint32_t lost = readlane32((uint32_t)scan_sum_i32((int32_t)Q.lost), kWave - 1);
   const uint64_t bytes = wave_sum(Q.bytes);
-  const uint64_t qbytes = 16ull * Q.qn + 8ull * Q.rn;
+  const uint64_t qbytes = 16ull * (Q.qn + Q.pn) + 8ull * Q.rn;
   const bool err = __ballot(perr != 0) != 0;
   const uint32_t c_clone = readlane32((uint32_t)scan_sum_i32((int32_t)n_clone), kWave - 1);
   flush_verdicts();
@@ -1037,7 +1158,7 @@ __global__ void k_apply_cfg(const CfgPatch* __restrict__ patches, uint32_t n, Sr
   if (c.mask & 16u) {
     const uint32_t k = st.heap_n + st.ring_n;
     if (k) atomicAdd(&stats[(size_t)(i % kStatCopies) * kStSlots + kStFlushed], (unsigned long long)k);
-    st.heap_n = st.ring_n = st.ring_head = 0;
+    st.heap_n = st.ring_n = st.near_n = 0;
   }
   state[c.s] = st;
 }
