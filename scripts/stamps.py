@@ -48,7 +48,7 @@ for _ in range(a.steps):
 n = e._lib.tgsim_debug_stamps(e._h, None, 0)
 st = np.zeros(n, dtype=np.uint64)
 e._lib.tgsim_debug_stamps(e._h, st.ctypes.data, n)
-st = st.reshape(-1, 24).astype(np.int64)
+st = st.reshape(-1, 32).astype(np.int64)
 t0 = st[:, 0].min()
 ph = np.diff(st[:, :5], axis=1) * 10 / 1000  # us (100 MHz)
 tot = (st[:, 4] - st[:, 0]) * 10 / 1000
@@ -65,18 +65,22 @@ start = (st[:, 0] - t0) * 10 / 1000
 end = (st[:, 4] - t0) * 10 / 1000
 ts = np.linspace(0, end.max(), 20)
 print("  concurrency over time:", [int(((start <= t) & (end > t)).sum()) for t in ts])
-pf = st[:, 8:24]  # profile build counters (see k_sim PROF_* slots)
+pf = st[:, 8:32]  # profile build counters (see k_sim PROF_* slots)
 nb = np.maximum(nbat, 1)
 names = {0: "parallel", 1: "windows", 7: "S+htb", 8: "departures", 9: "decide", 10: "window-end",
-         11: "commit", 4: "insert", 14: "ins-search", 15: "ins-shift", 12: "serve-mid", 13: "serve-end"}
+         11: "commit", 4: "insert", 14: "ins-search", 15: "ins-shift", 12: "serve-mid", 13: "serve-end",
+         16: "refill"}
 print("  cycles per batch (mean over wgs): " + ", ".join(f"{v} {np.mean(pf[:, k] / nb):.0f}" for k, v in names.items()))
 print(f"  per batch: {np.mean(pf[:, 3] / nb):.2f} windows, {np.mean(pf[:, 2] / nb):.2f} full-queue runs, "
-      f"{np.mean(pf[:, 5] / nb):.2f} inserted items, {np.mean(pf[:, 6] / nb):.2f} shift chunks")
+      f"{np.mean(pf[:, 5] / nb):.2f} inserted items, {np.mean(pf[:, 6] / nb):.2f} shift chunks, "
+      f"{np.mean(pf[:, 17] / nb):.2f} refill rounds, {np.mean(pf[:, 18] / nb):.2f} refilled items, "
+      f"{np.mean(pf[:, 19] / nb):.2f} pool appends")
 shapes = workloads.storm_shapes(a.peers) if a.workload == "storm" else None
 print("  slowest workgroups (= sources):")
 for i in np.argsort(-tot)[:a.top]:
     line = (f"    src {src_of[i]:7d} start {start[i]:7.1f} us {tot[i]:8.1f} us  batches {nbat[i]:3d}  "
-            f"q {st[i, 7] >> 32}/{st[i, 7] & 0xffffffff}  win x{pf[i, 3]} items {pf[i, 5]} chunks {pf[i, 6]}  "
+            f"q {st[i, 7] >> 32}/{st[i, 7] & 0xffffffff}  win x{pf[i, 3]} items {pf[i, 5]} chunks {pf[i, 6]} "
+            f"refills {pf[i, 17]}/{pf[i, 18]} pool+ {pf[i, 19]}  "
             + " ".join(f"{v} {pf[i, k] // nb[i]}" for k, v in names.items()))
     if shapes:
         s = shapes[src_of[i]]

@@ -298,6 +298,8 @@ struct tgsim_engine_s {
   uint64_t sim_launches = 0;
   bool stamps_on = false;
   DevBuf<uint32_t> d_order;  // dispatch order of the next k_sim, computed behind this one
+  DevBuf<uint32_t> d_work;   // sparse steps: k_sim_open's deferred sources, [0] = count, then ids
+  int sparse_mode = -1;      // TGSIM_SPARSE: -1 auto, 0 never, 1 always
   bool order_valid = false;
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
@@ -770,11 +772,25 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     }
     a.dst_cnt = reinterpret_cast<unsigned long long*>(E->d_lcnt.p);
   }
+  // Sparse steps (few packets per source, or more sources than the order kernel ranks): open
+  // queues run in the small-LDS k_sim_open, the rest in k_sim_list; dense steps: k_sim in
+  // heavy-first order.  The results are the same either way.
+  const bool sparse = E->sparse_mode == 1 ||
+                      (E->sparse_mode < 0 && (E->S > kOrderMaxSources || E->n_in < 16ull * E->S));
+  a.worklist = a.worklist_n = nullptr;
+  if (sparse) {
+    HIPCHK(E->d_work.ensure(static_cast<size_t>(E->S) + 1));
+    HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t), E->st));
+    a.worklist_n = E->d_work.p;
+    a.worklist = E->d_work.p + 1;
+    a.order = nullptr;  // (stamps, when on, are indexed by source: n_wg = S)
+  }
   hipEvent_t ev0, ev1;
   HIPCHK(take_event(E, &ev0));
   HIPCHK(take_event(E, &ev1));
   HIPCHK(hipEventRecord(ev0, E->st));
-  launch_sim(a, n_wg, E->st);
+  if (sparse) launch_sim_sparse(a, E->st);
+  else launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.emplace_back(ev0, ev1);
@@ -794,7 +810,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   }
   // heavy-first dispatch order for the next step: it shortens the tail when only a few rounds of
   // workgroups fit; with many more sources than resident workgroups the dispatcher balances alone
-  if (ordered) {
+  if (ordered && !sparse) {
     HIPCHK(E->d_order.ensure(E->S));
     launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
     HIPCHK(hipGetLastError());
@@ -1154,6 +1170,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
     if ((rc = E->hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return bail(rc);
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
+  if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
   E->ip6_set.assign(E->N, 0);
   E->ip6.resize(E->N);
@@ -1240,7 +1257,7 @@ void tgsim_destroy(void* e) {
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
-  E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release();
+  E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
   for (auto& pr : E->ev_pending) {

@@ -87,13 +87,16 @@ __device__ __forceinline__ bool item_lt(const uint4& a, const uint4& b) {
 //   5. admitted items are merged into the sorted queue (binary search + tail shift).
 // Sources with correlated draws (get_crandom, rho != 0) consume state in admission order and take
 // the per-packet path built from the same wave-wide primitives.
-struct SimLds {
-  uint4 slot[kHeapCap];     // circular: departure ring, then the sorted eligibility queue
+template <uint32_t kCap>
+struct SimLdsT {
+  uint4 slot[kCap];         // circular: departure ring, then the eligibility queue (near, pool)
 };
-static_assert(sizeof(SimLds) <= 65536, "simulate workgroup LDS");
+static_assert(sizeof(SimLdsT<kHeapCap>) <= 65536, "simulate workgroup LDS");
+// Sources whose whole step fits an open queue (the netem limit cannot be reached: sparse senders
+// such as the gossip flood) run in k_sim_open with a 256-slot LDS queue, 4 KiB instead of 16.
+constexpr uint32_t kOpenCap = 256;
 
 constexpr uint32_t kFvPass = 0xFFu;
-constexpr uint32_t kSlotMask = kHeapCap - 1;
 
 __device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
@@ -234,8 +237,8 @@ __device__ __forceinline__ void wave_lds_sync() {
   __asm__ volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ void stamp(const SimArgs& a, uint32_t lane, uint32_t k, uint64_t v) {
-  if (a.stamps && lane == 0) a.stamps[(size_t)blockIdx.x * kStampSlots + k] = v;
+__device__ __forceinline__ void stamp(const SimArgs& a, uint32_t wg, uint32_t lane, uint32_t k, uint64_t v) {
+  if (a.stamps && lane == 0) a.stamps[(size_t)wg * kStampSlots + k] = v;
 }
 
 #ifdef TGSIM_PROFILE
@@ -250,8 +253,10 @@ __device__ __forceinline__ void stamp(const SimArgs& a, uint32_t lane, uint32_t 
 
 // Wave-uniform queue state of the source plus the helpers that operate on it.  Every member is
 // identical in all 64 lanes; per-lane scratch is passed in and out.
+template <uint32_t kCap>
 struct SimQueue {
-  SimLds& lds;
+  static constexpr uint32_t kSlotMask = kCap - 1;
+  SimLdsT<kCap>& lds;
   const SrcParams& p;
   uint32_t lane;
   uint32_t rh, rn, qn, pn;  // ring head slot, ring length, near-region length, pool length
@@ -264,7 +269,7 @@ struct SimQueue {
   uint32_t sched, corrupted, lost;
   uint64_t bytes;
 #ifdef TGSIM_PROFILE
-  uint64_t pf[16];
+  uint64_t pf[24];
 #endif
 
   __device__ __forceinline__ uint4& slot(uint32_t k) { return lds.slot[(rh + k) & kSlotMask]; }
@@ -353,6 +358,7 @@ struct SimQueue {
     if (!m) return;
     if (far) slot(rn + qn + pn + (uint32_t)__popcll(m & ((1ull << lane) - 1))) = it;
     pn += (uint32_t)__popcll(m);
+    PROF_CNT(19, (uint32_t)__popcll(m));
     wave_lds_sync();
   }
 
@@ -375,7 +381,10 @@ struct SimQueue {
   // land at its end: every pool item is >= B > every near item.  More than 64 pool items below h
   // itself take several rounds.
   __device__ __forceinline__ void refill(uint64_t h) {
+    if (!(pn && B < h)) return;
+    PROF_T0(rf);
     while (pn && B < h) {
+      PROF_CNT(17, 1);
       constexpr int kCand = 11;
       uint32_t cnt[kCand];
 #pragma unroll
@@ -443,9 +452,11 @@ struct SimQueue {
       }
       wave_lds_sync();
       pn -= nx;  // the pool now starts nx slots further; those slots are free
+      PROF_CNT(18, nx);
       insert_near(lane < nx, xv, false);
       if (total <= kWave) B = Bp;
     }
+    PROF_ADD(16, rf);
   }
 
   // Merges the lanes' new items (has) into the sorted near region: each item's position among
@@ -640,16 +651,17 @@ __device__ __forceinline__ uint4 make_item(uint64_t e, uint32_t len, uint32_t fl
   return make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst);
 }
 
-__global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
-  __shared__ SimLds lds;
+// One source's step (K1-K4), run by one wavefront.  kOpen: the caller has checked that the step
+// is an open queue without correlated draws, so only the open path is compiled in (fewer
+// registers, a kCap-slot LDS queue).  wg: the slot of the stamps and the statistics copy.
+template <bool kOpen, uint32_t kCap>
+__device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds) {
   const uint32_t lane = threadIdx.x;
-  // heavy-first dispatch order (previous step's HTB work per source), identity when absent
-  const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
-  if (s >= a.n_src) return;
-  stamp(a, lane, 0, __builtin_amdgcn_s_memrealtime());
+  constexpr uint32_t kSlotMask = kCap - 1;
+  stamp(a, wg, lane, 0, __builtin_amdgcn_s_memrealtime());
   const SrcParams pp = a.params[s];
   const SrcState st = a.state[s];  // dead after the set-up: the end writes a fresh state
-  SimQueue Q{lds, pp, lane};
+  SimQueue<kCap> Q{lds, pp, lane};
   Q.rh = 0;
   Q.rn = st.ring_n;
   Q.qn = st.near_n;
@@ -662,7 +674,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
 #ifdef TGSIM_PROFILE
-  for (int k = 0; k < 16; ++k) Q.pf[k] = 0;
+  for (int k = 0; k < 24; ++k) Q.pf[k] = 0;
   uint64_t* pf = Q.pf;
 #endif
   // ---- load the departure ring (compacted) and the sorted eligibility queue into LDS
@@ -672,16 +684,16 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     const uint32_t rn = Q.rn, qn = Q.qn + Q.pn;
     // every load of the ring and the queue in flight before the first LDS write (one HBM
     // latency instead of one per 256 slots)
-    uint64_t rv[kHeapCap / kWave];
-    uint4 qv[kHeapCap / kWave];
+    uint64_t rv[kCap / kWave];
+    uint4 qv[kCap / kWave];
 #pragma unroll
-    for (uint32_t u = 0; u < kHeapCap / kWave; ++u) {
+    for (uint32_t u = 0; u < kCap / kWave; ++u) {
       const uint32_t k = u * kWave + lane;
       rv[u] = k < rn ? gr[k] : 0ull;
       qv[u] = k < qn ? gh[k] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (uint32_t u = 0; u < kHeapCap / kWave; ++u) {
+    for (uint32_t u = 0; u < kCap / kWave; ++u) {
       const uint32_t k = u * kWave + lane;
       if (k < rn) *reinterpret_cast<uint2*>(&lds.slot[k]) = make_uint2((uint32_t)rv[u], (uint32_t)(rv[u] >> 32));
       if (k < qn) lds.slot[(rn + k) & kSlotMask] = qv[u];
@@ -700,7 +712,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   // in SGPRs through the loop): 16-bit fields, verdicts 0..3 in vc_lo and 4..7 in vc_hi, emptied
   // into the statistics every 2^14 batches (at most 2 counts per lane and batch), before a field
   // can overflow
-  unsigned long long* const sc = a.stats + (size_t)(blockIdx.x % kStatCopies) * kStSlots;
+  unsigned long long* const sc = a.stats + (size_t)(wg % kStatCopies) * kStSlots;
   if (lane == 0 && (Q.qn | Q.pn | Q.rn))  // the queue state loaded (the stored part is added at the end)
     atomicAdd(&sc[kStQueue], (unsigned long long)(16ull * (Q.qn + Q.pn) + 8ull * Q.rn));
   uint64_t vc_lo = 0, vc_hi = 0;
@@ -719,12 +731,12 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   // every pool item is >= the B of the previous step > every near item, so both of these are
   // valid boundaries; with an empty near region every new item starts in the pool
   Q.B = Q.qn ? (w0_of(Q.slot(Q.rn + Q.qn - 1)) & kEMask) + 1 : a.t0_ns;
-  stamp(a, lane, 1, __builtin_amdgcn_s_memrealtime());
+  stamp(a, wg, lane, 1, __builtin_amdgcn_s_memrealtime());
 
   const uint32_t n_batches = (uint32_t)((send - sbeg + kWave - 1) / kWave);
   // open queue: even if every offered packet and its clone were admitted the queue would stay
   // below the netem limit (sparse sources: gossip, ping-pong, splitbrain)
-  const bool open_q = !corr && (uint64_t)Q.rn + Q.qn + Q.pn + 2 * (send - sbeg) < lim;
+  const bool open_q = kOpen || (!corr && (uint64_t)Q.rn + Q.qn + Q.pn + 2 * (send - sbeg) < lim);
   uint64_t T_enq = 0;  // open queue: offer time of the last packet that reached the netem enqueue
   uint64_t idx = sbeg + lane;
   InRec rec = {}, rec2 = {};  // records of batches b and b + 1 (two batches in flight)
@@ -745,7 +757,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     else if (staged) fv = filter(a, pp, src_on, r.dst);
     if (!staged) fv = 0u;
     uint32_t vout = 0xF0u | fv;  // verdict byte (final for filtered packets)
-    if (!corr) {
+    if (kOpen || !corr) {
       // ---------- parallel phase: every decision that does not depend on queue state
       bool cand = false, reo_o = false;
       uint32_t cst = 0, flo = 0, flc = TGSIM_FLAG_DUP;
@@ -800,8 +812,8 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         if (mc) T_enq = readlane64(T, 63u - (uint32_t)__builtin_clzll(mc));
       }
       // ---------- windows
-      uint64_t pend = open_q ? 0ull : __ballot(cand);
-      while (pend) {
+      uint64_t pend = (kOpen || open_q) ? 0ull : __ballot(cand);
+      if constexpr (!kOpen) while (pend) {
         PROF_CNT(3, 1);
         if (Q.rn + Q.qn + Q.pn >= lim) {
           // full queue: nothing changes before the next eligibility or departure time, so every
@@ -974,7 +986,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
         if (mwin) pend &= lw >= 63u ? 0ull : ~((1ull << (lw + 1)) - 1);
       }
       PROF_ADD(1, w);
-    } else {
+    } else if constexpr (!kOpen) {
       // ---------- correlated draws: per-packet netem_enqueue in order, wave-wide queue ops
       uint4 r0 = make_uint4(0, 0, 0, 0), r2 = make_uint4(0, 0, 0, 0);
       uint32_t r1x = 0;
@@ -1048,7 +1060,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     }
     if ((b & 0x3FFFu) == 0x3FFFu) flush_verdicts();
   }
-  stamp(a, lane, 2, __builtin_amdgcn_s_memrealtime());
+  stamp(a, wg, lane, 2, __builtin_amdgcn_s_memrealtime());
   if (open_q && T_enq) {  // what the last enqueue saw: service before its offer time, then departures
     Q.serve_until(T_enq);
     Q.depart_before(T_enq);
@@ -1057,7 +1069,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   Q.serve_until(a.horizon_ns);
   PROF_ADD(13, e);
   if (lane == 0) a.emit_n[s] = Q.n_emit;
-  stamp(a, lane, 3, __builtin_amdgcn_s_memrealtime());
+  stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   // ---- write back the compacted ring, the sorted queue and the state
   {
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
@@ -1076,12 +1088,12 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
     ns.last_reo = last_reo;
     a.state[s] = ns;
   }
-  stamp(a, lane, 4, __builtin_amdgcn_s_memrealtime());
-  stamp(a, lane, 5, ((uint64_t)s << 32) | n_batches);
-  stamp(a, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
-  stamp(a, lane, 7, ((uint64_t)(Q.qn + Q.pn) << 32) | Q.rn);
+  stamp(a, wg, lane, 4, __builtin_amdgcn_s_memrealtime());
+  stamp(a, wg, lane, 5, ((uint64_t)s << 32) | n_batches);
+  stamp(a, wg, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
+  stamp(a, wg, lane, 7, ((uint64_t)(Q.qn + Q.pn) << 32) | Q.rn);
 #ifdef TGSIM_PROFILE
-  for (int k = 0; k < 16; ++k) stamp(a, lane, 8 + k, Q.pf[k]);
+  for (int k = 0; k < 24; ++k) stamp(a, wg, lane, 8 + k, Q.pf[k]);
 #endif
   const uint32_t sched = readlane32((uint32_t)scan_sum_i32((int32_t)Q.sched), kWave - 1);
   const uint32_t corrupted = readlane32((uint32_t)scan_sum_i32((int32_t)Q.corrupted), kWave - 1);
@@ -1104,6 +1116,43 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
       if (a.err_host)  // the host's pinned copy (sticky; read at its sync points)
         __hip_atomic_store(a.err_host, (uint64_t)kErrTimeOverflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
+  __shared__ SimLdsT<kHeapCap> lds;
+  // heavy-first dispatch order (previous step's HTB work per source), identity when absent
+  const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
+  if (s >= a.n_src) return;
+  sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
+}
+
+// Sparse steps (many sources, few packets each): every source whose step is an open queue that
+// fits kOpenCap slots runs here; the others are appended to the worklist for k_sim_list.  Both
+// produce exactly what k_sim would: every source's step is independent of the others'.
+__global__ __launch_bounds__(kWave) void k_sim_open(SimArgs a) {
+  __shared__ SimLdsT<kOpenCap> lds;
+  const uint32_t s = blockIdx.x;
+  if (s >= a.n_src) return;
+  const SrcState st = a.state[s];
+  const SrcParams& p = a.params[s];
+  const uint64_t occ = (uint64_t)st.ring_n + st.heap_n + 2 * (a.off[s + 1] - a.off[s]);
+  if ((p.rho_dup | p.rho_cor | p.rho_reo) != 0 || occ >= a.queue_limit || occ > kOpenCap) {
+    if (threadIdx.x == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
+    return;
+  }
+  sim_source<true, kOpenCap>(a, s, s, lds);
+}
+
+// The general path for the worklist k_sim_open left: a grid-stride loop over the list (its length
+// is read on the device, so the launch needs no host round trip).
+__global__ __launch_bounds__(kWave) void k_sim_list(SimArgs a) {
+  __shared__ SimLdsT<kHeapCap> lds;
+  const uint32_t n = *a.worklist_n;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t s = a.worklist[i];
+    sim_source<false, kHeapCap>(a, s, s, lds);
+    wave_lds_sync();  // the write-back's LDS reads are done before the next source's loads land
   }
 }
 
@@ -1803,6 +1852,12 @@ __global__ __launch_bounds__(256) void k_metrics_dst(const tgsim_delivery* recs,
 // Host-side launchers.
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
+}
+
+void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
+  if (!a.n_src) return;
+  hipLaunchKernelGGL(k_sim_open, dim3(a.n_src), dim3(kWave), 0, st, a);
+  hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
 }
 
 void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream_t st) {

@@ -514,3 +514,45 @@ def test_three_shards_slotted_exchange_equal_one():
     for r, s in enumerate(shards):
         sel = (pk["src"] >= bounds[r]) & (pk["src"] < bounds[r + 1])
         assert (s.verdicts() == v_ref[sel]).all()
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_sparse_and_dense_kernels_agree(make_oracle, monkeypatch, mode):
+    """The same steps through the dense k_sim (TGSIM_SPARSE=0) and through k_sim_open + k_sim_list
+    (TGSIM_SPARSE=1: open queues in the small-LDS kernel, the rest deferred to the worklist):
+    bit-exact with the oracle either way, on a mix of sparse and dense, correlated and plain
+    senders."""
+    monkeypatch.setenv("TGSIM_SPARSE", mode)
+    n = 200
+    rng = np.random.default_rng(41)
+    g, c = both(make_oracle, n, queue_limit=300, lookahead_ns=200_000)
+    shapes = wl.storm_shapes(n, 3)
+    for i, s in enumerate(shapes):
+        if i % 7 == 0:
+            s.DuplicateCorr, s.CorruptCorr = 30.0, 20.0
+        s.Latency = int(rng.integers(0, 8)) * nw.Millisecond
+        for e in (g, c):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=s))
+    seq = np.zeros(n, dtype=np.uint32)
+    for step in range(5):
+        # a few heavy senders, many light ones
+        heavy = rng.random(n) < 0.1
+        m = 20_000
+        src = np.where(rng.random(m) < 0.7, rng.choice(np.nonzero(heavy)[0], m), rng.integers(0, n, m))
+        pk = np.zeros(m, dtype=abi.PKT_DTYPE)
+        pk["src"] = src
+        pk["dst"] = (src + 1 + rng.integers(0, n - 1, m)) % n
+        pk["len"] = rng.integers(40, 1500, m)
+        pk["tick"] = rng.integers(0, 3000, m)
+        order = np.lexsort((pk["tick"], src))
+        counts = np.bincount(src, minlength=n)
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        sq = np.empty(m, dtype=np.uint32)
+        sq[order] = np.arange(m) - starts[src[order]] + seq[src[order]]
+        seq += counts.astype(np.uint32)
+        pk["seq"] = sq
+        g.submit(pk)
+        c.submit(pk)
+        g.step(3000)
+        c.step(3000)
+        assert_same(g, c, f"mode {mode} step {step}")
