@@ -298,7 +298,7 @@ struct tgsim_engine_s {
   uint64_t sim_launches = 0;
   bool stamps_on = false;
   DevBuf<uint32_t> d_order;  // dispatch order of the next k_sim, computed behind this one
-  DevBuf<uint32_t> d_work;   // sparse steps: k_sim_open's deferred sources, [0] = count, then ids
+  DevBuf<uint32_t> d_work;   // sparse steps: k_sim_sparse's deferred sources, [0] = count, then ids
   int sparse_mode = -1;      // TGSIM_SPARSE: -1 auto, 0 never, 1 always
   bool order_valid = false;
   DevBuf<uint64_t> d_stamps;
@@ -773,7 +773,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     a.dst_cnt = reinterpret_cast<unsigned long long*>(E->d_lcnt.p);
   }
   // Sparse steps (few packets per source, or more sources than the order kernel ranks): open
-  // queues run in the small-LDS k_sim_open, the rest in k_sim_list; dense steps: k_sim in
+  // queues run in the register-only k_sim_sparse, the rest in k_sim_list; dense steps: k_sim in
   // heavy-first order.  The results are the same either way.
   const bool sparse = E->sparse_mode == 1 ||
                       (E->sparse_mode < 0 && (E->S > kOrderMaxSources || E->n_in < 16ull * E->S));

@@ -103,8 +103,8 @@ struct SimArgs {
   uint64_t* stamps;         // diagnostics: kStampSlots s_memrealtime stamps per workgroup, or null
   unsigned long long* dst_cnt;  // single shard: per-destination histogram of the emitted records, or null
   uint64_t* err_host;       // pinned host word: the sticky error bits, or null
-  uint32_t* worklist;       // sparse steps: sources k_sim_open left for k_sim_list
-  uint32_t* worklist_n;     // their count (zeroed before k_sim_open)
+  uint32_t* worklist;       // sparse steps: sources k_sim_sparse left for k_sim_list
+  uint32_t* worklist_n;     // their count (zeroed before k_sim_sparse)
 };
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 

@@ -92,9 +92,6 @@ struct SimLdsT {
   uint4 slot[kCap];         // circular: departure ring, then the eligibility queue (near, pool)
 };
 static_assert(sizeof(SimLdsT<kHeapCap>) <= 65536, "simulate workgroup LDS");
-// Sources whose whole step fits an open queue (the netem limit cannot be reached: sparse senders
-// such as the gossip flood) run in k_sim_open with a 256-slot LDS queue, 4 KiB instead of 16.
-constexpr uint32_t kOpenCap = 256;
 
 constexpr uint32_t kFvPass = 0xFFu;
 
@@ -1127,25 +1124,272 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
 }
 
-// Sparse steps (many sources, few packets each): every source whose step is an open queue that
-// fits kOpenCap slots runs here; the others are appended to the worklist for k_sim_list.  Both
-// produce exactly what k_sim would: every source's step is independent of the others'.
-__global__ __launch_bounds__(kWave) void k_sim_open(SimArgs a) {
-  __shared__ SimLdsT<kOpenCap> lds;
+// Register-only form of an open-queue step (the sparse senders of a gossip flood): no LDS queue.
+// Every queued item (near and pool, up to 256) and every new item stay in registers; the items
+// HTB serves this step (e < horizon: at most 64, else the source is deferred) are gathered into
+// one lane each, ranked by key and served with one max-plus scan; what is not served is written
+// back as the pool (no order needed), the departure ring as the general path leaves it.  Exactly
+// the open path of sim_source: HTB serves in key order whatever the interleaving, the ring is
+// released up to the last enqueue's offer time, every candidate is admitted.  A source that does
+// not fit (correlated draws, a queue that could reach the limit, more than 64 offered packets, 256
+// queued items, 256 ring entries or 64 items to serve) writes nothing and goes to the worklist.
+constexpr uint32_t kSparseQ = 4;  // chunks of 64 queued items / ring entries held in registers
+__global__ __launch_bounds__(kWave) void k_sim_sparse(SimArgs a) {
   const uint32_t s = blockIdx.x;
   if (s >= a.n_src) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t below = (1ull << lane) - 1;
   const SrcState st = a.state[s];
-  const SrcParams& p = a.params[s];
-  const uint64_t occ = (uint64_t)st.ring_n + st.heap_n + 2 * (a.off[s + 1] - a.off[s]);
-  if ((p.rho_dup | p.rho_cor | p.rho_reo) != 0 || occ >= a.queue_limit || occ > kOpenCap) {
-    if (threadIdx.x == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
+  const SrcParams pp = a.params[s];
+  const uint64_t sbeg = a.off[s], send = a.off[s + 1];
+  const uint32_t n = (uint32_t)(send - sbeg);
+  const uint32_t rn = st.ring_n, qn = st.heap_n;
+  auto defer = [&]() {
+    if (lane == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
+  };
+  if ((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 || (uint64_t)rn + qn + 2ull * n >= a.queue_limit || n > kWave ||
+      qn > kSparseQ * kWave || rn > kSparseQ * kWave) {
+    defer();
     return;
   }
-  sim_source<true, kOpenCap>(a, s, s, lds);
+  const uint32_t src = a.shard_begin + s;
+  // ---- loads: the queue and the ring (whole chunks, masked), the offered packets
+  const uint4* gh = a.heap + (size_t)s * kHeapCap;
+  const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+  uint4 q[kSparseQ];
+  uint64_t rg[kSparseQ];
+#pragma unroll
+  for (uint32_t u = 0; u < kSparseQ; ++u) {
+    const uint32_t k = u * kWave + lane;
+    q[u] = k < qn ? gh[k] : make_uint4(0, 0, 0, 0);
+    rg[u] = k < rn ? gr[k] : ~0ull;
+  }
+  InRec r = {};
+  const bool staged = lane < n;
+  if (staged) r = a.in[sbeg + lane];
+  const uint64_t T = a.t0_ns + (uint64_t)r.tick * a.tick_ns;
+  const uint32_t len = r.len & 0xFFFFu;
+  // ---- filter and netem decisions (queue-independent; every candidate is admitted)
+  const bool src_on = a.enabled[src] != 0;
+  const bool plain = src_on && !a.any_disabled && pp.rule_n == 0;
+  const uint32_t ext_v = (pp.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE;
+  uint32_t fv = 0u;
+  if (staged) fv = plain ? (r.dst == TGSIM_EXTERNAL ? ext_v : kFvPass) : filter(a, pp, src_on, r.dst);
+  uint32_t vout = 0xF0u | fv;
+  bool cand = false;
+  uint32_t cst = 0, perr = 0;
+  uint4 io = make_uint4(0, 0, 0, 0), ic = make_uint4(0, 0, 0, 0);
+  if (staged && fv == kFvPass) {
+    uint32_t r0[4];
+    philox(src, r.dst, r.seq, 0, a.key0, a.key1, r0);
+    const int count = 1 + (pp.thr_dup && pp.thr_dup >= r0[0]) - (pp.thr_loss && pp.thr_loss >= r0[1]);
+    if (count == 0) {
+      vout = 0xF0u | TGSIM_V_LOSS;
+    } else {
+      cand = true;
+      if (count == 2) {
+        uint32_t r2[4];
+        philox(src, r.dst, r.seq, 2, a.key0, a.key1, r2);
+        if (pp.thr_loss && pp.thr_loss >= r2[0]) {
+          cst = 1;
+        } else {
+          cst = 2;
+          uint32_t flc = TGSIM_FLAG_DUP;
+          if (pp.thr_cor && pp.thr_cor >= r2[1]) flc |= TGSIM_FLAG_CORRUPT;
+          uint64_t ec = (pp.thr_reo && pp.thr_reo >= r2[2]) ? T : delayed(pp, T, r2[3]);
+          if (ec > kEMask) { perr = 1; ec = kEMask; }
+          ic = make_item(ec, len, flc, r.seq, r.dst);
+        }
+      }
+      const uint32_t flo = (pp.thr_cor && pp.thr_cor >= r0[2]) ? TGSIM_FLAG_CORRUPT : 0u;
+      const bool reo_o = pp.thr_reo && pp.thr_reo >= r0[3];
+      uint64_t eo = reo_o ? T : T + pp.lat_ns;
+      if (!reo_o && pp.sigma != 0) {
+        uint32_t r1[4];
+        philox(src, r.dst, r.seq, 1, a.key0, a.key1, r1);
+        eo = delayed(pp, T, r1[0]);
+      }
+      if (eo > kEMask) { perr = 1; eo = kEMask; }
+      io = make_item(eo, len, flo, r.seq, r.dst);
+      const uint32_t cv = cst == 0 ? TGSIM_V_NONE : cst == 1 ? TGSIM_V_LOSS : TGSIM_V_SCHEDULED;
+      vout = (cv << 4) | TGSIM_V_SCHEDULED;
+    }
+  }
+  const uint64_t mc = __ballot(cand);
+  const uint64_t T_enq = mc ? readlane64(T, 63u - (uint32_t)__builtin_clzll(mc)) : 0ull;
+  const uint64_t h = a.horizon_ns;
+  // ---- gather every item HTB serves this step (e < horizon) into lanes [0, ns)
+  uint4 x = make_uint4(0, 0, 0, 0);
+  uint32_t ns = 0;
+  bool over = false;
+  auto gather = [&](bool f, const uint4& v) {
+    const uint64_t m = __ballot(f);
+    if (!m) return;
+    const uint32_t k = (uint32_t)__popcll(m);
+    if (ns + k > kWave) {
+      over = true;
+      return;
+    }
+    const uint32_t to = (f ? ns + (uint32_t)__popcll(m & below) : ns + k + (uint32_t)__popcll(~m & below)) & (kWave - 1);
+    const uint4 pv = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.x),
+                                (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.y),
+                                (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.z),
+                                (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.w));
+    if (lane >= ns && lane < ns + k) x = pv;
+    ns += k;
+  };
+  bool due_q[kSparseQ];
+#pragma unroll
+  for (uint32_t u = 0; u < kSparseQ; ++u) {
+    due_q[u] = u * kWave + lane < qn && (w0_of(q[u]) & kEMask) < h;
+    gather(due_q[u], q[u]);
+  }
+  const bool due_o = cand && (w0_of(io) & kEMask) < h, due_c = cand && cst == 2 && (w0_of(ic) & kEMask) < h;
+  gather(due_o, io);
+  gather(due_c, ic);
+  // remaining items: everything not served, written back as the pool
+  uint32_t nrem = qn + (uint32_t)__popcll(mc) + (uint32_t)__popcll(__ballot(cand && cst == 2)) - ns;
+  if (over || nrem > kSparseQ * kWave) {
+    defer();
+    return;
+  }
+  // ---- rank the served items by (e, seq, clone first) and put each in its rank's lane
+  const bool hs = lane < ns;
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < ns; ++j) {
+    const uint4 o = make_uint4(readlane32(x.x, j), readlane32(x.y, j), readlane32(x.z, j), 0u);
+    rank += (hs && (item_lt(o, x) || (!item_lt(x, o) && j < lane))) ? 1u : 0u;
+  }
+  {
+    const uint32_t to = (hs ? rank : lane) & (kWave - 1);
+    x = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.x),
+                   (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.y),
+                   (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.z),
+                   (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.w));
+  }
+  // ---- HTB: d = max(e, TAT before), TAT' = max(TAT, e - burst) + cost, one max-plus scan
+  const uint64_t e = w0_of(x) & kEMask;
+  const uint32_t xlen = x.y >> 14 & 0xFFFFu;
+  const uint64_t c = ((uint64_t)xlen * pp.mult) >> (pp.shift_ext & 0xFFu);
+  uint64_t A = hs ? c : 0, Bm = hs ? (e > pp.burst_ns ? e - pp.burst_ns : 0) + c : 0;
+  scan_maxplus(A, Bm);
+  const uint64_t ta = st.tat + A;
+  const uint64_t tat_after = ta > Bm ? ta : Bm;
+  const uint64_t before = shr1_u64(tat_after, st.tat);
+  const uint64_t d = e > before ? e : before;
+  const uint64_t tat_end = ns ? readlane64(tat_after, ns - 1) : st.tat;
+  // ---- records of the served items (dead destinations leave the sender and are lost)
+  const bool live = hs && x.w != kDeadDst;
+  const uint64_t lm = __ballot(live);
+  const uint32_t n_live = (uint32_t)__popcll(lm);
+  tgsim_delivery* emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
+  uint32_t sched = 0, corrupted = 0, lost = 0;
+  uint64_t bytes = 0;
+  if (live) {
+    const uint32_t flags = x.y >> 30;
+    uint64_t* rw = reinterpret_cast<uint64_t*>(emit + (uint32_t)__popcll(lm & below));
+    rw[0] = d;
+    rw[1] = ((uint64_t)x.w << 32) | src;
+    rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
+    if (a.dst_cnt) atomicAdd(&a.dst_cnt[x.w], 1ull);
+    sched = 1;
+    bytes = xlen;
+    corrupted = (flags >> 1) & 1u;
+  } else if (hs) {
+    lost = 1;
+  }
+  // ---- the departure ring: old ring ++ served; the last enqueue (at T_enq, after serving the
+  // items eligible before it) released the prefix departing before T_enq
+  const uint32_t n1 = T_enq ? (uint32_t)__popcll(__ballot(hs && e < T_enq)) : 0u;
+  uint32_t k0 = 0;  // released prefix of old ring ++ served[0, n1)
+  if (T_enq) {
+    bool stop = false;
+#pragma unroll
+    for (uint32_t u = 0; u < kSparseQ; ++u) {
+      if (!stop && u * kWave < rn) {
+        const uint64_t m = __ballot(u * kWave + lane < rn && rg[u] >= T_enq);
+        const uint32_t cnt = rn - u * kWave < kWave ? rn - u * kWave : kWave;
+        if (m) {
+          k0 += (uint32_t)__builtin_ctzll(m);
+          stop = true;
+        } else {
+          k0 += cnt;
+        }
+      }
+    }
+    if (!stop) {
+      const uint64_t m = __ballot(lane < n1 && d >= T_enq);
+      k0 += m ? (uint32_t)__builtin_ctzll(m) : n1;
+    }
+  }
+  // ---- write back: the ring from k0 on, then the pool of unserved items; the state
+  uint64_t* wr = a.ring + (size_t)s * kHeapCap;
+#pragma unroll
+  for (uint32_t u = 0; u < kSparseQ; ++u) {
+    const uint32_t k = u * kWave + lane;
+    if (k < rn && k >= k0) wr[k - k0] = rg[u];
+  }
+  const uint32_t old_kept = rn > k0 ? rn - k0 : 0u;  // old entries still in the ring
+  const uint32_t sk0 = k0 > rn ? k0 - rn : 0u;        // served entries released
+  if (hs && lane >= sk0) wr[old_kept + lane - sk0] = d;
+  const uint32_t rn_new = old_kept + ns - sk0;
+  uint4* wq = a.heap + (size_t)s * kHeapCap;
+  uint32_t wpos = 0;
+  auto keep = [&](bool f, const uint4& v) {
+    const uint64_t m = __ballot(f);
+    if (f) wq[wpos + (uint32_t)__popcll(m & below)] = v;
+    wpos += (uint32_t)__popcll(m);
+  };
+#pragma unroll
+  for (uint32_t u = 0; u < kSparseQ; ++u) keep(u * kWave + lane < qn && !due_q[u], q[u]);
+  keep(cand && !due_o, io);
+  keep(cand && cst == 2 && !due_c, ic);
+  if (lane == 0) {
+    SrcState ns_;
+    ns_.tat = tat_end;
+    ns_.heap_n = wpos;
+    ns_.near_n = 0;  // all of it pool
+    ns_.ring_n = rn_new;
+    ns_.last_dup = st.last_dup;
+    ns_.last_cor = st.last_cor;
+    ns_.last_reo = st.last_reo;
+    a.state[s] = ns_;
+    a.emit_n[s] = n_live;
+  }
+  if (staged) a.verdict[sbeg + lane] = (uint8_t)vout;
+  // ---- statistics (per-lane counts reduced over the wave)
+  const uint32_t vo = vout & 15u, vc = vout >> 4;
+  uint32_t vcnt = 0;  // lane v < 8: packets and clones with verdict v
+#pragma unroll
+  for (uint32_t v = 0; v < 8; ++v) {
+    const uint32_t t = ballot_count(staged && vo == v) + ballot_count(staged && vc == v);
+    if (lane == v) vcnt = t;
+  }
+  const uint32_t t_sched = ballot_count(sched != 0), t_cor = ballot_count(corrupted != 0), t_lost = ballot_count(lost != 0);
+  const uint32_t t_clone = ballot_count(staged && vc != TGSIM_V_NONE);
+  const uint64_t t_bytes = wave_sum(bytes);
+  const bool err = __ballot(perr != 0) != 0;
+  unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
+  if (lane < 8 && vcnt) atomicAdd(&sc[kStVerdict0 + lane], (unsigned long long)vcnt);
+  if (lane == 0) {
+    const uint64_t qb = 16ull * qn + 8ull * rn + 16ull * wpos + 8ull * rn_new;
+    if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
+    if (t_sched) atomicAdd(&sc[kStScheduled], (unsigned long long)t_sched);
+    if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
+    if (t_cor) atomicAdd(&sc[kStCorrupted], (unsigned long long)t_cor);
+    if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
+    if (t_bytes) atomicAdd(&sc[kStBytes], (unsigned long long)t_bytes);
+    if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
+    if (err) {
+      atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
+      if (a.err_host)
+        __hip_atomic_store(a.err_host, (uint64_t)kErrTimeOverflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
-// The general path for the worklist k_sim_open left: a grid-stride loop over the list (its length
-// is read on the device, so the launch needs no host round trip).
+// The general path for the worklist k_sim_sparse left: a grid-stride loop over the list (its
+// length is read on the device, so the launch needs no host round trip).
 __global__ __launch_bounds__(kWave) void k_sim_list(SimArgs a) {
   __shared__ SimLdsT<kHeapCap> lds;
   const uint32_t n = *a.worklist_n;
@@ -1856,7 +2100,7 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
 
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
   if (!a.n_src) return;
-  hipLaunchKernelGGL(k_sim_open, dim3(a.n_src), dim3(kWave), 0, st, a);
+  hipLaunchKernelGGL(k_sim_sparse, dim3(a.n_src), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
 }
 

@@ -25,7 +25,7 @@ struct RouteArgsHost {
 };
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
-// sparse step: k_sim_open over every source, then k_sim_list over the ones it deferred
+// sparse step: k_sim_sparse over every source, then k_sim_list over the ones it deferred
 void launch_sim_sparse(const SimArgs& a, hipStream_t st);
 // no-op above kOrderMax (32768) sources
 void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream_t st);

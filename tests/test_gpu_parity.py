@@ -518,8 +518,8 @@ def test_three_shards_slotted_exchange_equal_one():
 
 @pytest.mark.parametrize("mode", ["0", "1"])
 def test_sparse_and_dense_kernels_agree(make_oracle, monkeypatch, mode):
-    """The same steps through the dense k_sim (TGSIM_SPARSE=0) and through k_sim_open + k_sim_list
-    (TGSIM_SPARSE=1: open queues in the small-LDS kernel, the rest deferred to the worklist):
+    """The same steps through the dense k_sim (TGSIM_SPARSE=0) and through k_sim_sparse + k_sim_list
+    (TGSIM_SPARSE=1: open queues in the register-only kernel, the rest deferred to the worklist):
     bit-exact with the oracle either way, on a mix of sparse and dense, correlated and plain
     senders."""
     monkeypatch.setenv("TGSIM_SPARSE", mode)
