@@ -54,7 +54,7 @@ ph = np.diff(st[:, :5], axis=1) * 10 / 1000  # us (100 MHz)
 tot = (st[:, 4] - st[:, 0]) * 10 / 1000
 print(f"{a.workload} steps={a.steps} peers={a.peers} lam={a.lam} ql={a.ql} wgs={len(st)} "
       f"kernel span {(st[:, 4].max() - t0) * 10 / 1e6:.3f} ms")
-for name, col in zip(["load", "batches", "end_htb", "writeback"], ph.T):
+for name, col in zip(["load", "batches", "end_htb", "writeback"] if a.workload == "storm" else ["lvl1", "lvl2+draws", "gather+htb", "writes"], ph.T):
     print(f"  {name:10s} mean {col.mean():8.2f} us  p50 {np.median(col):8.2f}  max {col.max():8.2f}")
 print(f"  total      mean {tot.mean():8.2f} us  p50 {np.median(tot):8.2f}  max {tot.max():8.2f}")
 src_of = st[:, 5] >> 32

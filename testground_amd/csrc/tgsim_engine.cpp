@@ -165,7 +165,7 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    size_t c = n < 64 ? 64 : n + n / 4;
+    size_t c = n < 64 ? 64 : n + n / 2;  // growing buffers (gossip windows) reallocate rarely
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
     if (e == hipSuccess) cap = c;
     return e;
@@ -210,6 +210,10 @@ struct tgsim_engine_s {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
   std::vector<hipEvent_t> ev_pool;
   uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
+  uint64_t* h_pub = nullptr;    // pinned words a scan publishes: [0] total, [1] flag, [2] sequence
+  uint64_t* dm_pub = nullptr;
+  uint64_t pub_seq = 0;
+  hipEvent_t ev_pub = nullptr;
   uint64_t* h_err = nullptr;    // pinned host word k_sim stores the sticky error bits into
   uint64_t* d_err_host = nullptr;  // its device address
   uint32_t* h_xerr = nullptr;   // pinned sticky flag: a slotted exchange chunk overflowed (k_route_edges)
@@ -637,17 +641,28 @@ int stage_host_input(Eng* E, uint32_t n_ticks) {
 }
 
 // Device exclusive scan of cnt[0..n) into off[0..n] (off[n] = total); returns total on host.
+int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev);
+
+// Device exclusive scan of cnt[0..n) into off[0..n] (off[n] = total); returns total on host.  The
+// total (and *flag, when given) reach the host through pinned words the device publishes behind a
+// sequence number: the host spins on them instead of synchronizing the stream, whose wake-up can
+// lag the device by hundreds of microseconds (the closed gossip loop pays it every window).
 int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uint64_t>& blk,
                 DevBuf<uint64_t>& tot, uint64_t n, uint64_t* total, uint64_t* pos = nullptr,
-                hipStream_t stream = nullptr) {
+                hipStream_t stream = nullptr, const uint32_t* flag = nullptr, uint32_t* flag_out = nullptr) {
   hipStream_t sq = stream ? stream : E->st;
   HIPCHK(off.ensure(n + 1));
   HIPCHK(blk.ensure((n + 1023) / 1024 + 1));
   HIPCHK(tot.ensure(1));
   launch_scan(cnt.p, off.p, n, blk.p, tot.p, sq, pos);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(total, tot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
-  HIPCHK(hipStreamSynchronize(sq));
+  launch_publish(tot.p, flag, E->dm_pub, ++E->pub_seq, sq);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(E->ev_pub, sq));
+  int rc = wait_published(E, &E->h_pub[2], E->pub_seq, E->ev_pub);
+  if (rc) return rc;
+  *total = __atomic_load_n(&E->h_pub[0], __ATOMIC_ACQUIRE);
+  if (flag_out) *flag_out = static_cast<uint32_t>(__atomic_load_n(&E->h_pub[1], __ATOMIC_ACQUIRE));
   return 0;
 }
 
@@ -1158,6 +1173,13 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
     return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_gerr), sizeof(uint32_t)), "pinned"))) return bail(rc);
   *E->h_gerr = 0;
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_pub), 4 * sizeof(uint64_t),
+                                 hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
+    return bail(rc);
+  memset(E->h_pub, 0, 4 * sizeof(uint64_t));
+  if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->dm_pub), E->h_pub, 0), "pinned")))
+    return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_pub, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_err_host), E->h_err, 0), "pinned")))
     return bail(rc);
 
@@ -1268,6 +1290,8 @@ void tgsim_destroy(void* e) {
   if (E->h_err) (void)hipHostFree(E->h_err);
   if (E->h_xerr) (void)hipHostFree(E->h_xerr);
   if (E->h_gerr) (void)hipHostFree(E->h_gerr);
+  if (E->h_pub) (void)hipHostFree(E->h_pub);
+  if (E->ev_pub) (void)hipEventDestroy(E->ev_pub);
   if (E->h_edges) (void)hipHostFree(E->h_edges);
   for (hipEvent_t ev : E->ev_route)
     if (ev) (void)hipEventDestroy(ev);
@@ -1392,6 +1416,18 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
     HIPCHK(hipStreamSynchronize(E->st));  // `t` lives on this stack frame
   }
   HIPCHK(hipStreamSynchronize(E->st));
+  // a flood's windows grow geometrically while it spreads: reserve the window buffers (generated
+  // input of two windows, the step's input and verdicts) for two forwards per peer and
+  // out-neighbour, so the first windows do not reallocate one after another (each hipFree +
+  // hipMalloc stalls the closed loop for 0.3-0.5 ms)
+  const size_t reserve = static_cast<size_t>(E->S) * g->degree * 2;
+  while (E->gen_free.size() < 2) E->gen_free.emplace_back();
+  for (auto& w : E->gen_free) {
+    HIPCHK(w.off.ensure(E->S + 1));
+    HIPCHK(w.in.ensure(reserve));
+  }
+  HIPCHK(E->d_in.ensure(reserve));
+  HIPCHK(E->d_verdict.ensure(reserve));
   E->gossip_on = true;
   return 0;
 }
@@ -1414,16 +1450,16 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   HIPCHK(E->d_cnt.ensure(E->S));
   launch_gossip(g, nullptr, 0, E->d_cnt.p, nullptr, nullptr, 1, E->st);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(E->h_gerr, E->d_gerr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
   uint64_t total = 0;
-  int rc = scan_counts(E, E->d_cnt, w.off, E->d_blk, E->d_tot, E->S, &total);  // synchronizes the stream
+  uint32_t late = 0;
+  int rc = scan_counts(E, E->d_cnt, w.off, E->d_blk, E->d_tot, E->S, &total, nullptr, nullptr, E->d_gerr.p, &late);
   if (rc) return rc;
-  if (*E->h_gerr) {
+  if (late) {
     E->gen_free.push_back(std::move(w));
     return E->fail(-EINVAL, "gossip: a receipt precedes the window at tick %llu (lookahead shorter than the window)",
                    static_cast<unsigned long long>(win0));
   }
-  HIPCHK(w.in.ensure(total ? total : 1));
+  HIPCHK(w.in.ensure(total ? total : 1));  // reserved by tgsim_gossip_init for typical windows
   launch_gossip(g, nullptr, 0, nullptr, w.off.p, w.in.p, 2, E->st);  // the step runs behind it on E->st
   HIPCHK(hipGetLastError());
   w.n = total;

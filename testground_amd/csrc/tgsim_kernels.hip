@@ -1134,11 +1134,18 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
 // not fit (correlated draws, a queue that could reach the limit, more than 64 offered packets, 256
 // queued items, 256 ring entries or 64 items to serve) writes nothing and goes to the worklist.
 constexpr uint32_t kSparseQ = 4;  // chunks of 64 queued items / ring entries held in registers
-__global__ __launch_bounds__(kWave) void k_sim_sparse(SimArgs a) {
+__global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
   const uint32_t s = blockIdx.x;
   if (s >= a.n_src) return;
   const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1;
+  stamp(a, s, lane, 0, __builtin_amdgcn_s_memrealtime());
+  // the first 64 queued items and ring entries are read before the state says how many there are
+  // (the arrays have room for 1024 per source): one dependent load level instead of two
+  const uint4* gh = a.heap + (size_t)s * kHeapCap;
+  const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+  const uint4 q0 = gh[lane];
+  const uint64_t r0 = gr[lane];
   const SrcState st = a.state[s];
   const SrcParams pp = a.params[s];
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
@@ -1153,13 +1160,14 @@ __global__ __launch_bounds__(kWave) void k_sim_sparse(SimArgs a) {
     return;
   }
   const uint32_t src = a.shard_begin + s;
-  // ---- loads: the queue and the ring (whole chunks, masked), the offered packets
-  const uint4* gh = a.heap + (size_t)s * kHeapCap;
-  const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+  stamp(a, s, lane, 1, __builtin_amdgcn_s_memrealtime());
+  // ---- loads: the rest of the queue and the ring (whole chunks, masked), the offered packets
   uint4 q[kSparseQ];
   uint64_t rg[kSparseQ];
+  q[0] = lane < qn ? q0 : make_uint4(0, 0, 0, 0);
+  rg[0] = lane < rn ? r0 : ~0ull;
 #pragma unroll
-  for (uint32_t u = 0; u < kSparseQ; ++u) {
+  for (uint32_t u = 1; u < kSparseQ; ++u) {
     const uint32_t k = u * kWave + lane;
     q[u] = k < qn ? gh[k] : make_uint4(0, 0, 0, 0);
     rg[u] = k < rn ? gr[k] : ~0ull;
@@ -1217,6 +1225,7 @@ __global__ __launch_bounds__(kWave) void k_sim_sparse(SimArgs a) {
   }
   const uint64_t mc = __ballot(cand);
   const uint64_t T_enq = mc ? readlane64(T, 63u - (uint32_t)__builtin_clzll(mc)) : 0ull;
+  stamp(a, s, lane, 2, __builtin_amdgcn_s_memrealtime());
   const uint64_t h = a.horizon_ns;
   // ---- gather every item HTB serves this step (e < horizon) into lanes [0, ns)
   uint4 x = make_uint4(0, 0, 0, 0);
@@ -1278,6 +1287,7 @@ __global__ __launch_bounds__(kWave) void k_sim_sparse(SimArgs a) {
   const uint64_t before = shr1_u64(tat_after, st.tat);
   const uint64_t d = e > before ? e : before;
   const uint64_t tat_end = ns ? readlane64(tat_after, ns - 1) : st.tat;
+  stamp(a, s, lane, 3, __builtin_amdgcn_s_memrealtime());
   // ---- records of the served items (dead destinations leave the sender and are lost)
   const bool live = hs && x.w != kDeadDst;
   const uint64_t lm = __ballot(live);
@@ -1357,6 +1367,9 @@ __global__ __launch_bounds__(kWave) void k_sim_sparse(SimArgs a) {
     a.emit_n[s] = n_live;
   }
   if (staged) a.verdict[sbeg + lane] = (uint8_t)vout;
+  stamp(a, s, lane, 4, __builtin_amdgcn_s_memrealtime());
+  stamp(a, s, lane, 5, ((uint64_t)s << 32) | n);
+  stamp(a, s, lane, 7, ((uint64_t)qn << 32) | rn);
   // ---- statistics (per-lane counts reduced over the wave)
   const uint32_t vo = vout & 15u, vc = vout >> 4;
   uint32_t vcnt = 0;  // lane v < 8: packets and clones with verdict v
@@ -1586,50 +1599,74 @@ __global__ __launch_bounds__(256) void k_gossip_recv_dev(GossipArgs g, const tgs
     gossip_recv_one(g, in[i]);
 }
 
-// Floods due in [win0, win0 + n_ticks) for local peer s: one wavefront per peer, lane f holds
-// flood f's earliest receipt tick (a coalesced 256-B read); late receipts are flagged.
-__device__ __forceinline__ bool gossip_due_lane(const GossipArgs& g, uint32_t s, uint32_t lane, uint32_t& t) {
-  const uint64_t done = g.fwd[s];
-  t = lane < g.n_floods ? g.first[(uint64_t)s * 64 + lane] : 0xFFFFFFFFu;
+// Floods due in [win0, win0 + n_ticks) for local peer s: lane f holds flood f's earliest receipt
+// tick (a coalesced 256-B row); late receipts are flagged.  One wavefront handles kGossipPeers
+// peers with all their rows in flight at once (one peer per wavefront left every wave waiting on
+// two dependent loads: the launch was latency-bound at a third of the HBM rate).
+constexpr uint32_t kGossipPeers = 8;
+__device__ __forceinline__ bool gossip_due(const GossipArgs& g, uint64_t done, uint32_t t, uint32_t lane) {
   const bool due = lane < g.n_floods && !(done >> lane & 1ull) && t != 0xFFFFFFFFu &&
                    (uint64_t)t < g.win0 + g.n_ticks;
   if (due && (uint64_t)t < g.win0) atomicOr(g.err, 1u);
   return due;
 }
 
+__device__ __forceinline__ void gossip_rows(const GossipArgs& g, uint32_t s0, uint32_t lane, uint32_t (&t)[kGossipPeers],
+                                            uint64_t (&done)[kGossipPeers]) {
+#pragma unroll
+  for (uint32_t i = 0; i < kGossipPeers; ++i) {
+    const uint32_t s = s0 + i;
+    done[i] = s < g.n_src ? g.fwd[s] : ~0ull;
+    t[i] = (s < g.n_src && lane < g.n_floods) ? g.first[(uint64_t)s * 64 + lane] : 0xFFFFFFFFu;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_gossip_count(GossipArgs g, uint64_t* counts) {
-  const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (s >= g.n_src) return;
-  uint32_t t;
-  const uint64_t due = __ballot(gossip_due_lane(g, s, lane, t));
-  if (lane == 0) counts[s] = (uint64_t)__popcll(due) * g.degree;
+  const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
+  if (s0 >= g.n_src) return;
+  uint32_t t[kGossipPeers];
+  uint64_t done[kGossipPeers];
+  gossip_rows(g, s0, lane, t, done);
+  uint64_t c = 0;  // lane i: the count of peer s0 + i
+#pragma unroll
+  for (uint32_t i = 0; i < kGossipPeers; ++i) {
+    const uint64_t n = (uint64_t)ballot_count(gossip_due(g, done[i], t[i], lane)) * g.degree;
+    if (lane == i) c = n;
+  }
+  if (lane < kGossipPeers && s0 + lane < g.n_src) counts[s0 + lane] = c;
 }
 
 __global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64_t* off, InRec* out) {
-  const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (s >= g.n_src) return;
-  uint32_t t;
-  const bool me = gossip_due_lane(g, s, lane, t);
-  const uint64_t due = __ballot(me);
-  if (!due) return;
-  if (lane == 0) g.fwd[s] |= due;
-  // earliest receipt first, ties by flood id (seq order within a tick)
-  uint32_t rank = 0;
-  for (uint64_t m = due; m; m &= m - 1) {
-    const uint32_t j = (uint32_t)__builtin_ctzll(m);
-    const uint32_t tj = readlane32(t, j);
-    rank += (tj < t || (tj == t && j < lane)) ? 1u : 0u;
-  }
-  if (!me) return;
-  const uint32_t src = g.shard_begin + s;
-  const uint64_t o = off[s] + (uint64_t)rank * g.degree;
-  for (uint32_t k = 0; k < g.degree; ++k) {
-    InRec rec;
-    rec.dst = gossip_neighbour(g, src, k);
-    rec.seq = lane * g.degree + k;
-    rec.tick = (uint32_t)(t - g.win0);
-    rec.len = g.msg_len;
-    out[o + k] = rec;
+  const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
+  if (s0 >= g.n_src) return;
+  uint32_t t[kGossipPeers];
+  uint64_t done[kGossipPeers];
+  gossip_rows(g, s0, lane, t, done);
+#pragma unroll
+  for (uint32_t i = 0; i < kGossipPeers; ++i) {
+    const uint32_t s = s0 + i;
+    const bool me = gossip_due(g, done[i], t[i], lane);
+    const uint64_t due = __ballot(me);
+    if (!due) continue;
+    if (lane == 0) g.fwd[s] |= due;
+    // earliest receipt first, ties by flood id (seq order within a tick)
+    uint32_t rank = 0;
+    for (uint64_t m = due; m; m &= m - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      const uint32_t tj = readlane32(t[i], j);
+      rank += (tj < t[i] || (tj == t[i] && j < lane)) ? 1u : 0u;
+    }
+    if (!me) continue;
+    const uint32_t src = g.shard_begin + s;
+    const uint64_t o = off[s] + (uint64_t)rank * g.degree;
+    for (uint32_t k = 0; k < g.degree; ++k) {
+      InRec rec;
+      rec.dst = gossip_neighbour(g, src, k);
+      rec.seq = lane * g.degree + k;
+      rec.tick = (uint32_t)(t[i] - g.win0);
+      rec.len = g.msg_len;
+      out[o + k] = rec;
+    }
   }
 }
 
@@ -2119,6 +2156,19 @@ void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint
   if (n_src) hipLaunchKernelGGL(k_purge, dim3((n_src + 3) / 4), dim3(256), 0, st, heap, state, n_src, gone);
 }
 
+// Publishes *v0 (and *v1 when given) into pinned host words, then the sequence number (release):
+// the host spins on slot[2] instead of synchronizing a stream.
+__global__ void k_publish(const uint64_t* v0, const uint32_t* v1, uint64_t* slot, uint64_t seq) {
+  __hip_atomic_store(&slot[0], *v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&slot[1], (uint64_t)(v1 ? *v1 : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __hip_atomic_store(&slot[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_publish(const uint64_t* v0, const uint32_t* v1, uint64_t* slot, uint64_t seq, hipStream_t st) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(1), 0, st, v0, v1, slot, seq);
+}
+
 void launch_signal(unsigned long long* table, uint64_t* mirror, uint32_t state, uint32_t n, uint64_t* result,
                    uint64_t* marker, uint64_t seq, hipStream_t st) {
   hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, st, table, mirror, state, n, result, marker, seq);
@@ -2154,7 +2204,8 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
     if (n) hipLaunchKernelGGL(k_gossip_recv, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, g, recs, n);
     return;
   }
-  const dim3 grid((g.n_src + 3) / 4), blk(256);  // one wavefront per peer
+  const uint32_t waves = (g.n_src + kGossipPeers - 1) / kGossipPeers;  // kGossipPeers peers per wavefront
+  const dim3 grid((waves + 3) / 4), blk(256);
   if (phase == 1) hipLaunchKernelGGL(k_gossip_count, grid, blk, 0, st, g, counts);
   else hipLaunchKernelGGL(k_gossip_write, grid, blk, 0, st, g, off, out);
 }

@@ -33,6 +33,8 @@ void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState
                       unsigned long long* stats, hipStream_t st);
 // marks queued items towards gone[dst] != 0 dead (kDeadDst)
 void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone, hipStream_t st);
+// *v0 (and *v1) into pinned slot[0], slot[1], then seq into slot[2] (system-scope release)
+void launch_publish(const uint64_t* v0, const uint32_t* v1, uint64_t* slot, uint64_t seq, hipStream_t st);
 // K7: table[state] += n; new value -> mirror[state] and *result (pinned), then *marker = seq
 void launch_signal(unsigned long long* table, uint64_t* mirror, uint32_t state, uint32_t n, uint64_t* result,
                    uint64_t* marker, uint64_t seq, hipStream_t st);
