@@ -802,7 +802,7 @@ int64_t tgo_metrics(void* p, uint32_t kind, uint64_t* out, size_t cap) {
     size_t n = kind == TGSIM_METRICS_SRC   ? (size_t)o->nsrc * TGSIM_METRICS_SRC_WORDS
                : kind == TGSIM_METRICS_DST ? (size_t)o->nsrc * TGSIM_METRICS_DST_WORDS
                                            : 2 * TGSIM_METRICS_BINS;
-    memcpy(out, b, sizeof(uint64_t) * (cap < n ? cap : n));
+    if (cap && n) memcpy(out, b, sizeof(uint64_t) * (cap < n ? cap : n));
     return (int64_t)n;
 }
 
@@ -817,13 +817,13 @@ static int step_core(oracle* o, uint32_t n_ticks) {
         o->n_off = o->gq[0].n;
         o->cap_off = o->gq[0].cap;
         o->gq_ticks -= n_ticks;
-        memmove(o->gq, o->gq + 1, (o->gq_n - 1) * sizeof *o->gq);
+        if (o->gq_n > 1) memmove(o->gq, o->gq + 1, (o->gq_n - 1) * sizeof *o->gq);
         o->gq_n--;
     }
     for (size_t i = 0; i < o->n_off; ++i)
         if (o->off[i].p.tick >= n_ticks)
             return fail(o, -EINVAL, "packet %zu: tick %u beyond step of %u ticks", i, o->off[i].p.tick, n_ticks);
-    qsort(o->off, o->n_off, sizeof(offered), cmp_off);
+    if (o->n_off) qsort(o->off, o->n_off, sizeof(offered), cmp_off);
     o->st.queue_state_bytes += queue_bytes(o);
     free(o->verdicts);
     o->verdicts = (uint8_t*)malloc(o->n_off ? o->n_off : 1);
@@ -868,8 +868,10 @@ static void deliver_records(oracle* o, const tgsim_delivery* recs, size_t n) {
         free(cnt);
     }
     o->out = (tgsim_delivery*)grow(o->out, &o->cap_out, o->n_out + n, sizeof(tgsim_delivery));
-    memcpy(o->out + o->n_out, recs, n * sizeof(tgsim_delivery));
-    qsort(o->out + o->n_out, n, sizeof(tgsim_delivery), cmp_del);
+    if (n) { /* (UBSan: no null pointers into memcpy/qsort, even for zero records) */
+        memcpy(o->out + o->n_out, recs, n * sizeof(tgsim_delivery));
+        qsort(o->out + o->n_out, n, sizeof(tgsim_delivery), cmp_del);
+    }
     o->n_out += n;
 }
 
@@ -976,7 +978,7 @@ int64_t tgo_drain(void* p, tgsim_delivery* out, size_t cap) {
     oracle* o = (oracle*)p;
     size_t avail = o->n_out - o->out_head;
     size_t n = avail < cap ? avail : cap;
-    memcpy(out, o->out + o->out_head, n * sizeof(tgsim_delivery));
+    if (n) memcpy(out, o->out + o->out_head, n * sizeof(tgsim_delivery));
     o->out_head += n;
     if (o->out_head == o->n_out) o->out_head = o->n_out = 0;
     return (int64_t)n;
@@ -985,7 +987,7 @@ int64_t tgo_drain(void* p, tgsim_delivery* out, size_t cap) {
 int64_t tgo_verdicts(void* p, uint8_t* out, size_t cap) {
     oracle* o = (oracle*)p;
     size_t n = o->n_verdicts < cap ? o->n_verdicts : cap;
-    memcpy(out, o->verdicts, n);
+    if (n) memcpy(out, o->verdicts, n);
     return (int64_t)o->n_verdicts;
 }
 

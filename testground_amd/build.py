@@ -57,11 +57,31 @@ def build_engine(force: bool = False, verbose: bool = False, profile: bool = Fal
 
 
 def build_oracle(force: bool = False) -> Path:
-    """Compiles the CPU golden model (test infrastructure)."""
+    """Compiles the CPU golden model (test infrastructure).  TGORACLE_LIB names another build of
+    it (the sanitizer build of scripts/sanitize.sh) to load instead."""
+    if os.environ.get("TGORACLE_LIB"):
+        return Path(os.environ["TGORACLE_LIB"])
     if force or _stale(ORACLE_LIB, [ORACLE_DIR / "tgoracle.c", ORACLE_DIR / "tgoracle.h", ROOT / "include" / "tgsim.h"]):
         subprocess.run(["make", "-C", str(ORACLE_DIR), "-B" if force else "all"], check=True,
                        stdout=subprocess.DEVNULL)
     return ORACLE_LIB
+
+
+def build_engine_host_asan() -> Path:
+    """libtgsim built with AddressSanitizer + UBSan on its HOST code only (-Xarch_host; GPU code is
+    never sanitized on this pool): the CPU tests of the C ABI (tests/test_abi.py) load it."""
+    lib = PKG / "build_asan" / "libtgsim_asan.so"
+    lib.parent.mkdir(exist_ok=True)
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+           "-Xarch_host", "-fno-sanitize-recover=all", "-Xarch_host", "-fno-omit-frame-pointer"]
+    objs = []
+    for src in SOURCES:
+        obj = lib.parent / (src.stem + ".o")
+        subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", "-fPIC", *san, "-c", str(src),
+                        "-o", str(obj)], check=True)
+        objs.append(str(obj))
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *san, "-o", str(lib), *objs], check=True)
+    return lib
 
 
 if __name__ == "__main__":
