@@ -52,7 +52,7 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None, help="timed steps (default: storm 30, epochs 10, gossip 70 windows)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; gossip: 0)")
-    p.add_argument("--workload", default="storm", choices=["storm", "gossip", "epochs"])
+    p.add_argument("--workload", default="storm", choices=["storm", "gossip", "epochs", "bridge"])
     p.add_argument("--peers", type=int, default=0,
                    help="instances per GPU (default: storm 10,000; gossip 125,000; epochs 100,000)")
     p.add_argument("--floods", type=int, default=64, help="gossip: flood messages")
@@ -81,13 +81,13 @@ def parse(argv=None):
                    help="launcher self-test: every rank reports RANK/WORLD_SIZE and exits before any GPU call")
     a = p.parse_args(argv)
     if not a.peers:
-        a.peers = {"storm": 10_000, "gossip": 125_000, "epochs": 100_000}[a.workload]
-    if a.workload == "epochs":
+        a.peers = {"storm": 10_000, "gossip": 125_000, "epochs": 100_000, "bridge": 1000}[a.workload]
+    if a.workload in ("epochs", "bridge"):
         a.lam, a.window = 0.2, 1000
     if a.workload == "gossip":
         a.window = 5000
     if a.steps is None:
-        a.steps = {"gossip": 70, "epochs": 10}.get(a.workload, 30)  # storm: amortizes the pipeline fill and drain
+        a.steps = {"gossip": 70, "epochs": 10, "bridge": 200}.get(a.workload, 30)  # storm: amortizes the pipeline fill and drain
     if a.warmup is None:
         a.warmup = 0 if a.workload == "gossip" else 3
     return a
@@ -224,7 +224,114 @@ WORKLOAD_NAMES = {
     "gossip": "C4 gossip flood: degree 8, 1 KiB, L~U[5,50] ms, loss 1 % (BASELINE.json configs[3])",
     "epochs": "C5 epochs: C3 traffic at lambda 0.2, 10 % reshaped per 1,000-tick epoch, barrier per epoch "
               "(BASELINE.json configs[4])",
+    "bridge": "C6 bridge: real payloads (U[64,512] B) through the native packet bridge, 16 datagrams per "
+              "instance per 1 ms window to random peers, L~U[1,10] ms, J~U[0,1] ms, loss/dup/corrupt 1 %, 1 Gbit/s",
 }
+
+
+def run_bridge(a, world, rank, local, dist, want_cpu):
+    """C6: datagrams with payloads through tgsim_bridge_* (send -> engine step -> payload matching
+    -> per-destination FIFOs -> receive into the caller's buffers), one bridge of --peers instances
+    per rank (independent replicas).  The payloads live in host memory, so this line is host-inclusive
+    by construction: it measures the whole datagram path a plan's packets take, not the kernel."""
+    import numpy as np
+    import torch
+
+    from testground_amd import bridge as br
+    from testground_amd import workloads
+    from testground_amd.engine import Engine
+
+    n, window = a.peers, 1000
+    eng = Engine(n, device=local, lookahead_ns=window * 1000)
+    workloads.configure_bridge(eng, n)
+    b = br.NativeBridge(eng, n, window)
+    src, dst, data, off = workloads.bridge_traffic(n)
+    msgs = np.empty(4 * len(src), dtype=br.MSG_DTYPE)
+    buf = np.empty(4 * len(data) + (1 << 20), dtype=np.uint8)
+    got = [0, 0]
+
+    def one():
+        b.send_many(src, dst, data, off)
+        b.step()
+        while True:
+            k = b.recv_into(msgs, buf)
+            got[0] += k
+            got[1] += int(msgs["len"][:k].sum()) if k else 0
+            if k < len(msgs):
+                break
+
+    for _ in range(20 + a.warmup):  # past the largest latency + jitter: the FIFOs are in steady state
+        one()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    got[:] = [0, 0]
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    s = eng.stats()
+    b.close()
+    eng.close()
+    if dist:
+        t = torch.tensor([el, float(got[0]), float(got[1])], dtype=torch.float64, device=f"cuda:{local}")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        el, delivered, nbytes = float(mx[0]), float(t[1]), float(t[2])
+    else:
+        delivered, nbytes = float(got[0]), float(got[1])
+    if rank != 0:
+        return None
+    res = {
+        "metric": "datagrams/s delivered with payloads through the native packet bridge",
+        "value": delivered / el, "unit": "datagrams/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8 payloads, u32/u64 records",
+        "data": "synthetic (host-generated datagrams, fixed per-window pattern)",
+        "config": {"workload": WORKLOAD_NAMES["bridge"], "peers_per_gpu": n, "peers_total": n * world,
+                   "window_ticks": window, "tick_ns": 1000, "datagrams_sent_per_step": len(src) * world,
+                   "parallelism": f"independent replicas x{world}"},
+        "sent_per_s": len(src) * world * a.steps / el,
+        "payload_bytes_per_s": nbytes / el,
+        "engine_by_verdict": s["by_verdict"],
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    if world == 1 and want_cpu:
+        res["cpu_baseline"] = cpu_bridge_baseline(n, window, a.cpu_seconds)
+        res["cpu_baseline"]["gpu_over_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    return res
+
+
+def cpu_bridge_baseline(n, window, seconds):
+    """The Python PacketBridge over the CPU oracle, same instances, shapes and send pattern."""
+    from testground_amd import abi, workloads
+    from testground_amd.bridge import PacketBridge
+    from testground_amd.build import build_oracle
+    from testground_amd.engine import CABIEngine
+
+    lib = ctypes.CDLL(str(build_oracle()))
+    abi.declare(lib, "tgo_")
+    e = CABIEngine(lib, "tgo_", n, lookahead_ns=window * 1000)
+    workloads.configure_bridge(e, n)
+    b = PacketBridge(e, n, window)
+    src, dst, data, off = workloads.bridge_traffic(n)
+    items = [(int(s), int(d), data[int(off[i]):int(off[i + 1])]) for i, (s, d) in enumerate(zip(src, dst))]
+    got, steps, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for s, d, p in items:
+            b.send(s, d, p)
+        b.step()
+        got += sum(len(b.recv(p)) for p in range(n))
+        steps += 1
+    el = time.perf_counter() - t0
+    return {"value": got / el, "unit": "datagrams/s", "cores": 1, "kind": "port",
+            "sample": f"testground_amd/bridge.py PacketBridge over oracle/tgoracle.c, {n} instances, "
+                      f"{steps} windows of {len(items)} sends ({el:.1f} s, including the fill of the first windows)"}
 
 
 def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, local, dist, want_cpu):
@@ -441,8 +548,11 @@ def main(argv=None):
         import torch.distributed as dist
         from testground_amd.shard import init_rccl
         init_rccl(torch.device("cuda", local))
-    res = run_workload(a, a.workload, a.peers, a.steps, a.warmup, a.window, a.lam, world, rank, local, dist,
-                       want_cpu=not a.no_cpu)
+    if a.workload == "bridge":
+        res = run_bridge(a, world, rank, local, dist, want_cpu=not a.no_cpu)
+    else:
+        res = run_workload(a, a.workload, a.peers, a.steps, a.warmup, a.window, a.lam, world, rank, local, dist,
+                           want_cpu=not a.no_cpu)
     if a.workload == "storm" and not a.no_1m:
         # the 1M-peer half of the metric: C4 gossip over 1M peers in total, split over the ranks
         g = run_workload(a, "gossip", a.gossip_1m_peers // world, 70, 0, 5000, a.lam, world, rank, local, dist,

@@ -322,6 +322,57 @@ enum tgsim_metrics_kind { TGSIM_METRICS_SRC = 0, TGSIM_METRICS_DST = 1, TGSIM_ME
 #define TGSIM_METRICS_BINS 64u
 int64_t tgsim_metrics(void* engine, uint32_t kind, uint64_t* out, size_t cap);
 
+/* ---- packet bridge: plan payloads through the simulated network ------- */
+/* The payload bytes stay on the host; each datagram becomes a 16-B tgsim_pkt for the engine, and
+ * every delivery the engine drains is handed back with its payload: twice for a netem duplicate,
+ * with one bit flipped for a corrupted copy (the bit from a hash of (src, seq, clone)), never for
+ * a lost, filtered or queue-full one.  Packet lengths seen by netem/HTB are payload + 28 B
+ * (IPv4 + UDP headers).  Replaces the veth -> bridge hop of pkg/runner/local_docker.go:706-721 for
+ * plans whose sockets are bridged (tgsim_udp_front below). */
+typedef struct {
+    uint64_t t_ns;  /* delivery time                                    */
+    uint32_t src, dst, seq;
+    uint16_t flags; /* TGSIM_FLAG_*                                     */
+    uint16_t _pad;
+    uint64_t off;   /* payload: data[off, off + len) of the recv buffer */
+    uint32_t len;
+    uint32_t _pad2;
+} tgsim_msg;
+/* The engine calls a bridge makes (NULL ops: this library's tgsim_* functions).  The CPU tests
+ * drive the same bridge over the oracle's tgo_* functions. */
+typedef struct {
+    int (*submit)(void*, const tgsim_pkt*, size_t);
+    int (*step)(void*, uint32_t);
+    int64_t (*verdicts)(void*, uint8_t*, size_t);
+    int64_t (*drain)(void*, tgsim_delivery*, size_t);
+} tgsim_engine_ops;
+int tgsim_bridge_create(void* engine, const tgsim_engine_ops* ops, uint32_t n_peers, uint32_t window_ticks,
+                        uint64_t now_tick, void** out_bridge);
+void tgsim_bridge_destroy(void* bridge);
+/* Queues n datagrams: src[i] -> dst[i] (TGSIM_EXTERNAL allowed) with payload data[off[i], off[i+1]),
+ * offered at absolute tick ticks[i] (ticks NULL: the start of the next window).  seq_out (may be
+ * NULL) receives each datagram's per-source sequence number.  Returns n or -errno. */
+int64_t tgsim_bridge_send(void* bridge, size_t n, const uint32_t* src, const uint32_t* dst, const uint8_t* data,
+                          const uint64_t* off, const uint64_t* ticks, uint32_t* seq_out);
+/* One window: submits the datagrams due in it, steps the engine, resolves every verdict and queues
+ * every delivery with its payload.  Returns the deliveries queued. */
+int64_t tgsim_bridge_step(void* bridge);
+/* Moves up to max queued deliveries of `peer` (UINT32_MAX: of every peer, by destination) and their
+ * payloads (packed into data, cap bytes) to the caller, oldest first; returns the count. */
+int64_t tgsim_bridge_recv(void* bridge, uint32_t peer, tgsim_msg* msgs, size_t max, uint8_t* data, size_t cap);
+int64_t tgsim_bridge_pending(void* bridge, uint32_t peer); /* deliveries queued (UINT32_MAX: all) */
+int64_t tgsim_bridge_in_flight(void* bridge);              /* datagrams sent, not yet resolved  */
+uint64_t tgsim_bridge_now_tick(void* bridge);              /* start of the next window          */
+/* UDP front end: one socket on 127.0.0.1 receives every instance's datagrams (a 4-byte big-endian
+ * destination header, then the payload) from the instance's registered address; pump() moves what
+ * arrived into the bridge (recvmmsg), steps one window and sends each delivery to its destination's
+ * address with a 4-byte big-endian source header (sendmmsg). */
+int tgsim_udp_front_create(void* bridge, uint16_t port, void** out_front);
+int tgsim_udp_front_port(void* front);
+int tgsim_udp_front_register(void* front, uint32_t peer, uint32_t ipv4, uint16_t port);
+int64_t tgsim_udp_front_pump(void* front);
+void tgsim_udp_front_destroy(void* front);
+
 /* ---- device timing (bench instrumentation) ------------------------------------------------ */
 /* Average device time (ms) of the simulate kernel over the steps since the last reset, measured
  * with HIP events on the engine's stream. */

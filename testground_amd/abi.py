@@ -129,6 +129,10 @@ EXPORTS = [
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
+    "tgsim_bridge_create", "tgsim_bridge_destroy", "tgsim_bridge_send", "tgsim_bridge_step",
+    "tgsim_bridge_recv", "tgsim_bridge_pending", "tgsim_bridge_in_flight", "tgsim_bridge_now_tick",
+    "tgsim_udp_front_create", "tgsim_udp_front_port", "tgsim_udp_front_register",
+    "tgsim_udp_front_pump", "tgsim_udp_front_destroy",
 ]
 
 

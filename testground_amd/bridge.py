@@ -26,6 +26,7 @@ headers (`len` is a u16, so payloads up to 65,507 bytes).
 """
 from __future__ import annotations
 
+import ctypes as C
 import socket
 import struct
 from collections import deque
@@ -136,6 +137,176 @@ class PacketBridge:
     def in_flight(self) -> int:
         """Datagrams sent and not yet delivered (or known lost)."""
         return len(self._payload)
+
+
+class TgsimMsg(C.Structure):
+    _fields_ = [("t_ns", C.c_uint64), ("src", C.c_uint32), ("dst", C.c_uint32), ("seq", C.c_uint32),
+                ("flags", C.c_uint16), ("_pad", C.c_uint16), ("off", C.c_uint64), ("len", C.c_uint32),
+                ("_pad2", C.c_uint32)]
+
+
+class EngineOps(C.Structure):
+    _fields_ = [("submit", C.c_void_p), ("step", C.c_void_p), ("verdicts", C.c_void_p), ("drain", C.c_void_p)]
+
+
+MSG_DTYPE = np.dtype([("t_ns", "<u8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("flags", "<u2"),
+                      ("_pad", "<u2"), ("off", "<u8"), ("len", "<u4"), ("_pad2", "<u4")])
+assert MSG_DTYPE.itemsize == C.sizeof(TgsimMsg) == 40
+
+
+def _declare_bridge(lib: C.CDLL) -> None:
+    vp = C.c_void_p
+    for name, res, args in (
+            ("tgsim_bridge_create", C.c_int, [vp, vp, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(vp)]),
+            ("tgsim_bridge_destroy", None, [vp]),
+            ("tgsim_bridge_send", C.c_int64, [vp, C.c_size_t, vp, vp, vp, vp, vp, vp]),
+            ("tgsim_bridge_step", C.c_int64, [vp]),
+            ("tgsim_bridge_recv", C.c_int64, [vp, C.c_uint32, vp, C.c_size_t, vp, C.c_size_t]),
+            ("tgsim_bridge_pending", C.c_int64, [vp, C.c_uint32]),
+            ("tgsim_bridge_in_flight", C.c_int64, [vp]),
+            ("tgsim_bridge_now_tick", C.c_uint64, [vp]),
+            ("tgsim_udp_front_create", C.c_int, [vp, C.c_uint16, C.POINTER(vp)]),
+            ("tgsim_udp_front_port", C.c_int, [vp]),
+            ("tgsim_udp_front_register", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint16]),
+            ("tgsim_udp_front_pump", C.c_int64, [vp]),
+            ("tgsim_udp_front_destroy", None, [vp])):
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+class NativeBridge:
+    """The packet bridge in libtgsim (tgsim_bridge_*: C++ payload arena, per-source sequence
+    windows, per-destination FIFOs), with PacketBridge's interface.  It drives the HIP engine
+    directly, or any engine-shaped library (the oracle in the CPU tests) through an ops table."""
+
+    ALL = 0xFFFFFFFF
+
+    def __init__(self, engine, n_peers: int, window_ticks: int = 1000, tick_ns: int = 1000):
+        from .engine import EngineError, load_library
+        self._err = EngineError
+        self._lib = load_library()
+        _declare_bridge(self._lib)
+        self.engine = engine
+        self.n = n_peers
+        self.window = window_ticks
+        self.tick_ns = tick_ns
+        ops = None
+        if engine._p != "tgsim_":  # another library's engine: call it through its own functions
+            f = lambda name: C.cast(getattr(engine._lib, engine._p + name), C.c_void_p).value  # noqa: E731
+            self._ops = EngineOps(f("submit"), f("step"), f("verdicts"), f("drain"))
+            ops = C.byref(self._ops)
+        h = C.c_void_p()
+        rc = self._lib.tgsim_bridge_create(engine._h, ops, n_peers, window_ticks, int(engine.stats()["now_tick"]),
+                                           C.byref(h))
+        if rc:
+            raise self._err(rc, "tgsim_bridge_create")
+        self._h = h
+        self._buf = np.empty(1 << 20, dtype=np.uint8)
+
+    def _chk(self, rc: int, what: str) -> int:
+        if rc < 0:
+            raise self._err(rc, what)
+        return rc
+
+    @property
+    def now_tick(self) -> int:
+        return int(self._lib.tgsim_bridge_now_tick(self._h))
+
+    def send_many(self, src, dst, payloads: bytes, off, ticks=None) -> np.ndarray:
+        """Batch send: datagram i is payloads[off[i]:off[i+1]] from src[i] to dst[i]."""
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        dst = np.ascontiguousarray(dst, dtype=np.uint32)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        data = np.frombuffer(payloads, dtype=np.uint8) if len(payloads) else np.zeros(1, dtype=np.uint8)
+        t = None if ticks is None else np.ascontiguousarray(ticks, dtype=np.uint64)
+        seq = np.empty(len(src), dtype=np.uint32)
+        self._chk(self._lib.tgsim_bridge_send(self._h, len(src), src.ctypes.data, dst.ctypes.data, data.ctypes.data,
+                                              off.ctypes.data, None if t is None else t.ctypes.data,
+                                              seq.ctypes.data), "tgsim_bridge_send")
+        return seq
+
+    def send(self, src: int, dst: int, data: bytes, at_tick: Optional[int] = None) -> int:
+        if len(data) > MAX_PAYLOAD:
+            raise ValueError(f"payload of {len(data)} bytes exceeds {MAX_PAYLOAD}")
+        t = None if at_tick is None else [int(at_tick)]
+        if t is not None and t[0] < self.now_tick:
+            raise ValueError(f"tick {t[0]} is before the next window (tick {self.now_tick})")
+        return int(self.send_many([src], [dst], bytes(data), [0, len(data)], t)[0])
+
+    def step(self) -> int:
+        return self._chk(self._lib.tgsim_bridge_step(self._h), "tgsim_bridge_step")
+
+    def recv_raw(self, peer: int = ALL):
+        """Everything queued for peer (ALL: every peer, by destination): (messages, payload bytes)."""
+        n = self._chk(self._lib.tgsim_bridge_pending(self._h, peer), "tgsim_bridge_pending")
+        msgs = np.empty(max(n, 1), dtype=MSG_DTYPE)
+        out, got = [], 0
+        while got < n:
+            k = self._chk(self._lib.tgsim_bridge_recv(self._h, peer, msgs[got:].ctypes.data, n - got,
+                                                      self._buf.ctypes.data, len(self._buf)), "tgsim_bridge_recv")
+            if k == 0:  # the next payload does not fit: grow the buffer
+                self._buf = np.empty(2 * len(self._buf), dtype=np.uint8)
+                continue
+            m = msgs[got:got + k].copy()
+            end = int(m["off"][-1] + m["len"][-1])
+            out.append((m, self._buf[:end].tobytes()))
+            got += k
+        return out
+
+    def recv_into(self, msgs: np.ndarray, buf: np.ndarray, peer: int = ALL) -> int:
+        """Moves up to len(msgs) queued deliveries (and their payloads, into buf) out of the bridge;
+        returns how many.  Zero-copy for the caller: no Python object per datagram."""
+        return self._chk(self._lib.tgsim_bridge_recv(self._h, peer, msgs.ctypes.data, len(msgs), buf.ctypes.data,
+                                                     len(buf)), "tgsim_bridge_recv")
+
+    def recv(self, peer: int) -> List[Tuple[int, int, int, bytes, int]]:
+        """Everything delivered to peer so far: (t_ns, src, seq, payload, flags), in delivery order."""
+        res = []
+        for m, data in self.recv_raw(peer):
+            for r in m:
+                o = int(r["off"])
+                res.append((int(r["t_ns"]), int(r["src"]), int(r["seq"]), data[o:o + int(r["len"])], int(r["flags"])))
+        return res
+
+    def in_flight(self) -> int:
+        return self._chk(self._lib.tgsim_bridge_in_flight(self._h), "tgsim_bridge_in_flight")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.tgsim_bridge_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class NativeUdpFront:
+    """tgsim_udp_front_*: the UDP front end in C (recvmmsg/sendmmsg), over a NativeBridge."""
+
+    def __init__(self, bridge: NativeBridge, port: int = 0):
+        self.bridge = bridge
+        self._lib = bridge._lib
+        h = C.c_void_p()
+        bridge._chk(self._lib.tgsim_udp_front_create(bridge._h, port, C.byref(h)), "tgsim_udp_front_create")
+        self._h = h
+        self.addr = ("127.0.0.1", self._lib.tgsim_udp_front_port(h))
+
+    def register(self, peer: int, addr: Tuple[str, int]) -> None:
+        import ipaddress
+        self.bridge._chk(self._lib.tgsim_udp_front_register(self._h, peer, int(ipaddress.IPv4Address(addr[0])), addr[1]),
+                         "tgsim_udp_front_register")
+
+    def pump(self) -> int:
+        return self.bridge._chk(self._lib.tgsim_udp_front_pump(self._h), "tgsim_udp_front_pump")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.tgsim_udp_front_destroy(self._h)
+            self._h = None
 
 
 class UdpFront:

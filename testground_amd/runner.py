@@ -38,7 +38,8 @@ import threading
 import time
 from typing import Callable, Dict, List, Optional, Tuple
 
-from .bridge import PacketBridge
+from .bridge import NativeBridge, PacketBridge
+from .engine import LIB_PATH
 from .sidecar import Context, NetClient, SimReactor, SyncClient, handler
 
 OUTCOME_UNKNOWN = "unknown"     # pkg/task/task.go:25-28
@@ -137,6 +138,15 @@ class LocalSimRunnerCfg:
     max_sim_ns: int = 3600 * 10**9
     # engine_factory(n_peers, **engine kwargs) -> engine; default: the HIP engine (engine.Engine)
     engine_factory: Optional[Callable] = None
+
+
+def _make_bridge(engine, n: int, cfg):
+    """The native bridge (libtgsim's tgsim_bridge_*) whenever the library loads: always with the HIP
+    engine, which needs it anyway; the Python PacketBridge only for an engine_factory engine on a
+    host where libtgsim.so has not been built."""
+    if cfg.engine_factory is None or LIB_PATH.exists():
+        return NativeBridge(engine, n, cfg.window_ticks, cfg.tick_ns)
+    return PacketBridge(engine, n, cfg.window_ticks, cfg.tick_ns)
 
 
 class _Clock:
@@ -400,7 +410,7 @@ class LocalSimRunner:
         result = Result(Outcomes={g.ID: GroupOutcome(0, g.Instances) for g in job.Groups})
         reactor = SimReactor(engine, n)
         sync_client = reactor.Client
-        bridge = PacketBridge(engine, n, cfg.window_ticks, cfg.tick_ns)
+        bridge = _make_bridge(engine, n, cfg)
         clock = _Clock(bridge, reactor.lock, n, run_ctx, cfg.max_sim_ns)
         run_dir = os.path.join(self._outputs_dir(cfg), job.TestPlan, job.RunID)
         threads: List[threading.Thread] = []

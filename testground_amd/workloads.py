@@ -258,3 +258,33 @@ def run_epoch(eng, n_peers: int, epoch: int, n_local: int, step=None, barrier=No
     ok = barrier(state, rnd * n_peers) if barrier else eng.barrier_poll(state, rnd * n_peers)
     if not ok:
         raise RuntimeError(f"barrier epoch-{epoch} did not release")
+
+
+# ---------------------------------------------------------------------------------------------
+# C6: bridge — real payloads through the native packet bridge: every
+# instance sends BRIDGE_PER_WINDOW datagrams per window to random peers.
+BRIDGE_PER_WINDOW = 16
+
+
+def bridge_shape_arrays(n_peers: int, seed: int = SEED) -> Dict[str, np.ndarray]:
+    """L~U[1,10] ms, J~U[0,1] ms, loss/dup/corrupt 1 %, 1 Gbit/s."""
+    rng = np.random.default_rng((seed >> 16) & 0xFFFFFFFF)
+    return dict(latency_ns=rng.integers(1 * Millisecond, 10 * Millisecond + 1, n_peers),
+                jitter_ns=rng.integers(0, 1 * Millisecond + 1, n_peers),
+                bandwidth_bps=np.full(n_peers, 1_000_000_000, dtype=np.int64),
+                loss=np.full(n_peers, 1.0, np.float32), duplicate=np.full(n_peers, 1.0, np.float32),
+                corrupt=np.full(n_peers, 1.0, np.float32))
+
+
+def configure_bridge(eng, n_peers: int, seed: int = SEED) -> None:
+    eng.configure_batch(np.arange(n_peers), configs_array(**bridge_shape_arrays(n_peers, seed)))
+
+
+def bridge_traffic(n_peers: int, per_instance: int = BRIDGE_PER_WINDOW, seed: int = SEED):
+    """One window of sends: (src, dst, payload bytes, offsets); payloads of U[64,512] bytes."""
+    rng = np.random.default_rng(seed & 0xFFFF)
+    src = np.repeat(np.arange(n_peers, dtype=np.uint32), per_instance)
+    dst = ((src + 1 + rng.integers(0, n_peers - 1, len(src))) % n_peers).astype(np.uint32)
+    lens = rng.integers(64, 513, len(src))
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    return src, dst, rng.bytes(int(off[-1])), off

@@ -133,3 +133,130 @@ def test_bridge_pingpong_gpu_equals_oracle(make_oracle):
         res.append(pingpong(PacketBridge(e, 2, WINDOW)))
     assert res[0] == res[1]
     assert all(200 * nw.Millisecond <= r <= 215 * nw.Millisecond for r in res[0][0])
+
+
+def _native_available():
+    from testground_amd.engine import LIB_PATH
+    return LIB_PATH.exists()
+
+
+native = pytest.mark.skipif(not _native_available(), reason="libtgsim.so not built (run __graft_entry__.build())")
+
+
+def _lossy_pair(make_oracle, n):
+    shape = nw.LinkShape(Latency=2 * nw.Millisecond, Jitter=1 * nw.Millisecond, Loss=20.0,
+                         Duplicate=30.0, Corrupt=40.0, Bandwidth=10**7)
+    out = []
+    for _ in range(2):
+        e = make_oracle(n, lookahead_ns=WINDOW * 1000, queue_limit=64)
+        for i in range(n):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=shape))
+        out.append(e)
+    return out
+
+
+@native
+def test_native_bridge_equals_python_bridge(make_oracle):
+    """The C++ bridge (tgsim_bridge_*) and the Python PacketBridge, each over its own oracle engine
+    fed the same datagrams: identical deliveries per destination (time, source, sequence number,
+    payload bytes incl. duplicates and the flipped bit of corrupted copies, flags)."""
+    from testground_amd.bridge import NativeBridge
+
+    n = 6
+    ep, en = _lossy_pair(make_oracle, n)
+    bp, bn = PacketBridge(ep, n, WINDOW), NativeBridge(en, n, WINDOW)
+    rng = np.random.default_rng(7)
+    for w in range(25):
+        k = 80
+        src = rng.integers(0, n, k)
+        dst = (src + 1 + rng.integers(0, n - 1, k)) % n
+        lens = rng.integers(0, 900, k)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        data = rng.bytes(int(off[-1]))
+        ticks = bp.now_tick + rng.integers(0, 2 * WINDOW, k)
+        seq_n = bn.send_many(src, dst, data, off, ticks)
+        seq_p = [bp.send(int(s), int(d), data[int(off[i]):int(off[i + 1])], at_tick=int(ticks[i]))
+                 for i, (s, d) in enumerate(zip(src, dst))]
+        assert list(seq_n) == seq_p
+        assert bp.step() == bn.step()
+        if w % 5 == 4:
+            for peer in range(n):
+                assert bp.recv(peer) == bn.recv(peer), (w, peer)
+    for _ in range(10):
+        bp.step()
+        bn.step()
+    for peer in range(n):
+        assert bp.recv(peer) == bn.recv(peer)
+    assert bp.in_flight() == bn.in_flight() == 0
+
+
+@native
+def test_native_udp_front(make_oracle):
+    """The C UDP front end (recvmmsg/sendmmsg) over the native bridge: datagrams from registered
+    instance sockets cross the simulated link and reach the destination socket with a source
+    header."""
+    from testground_amd.bridge import NativeBridge, NativeUdpFront
+
+    n = 3
+    e = make_oracle(n, lookahead_ns=WINDOW * 1000)
+    for i in range(n):
+        e.configure(i, nw.Config(Network="default", Enable=True, Default=nw.LinkShape(Latency=3 * nw.Millisecond)))
+    front = NativeUdpFront(NativeBridge(e, n, WINDOW))
+    socks = []
+    try:
+        for i in range(n):
+            s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            s.bind(("127.0.0.1", 0))
+            s.settimeout(5)
+            front.register(i, s.getsockname())
+            socks.append(s)
+        for k in range(50):
+            socks[0].sendto(struct.pack("!I", 1 + k % 2) + b"msg%03d" % k, front.addr)
+        socks[2].sendto(struct.pack("!I", 0) + b"back", front.addr)
+        time.sleep(0.05)
+        delivered = sum(front.pump() for _ in range(6))
+        assert delivered == 51
+        got1 = sorted(socks[1].recvfrom(65536)[0] for _ in range(25))
+        assert got1 == sorted(struct.pack("!I", 0) + b"msg%03d" % k for k in range(0, 50, 2))
+        msg, addr = socks[0].recvfrom(65536)
+        assert addr == front.addr and msg == struct.pack("!I", 2) + b"back"
+    finally:
+        front.close()
+        for s in socks:
+            s.close()
+
+
+@pytest.mark.gpu
+def test_native_bridge_gpu_equals_oracle(make_oracle):
+    """The native bridge over the HIP engine delivers exactly what the Python bridge delivers over
+    the oracle (payloads, duplicates, corrupted bits, times)."""
+    import torch
+
+    from testground_amd.bridge import NativeBridge
+    from testground_amd.engine import Engine
+
+    if torch.cuda.is_available():
+        torch.cuda.init()
+    n = 6
+    shape = nw.LinkShape(Latency=2 * nw.Millisecond, Jitter=1 * nw.Millisecond, Loss=20.0,
+                         Duplicate=30.0, Corrupt=40.0, Bandwidth=10**7)
+    eg = Engine(n, lookahead_ns=WINDOW * 1000, queue_limit=64)
+    ec = make_oracle(n, lookahead_ns=WINDOW * 1000, queue_limit=64)
+    for e in (eg, ec):
+        for i in range(n):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=shape))
+    bn, bp = NativeBridge(eg, n, WINDOW), PacketBridge(ec, n, WINDOW)
+    rng = np.random.default_rng(9)
+    for w in range(20):
+        k = 100
+        src = rng.integers(0, n, k)
+        dst = (src + 1 + rng.integers(0, n - 1, k)) % n
+        lens = rng.integers(1, 900, k)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        data = rng.bytes(int(off[-1]))
+        bn.send_many(src, dst, data, off)
+        for i, (s, d) in enumerate(zip(src, dst)):
+            bp.send(int(s), int(d), data[int(off[i]):int(off[i + 1])])
+        assert bn.step() == bp.step()
+    for peer in range(n):
+        assert bn.recv(peer) == bp.recv(peer)
