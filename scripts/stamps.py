@@ -69,7 +69,7 @@ pf = st[:, 8:32]  # profile build counters (see k_sim PROF_* slots)
 nb = np.maximum(nbat, 1)
 names = {0: "parallel", 1: "windows", 7: "S+htb", 8: "departures", 9: "decide", 10: "window-end",
          11: "commit", 4: "insert", 14: "ins-search", 15: "ins-shift", 12: "serve-mid", 13: "serve-end",
-         16: "refill"}
+         16: "refill", 20: "rf-count", 21: "rf-take", 22: "rf-insert"}
 print("  cycles per batch (mean over wgs): " + ", ".join(f"{v} {np.mean(pf[:, k] / nb):.0f}" for k, v in names.items()))
 print(f"  per batch: {np.mean(pf[:, 3] / nb):.2f} windows, {np.mean(pf[:, 2] / nb):.2f} full-queue runs, "
       f"{np.mean(pf[:, 5] / nb):.2f} inserted items, {np.mean(pf[:, 6] / nb):.2f} shift chunks, "

@@ -250,6 +250,28 @@ __device__ __forceinline__ void stamp(const SimArgs& a, uint32_t wg, uint32_t la
 
 // Wave-uniform queue state of the source plus the helpers that operate on it.  Every member is
 // identical in all 64 lanes; per-lane scratch is passed in and out.
+// Bitonic sort of one item per lane across the wave (ascending by item_lt; lanes without an
+// item, has = false, sort behind every item).  21 compare-exchange stages of 5 lane exchanges.
+__device__ __forceinline__ void wave_sort_items(uint4& v, bool has, uint32_t lane) {
+  uint32_t vf = has ? 0u : 1u;
+#pragma unroll
+  for (uint32_t k = 2; k <= kWave; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint4 pv = make_uint4((uint32_t)__shfl_xor((int)v.x, (int)j, 64), (uint32_t)__shfl_xor((int)v.y, (int)j, 64),
+                                  (uint32_t)__shfl_xor((int)v.z, (int)j, 64), (uint32_t)__shfl_xor((int)v.w, (int)j, 64));
+      const uint32_t pf = (uint32_t)__shfl_xor((int)vf, (int)j, 64);
+      // mine < partner (an empty lane is greater than every item)
+      const bool m_lt = vf < pf || (vf == pf && item_lt(v, pv));
+      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      if (keep_min != m_lt) {  // take the partner's item
+        v = pv;
+        vf = pf;
+      }
+    }
+  }
+}
+
 template <uint32_t kCap>
 struct SimQueue {
   static constexpr uint32_t kSlotMask = kCap - 1;
@@ -386,12 +408,14 @@ struct SimQueue {
       uint32_t cnt[kCand];
 #pragma unroll
       for (int c = 0; c < kCand; ++c) cnt[c] = 0;
+      PROF_T0(rc);
       for (uint32_t base = 0; base < pn; base += kWave) {
         const uint32_t k = base + lane;
         const uint64_t e = k < pn ? (ring_d(rn + qn + k) & kEMask) : ~0ull;
 #pragma unroll
         for (int c = 0; c < kCand; ++c) cnt[c] += ballot_count(e < h + (c ? (4096ull << c) : 0ull));
       }
+      PROF_ADD(20, rc);
       uint64_t Bp = h;
       uint32_t total = cnt[0];
 #pragma unroll
@@ -408,6 +432,7 @@ struct SimQueue {
       const uint64_t below = (1ull << lane) - 1;
       uint4 xv = make_uint4(0, 0, 0, 0), av = make_uint4(0, 0, 0, 0);
       uint32_t gx = 0, gh = 0;  // items taken so far, holes refilled so far
+      PROF_T0(rt);
       for (uint32_t base = 0; gx < nx; base += kWave) {
         const uint32_t k = base + lane;
         const bool in = k < pn;
@@ -448,9 +473,24 @@ struct SimQueue {
         gx += cx;
       }
       wave_lds_sync();
+      PROF_ADD(21, rt);
       pn -= nx;  // the pool now starts nx slots further; those slots are free
       PROF_CNT(18, nx);
-      insert_near(lane < nx, xv, false);
+      // every pool item is >= B > every near item, so the taken items, sorted, extend the near
+      // region into the nx free slots behind it; only when more than 64 pool items are below h
+      // (B not raised) can a later round take items below those taken before: merged then
+      PROF_T0(ri);
+      wave_sort_items(xv, lane < nx, lane);
+      const uint4 first = make_uint4(readlane32(xv.x, 0), readlane32(xv.y, 0), readlane32(xv.z, 0), 0u);
+      if (qn == 0 || item_lt(slot(rn + qn - 1), first)) {
+        if (lane < nx) slot(rn + qn + lane) = xv;
+        qn += nx;
+        wave_lds_sync();
+        PROF_CNT(5, nx);
+      } else {
+        insert_near(lane < nx, xv, false);
+      }
+      PROF_ADD(22, ri);
       if (total <= kWave) B = Bp;
     }
     PROF_ADD(16, rf);
@@ -1121,6 +1161,10 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   // heavy-first dispatch order (previous step's HTB work per source), identity when absent
   const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
   if (s >= a.n_src) return;
+#ifndef TGSIM_PRIO
+#define TGSIM_PRIO 0
+#endif
+  if (TGSIM_PRIO && a.order && blockIdx.x < TGSIM_PRIO) __builtin_amdgcn_s_setprio(3);
   sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
 }
 
