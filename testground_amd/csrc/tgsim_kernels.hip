@@ -251,25 +251,39 @@ __device__ __forceinline__ void stamp(const SimArgs& a, uint32_t wg, uint32_t la
 // Wave-uniform queue state of the source plus the helpers that operate on it.  Every member is
 // identical in all 64 lanes; per-lane scratch is passed in and out.
 // Bitonic sort of one item per lane across the wave (ascending by item_lt; lanes without an
-// item, has = false, sort behind every item).  21 compare-exchange stages of 5 lane exchanges.
+// item, has = false, sort behind every item): 21 compare-exchange stages.  Partner lane lane ^ J:
+// DPP quad_perm for J = 1, 2, ds_swizzle (xor mode, within 32 lanes) for J = 4..16, a
+// ds_bpermute for J = 32.
+template <uint32_t J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  uint32_t r;
+  if constexpr (J == 1) r = dpp<0xB1, 0xF>(0u, v);       // quad_perm [1, 0, 3, 2]
+  else if constexpr (J == 2) r = dpp<0x4E, 0xF>(0u, v);  // quad_perm [2, 3, 0, 1]
+  else if constexpr (J < 32) r = (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (int)(0x1Fu | (J << 10)));
+  else r = (uint32_t)__shfl_xor((int)v, 32, 64);
+  __asm__ volatile("" : "+v"(r));  // keep the DPP moves plain (see shr1_u32)
+  return r;
+}
+template <uint32_t K, uint32_t J>
+__device__ __forceinline__ void sort_stage(uint4& v, uint32_t& vf, uint32_t lane) {
+  const uint4 pv = make_uint4(xor_lane<J>(v.x), xor_lane<J>(v.y), xor_lane<J>(v.z), xor_lane<J>(v.w));
+  const uint32_t pf = xor_lane<J>(vf);
+  const bool m_lt = vf < pf || (vf == pf && item_lt(v, pv));  // mine < partner's
+  const bool keep_min = ((lane & J) == 0) == ((lane & K) == 0);
+  if (keep_min != m_lt) {  // take the partner's item
+    v = pv;
+    vf = pf;
+  }
+  if constexpr (J > 1) sort_stage<K, J / 2>(v, vf, lane);
+}
+template <uint32_t K>
+__device__ __forceinline__ void sort_merge(uint4& v, uint32_t& vf, uint32_t lane) {
+  sort_stage<K, K / 2>(v, vf, lane);
+  if constexpr (K < kWave) sort_merge<K * 2>(v, vf, lane);
+}
 __device__ __forceinline__ void wave_sort_items(uint4& v, bool has, uint32_t lane) {
   uint32_t vf = has ? 0u : 1u;
-#pragma unroll
-  for (uint32_t k = 2; k <= kWave; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint4 pv = make_uint4((uint32_t)__shfl_xor((int)v.x, (int)j, 64), (uint32_t)__shfl_xor((int)v.y, (int)j, 64),
-                                  (uint32_t)__shfl_xor((int)v.z, (int)j, 64), (uint32_t)__shfl_xor((int)v.w, (int)j, 64));
-      const uint32_t pf = (uint32_t)__shfl_xor((int)vf, (int)j, 64);
-      // mine < partner (an empty lane is greater than every item)
-      const bool m_lt = vf < pf || (vf == pf && item_lt(v, pv));
-      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-      if (keep_min != m_lt) {  // take the partner's item
-        v = pv;
-        vf = pf;
-      }
-    }
-  }
+  sort_merge<2>(v, vf, lane);
 }
 
 template <uint32_t kCap>
