@@ -57,7 +57,8 @@ def parse(argv=None):
                    help="instances per GPU (default: storm 10,000; gossip 125,000; epochs 100,000)")
     p.add_argument("--floods", type=int, default=64, help="gossip: flood messages")
     p.add_argument("--flood-gap", type=int, default=1000, help="gossip: ticks between flood starts")
-    p.add_argument("--lam", type=float, default=0.5)
+    p.add_argument("--lam", type=float, default=None,
+                   help="packets per us per source (default: storm 0.5, storm --shapes open 0.008, epochs 0.2)")
     p.add_argument("--window", type=int, default=2000, help="ticks (1 us) per step")
     p.add_argument("--settle-ms", type=float, default=120.0,
                    help="untimed simulated time before warm-up so every netem queue is in its sustained "
@@ -67,8 +68,9 @@ def parse(argv=None):
     p.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
                    help="threads of the all-core CPU oracle leg (the GPU box's CPU share is 16)")
     p.add_argument("--queue-limit", type=int, default=0, help="netem limit (0 = netlink default 1000)")
-    p.add_argument("--shapes", default="storm", choices=["storm", "fixed"],
-                   help="storm: C3 heterogeneous shapes; fixed: L=5 ms, no jitter/loss/reorder (probe)")
+    p.add_argument("--shapes", default="storm", choices=["storm", "open", "fixed"],
+                   help="storm: C3 heterogeneous shapes; open: C3 shapes at 1 Gbit/s driven below capacity "
+                        "(the sub-capacity variant); fixed: L=5 ms, no jitter/loss/reorder (probe)")
     p.add_argument("--sharded", action="store_true",
                    help="use the peer-sharded step (RCCL exchange) even at one rank, to time the N>1 path")
     p.add_argument("--exact-exchange", action="store_true",
@@ -84,6 +86,9 @@ def parse(argv=None):
         a.peers = {"storm": 10_000, "gossip": 125_000, "epochs": 100_000, "bridge": 1000}[a.workload]
     if a.workload in ("epochs", "bridge"):
         a.lam, a.window = 0.2, 1000
+    if a.lam is None:
+        from testground_amd.workloads import STORM_OPEN_LAMBDA
+        a.lam = STORM_OPEN_LAMBDA if a.shapes == "open" else 0.5
     if a.workload == "gossip":
         a.window = 5000
     if a.steps is None:
@@ -161,7 +166,7 @@ def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds):
     def leg(lo, hi, seconds):
         """One oracle shard [lo, hi) of the same workload stepped for ~seconds of step time."""
         e = CABIEngine(lib, "tgo_", peers_total, shard=(lo, hi))
-        workloads.configure_storm(e, peers_total)
+        workloads.configure_storm(e, peers_total, open_links=a.shapes == "open")
         busy, steps = 0.0, 0
         while busy < seconds:
             if workload == "epochs" and steps:
@@ -199,11 +204,12 @@ def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds):
     return {"value": pkts / busy, "unit": "packets/s", "cores": 1, "kind": "port", "sample": sample}
 
 
-def load_pmc(workload, window, peers, lam):
+def load_pmc(workload, window, peers, lam, shapes="storm"):
     """HBM traffic of k_sim from the committed PMC passes (rocprofv3 cannot run inside the bench).
     Reported only when the file was collected on the same k_sim source (sha of tgsim_kernels.hip)
     and the same workload configuration; the line names the file and its provenance either way."""
-    f = ROOT / "profiles" / ("pmc_k_sim.json" if workload == "storm" else f"pmc_k_sim_{workload}.json")
+    tag = workload if workload != "storm" or shapes == "storm" else f"storm_{shapes}"
+    f = ROOT / "profiles" / ("pmc_k_sim.json" if tag == "storm" else f"pmc_k_sim_{tag}.json")
     src = {"file": str(f.relative_to(ROOT)), "kernel_sha16_now": kernel_sha16()}
     if not f.exists():
         return None, dict(src, status="absent")
@@ -214,13 +220,16 @@ def load_pmc(workload, window, peers, lam):
     src.update({k: pmc.get(k) for k in ("kernel_sha16", "commit", "peers", "lam", "window")})
     if pmc.get("kernel_sha16") != src["kernel_sha16_now"]:
         return None, dict(src, status="stale: collected on another k_sim source")
-    if pmc.get("window") != window or pmc.get("peers") != peers or pmc.get("lam", lam) != lam:
+    if (pmc.get("window") != window or pmc.get("peers") != peers or pmc.get("lam", lam) != lam
+            or pmc.get("shapes", "storm") != shapes):
         return None, dict(src, status="other configuration")
     return pmc.get("hbm_bytes_per_launch"), dict(src, status="matches this kernel and configuration")
 
 
 WORKLOAD_NAMES = {
     "storm": "C3 storm: random all-to-all, heterogeneous LinkShape (BASELINE.json configs[2])",
+    "storm_open": "C3 storm, sub-capacity variant: C3 shapes with every link at 1 Gbit/s, lambda 0.008 "
+                  "(no netem queue at its limit)",
     "gossip": "C4 gossip flood: degree 8, 1 KiB, L~U[5,50] ms, loss 1 % (BASELINE.json configs[3])",
     "epochs": "C5 epochs: C3 traffic at lambda 0.2, 10 % reshaped per 1,000-tick epoch, barrier per epoch "
               "(BASELINE.json configs[4])",
@@ -354,8 +363,8 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     t_setup = time.perf_counter()
     if workload == "gossip":
         workloads.configure_gossip(eng, peers_total)
-    elif a.shapes == "storm":
-        workloads.configure_storm(eng, peers_total)
+    elif a.shapes in ("storm", "open"):
+        workloads.configure_storm(eng, peers_total, open_links=a.shapes == "open")
     else:
         eng.configure_batch(np.arange(peers_total), configs_array(np.full(peers_total, 5_000_000), routing_policy=2))
     bounds = [r * peers for r in range(world)] + [peers_total]
@@ -468,7 +477,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         return None
     per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled + qbytes) / max(1, steps) + B_SOURCE * peers
     achieved = per_launch / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else None
-    traffic, traffic_src = load_pmc(workload, window, peers, lam)
+    traffic, traffic_src = load_pmc(workload, window, peers, lam, a.shapes)
     tot_v = max(1.0, float(verd_all.sum()))
     res = {
         "metric": METRIC,
@@ -483,7 +492,8 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
         "data": f"synthetic (device-generated {workload} traffic, Philox-keyed)",
-        "config": dict({"workload": WORKLOAD_NAMES[workload],
+        "config": dict({"workload": WORKLOAD_NAMES["storm_open" if workload == "storm" and a.shapes == "open"
+                                                   else workload],
                         "peers_per_gpu": peers, "peers_total": peers_total, "lambda_per_tick": lam,
                         "tick_ns": 1000, "window_ticks": window, "settle_sim_ms": settle * window / 1000,
                         "shapes": a.shapes if workload == "storm" else workload,
@@ -496,7 +506,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         "scheduled_per_s": scheduled_all / el,
         "verdict_mix": {k: float(v) / tot_v for k, v in zip(abi.VERDICT_NAMES, verd_all)},
         "setup_s": setup_s,
-        "roofline": {"bound": "hbm", "kernel": "k_sim", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_sim (dense steps) | k_sim_sparse + k_sim_list (sparse steps)", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": per_launch, "kernel_ms_avg": sim_ms, "launches": n_launch},

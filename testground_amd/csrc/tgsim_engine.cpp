@@ -217,6 +217,7 @@ struct tgsim_engine_s {
   uint64_t* h_err = nullptr;    // pinned host word k_sim stores the sticky error bits into
   uint64_t* d_err_host = nullptr;  // its device address
   uint32_t* h_xerr = nullptr;   // pinned sticky flag: a slotted exchange chunk overflowed (k_route_edges)
+  uint32_t* h_work = nullptr;   // pinned: sources the last sparse step deferred to k_sim_list
   uint32_t* d_xerr = nullptr;   // its device address
   // launched, unfinished routed steps (tgsim_step_sim_launch), oldest at route_head: pinned
   // per-rank record edges behind an event, per slot
@@ -304,6 +305,8 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_order;  // dispatch order of the next k_sim, computed behind this one
   DevBuf<uint32_t> d_work;   // sparse steps: k_sim_sparse's deferred sources, [0] = count, then ids
   int sparse_mode = -1;      // TGSIM_SPARSE: -1 auto, 0 never, 1 always
+  bool sparse_seen = false;  // h_work holds a measured worklist size
+  uint32_t dense_streak = 0; // dense steps chosen because the last sparse step deferred too much
   bool order_valid = false;
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
@@ -790,8 +793,20 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   // Sparse steps (few packets per source, or more sources than the order kernel ranks): open
   // queues run in the register-only k_sim_sparse, the rest in k_sim_list; dense steps: k_sim in
   // heavy-first order.  The results are the same either way.
-  const bool sparse = E->sparse_mode == 1 ||
-                      (E->sparse_mode < 0 && (E->S > kOrderMaxSources || E->n_in < 16ull * E->S));
+  bool sparse;
+  if (E->sparse_mode >= 0) {
+    sparse = E->sparse_mode == 1;
+  } else if (E->S > kOrderMaxSources || E->n_in >= 16ull * E->S) {
+    sparse = E->S > kOrderMaxSources;
+  } else {
+    // few packets per source: the register-only kernel wins unless the queues are too long for
+    // registers and it defers most sources to k_sim_list (2 waves/SIMD).  The worklist size of the
+    // last sparse step (copied to pinned memory behind it, read without waiting) decides; every
+    // 64th such step runs sparse again to re-measure
+    const uint32_t deferred = __atomic_load_n(E->h_work, __ATOMIC_RELAXED);
+    sparse = !(E->sparse_seen && 4ull * deferred > E->S) || ++E->dense_streak >= 64;
+    if (sparse) E->dense_streak = 0;
+  }
   a.worklist = a.worklist_n = nullptr;
   if (sparse) {
     HIPCHK(E->d_work.ensure(static_cast<size_t>(E->S) + 1));
@@ -808,6 +823,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   else launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
+  if (sparse) {
+    HIPCHK(hipMemcpyAsync(E->h_work, E->d_work.p, sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
+    E->sparse_seen = true;
+  }
   E->ev_pending.emplace_back(ev0, ev1);
   if (E->metrics_on) {
     MetricsArgs m;
@@ -1169,6 +1188,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
                                  hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
     return bail(rc);
   *E->h_xerr = 0;
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_work), sizeof(uint32_t),
+                                 hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
+    return bail(rc);
+  *E->h_work = 0;
   if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_xerr), E->h_xerr, 0), "pinned")))
     return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_gerr), sizeof(uint32_t)), "pinned"))) return bail(rc);
@@ -1289,6 +1312,7 @@ void tgsim_destroy(void* e) {
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
   if (E->h_err) (void)hipHostFree(E->h_err);
   if (E->h_xerr) (void)hipHostFree(E->h_xerr);
+  if (E->h_work) (void)hipHostFree(E->h_work);
   if (E->h_gerr) (void)hipHostFree(E->h_gerr);
   if (E->h_pub) (void)hipHostFree(E->h_pub);
   if (E->ev_pub) (void)hipEventDestroy(E->ev_pub);

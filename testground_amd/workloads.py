@@ -50,13 +50,25 @@ def storm_shapes(n_peers: int, seed: int = SEED) -> List[LinkShape]:
             for i in range(n_peers)]
 
 
-def storm_configs(n_peers: int, seed: int = SEED) -> np.ndarray:
-    """The storm shapes as tgsim_config records (RoutingPolicy DenyAll), for configure_batch."""
-    return configs_array(routing_policy=2, **storm_shape_arrays(n_peers, seed))
+def storm_configs(n_peers: int, seed: int = SEED, open_links: bool = False) -> np.ndarray:
+    """The storm shapes as tgsim_config records (RoutingPolicy DenyAll), for configure_batch.
+    open_links: the sub-capacity variant, every link at 1 Gbit/s (latency, jitter, loss, dup,
+    corrupt, reorder unchanged), driven at STORM_OPEN_LAMBDA so no netem queue reaches its limit."""
+    a = storm_shape_arrays(n_peers, seed)
+    if open_links:
+        a["bandwidth_bps"] = np.full(n_peers, 1_000_000_000, dtype=np.int64)
+    return configs_array(routing_policy=2, **a)
 
 
-def configure_storm(eng, n_peers: int, seed: int = SEED) -> None:
-    eng.configure_batch(np.arange(n_peers), storm_configs(n_peers, seed))
+# Sub-capacity C3: 0.008 packets per us per source of U[64,1500] B is ~50 Mbit/s offered against
+# 1 Gbit/s, and the netem queue holds lambda * (L + J) <= 0.008 * 110,000 us = 880 items at the very
+# worst shape (~440 on average) against the limit of 1,000: the delay, HTB and delivery path is
+# exercised, not the full-queue ballot.
+STORM_OPEN_LAMBDA = 0.008
+
+
+def configure_storm(eng, n_peers: int, seed: int = SEED, open_links: bool = False) -> None:
+    eng.configure_batch(np.arange(n_peers), storm_configs(n_peers, seed, open_links))
 
 
 # ---------------------------------------------------------------------------------------------
