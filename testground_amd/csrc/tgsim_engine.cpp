@@ -796,8 +796,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   bool sparse;
   if (E->sparse_mode >= 0) {
     sparse = E->sparse_mode == 1;
-  } else if (E->S > kOrderMaxSources || E->n_in >= 16ull * E->S) {
-    sparse = E->S > kOrderMaxSources;
+  } else if (E->n_in >= 16ull * E->S) {
+    sparse = false;  // dense traffic (C3, C5 at 100k peers): the LDS queue, in heavy-first order when ranked
   } else {
     // few packets per source: the register-only kernel wins unless the queues are too long for
     // registers and it defers most sources to k_sim_list (2 waves/SIMD).  The worklist size of the
