@@ -1239,10 +1239,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(E->d_gen_seq.ensure(E->S), "alloc gen_seq"))) return bail(rc);
   if ((rc = E->hip(E->d_stats.ensure(kStSlots * kStatCopies), "alloc stats"))) return bail(rc);
   // K7 sync counters: device table, pinned mirror and result/marker words, their own stream
-  if ((rc = E->hip(hipStreamCreateWithPriority(&E->sy_st, hipStreamNonBlocking, prio_hi), "stream")))
-    return bail(rc);
+  // (the sync stream is created at the first signal: HIP maps the streams of a process onto
+  // GPU_MAX_HW_QUEUES hardware queues, and an idle fifth stream made the exchange share a queue
+  // with the simulate stream)
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sig, hipEventDisableTiming), "event"))) return bail(rc);
-  if ((rc = E->hip(hipEventRecord(E->ev_sig, E->sy_st), "event"))) return bail(rc);
   if ((rc = E->hip(E->d_sync.ensure(kStates), "alloc sync"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_sync.p, 0, sizeof(unsigned long long) * kStates), "memset"))) return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_mirror), sizeof(uint64_t) * kStates,
@@ -1715,11 +1715,23 @@ int tgsim_stats(void* e, tgsim_stats_t* out) {
   return 0;
 }
 
+// The sync stream (high priority), created on first use.
+static hipError_t sync_stream_ready(Eng* E) {
+  if (E->sy_st) return hipSuccess;
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e != hipSuccess) return e;
+  e = hipStreamCreateWithPriority(&E->sy_st, hipStreamNonBlocking, hi);
+  if (e != hipSuccess) return e;
+  return hipEventRecord(E->ev_sig, E->sy_st);
+}
+
 // K7: SignalEntry on the device counter table (sync stream; see include/tgsim.h).
 int tgsim_signal_async(void* e, uint32_t state, uint32_t n) {
   Eng* E = as_eng(e);
   if (!E || state >= kStates) return -EINVAL;
   HIPCHK(hipSetDevice(E->dev));
+  HIPCHK(sync_stream_ready(E));
   launch_signal(E->d_sync.p, E->dm_mirror, state, n, E->dm_sig, E->dm_sig + 1, ++E->sig_seq, E->sy_st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(E->ev_sig, E->sy_st));
@@ -1747,6 +1759,7 @@ int tgsim_sync_counters(void* e, void** d_table, uint32_t* n_states, void* event
   HIPCHK(hipSetDevice(E->dev));
   *d_table = E->d_sync.p;
   *n_states = kStates;
+  HIPCHK(sync_stream_ready(E));
   if (event) HIPCHK(hipEventRecord(static_cast<hipEvent_t>(event), E->sy_st));
   return 0;
 }
