@@ -914,10 +914,12 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
           for (uint32_t base = 0;; base += kWave) {
             const uint32_t k = base + lane;
             const uint32_t ks = k - Q.rn;  // index among the newly served items when k >= rn
-            const uint64_t dfs = shfl64(dS, (k >= Q.rn && ks < kWave) ? ks : 0u);
             uint64_t dep = ~0ull;
+            if (base + kWave > Q.rn && nS) {  // the chunk reaches past the ring (wave-uniform)
+              const uint64_t dfs = shfl64(dS, (k >= Q.rn && ks < kWave) ? ks : 0u);
+              if (k >= Q.rn && ks < nS) dep = dfs;
+            }
             if (k < Q.rn) dep = Q.ring_d(k);
-            else if (ks < nS) dep = dfs;
             // the netem queue releases departures from the ring head while head < T (a prefix:
             // with a lookahead the ring need not be sorted across a step boundary)
             const uint64_t stop = __ballot(dep >= T_max);
