@@ -292,8 +292,10 @@ struct SimQueue {
   SimLdsT<kCap>& lds;
   const SrcParams& p;
   uint32_t lane;
-  uint32_t rh, rn, qn, pn;  // ring head slot, ring length, near-region length, pool length
+  uint32_t rh, rn, qn, pn;  // ring head slot, ring length, near-region length, soon-pool length
+  uint32_t fn;              // far-pool length (behind the soon pool)
   uint64_t B;               // near/pool boundary: near items have e < B, pool items e >= B
+  uint64_t H;               // the step's horizon: every serve is before it; soon items e < H <= far
   uint64_t tat;             // HTB theoretical arrival time
   tgsim_delivery* emit;
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
@@ -310,6 +312,40 @@ struct SimQueue {
     const uint2 v = *reinterpret_cast<const uint2*>(&lds.slot[(rh + k) & kSlotMask]);
     return ((uint64_t)v.y << 32) | v.x;
   }
+
+#ifdef TGSIM_CHECK
+  // Debug: near < B <= soon < H <= far, near sorted; prints the first violation.
+  __device__ void check(int tag) {
+    uint32_t bad = 0;
+    uint64_t be = 0;
+    for (uint32_t k = lane; k < qn; k += kWave) {
+      const uint64_t e = w0_of(slot(rn + k)) & kEMask;
+      if (e >= B) { bad |= 1; be = e; }
+      if (k + 1 < qn && item_lt(slot(rn + k + 1), slot(rn + k))) bad |= 2;
+    }
+    for (uint32_t k = lane; k < pn; k += kWave) {
+      const uint64_t e = w0_of(slot(rn + qn + k)) & kEMask;
+      if (e < B || e >= H) { bad |= 4; be = e; }
+    }
+    for (uint32_t k = lane; k < fn; k += kWave) {
+      const uint64_t e = w0_of(slot(rn + qn + pn + k)) & kEMask;
+      if (e < H) { bad |= 8 | (k << 8); be = e; }
+    }
+    if (B > H) bad |= 16;
+    const uint64_t m = __ballot(bad != 0);
+    if (m) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(m);
+      const uint32_t bb = readlane32(bad, l);
+      const uint64_t ee = readlane64(be, l);
+      if (lane == 0)
+        printf("CHECK tag %d src %u rn %u qn %u pn %u fn %u B %llu H %llu bad %x e %llu lanes %llx\n", tag, src, rn, qn,
+               pn, fn, (unsigned long long)B, (unsigned long long)H, bb, (unsigned long long)ee, (unsigned long long)m);
+    }
+  }
+#define QCHECK(t) Q.check(t)
+#else
+#define QCHECK(t) do {} while (0)
+#endif
 
   // HTB departure times of the queue-head items held one per lane (in = lane < n, e/len of the
   // lane's item): d = max(e, TAT_before), and the TAT after each item.
@@ -383,21 +419,44 @@ struct SimQueue {
   }
 
   // New items of the lanes (has): into the near region when eligible before B, else appended to
-  // the pool.
+  // the pool: the SOON part when eligible before the step's horizon H (refill may need them), the
+  // FAR part behind it otherwise (never needed in this step, so refill never scans them).
   __device__ __forceinline__ void insert(bool has, const uint4& it) {
-    const bool far = has && (w0_of(it) & kEMask) >= B;
-    insert_near(has && !far, it, true);
-    const uint64_t m = __ballot(far);
-    if (!m) return;
-    if (far) slot(rn + qn + pn + (uint32_t)__popcll(m & ((1ull << lane) - 1))) = it;
-    pn += (uint32_t)__popcll(m);
-    PROF_CNT(19, (uint32_t)__popcll(m));
+    const uint64_t e = w0_of(it) & kEMask;
+    const bool pool = has && e >= B;
+    insert_near(has && !pool, it, true);
+    const bool vfar = pool && e >= H;
+    const uint64_t ms = __ballot(pool && !vfar), mf = __ballot(vfar);
+    if (!(ms | mf)) return;
+    const uint64_t below = (1ull << lane) - 1;
+    const uint32_t ks = (uint32_t)__popcll(ms);
+    relocate_far(ks);  // ks free slots behind the soon part
+    if (pool && !vfar) slot(rn + qn + pn + (uint32_t)__popcll(ms & below)) = it;
+    pn += ks;
+    if (vfar) slot(rn + qn + pn + fn + (uint32_t)__popcll(mf & below)) = it;
+    fn += (uint32_t)__popcll(mf);
+    PROF_CNT(19, (uint32_t)__popcll(ms | mf));
     wave_lds_sync();
   }
 
-  // The near region grows by k at its end: the first min(k, pn) pool items move behind the pool
-  // (the pool has no order), so the near suffix can shift up into their slots.
+  // k free slots right behind the soon pool: the first min(k, fn) far items move behind the far
+  // pool (it has no order).
+  __device__ __forceinline__ void relocate_far(uint32_t k) {
+    const uint32_t mv = k < fn ? k : fn, off = k > fn ? k : fn;
+    if (!mv) return;
+    const uint32_t b = rn + qn + pn;
+    const bool l = lane < mv;
+    const uint4 v = l ? slot(b + lane) : make_uint4(0, 0, 0, 0);
+    __asm__ volatile("" ::: "memory");
+    if (l) slot(b + off + lane) = v;
+    __asm__ volatile("" ::: "memory");
+  }
+
+  // The near region grows by k at its end: k slots open behind the soon pool (relocate_far), then
+  // the first min(k, pn) soon items move into them (no order either), so the near suffix can
+  // shift up into their slots.
   __device__ __forceinline__ void relocate_pool(uint32_t k) {
+    relocate_far(k);
     const uint32_t mv = k < pn ? k : pn, off = k > pn ? k : pn;
     if (!mv) return;
     const bool l = lane < mv;
@@ -438,6 +497,7 @@ struct SimQueue {
           Bp = h + (4096ull << c);
           total = cnt[c];
         }
+      if (Bp > H) Bp = H;  // far items are >= H; the soon items (all < H) counted below Bp stay the same
       if (!total) {
         B = Bp;
         break;
@@ -597,10 +657,12 @@ struct SimQueue {
       // moving the suffix [minR, qn) up; kL minimizes the slots moved.  Items eligible at once
       // (delay 0, reorder) land at the head and cost only the ring.
       const uint32_t spm1 = shr1_u32(sp, 0u);
-      const uint32_t pmv = reloc ? (nm - lane < pn ? nm - lane : pn) : 0u;  // pool items moved aside
+      const uint32_t pmv = reloc ? (nm - lane < pn ? nm - lane : pn) + (nm - lane < fn ? nm - lane : fn) : 0u;  // pool items moved aside
       const uint32_t cost = lane <= nm ? (lane > 0 ? rn + spm1 : 0u) + (lane < nm ? qn - sp + pmv : 0u) : 0xFFFFFFFFu;
+      // without reloc (refill) the pool already starts nm slots behind the near region: the new
+      // items must fill exactly those slots, so nothing moves down (kL = 0)
       uint32_t best = readlane32(cost, 0);
-      for (uint32_t k = 1; k <= nm; ++k) {
+      for (uint32_t k = 1; reloc && k <= nm; ++k) {
         const uint32_t c = readlane32(cost, k);
         if (c < best) {
           best = c;
@@ -716,7 +778,9 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   Q.rh = 0;
   Q.rn = st.ring_n;
   Q.qn = st.near_n;
-  Q.pn = st.heap_n - st.near_n;
+  Q.pn = st.heap_n - st.near_n;  // the whole pool until the load below splits it
+  Q.fn = 0;
+  Q.H = a.horizon_ns;
   Q.tat = st.tat;
   Q.src = a.shard_begin + s;
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
@@ -735,20 +799,41 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     const uint32_t rn = Q.rn, qn = Q.qn + Q.pn;
     // every load of the ring and the queue in flight before the first LDS write (one HBM
     // latency instead of one per 256 slots)
+    // (branch-free: a lane past the end re-reads the last entry, the same line as its neighbours,
+    // and drops it; a conditional load made the compiler wait for each chunk inside its branch)
     uint64_t rv[kCap / kWave];
     uint4 qv[kCap / kWave];
+    const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0;
 #pragma unroll
     for (uint32_t u = 0; u < kCap / kWave; ++u) {
       const uint32_t k = u * kWave + lane;
-      rv[u] = k < rn ? gr[k] : 0ull;
-      qv[u] = k < qn ? gh[k] : make_uint4(0, 0, 0, 0);
+      rv[u] = gr[k < rn ? k : rl];
+      qv[u] = gh[k < qn ? k : ql];
     }
+    // every load issued before the partition's ballots, which the scheduler would otherwise
+    // interleave with them (one HBM round trip per chunk)
+    __builtin_amdgcn_sched_barrier(0);
+    // the pool (queue items near_n .. qn) splits into the soon part (e < H), placed from the pool's
+    // front, and the far part, placed from its back (no order in either): one pass
+    const uint32_t nq = Q.qn;
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t cs = 0, cf = 0;
 #pragma unroll
     for (uint32_t u = 0; u < kCap / kWave; ++u) {
       const uint32_t k = u * kWave + lane;
       if (k < rn) *reinterpret_cast<uint2*>(&lds.slot[k]) = make_uint2((uint32_t)rv[u], (uint32_t)(rv[u] >> 32));
-      if (k < qn) lds.slot[(rn + k) & kSlotMask] = qv[u];
+      const bool pool = k >= nq && k < qn;
+      const bool soon = pool && (w0_of(qv[u]) & kEMask) < Q.H;
+      const uint64_t msn = __ballot(soon), mfr = __ballot(pool && !soon);
+      uint32_t d = k;  // near items keep their place
+      if (soon) d = nq + cs + (uint32_t)__popcll(msn & below);
+      else if (pool) d = qn - 1 - cf - (uint32_t)__popcll(mfr & below);
+      if (k < qn) lds.slot[(rn + d) & kSlotMask] = qv[u];
+      cs += (uint32_t)__popcll(msn);
+      cf += (uint32_t)__popcll(mfr);
     }
+    Q.pn = cs;
+    Q.fn = cf;
   }
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const bool src_on = a.enabled[Q.src] != 0;
@@ -764,8 +849,8 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   // into the statistics every 2^14 batches (at most 2 counts per lane and batch), before a field
   // can overflow
   unsigned long long* const sc = a.stats + (size_t)(wg % kStatCopies) * kStSlots;
-  if (lane == 0 && (Q.qn | Q.pn | Q.rn))  // the queue state loaded (the stored part is added at the end)
-    atomicAdd(&sc[kStQueue], (unsigned long long)(16ull * (Q.qn + Q.pn) + 8ull * Q.rn));
+  if (lane == 0 && (Q.qn | Q.pn | Q.fn | Q.rn))  // the queue state loaded (the stored part is added at the end)
+    atomicAdd(&sc[kStQueue], (unsigned long long)(16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn));
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
   auto flush_verdicts = [&]() {
@@ -782,12 +867,13 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   // every pool item is >= the B of the previous step > every near item, so both of these are
   // valid boundaries; with an empty near region every new item starts in the pool
   Q.B = Q.qn ? (w0_of(Q.slot(Q.rn + Q.qn - 1)) & kEMask) + 1 : a.t0_ns;
+  QCHECK(1);
   stamp(a, wg, lane, 1, __builtin_amdgcn_s_memrealtime());
 
   const uint32_t n_batches = (uint32_t)((send - sbeg + kWave - 1) / kWave);
   // open queue: even if every offered packet and its clone were admitted the queue would stay
   // below the netem limit (sparse sources: gossip, ping-pong, splitbrain)
-  const bool open_q = kOpen || (!corr && (uint64_t)Q.rn + Q.qn + Q.pn + 2 * (send - sbeg) < lim);
+  const bool open_q = kOpen || (!corr && (uint64_t)Q.rn + Q.qn + Q.pn + Q.fn + 2 * (send - sbeg) < lim);
   uint64_t T_enq = 0;  // open queue: offer time of the last packet that reached the netem enqueue
   uint64_t idx = sbeg + lane;
   InRec rec = {}, rec2 = {};  // records of batches b and b + 1 (two batches in flight)
@@ -866,10 +952,11 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
       uint64_t pend = (kOpen || open_q) ? 0ull : __ballot(cand);
       if constexpr (!kOpen) while (pend) {
         PROF_CNT(3, 1);
-        if (Q.rn + Q.qn + Q.pn >= lim) {
+        if (Q.rn + Q.qn + Q.pn + Q.fn >= lim) {
           // full queue: nothing changes before the next eligibility or departure time, so every
-          // packet offered up to then is a QUEUE_FULL drop (B bounds the pool's earliest e)
-          const uint64_t qh = Q.qn ? (w0_of(Q.slot(Q.rn)) & kEMask) : (Q.pn ? Q.B : ~0ull);
+          // packet offered up to then is a QUEUE_FULL drop (B bounds the soon pool's earliest e,
+          // H the far pool's)
+          const uint64_t qh = Q.qn ? (w0_of(Q.slot(Q.rn)) & kEMask) : Q.pn ? Q.B : Q.fn ? Q.H : ~0ull;
           const uint64_t dh = Q.rn ? Q.ring_d(0) : ~0ull;
           const uint64_t t_ev = qh < dh ? qh : dh;
           const uint64_t mf = __ballot(((pend >> lane) & 1ull) && T <= t_ev);
@@ -886,7 +973,9 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
         const uint32_t w0 = (uint32_t)__builtin_ctzll(pend);
         const uint32_t wl = 63u - (uint32_t)__builtin_clzll(pend);
         const uint64_t T_last = readlane64(T, wl);
+        QCHECK(10);
         Q.refill(T_last);  // every item eligible before the window's last packet in the near region
+        QCHECK(8);
         PROF_T0(s1);
         // (1) queue-head items eligible before the last pending packet, served optimistically
         const bool hq = lane < Q.qn;
@@ -954,7 +1043,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
         const int32_t cnt = inw ? 1 + (cst == 2) : 0;
         const int32_t P = scan_sum_i32(cnt - delta);
         const int32_t M = scan_max_i32(P);
-        const int32_t x0 = (int32_t)(Q.rn + Q.qn + Q.pn), ilim = (int32_t)lim;
+        const int32_t x0 = (int32_t)(Q.rn + Q.qn + Q.pn + Q.fn), ilim = (int32_t)lim;
         const int32_t Pex = (int32_t)shr1_u32((uint32_t)P, 0u);
         const int32_t Mex = (int32_t)shr1_u32((uint32_t)M, 0u);  // lane 0: 0 = identity here
         const int32_t xb = Pex + min(x0, ilim - Mex);
@@ -1019,6 +1108,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
         const bool inC = inS && qe < t_c;
         const uint32_t nC = ballot_count(inC);
         if (nC) Q.commit(inC, nC, qi, dS, tatS);
+        QCHECK(5);
         Q.rh = (Q.rh + Dw) & kSlotMask;
         Q.rn -= Dw;
         PROF_ADD(11, s5);
@@ -1030,13 +1120,17 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
         }
         // (5) merge the admitted items into the sorted queue
         Q.insert(inwin && orig_adm, make_item(eo, len, flo, r.seq, r.dst));
+        QCHECK(6);
         Q.insert(inwin && clone_adm, make_item(ec, len, flc, r.seq, r.dst));
+        QCHECK(7);
         if (e_new < T_w) {
           PROF_T0(s6);
           Q.serve_until(T_w);
           PROF_ADD(12, s6);
+          QCHECK(9);
         }
         if (mwin) pend &= lw >= 63u ? 0ull : ~((1ull << (lw + 1)) - 1);
+        QCHECK(2);
       }
       PROF_ADD(1, w);
     } else if constexpr (!kOpen) {
@@ -1074,7 +1168,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
           auto enq = [&](uint32_t reo_raw, uint32_t delay_raw, uint32_t fl) -> uint32_t {
             Q.serve_until(Tj);
             Q.depart_before(Tj);
-            if (Q.rn + Q.qn + Q.pn >= lim) return TGSIM_V_QUEUE_FULL;
+            if (Q.rn + Q.qn + Q.pn + Q.fn >= lim) return TGSIM_V_QUEUE_FULL;
             bool reordered = false;
             if (pp.thr_reo) reordered = !(pp.thr_reo < crand(reo_raw, pp.rho_reo, last_reo));
             uint64_t e = reordered ? Tj : delayed(pp, Tj, delay_raw);
@@ -1118,8 +1212,10 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     Q.serve_until(T_enq);
     Q.depart_before(T_enq);
   }
+  QCHECK(3);
   PROF_T0(e);
   Q.serve_until(a.horizon_ns);
+  QCHECK(4);
   PROF_ADD(13, e);
   if (lane == 0) a.emit_n[s] = Q.n_emit;
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
@@ -1128,12 +1224,12 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     uint4* gh = a.heap + (size_t)s * kHeapCap;
     for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
-    for (uint32_t k = lane; k < Q.qn + Q.pn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
+    for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
   }
   if (lane == 0) {
     SrcState ns;
     ns.tat = Q.tat;
-    ns.heap_n = Q.qn + Q.pn;
+    ns.heap_n = Q.qn + Q.pn + Q.fn;
     ns.near_n = Q.qn;
     ns.ring_n = Q.rn;
     ns.last_dup = last_dup;
@@ -1144,7 +1240,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   stamp(a, wg, lane, 4, __builtin_amdgcn_s_memrealtime());
   stamp(a, wg, lane, 5, ((uint64_t)s << 32) | n_batches);
   stamp(a, wg, lane, 6, __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
-  stamp(a, wg, lane, 7, ((uint64_t)(Q.qn + Q.pn) << 32) | Q.rn);
+  stamp(a, wg, lane, 7, ((uint64_t)(Q.qn + Q.pn + Q.fn) << 32) | Q.rn);
 #ifdef TGSIM_PROFILE
   for (int k = 0; k < 24; ++k) stamp(a, wg, lane, 8 + k, Q.pf[k]);
 #endif
@@ -1152,7 +1248,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   const uint32_t corrupted = readlane32((uint32_t)scan_sum_i32((int32_t)Q.corrupted), kWave - 1);
   const uint32_t lost = readlane32((uint32_t)scan_sum_i32((int32_t)Q.lost), kWave - 1);
   const uint64_t bytes = wave_sum(Q.bytes);
-  const uint64_t qbytes = 16ull * (Q.qn + Q.pn) + 8ull * Q.rn;
+  const uint64_t qbytes = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
   const bool err = __ballot(perr != 0) != 0;
   const uint32_t c_clone = readlane32((uint32_t)scan_sum_i32((int32_t)n_clone), kWave - 1);
   flush_verdicts();
