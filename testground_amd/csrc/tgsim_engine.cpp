@@ -308,6 +308,8 @@ struct tgsim_engine_s {
   bool sparse_seen = false;  // h_work holds a measured worklist size
   uint32_t dense_streak = 0; // dense steps chosen because the last sparse step deferred too much
   bool order_valid = false;
+  int order_by = 0;          // TGSIM_ORDER_BY: 0 HTB records of the last step, 1 its k_sim time per source
+  DevBuf<uint32_t> d_dur;
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
 
@@ -775,6 +777,11 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   const uint32_t n_wg = (E->S + kSpw - 1) / kSpw;
   const bool ordered = kSpw == 1 && E->S <= kOrderMaxSources;
   a.order = ordered && E->order_valid ? E->d_order.p : nullptr;
+  a.dur = nullptr;
+  if (ordered && E->order_by == 1) {
+    HIPCHK(E->d_dur.ensure(E->S));
+    a.dur = E->d_dur.p;
+  }
   a.stamps = nullptr;
   if (E->stamps_on) {
     HIPCHK(E->d_stamps.ensure(static_cast<size_t>(n_wg) * kStampSlots));
@@ -846,7 +853,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   // workgroups fit; with many more sources than resident workgroups the dispatcher balances alone
   if (ordered && !sparse) {
     HIPCHK(E->d_order.ensure(E->S));
-    launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
+    launch_order(a.dur ? a.dur : E->d_emit_n.p, E->S, E->d_order.p, E->st);
     HIPCHK(hipGetLastError());
     E->order_valid = true;
   }
@@ -1216,6 +1223,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
+  if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
   E->ip6_set.assign(E->N, 0);
   E->ip6.resize(E->N);
@@ -1301,7 +1309,7 @@ void tgsim_destroy(void* e) {
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
+  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release();
   E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }

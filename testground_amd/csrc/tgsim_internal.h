@@ -105,6 +105,7 @@ struct SimArgs {
   uint64_t* err_host;       // pinned host word: the sticky error bits, or null
   uint32_t* worklist;       // sparse steps: sources k_sim_sparse left for k_sim_list
   uint32_t* worklist_n;     // their count (zeroed before k_sim_sparse)
+  uint32_t* dur;            // per source: this step's k_sim time in 10-ns ticks (dispatch weight), or null
 };
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 

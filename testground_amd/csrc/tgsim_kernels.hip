@@ -772,6 +772,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   const uint32_t lane = threadIdx.x;
   constexpr uint32_t kSlotMask = kCap - 1;
   stamp(a, wg, lane, 0, __builtin_amdgcn_s_memrealtime());
+  const uint64_t t_begin = a.dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const SrcParams pp = a.params[s];
   const SrcState st = a.state[s];  // dead after the set-up: the end writes a fresh state
   SimQueue<kCap> Q{lds, pp, lane};
@@ -1218,6 +1219,10 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   QCHECK(4);
   PROF_ADD(13, e);
   if (lane == 0) a.emit_n[s] = Q.n_emit;
+  if (a.dur) {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) a.dur[s] = (uint32_t)(t_end - t_begin);
+  }
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   // ---- write back the compacted ring, the sorted queue and the state
   {
