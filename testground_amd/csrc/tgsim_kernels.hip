@@ -877,9 +877,19 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   const bool open_q = kOpen || (!corr && (uint64_t)Q.rn + Q.qn + Q.pn + Q.fn + 2 * (send - sbeg) < lim);
   uint64_t T_enq = 0;  // open queue: offer time of the last packet that reached the netem enqueue
   uint64_t idx = sbeg + lane;
-  InRec rec = {}, rec2 = {};  // records of batches b and b + 1 (two batches in flight)
-  if (idx < send) rec = a.in[idx];
-  if (idx + kWave < send) rec2 = a.in[idx + kWave];
+  // records of batches b and b + 1 (two batches in flight); branch-free loads, a lane past the end
+  // re-reads the last record (never used): a conditional load left a wait inside its branch
+  const uint64_t last_in = send > sbeg ? send - 1 : sbeg;
+  InRec rec = {}, rec2 = {};
+  if (send > sbeg) {
+    rec = a.in[idx < send ? idx : last_in];
+    rec2 = a.in[idx + kWave < send ? idx + kWave : last_in];
+  }
+  // the verdict bytes of batch b are stored during batch b + 1: stored last in their own batch,
+  // their write latency sat in front of the loop's back edge (vmcnt counts stores)
+  uint64_t v_idx = 0;
+  uint32_t v_out = 0;
+  bool v_pend = false;
   for (uint32_t b = 0; b < n_batches; ++b) {
     PROF_T0(b);
     const uint64_t my_idx = idx;
@@ -887,7 +897,8 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     const InRec r = rec;
     idx += kWave;
     rec = rec2;
-    if (idx + kWave < send) rec2 = a.in[idx + kWave];  // in flight two batches ahead
+    rec2 = a.in[idx + kWave < send ? idx + kWave : last_in];  // in flight two batches ahead
+    if (v_pend) a.verdict[v_idx] = (uint8_t)v_out;
     const uint64_t T = a.t0_ns + (uint64_t)r.tick * a.tick_ns;
     const uint32_t len = r.len & 0xFFFFu;
     uint32_t fv = 0u;
@@ -1196,8 +1207,10 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
         if (lane == j) vout = vj;
       }
     }
+    v_pend = staged;
+    v_idx = my_idx;
+    v_out = vout;
     if (staged) {
-      a.verdict[my_idx] = (uint8_t)vout;
       const uint32_t vo = vout & 15u, vc = vout >> 4;  // original 0..7, clone 0..7 or NONE
       const uint64_t uo = 1ull << (16u * (vo & 3u)), uc = 1ull << (16u * (vc & 3u));
       if (vo < 4) vc_lo += uo;
@@ -1208,6 +1221,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     }
     if ((b & 0x3FFFu) == 0x3FFFu) flush_verdicts();
   }
+  if (v_pend) a.verdict[v_idx] = (uint8_t)v_out;
   stamp(a, wg, lane, 2, __builtin_amdgcn_s_memrealtime());
   if (open_q && T_enq) {  // what the last enqueue saw: service before its offer time, then departures
     Q.serve_until(T_enq);
