@@ -6,6 +6,7 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 d=/tmp/tgv_$name; mkdir -p $d
 for src in tgsim_kernels.hip tgsim_engine.cpp tgsim_bridge.cpp; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result "$@" -c testground_amd/csrc/$src -o $d/${src%.*}.o
+  dev=""; [ "${src##*.}" = hip ] && dev="-mllvm -amdgpu-use-amdgpu-trackers=1"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result $dev "$@" -c testground_amd/csrc/$src -o $d/${src%.*}.o
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o testground_amd/libtgsim_$name.so $d/*.o
