@@ -803,10 +803,13 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   bool sparse;
   if (E->sparse_mode >= 0) {
     sparse = E->sparse_mode == 1;
-  } else if (E->n_in >= 16ull * E->S) {
-    sparse = false;  // dense traffic (C3, C5 at 100k peers): the LDS queue, in heavy-first order when ranked
+  } else if (E->n_in >= 64ull * E->S) {
+    // dense traffic (C3, C5 at 100k peers; k_sim_sparse would defer every source with more than
+    // 64 packets anyway): the LDS queue, in heavy-first order when ranked
+    sparse = false;
   } else {
-    // few packets per source: the register-only kernel wins unless the queues are too long for
+    // up to 64 packets per source (gossip, even at the flood's peak of ~20): the register-only
+    // kernel wins unless the queues are too long for
     // registers and it defers most sources to k_sim_list (2 waves/SIMD).  The worklist size of the
     // last sparse step (copied to pinned memory behind it, read without waiting) decides; every
     // 64th such step runs sparse again to re-measure
