@@ -18,6 +18,7 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "tgsim_launch.h"
@@ -321,7 +322,7 @@ struct tgsim_engine_s {
   bool gossip_on = false;
   tgsim_gossip gossip{};
   DevBuf<uint32_t> d_gfirst, d_gerr;
-  DevBuf<uint64_t> d_gfwd;
+  DevBuf<uint64_t> d_gfwd, d_gpend;
 
   int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -975,6 +976,7 @@ GossipArgs gossip_args(Eng* E, uint64_t win0, uint32_t n_ticks) {
   GossipArgs g;
   g.first = E->d_gfirst.p;
   g.fwd = E->d_gfwd.p;
+  g.pend = E->d_gpend.p;
   g.err = E->d_gerr.p;
   g.k0 = E->key0 ^ 0x3C6EF372u;
   g.k1 = E->key1 ^ 0xA54FF53Au;
@@ -1312,7 +1314,7 @@ void tgsim_destroy(void* e) {
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release();
+  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release();
   E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
@@ -1436,10 +1438,13 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   E->gossip = *g;
   HIPCHK(E->d_gfirst.ensure(static_cast<size_t>(E->S) * 64));
   HIPCHK(E->d_gfwd.ensure(E->S));
+  HIPCHK(E->d_gpend.ensure(E->S));
   HIPCHK(E->d_gerr.ensure(1));
   HIPCHK(hipMemsetAsync(E->d_gfirst.p, 0xFF, sizeof(uint32_t) * 64 * E->S, E->st));
   HIPCHK(hipMemsetAsync(E->d_gfwd.p, 0, sizeof(uint64_t) * E->S, E->st));
+  HIPCHK(hipMemsetAsync(E->d_gpend.p, 0, sizeof(uint64_t) * E->S, E->st));
   HIPCHK(hipMemsetAsync(E->d_gerr.p, 0, sizeof(uint32_t), E->st));
+  std::unordered_map<uint32_t, uint64_t> origin_pend;  // origin -> its floods (pending forwards)
   for (uint32_t f = 0; f < g->n_floods; ++f) {
     uint32_t r[4];
     philox_host(f, 0, 0x4F524947u, 0, E->key0 ^ 0x3C6EF372u, E->key1 ^ 0xA54FF53Au, r);
@@ -1449,6 +1454,11 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
     HIPCHK(hipMemcpyAsync(E->d_gfirst.p + static_cast<uint64_t>(origin - E->o.shard_begin) * 64 + f, &t,
                           sizeof t, hipMemcpyHostToDevice, E->st));
     HIPCHK(hipStreamSynchronize(E->st));  // `t` lives on this stack frame
+    origin_pend[origin - E->o.shard_begin] |= 1ull << f;
+  }
+  for (const auto& op : origin_pend) {
+    HIPCHK(hipMemcpyAsync(E->d_gpend.p + op.first, &op.second, sizeof(uint64_t), hipMemcpyHostToDevice, E->st));
+    HIPCHK(hipStreamSynchronize(E->st));
   }
   HIPCHK(hipStreamSynchronize(E->st));
   // a flood's windows grow geometrically while it spreads: reserve the window buffers (generated

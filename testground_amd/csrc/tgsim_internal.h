@@ -128,6 +128,7 @@ struct MetricsArgs {
 struct GossipArgs {
   uint32_t* first;          // [s][64] earliest receipt tick (0xFFFFFFFF: none)
   uint64_t* fwd;            // [s] floods already forwarded (or originated)
+  uint64_t* pend;           // [s] floods received (or originated), not yet forwarded
   uint32_t* err;            // bit 0: a receipt precedes the generated window
   uint32_t k0, k1;          // neighbour hash key
   uint32_t n_src, shard_begin, n_peers;

@@ -1759,7 +1759,10 @@ __device__ __forceinline__ void gossip_recv_one(const GossipArgs& g, const tgsim
   if (g.fwd[s] >> f & 1ull) return;
   uint64_t t = r.t_ns / g.tick_ns + 1;
   if (t > 0xFFFFFFFEull) t = 0xFFFFFFFEull;
-  atomicMin(&g.first[(uint64_t)s * 64 + f], (uint32_t)t);
+  // the first receipt ever of flood f at s (exactly one delivery sees "none") marks it pending, so
+  // the forward kernels read only the rows of peers with something to forward
+  if (atomicMin(&g.first[(uint64_t)s * 64 + f], (uint32_t)t) == 0xFFFFFFFFu)
+    atomicOr(reinterpret_cast<unsigned long long*>(&g.pend[s]), 1ull << f);
 }
 
 __global__ void k_gossip_recv(GossipArgs g, const tgsim_delivery* in, uint64_t n) {
@@ -1779,33 +1782,33 @@ __global__ __launch_bounds__(256) void k_gossip_recv_dev(GossipArgs g, const tgs
 // peers with all their rows in flight at once (one peer per wavefront left every wave waiting on
 // two dependent loads: the launch was latency-bound at a third of the HBM rate).
 constexpr uint32_t kGossipPeers = 8;
-__device__ __forceinline__ bool gossip_due(const GossipArgs& g, uint64_t done, uint32_t t, uint32_t lane) {
-  const bool due = lane < g.n_floods && !(done >> lane & 1ull) && t != 0xFFFFFFFFu &&
-                   (uint64_t)t < g.win0 + g.n_ticks;
+__device__ __forceinline__ bool gossip_due(const GossipArgs& g, uint64_t pend, uint32_t t, uint32_t lane) {
+  const bool due = (pend >> lane & 1ull) && (uint64_t)t < g.win0 + g.n_ticks;
   if (due && (uint64_t)t < g.win0) atomicOr(g.err, 1u);
   return due;
 }
 
+// Rows of kGossipPeers peers: the pending masks first (8 B per peer), then only the receipt ticks of
+// pending floods (most peers have none in a window: the 256-B rows stay unread).
 __device__ __forceinline__ void gossip_rows(const GossipArgs& g, uint32_t s0, uint32_t lane, uint32_t (&t)[kGossipPeers],
-                                            uint64_t (&done)[kGossipPeers]) {
+                                            uint64_t (&pend)[kGossipPeers]) {
 #pragma unroll
-  for (uint32_t i = 0; i < kGossipPeers; ++i) {
-    const uint32_t s = s0 + i;
-    done[i] = s < g.n_src ? g.fwd[s] : ~0ull;
-    t[i] = (s < g.n_src && lane < g.n_floods) ? g.first[(uint64_t)s * 64 + lane] : 0xFFFFFFFFu;
-  }
+  for (uint32_t i = 0; i < kGossipPeers; ++i) pend[i] = s0 + i < g.n_src ? g.pend[s0 + i] : 0ull;
+#pragma unroll
+  for (uint32_t i = 0; i < kGossipPeers; ++i)
+    t[i] = (pend[i] >> lane & 1ull) ? g.first[(uint64_t)(s0 + i) * 64 + lane] : 0xFFFFFFFFu;
 }
 
 __global__ __launch_bounds__(256) void k_gossip_count(GossipArgs g, uint64_t* counts) {
   const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
   if (s0 >= g.n_src) return;
   uint32_t t[kGossipPeers];
-  uint64_t done[kGossipPeers];
-  gossip_rows(g, s0, lane, t, done);
+  uint64_t pend[kGossipPeers];
+  gossip_rows(g, s0, lane, t, pend);
   uint64_t c = 0;  // lane i: the count of peer s0 + i
 #pragma unroll
   for (uint32_t i = 0; i < kGossipPeers; ++i) {
-    const uint64_t n = (uint64_t)ballot_count(gossip_due(g, done[i], t[i], lane)) * g.degree;
+    const uint64_t n = (uint64_t)ballot_count(gossip_due(g, pend[i], t[i], lane)) * g.degree;
     if (lane == i) c = n;
   }
   if (lane < kGossipPeers && s0 + lane < g.n_src) counts[s0 + lane] = c;
@@ -1815,15 +1818,18 @@ __global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64
   const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
   if (s0 >= g.n_src) return;
   uint32_t t[kGossipPeers];
-  uint64_t done[kGossipPeers];
-  gossip_rows(g, s0, lane, t, done);
+  uint64_t pend[kGossipPeers];
+  gossip_rows(g, s0, lane, t, pend);
 #pragma unroll
   for (uint32_t i = 0; i < kGossipPeers; ++i) {
     const uint32_t s = s0 + i;
-    const bool me = gossip_due(g, done[i], t[i], lane);
+    const bool me = gossip_due(g, pend[i], t[i], lane);
     const uint64_t due = __ballot(me);
     if (!due) continue;
-    if (lane == 0) g.fwd[s] |= due;
+    if (lane == 0) {
+      g.fwd[s] |= due;
+      g.pend[s] = pend[i] & ~due;  // receipts for a later window stay pending
+    }
     // earliest receipt first, ties by flood id (seq order within a tick)
     uint32_t rank = 0;
     for (uint64_t m = due; m; m &= m - 1) {
@@ -2207,17 +2213,21 @@ __global__ __launch_bounds__(256) void k_dst_sort_wide(tgsim_delivery* in, const
   if (lane == 0) cnt[d] = 0;
 }
 
-// Eight destinations per wavefront (a few records each: gossip): a destination with at most 8
-// records is ordered by its lane group of 8 (ranks from in-group shuffles); longer segments take
-// the whole wavefront in turn.
-__global__ __launch_bounds__(256) void k_dst_sort_narrow(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
-                                                  uint32_t n_dst, tgsim_delivery* out) {
+// 64/G destinations per wavefront (a few records each: gossip): a destination with at most G records
+// is ordered by its lane group of G (ranks from in-group shuffles); longer segments take the whole
+// wavefront in turn.  G follows the step's records per destination (8 below 4 on average, 16 up to
+// 10, 32 up to 24: the flood's peak windows): one wavefront per destination, as k_dst_sort_wide
+// runs, left 60 of its 64 lanes idle for most destinations.
+template <uint32_t G>
+__global__ __launch_bounds__(256) void k_dst_sort_group(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
+                                                        uint32_t n_dst, tgsim_delivery* out) {
+  constexpr uint32_t kPer = kWave / G;
   const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63u, g = lane >> 3, j = lane & 7u, d = w * 8 + g;
-  if (w * 8 >= n_dst) return;
+  const uint32_t lane = threadIdx.x & 63u, g = lane / G, j = lane % G, d = w * kPer + g;
+  if (w * kPer >= n_dst) return;
   const uint32_t n = d < n_dst ? (uint32_t)cnt[d] : 0u;
   const uint64_t b = d < n_dst ? off[d] : 0ull;
-  const bool have = n <= 8 && j < n;
+  const bool have = n <= G && j < n;
   tgsim_delivery r;
   RecKey k{~0ull, ~0ull, 1u};
   if (have) {
@@ -2226,14 +2236,14 @@ __global__ __launch_bounds__(256) void k_dst_sort_narrow(tgsim_delivery* in, con
   }
   uint32_t rank = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < 8; ++q) {  // ties: input order, as wave_rank
-    const uint32_t from = (g << 3) | q;
+  for (uint32_t q = 0; q < G; ++q) {  // ties: input order, as wave_rank
+    const uint32_t from = g * G + q;
     const uint64_t t = shfl64(k.t, from), sq = shfl64(k.sq, from);
     const uint32_t c = (uint32_t)__shfl((int)k.c, (int)from, 64);
     rank += (q < n && (rec_lt(t, sq, c, k.t, k.sq, k.c) || (!rec_lt(k.t, k.sq, k.c, t, sq, c) && q < j))) ? 1u : 0u;
   }
   if (have) out[b + rank] = r;
-  for (uint64_t big = __ballot(j == 0 && n > 8); big; big &= big - 1) {
+  for (uint64_t big = __ballot(j == 0 && n > G); big; big &= big - 1) {
     const uint32_t gl = (uint32_t)__builtin_ctzll(big);
     sort_segment(in, readlane64(b, gl), readlane32(n, gl), out, lane);
   }
@@ -2453,8 +2463,11 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                      tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
   if (!n_dst) return;
+  // n_hint bounds the step's records (offered packets or the exact count).  Measured at the 1M-peer
+  // flood's peak (up to ~20 records per destination): groups of 16 lanes 0.77 ms, of 32 3.8 ms
+  // (the in-group shuffles), the wavefront per destination 1.4 ms
   if (n_hint <= 8ull * n_dst)
-    hipLaunchKernelGGL(k_dst_sort_narrow, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
+    hipLaunchKernelGGL(k_dst_sort_group<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
   else
     hipLaunchKernelGGL(k_dst_sort_wide, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
 }
