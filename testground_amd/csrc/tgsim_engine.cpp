@@ -1173,11 +1173,16 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   };
   if ((rc = E->hip(hipSetDevice(E->dev), "hipSetDevice"))) return bail(rc);
   if ((rc = E->hip(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking), "stream"))) return bail(rc);
-  // the delivery stream gets the high priority: ROCclr puts it on a hardware queue of its own, so
-  // the delivery of one step runs beside the next k_sim instead of behind it in one queue
+  // the delivery stream gets a priority of its own (so ROCclr puts it on a hardware queue of its
+  // own, and the delivery of one step runs beside the next k_sim instead of behind it in one
+  // queue): the lowest, since the delivery is off the critical path (next k_sim; the gossip loop's
+  // generation) and at high priority its waves were dispatched first (A/B: storm +1.2 %, 1M-peer
+  // gossip +3 % at low priority; TGSIM_DST_PRIO=0 restores high)
   int prio_lo = 0, prio_hi = 0;
   if ((rc = E->hip(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), "stream"))) return bail(rc);
-  if ((rc = E->hip(hipStreamCreateWithPriority(&E->dst_st, hipStreamNonBlocking, prio_hi), "stream")))
+  const char* dp = getenv("TGSIM_DST_PRIO");
+  if ((rc = E->hip(hipStreamCreateWithPriority(&E->dst_st, hipStreamNonBlocking, dp && atoi(dp) == 0 ? prio_hi : prio_lo),
+                   "stream")))
     return bail(rc);
   if ((rc = E->hip(hipStreamCreateWithPriority(&E->rt_st, hipStreamNonBlocking, prio_hi), "stream")))
     return bail(rc);
