@@ -321,7 +321,7 @@ struct tgsim_engine_s {
   // gossip workload (C4)
   bool gossip_on = false;
   tgsim_gossip gossip{};
-  DevBuf<uint32_t> d_gfirst, d_gerr;
+  DevBuf<uint32_t> d_gfirst, d_gerr, d_gnbr;
   DevBuf<uint64_t> d_gfwd, d_gpend;
 
   int fail(int code, const char* fmt, ...) {
@@ -977,6 +977,7 @@ GossipArgs gossip_args(Eng* E, uint64_t win0, uint32_t n_ticks) {
   g.first = E->d_gfirst.p;
   g.fwd = E->d_gfwd.p;
   g.pend = E->d_gpend.p;
+  g.nbr = E->d_gnbr.cap ? E->d_gnbr.p : nullptr;
   g.err = E->d_gerr.p;
   g.k0 = E->key0 ^ 0x3C6EF372u;
   g.k1 = E->key1 ^ 0xA54FF53Au;
@@ -1084,6 +1085,12 @@ int deliver_local(Eng* E) {
   hipStream_t sq = E->dst_st;
   HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
   HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+  if (E->gossip_on) {  // receipts of the gossip workload, from the emit regions on the simulate
+                       // stream: the next window's generation waits for nothing on the delivery side
+    launch_gossip_recv_emit(gossip_args(E, 0, 0), E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, E->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(E->ev_recv, E->st));
+  }
 
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
@@ -1101,13 +1108,7 @@ int deliver_local(Eng* E) {
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
   launch_local_scatter(E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq);
   HIPCHK(hipGetLastError());
-  if (E->gossip_on) {  // receipts (before the sort, which may reuse the scatter buffer), the count
-                       // read on the device when the host never needed it
-    if (need_n) launch_gossip(gossip_args(E, 0, 0), E->d_scatter.p, n, nullptr, nullptr, nullptr, 0, sq);
-    else launch_gossip_recv_dev(gossip_args(E, 0, 0), E->d_scatter.p, E->d_dtot.p, sq);
-    HIPCHK(hipGetLastError());
-  }
-  HIPCHK(hipEventRecord(E->ev_recv, sq));  // the next window's generation needs no more than this
+  if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
   tgsim_delivery* dst = nullptr;
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
@@ -1319,7 +1320,7 @@ void tgsim_destroy(void* e) {
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release();
+  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release();
   E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
@@ -1445,6 +1446,10 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   HIPCHK(E->d_gfwd.ensure(E->S));
   HIPCHK(E->d_gpend.ensure(E->S));
   HIPCHK(E->d_gerr.ensure(1));
+  E->d_gnbr.release();  // the table of another degree, if any
+  HIPCHK(E->d_gnbr.ensure(static_cast<size_t>(E->S) * g->degree));
+  launch_gossip_nbr(gossip_args(E, 0, 0), E->d_gnbr.p, E->st);
+  HIPCHK(hipGetLastError());
   HIPCHK(hipMemsetAsync(E->d_gfirst.p, 0xFF, sizeof(uint32_t) * 64 * E->S, E->st));
   HIPCHK(hipMemsetAsync(E->d_gfwd.p, 0, sizeof(uint64_t) * E->S, E->st));
   HIPCHK(hipMemsetAsync(E->d_gpend.p, 0, sizeof(uint64_t) * E->S, E->st));

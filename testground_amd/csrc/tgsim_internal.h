@@ -129,6 +129,7 @@ struct GossipArgs {
   uint32_t* first;          // [s][64] earliest receipt tick (0xFFFFFFFF: none)
   uint64_t* fwd;            // [s] floods already forwarded (or originated)
   uint64_t* pend;           // [s] floods received (or originated), not yet forwarded
+  const uint32_t* nbr;      // [s][degree] out-neighbours (tabled at gossip_init), or null
   uint32_t* err;            // bit 0: a receipt precedes the generated window
   uint32_t k0, k1;          // neighbour hash key
   uint32_t n_src, shard_begin, n_peers;

@@ -1777,6 +1777,29 @@ __global__ __launch_bounds__(256) void k_gossip_recv_dev(GossipArgs g, const tgs
     gossip_recv_one(g, in[i]);
 }
 
+// The out-neighbour table (the hash of (seed, peer, k) once per peer and k, not at every forward).
+__global__ __launch_bounds__(256) void k_gossip_nbr(GossipArgs g, uint32_t* nbr) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)g.n_src * g.degree) return;
+  const uint32_t s = (uint32_t)(i / g.degree), k = (uint32_t)(i % g.degree);
+  nbr[i] = gossip_neighbour(g, g.shard_begin + s, k);
+}
+
+// Receipts straight from the step's emit regions (single shard), before any delivery ordering:
+// the gossip loop's next window then waits for k_sim and this kernel only, while the scatter and
+// the per-destination sort run beside it at low priority.  Receipts are order-free (earliest tick
+// wins), and a delivery of an already forwarded flood costs one read of its peer's mask.
+__global__ __launch_bounds__(256) void k_gossip_recv_emit(GossipArgs g, const tgsim_delivery* emit, const uint32_t* emit_n,
+                                                          const uint64_t* off, uint32_t n_src) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
+    const uint32_t n = emit_n[s];
+    const tgsim_delivery* base = emit + 2 * off[s] + (uint64_t)kHeapCap * s;
+    for (uint32_t i = lane; i < n; i += kWave) gossip_recv_one(g, base[i]);
+  }
+}
+
 // Floods due in [win0, win0 + n_ticks) for local peer s: lane f holds flood f's earliest receipt
 // tick (a coalesced 256-B row); late receipts are flagged.  One wavefront handles kGossipPeers
 // peers with all their rows in flight at once (one peer per wavefront left every wave waiting on
@@ -1842,7 +1865,7 @@ __global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64
     const uint64_t o = off[s] + (uint64_t)rank * g.degree;
     for (uint32_t k = 0; k < g.degree; ++k) {
       InRec rec;
-      rec.dst = gossip_neighbour(g, src, k);
+      rec.dst = g.nbr ? g.nbr[(uint64_t)s * g.degree + k] : gossip_neighbour(g, src, k);
       rec.seq = lane * g.degree + k;
       rec.tick = (uint32_t)(t[i] - g.win0);
       rec.len = g.msg_len;
@@ -2377,6 +2400,18 @@ void launch_metrics_src(const MetricsArgs& m, hipStream_t st) {
 void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_t n_dst, unsigned long long* dst,
                         unsigned long long* hist, hipStream_t st) {
   if (n_dst) hipLaunchKernelGGL(k_metrics_dst, dim3((n_dst + 3) / 4), dim3(256), 0, st, recs, off, n_dst, dst, hist);
+}
+
+void launch_gossip_nbr(const GossipArgs& g, uint32_t* nbr, hipStream_t st) {
+  const uint64_t n = (uint64_t)g.n_src * g.degree;
+  if (n) hipLaunchKernelGGL(k_gossip_nbr, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, g, nbr);
+}
+
+void launch_gossip_recv_emit(const GossipArgs& g, const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off,
+                             uint32_t n_src, hipStream_t st) {
+  if (!n_src) return;
+  const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);
+  hipLaunchKernelGGL(k_gossip_recv_emit, dim3(wgs), dim3(256), 0, st, g, emit, emit_n, off, n_src);
 }
 
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st) {

@@ -48,6 +48,9 @@ void launch_metrics_src(const MetricsArgs& m, hipStream_t st);
 void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_t n_dst, unsigned long long* dst,
                         unsigned long long* hist, hipStream_t st);
 // Receipts of n_dev[0] records (count read on the device).
+void launch_gossip_nbr(const GossipArgs& g, uint32_t* nbr, hipStream_t st);
+void launch_gossip_recv_emit(const GossipArgs& g, const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off,
+                             uint32_t n_src, hipStream_t st);
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st);
 // Exclusive scan of in[0..n) into out[0..n] (out[n] = total, also stored at *total when non-null);
 // pos (optional) receives a copy of out[0..n), the scatter cursors.
