@@ -417,6 +417,8 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     def run_steps(n):
         if stepper is not None and workload == "storm":  # pre-generated: simulate one step ahead
             stepper.run(n, window)
+        elif workload == "storm":  # pre-generated windows, up to four per launch (tgsim_step_n)
+            eng.step_n(window, n)
         else:
             for _ in range(n):
                 one_step()

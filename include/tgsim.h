@@ -216,6 +216,13 @@ int tgsim_gen_storm(void* engine, double lambda, uint32_t n_ticks);
  * call that reads results (drain, verdicts, stats, gossip_reached, sim_kernel_ms) synchronizes
  * first.  A simulated-time overflow (-EOVERFLOW) is then reported by the next step or reader. */
 int tgsim_step(void* engine, uint32_t n_ticks);
+/* n_steps consecutive tgsim_step(engine, n_ticks) calls, with identical results (verdicts then
+ * refer to the last window).  Windows of generated traffic (tgsim_gen_storm) on an engine that owns
+ * every peer run up to four per launch: a source's next window starts as soon as its previous one
+ * is done, so one window's slowest sources overlap the next window's first ones (no launch tail or
+ * gap between the windows of a group).  A source whose previous window does not complete in time
+ * (a hardware fault) is reported as -EIO. */
+int tgsim_step_n(void* engine, uint32_t n_ticks, uint32_t n_steps);
 
 /* Multi-shard form of tgsim_step.  Phase 1 simulates the owned sources and writes the scheduled
  * records into d_out (DEVICE memory, caller-owned, capacity out_cap records) grouped by the
@@ -382,6 +389,8 @@ void* tgsim_stream(void* engine);
  * workgroup (s_memrealtime at its phase boundaries, batch count, HW_ID, queue sizes); copies them
  * for the last step and returns the word count (0 when disabled). */
 int64_t tgsim_debug_stamps(void* engine, uint64_t* out, size_t cap);
+/* Diagnostics: windows simulated by fused launches (tgsim_step_n) since the engine was created. */
+int64_t tgsim_debug_fused_windows(void* engine);
 
 #ifdef __cplusplus
 }

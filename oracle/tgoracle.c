@@ -885,6 +885,16 @@ int tgo_step(void* p, uint32_t n_ticks) {
     return 0;
 }
 
+/* tgsim_step_n (include/tgsim.h): n_steps windows in order; the engine fuses them into launches,
+ * which changes no result, so the golden model simply steps n times. */
+int tgo_step_n(void* p, uint32_t n_ticks, uint32_t n_steps) {
+    for (uint32_t i = 0; i < n_steps; ++i) {
+        int rc = tgo_step(p, n_ticks);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
 /* Multi-shard form: scheduled records grouped by the destination's shard into `out` (host
  * memory here), counts per shard in `counts`. */
 static int step_sim_core(oracle* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out,

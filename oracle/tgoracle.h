@@ -34,6 +34,7 @@ int64_t tgo_configure_batch(void* o, const uint32_t* peers, const tgsim_config* 
 int tgo_submit(void* o, const tgsim_pkt* pkts, size_t n);
 int tgo_gen_storm(void* o, double lambda, uint32_t n_ticks);
 int tgo_step(void* o, uint32_t n_ticks);
+int tgo_step_n(void* o, uint32_t n_ticks, uint32_t n_steps);
 int tgo_step_sim(void* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out, size_t cap,
                  uint64_t* counts);
 int tgo_step_sim_launch(void* o, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* out, size_t cap);

@@ -128,6 +128,7 @@ EXPORTS = [
     "tgsim_deliver_slotted_async",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
+    "tgsim_debug_fused_windows", "tgsim_step_n",
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
     "tgsim_bridge_create", "tgsim_bridge_destroy", "tgsim_bridge_send", "tgsim_bridge_step",
     "tgsim_bridge_recv", "tgsim_bridge_pending", "tgsim_bridge_in_flight", "tgsim_bridge_now_tick",
@@ -155,6 +156,7 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("submit", C.c_int, vp, C.c_void_p, C.c_size_t)
     f("gen_storm", C.c_int, vp, C.c_double, C.c_uint32)
     f("step", C.c_int, vp, C.c_uint32)
+    f("step_n", C.c_int, vp, C.c_uint32, C.c_uint32)
     f("step_sim", C.c_int, vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), vp, C.c_size_t,
       C.POINTER(C.c_uint64))
     f("step_sim_launch", C.c_int, vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), vp, C.c_size_t)
@@ -180,6 +182,7 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("sim_kernel_ms", C.c_double, vp, C.POINTER(C.c_uint64), C.c_int)
     f("stream", vp, vp)
     f("debug_stamps", C.c_int64, vp, C.c_void_p, C.c_size_t)
+    f("debug_fused_windows", C.c_int64, vp)
     f("abi_version", C.c_uint32)
     f("gossip_init", C.c_int, vp, C.POINTER(Gossip))
     f("gen_gossip", C.c_int, vp, C.c_uint32)

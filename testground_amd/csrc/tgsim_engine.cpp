@@ -207,8 +207,13 @@ struct tgsim_engine_s {
   hipEvent_t ev_dst = nullptr;   // recorded after the last delivery on dst_st
   hipEvent_t ev_recv = nullptr;  // recorded after the last delivery's scatter (and gossip receipts)
   hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
-  // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize)
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+  // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize), with
+  // the number of windows the launch simulated (a fused launch counts each of its windows)
+  struct PendingTiming {
+    hipEvent_t first, second;
+    uint32_t windows;
+  };
+  std::vector<PendingTiming> ev_pending;
   std::vector<hipEvent_t> ev_pool;
   uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
   uint64_t* h_pub = nullptr;    // pinned words a scan publishes: [0] total, [1] flag, [2] sequence
@@ -311,6 +316,21 @@ struct tgsim_engine_s {
   bool order_valid = false;
   int order_by = 0;          // TGSIM_ORDER_BY: 0 HTB records of the last step, 1 its k_sim time per source
   DevBuf<uint32_t> d_dur;
+  // fused windows (tgsim_step_n): per group parity p and window i the emit regions, their counts
+  // and the per-destination histogram; ev_fgrp[p]: after the deliveries that last read set p
+  struct LocalSet {
+    DevBuf<tgsim_delivery> emit;
+    DevBuf<uint32_t> emit_n;
+  };
+  LocalSet fset[2][kFuseMax];
+  DevBuf<uint64_t> f_lcnt[2];  // [window][destination] histograms of a group (zero between groups)
+  hipEvent_t ev_fgrp[2] = {};
+  uint32_t fgrp = 0;                    // parity of the next fused group
+  DevBuf<uint8_t> f_verdict[kFuseMax];  // verdicts of a group's windows but the last (discarded)
+  DevBuf<uint32_t> d_done, d_ticket;    // per-source completion words, ticket counter
+  uint32_t step_no = 0, ticket_no = 0;  // windows and tickets issued by fused launches so far
+  uint64_t fused_windows = 0;
+  int fuse_max = static_cast<int>(kFuseMax);  // TGSIM_FUSE: windows per fused launch (1: never fuse)
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
 
@@ -696,7 +716,7 @@ int harvest_timing(Eng* E, bool wait) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
     E->sim_ms += ms;
-    E->sim_launches++;
+    E->sim_launches += pr.windows;
     E->ev_pool.push_back(pr.first);
     E->ev_pool.push_back(pr.second);
   }
@@ -707,8 +727,10 @@ int harvest_timing(Eng* E, bool wait) {
 // The sticky error word of k_sim (simulated time past 2^46 ns), as k_sim stores it into pinned host
 // memory: exact after a stream synchronization, possibly one step late otherwise.
 int check_sim_error(Eng* E) {
-  if (E->h_err && (__atomic_load_n(E->h_err, __ATOMIC_RELAXED) & kErrTimeOverflow))
-    return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
+  const uint64_t herr = E->h_err ? __atomic_load_n(E->h_err, __ATOMIC_RELAXED) : 0;
+  if (herr & kErrTimeOverflow) return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
+  if (herr & kErrHandoff)
+    return E->fail(-EIO, "fused step: a source's previous window did not complete (hand-off timed out)");
   if (E->h_xerr && __atomic_load_n(E->h_xerr, __ATOMIC_RELAXED))
     return E->fail(-ENOSPC, "exchange: a step's records for one rank exceed the slot capacity");
   return 0;
@@ -720,6 +742,29 @@ int sync_stream(Eng* E) {
   HIPCHK(hipStreamSynchronize(E->rt_st));
   HIPCHK(hipStreamSynchronize(E->dst_st));
   return harvest_timing(E, true);
+}
+
+// The step-independent part of k_sim's arguments (tables, state, statistics, keys).
+SimArgs base_sim_args(Eng* E) {
+  SimArgs a{};
+  a.params = E->d_params.p;
+  a.state = E->d_state.p;
+  a.enabled = E->d_enabled.p;
+  a.ip = E->d_ip.p;
+  a.rules = E->d_rules.p;
+  a.heap = E->d_heap.p;
+  a.ring = E->d_ring.p;
+  a.stats = E->d_stats.p;
+  a.key0 = E->key0;
+  a.key1 = E->key1;
+  a.n_src = E->S;
+  a.shard_begin = E->o.shard_begin;
+  a.n_peers = E->N;
+  a.queue_limit = E->o.queue_limit;
+  a.any_disabled = E->n_disabled ? 1u : 0u;
+  a.tick_ns = E->o.tick_ns;
+  a.err_host = E->d_err_host;
+  return a;
 }
 
 int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
@@ -751,28 +796,12 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
   HIPCHK(E->d_emit.ensure(emit_cap));
   HIPCHK(E->d_emit_n.ensure(E->S));
-  SimArgs a;
-  a.params = E->d_params.p;
-  a.state = E->d_state.p;
-  a.enabled = E->d_enabled.p;
-  a.ip = E->d_ip.p;
-  a.rules = E->d_rules.p;
+  SimArgs a = base_sim_args(E);
   a.off = E->d_off.p;
   a.in = E->d_in.p;
   a.verdict = E->d_verdict.p;
-  a.heap = E->d_heap.p;
-  a.ring = E->d_ring.p;
   a.emit = E->d_emit.p;
   a.emit_n = E->d_emit_n.p;
-  a.stats = E->d_stats.p;
-  a.key0 = E->key0;
-  a.key1 = E->key1;
-  a.n_src = E->S;
-  a.shard_begin = E->o.shard_begin;
-  a.n_peers = E->N;
-  a.queue_limit = E->o.queue_limit;
-  a.any_disabled = E->n_disabled ? 1u : 0u;
-  a.tick_ns = E->o.tick_ns;
   a.t0_ns = E->now_tick * E->o.tick_ns;
   a.horizon_ns = (E->now_tick + n_ticks) * E->o.tick_ns + E->o.lookahead_ns;
   const uint32_t n_wg = (E->S + kSpw - 1) / kSpw;
@@ -838,7 +867,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     HIPCHK(hipMemcpyAsync(E->h_work, E->d_work.p, sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
     E->sparse_seen = true;
   }
-  E->ev_pending.emplace_back(ev0, ev1);
+  E->ev_pending.push_back({ev0, ev1, 1u});
   if (E->metrics_on) {
     MetricsArgs m;
     m.off = E->d_off.p;
@@ -1076,12 +1105,46 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   return 0;
 }
 
+// The local delivery of one window on the delivery stream (after its k_sim): scan of the
+// per-destination histogram -> scatter straight from the emit regions -> per-destination order.
+int deliver_local_from(Eng* E, const tgsim_delivery* emit, const uint32_t* emit_n, uint64_t* lcnt,
+                       const uint64_t* off, uint64_t n_in) {
+  const uint32_t nd = E->N;
+  hipStream_t sq = E->dst_st;
+  HIPCHK(E->d_doff.ensure(nd + 1));
+  HIPCHK(E->d_dpos.ensure(nd));
+  HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
+  HIPCHK(E->d_dtot.ensure(1));
+  launch_scan(lcnt, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
+  HIPCHK(hipGetLastError());
+  const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
+  uint64_t n = 2 * n_in + static_cast<uint64_t>(kHeapCap) * E->S;  // upper bound
+  if (need_n) {
+    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
+    HIPCHK(hipStreamSynchronize(sq));
+    n = E->h_dtot;
+  }
+  HIPCHK(E->d_scatter.ensure(n ? n : 1));
+  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq);
+  HIPCHK(hipGetLastError());
+  if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
+  tgsim_delivery* dst = nullptr;
+  int rc = delivery_out(E, n, &dst, sq);
+  if (rc) return rc;
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, lcnt, nd, dst, sq, need_n ? n : n_in);
+  HIPCHK(hipGetLastError());
+  if (E->metrics_on) {
+    launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
+    HIPCHK(hipGetLastError());
+  }
+  return 0;
+}
+
 // Single shard: k_sim counted every emitted record per destination, so the step needs no host
 // round trip: scan -> scatter straight from the emit regions -> per-destination order, on the
 // delivery stream beside the next step's k_sim (which writes the other emit pair).  Only the drain
 // bookkeeping needs the record count on the host.
 int deliver_local(Eng* E) {
-  const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
   HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
   HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
@@ -1092,38 +1155,144 @@ int deliver_local(Eng* E) {
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
   }
 
-  HIPCHK(E->d_doff.ensure(nd + 1));
-  HIPCHK(E->d_dpos.ensure(nd));
-  HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
-  HIPCHK(E->d_dtot.ensure(1));
-  launch_scan(E->d_lcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
-  HIPCHK(hipGetLastError());
-  const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
-  uint64_t n = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;  // upper bound
-  if (need_n) {
-    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
-    HIPCHK(hipStreamSynchronize(sq));
-    n = E->h_dtot;
-  }
-  HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_local_scatter(E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq);
-  HIPCHK(hipGetLastError());
-  if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
-  tgsim_delivery* dst = nullptr;
-  int rc = delivery_out(E, n, &dst, sq);
+  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_lcnt.p, nd, dst, sq, need_n ? n : E->n_in);
-  HIPCHK(hipGetLastError());
-  if (E->metrics_on) {
-    launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
-    HIPCHK(hipGetLastError());
-  }
   HIPCHK(hipEventRecord(E->ev_local, sq));
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   std::swap(E->d_emit, E->d_emit_alt);
   std::swap(E->d_emit_n, E->d_emit_n_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
   std::swap(E->ev_local, E->ev_local_alt);
+  return 0;
+}
+
+// tgsim_step_n's fused path: can the next g windows run in one k_sim_fused launch?  Generated
+// dense windows on an engine that owns every peer, no host packets, no per-window diagnostics.
+bool fusable(Eng* E, uint32_t n_ticks, uint32_t g) {
+  if (g < 2 || E->S != E->N || !E->staged.empty() || E->gen_q.size() < g || E->metrics_on || E->stamps_on ||
+      E->gossip_on || E->sparse_mode == 1 || E->order_by != 0 || kSpw != 1)
+    return false;
+  for (uint32_t i = 0; i < g; ++i)
+    if (E->gen_q[i].ticks != n_ticks || E->gen_q[i].n < 64ull * E->S) return false;  // sparse windows
+  return true;
+}
+
+// g consecutive windows in one k_sim_fused launch, then the g local deliveries on the delivery
+// stream (beside the next group's launch, which writes the other parity's buffer sets).
+int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
+  int rc = check_sim_error(E);
+  if (rc) return rc;
+  rc = harvest_timing(E, false);
+  if (rc) return rc;
+  rc = flush_config(E);  // effective from the first window, as for g tgsim_step calls
+  if (rc) return rc;
+  const uint32_t p = E->fgrp;
+  Eng::GenWindow win[kFuseMax];
+  for (uint32_t i = 0; i < g; ++i) win[i] = std::move(E->gen_q[i]);
+  E->gen_q.erase(E->gen_q.begin(), E->gen_q.begin() + g);
+  E->gen_q_ticks -= static_cast<uint64_t>(g) * n_ticks;
+  HIPCHK(hipStreamWaitEvent(E->st, E->ev_fgrp[p], 0));  // the deliveries that last read set p
+  if (E->d_done.cap < E->S) {
+    HIPCHK(E->d_done.ensure(E->S));
+    HIPCHK(hipMemsetAsync(E->d_done.p, 0, sizeof(uint32_t) * E->d_done.cap, E->st));
+    HIPCHK(E->d_ticket.ensure(1));
+    HIPCHK(hipMemsetAsync(E->d_ticket.p, 0, sizeof(uint32_t), E->st));
+    E->step_no = E->ticket_no = 0;
+  }
+  SimArgs a = base_sim_args(E);
+  const bool ordered = E->S <= kOrderMaxSources;
+  a.order = ordered && E->order_valid ? E->d_order.p : nullptr;
+  FusedArgs f{};
+  const uint64_t nseg = static_cast<uint64_t>(g) * E->N;  // (window, destination) segments
+  if (E->f_lcnt[p].cap < static_cast<uint64_t>(kFuseMax) * E->N) {
+    HIPCHK(E->f_lcnt[p].ensure(static_cast<uint64_t>(kFuseMax) * E->N));
+    HIPCHK(hipMemsetAsync(E->f_lcnt[p].p, 0, sizeof(uint64_t) * E->f_lcnt[p].cap, E->st));
+  }
+  uint64_t rec_bound = 0;  // records the group's windows can emit
+  for (uint32_t i = 0; i < g; ++i) {
+    Eng::LocalSet& ls = E->fset[p][i];
+    HIPCHK(ls.emit.ensure(2 * win[i].n + static_cast<uint64_t>(kHeapCap) * E->S));
+    HIPCHK(ls.emit_n.ensure(E->S));
+    rec_bound += 2 * win[i].n + static_cast<uint64_t>(kHeapCap) * E->S;
+    DevBuf<uint8_t>& vb = i + 1 == g ? E->d_verdict : E->f_verdict[i];
+    HIPCHK(vb.ensure(win[i].n ? win[i].n : 1));
+    const uint64_t t0 = (E->now_tick + static_cast<uint64_t>(i) * n_ticks) * E->o.tick_ns;
+    f.w[i] = {win[i].off.p, win[i].in.p, vb.p, ls.emit.p, ls.emit_n.p,
+              reinterpret_cast<unsigned long long*>(E->f_lcnt[p].p + static_cast<uint64_t>(i) * E->N), t0,
+              t0 + n_ticks * E->o.tick_ns + E->o.lookahead_ns};
+  }
+  f.n_win = g;
+  f.step_base = E->step_no;
+  f.ticket_base = E->ticket_no;
+  f.ticket = E->d_ticket.p;
+  f.done = E->d_done.p;
+  hipEvent_t ev0, ev1;
+  HIPCHK(take_event(E, &ev0));
+  HIPCHK(take_event(E, &ev1));
+  HIPCHK(hipEventRecord(ev0, E->st));
+  launch_sim_fused(a, f, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ev1, E->st));
+  E->ev_pending.push_back({ev0, ev1, g});
+  E->step_no += g;
+  E->ticket_no += g * E->S;
+  E->fused_windows += g;
+  if (ordered) {  // the next launch's dispatch order, from the last window's HTB records
+    HIPCHK(E->d_order.ensure(E->S));
+    launch_order(E->fset[p][g - 1].emit_n.p, E->S, E->d_order.p, E->st);
+    HIPCHK(hipGetLastError());
+    E->order_valid = true;
+  }
+  // the group's deliveries, beside the next launch: one scan over the (window, destination)
+  // counts, one scatter of every window's emit regions, one sort per segment; the sorted output is
+  // window 0's deliveries, then window 1's, ... (the drain order of g tgsim_step calls)
+  hipStream_t sq = E->dst_st;
+  HIPCHK(hipEventRecord(E->ev_sim, E->st));
+  HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+  HIPCHK(E->d_doff.ensure(nseg + 1));
+  HIPCHK(E->d_dpos.ensure(nseg));
+  HIPCHK(E->d_dblk.ensure((nseg + 1023) / 1024 + 1));
+  HIPCHK(E->d_dtot.ensure(1));
+  launch_scan_w(E->f_lcnt[p].p, E->d_doff.p, nseg, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
+  HIPCHK(hipGetLastError());
+  uint64_t n_rec = rec_bound;
+  if (!(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES)) {
+    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
+    HIPCHK(hipStreamSynchronize(sq));
+    n_rec = E->h_dtot;
+  }
+  HIPCHK(E->d_scatter.ensure(n_rec ? n_rec : 1));
+  GroupDeliver gd{};
+  for (uint32_t i = 0; i < g; ++i) {
+    gd.emit[i] = E->fset[p][i].emit.p;
+    gd.emit_n[i] = E->fset[p][i].emit_n.p;
+    gd.off[i] = win[i].off.p;
+  }
+  gd.n_src = E->S;
+  gd.n_dst = E->N;
+  gd.pos = E->d_dpos.p;
+  gd.out = E->d_scatter.p;
+  launch_local_scatter_group(gd, g, sq);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(E->ev_recv, sq));
+  tgsim_delivery* dst = nullptr;
+  rc = delivery_out(E, n_rec, &dst, sq);
+  if (rc) return rc;
+  launch_dst_sort_w1(E->d_scatter.p, E->d_doff.p, E->f_lcnt[p].p, static_cast<uint32_t>(nseg), dst, sq);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(E->ev_fgrp[p], sq));
+  HIPCHK(hipEventRecord(E->ev_dst, E->dst_st));
+  E->fgrp = p ^ 1;
+  // the last window's input stays the engine's current input (as after tgsim_step); the replaced
+  // buffers and the other windows go back to the free list (a generation waits for ev_dst first)
+  std::swap(E->d_off, win[g - 1].off);
+  std::swap(E->d_in, win[g - 1].in);
+  E->n_in = win[g - 1].n;
+  E->n_verdict = E->n_in;
+  for (uint32_t i = 0; i < g; ++i) E->gen_free.push_back(std::move(win[i]));
+  E->perm.clear();
+  E->last_perm.clear();
+  E->now_tick += static_cast<uint64_t>(g) * n_ticks;
   return 0;
 }
 
@@ -1235,6 +1404,11 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
+  if (const char* fz = getenv("TGSIM_FUSE")) E->fuse_max = std::max(1, std::min(atoi(fz), static_cast<int>(kFuseMax)));
+  for (hipEvent_t& ev : E->ev_fgrp) {
+    if ((rc = E->hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return bail(rc);
+    if ((rc = E->hip(hipEventRecord(ev, E->dst_st), "event"))) return bail(rc);
+  }
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
   E->ip6_set.assign(E->N, 0);
   E->ip6.resize(E->N);
@@ -1328,6 +1502,13 @@ void tgsim_destroy(void* e) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
+  for (auto& grp : E->fset)
+    for (auto& ls : grp) { ls.emit.release(); ls.emit_n.release(); }
+  for (auto& v : E->f_lcnt) v.release();
+  for (auto& v : E->f_verdict) v.release();
+  E->d_done.release(); E->d_ticket.release();
+  for (hipEvent_t ev : E->ev_fgrp)
+    if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
   if (E->h_err) (void)hipHostFree(E->h_err);
   if (E->h_xerr) (void)hipHostFree(E->h_xerr);
@@ -1682,6 +1863,26 @@ int tgsim_step(void* e, uint32_t n_ticks) {
   return finish_sim_timing(E);
 }
 
+int tgsim_step_n(void* e, uint32_t n_ticks, uint32_t n_steps) {
+  Eng* E = as_eng(e);
+  if (!E || n_ticks == 0) return -EINVAL;
+  if (E->route_n) return E->fail(-EBUSY, "launched steps are not finished yet");
+  HIPCHK(hipSetDevice(E->dev));
+  while (n_steps) {
+    const uint32_t g = std::min(n_steps, static_cast<uint32_t>(E->fuse_max));
+    int rc;
+    if (fusable(E, n_ticks, g)) {
+      rc = step_fused(E, n_ticks, g);
+      n_steps -= g;
+    } else {
+      rc = tgsim_step(e, n_ticks);
+      n_steps -= 1;
+    }
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 int64_t tgsim_drain(void* e, tgsim_delivery* out, size_t cap) {
   Eng* E = as_eng(e);
   if (!E || (!out && cap)) return -EINVAL;
@@ -1842,6 +2043,11 @@ int64_t tgsim_debug_stamps(void* e, uint64_t* out, size_t cap) {
     HIPCHK(hipMemcpy(out, E->d_stamps.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   }
   return static_cast<int64_t>(n);
+}
+
+int64_t tgsim_debug_fused_windows(void* e) {
+  Eng* E = as_eng(e);
+  return E ? static_cast<int64_t>(E->fused_windows) : -EINVAL;
 }
 
 void* tgsim_stream(void* e) {

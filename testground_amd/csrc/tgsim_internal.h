@@ -109,6 +109,40 @@ struct SimArgs {
 };
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 
+// Fused launch of up to kFuseMax consecutive windows (k_sim_fused): ticket t -> window t / S, the
+// t % S-th source in dispatch order.  A source's window k > 0 starts once its window k - 1 has
+// stored done[s] = step_base + k (the hand-off); the windows differ only in these
+// per-window fields.
+constexpr uint32_t kFuseMax = 4;
+struct FusedWindow {
+  const uint64_t* off;
+  const InRec* in;
+  uint8_t* verdict;
+  tgsim_delivery* emit;
+  uint32_t* emit_n;
+  unsigned long long* dst_cnt;
+  uint64_t t0_ns, horizon_ns;
+};
+struct FusedArgs {
+  FusedWindow w[kFuseMax];
+  uint32_t n_win;
+  uint32_t step_base;   // done[] value that window 0's predecessors have reached
+  uint32_t ticket_base; // *ticket before this launch (tickets are counted across launches)
+  uint32_t* ticket;
+  uint32_t* done;       // [S] last completed window of each source (wrapping step counter)
+};
+constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
+// Local delivery of a fused group: window w's emit regions, counts and CSR offsets; pos holds the
+// scatter cursors of the g * n_dst (window, destination) segments.
+struct GroupDeliver {
+  const tgsim_delivery* emit[kFuseMax];
+  const uint32_t* emit_n[kFuseMax];
+  const uint64_t* off[kFuseMax];
+  uint32_t n_src, n_dst;
+  uint64_t* pos;
+  tgsim_delivery* out;
+};
+
 // K8 metrics tables (include/tgsim.h TGSIM_METRICS_*).
 constexpr uint32_t kMetricSrcWords = TGSIM_METRICS_SRC_WORDS, kMetricDstWords = TGSIM_METRICS_DST_WORDS;
 constexpr uint32_t kMetricBins = TGSIM_METRICS_BINS;

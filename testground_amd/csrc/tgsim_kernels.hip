@@ -764,17 +764,52 @@ __device__ __forceinline__ uint4 make_item(uint64_t e, uint32_t len, uint32_t fl
   return make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), seq, dst);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Hand-off of a source's carried state (netem queue, departure ring, SrcState) between the windows
+// of one fused launch (k_sim_fused): window k+1 of a source may run on another CU or XCD than
+// window k, inside the same kernel, where neither the L1s nor the per-XCD L2s are coherent.  The
+// producer writes every handed-off byte with write-through (sc1) stores, drains them
+// (vmcnt(0)), then one lane stores the source's completion word (sc1); the consumer polls that word
+// with sc1 loads and reads every handed-off byte with L1-bypassing sc1 buffer loads
+// (MI355X_MICROARCH.md, "Valid forms", first row of the hand-off table).
+using v4u = unsigned int __attribute__((ext_vector_type(4)));
+using v2u = unsigned int __attribute__((ext_vector_type(2)));
+constexpr int kSc1 = 16;  // buffer cache-policy bit SC1 (gfx940+)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t region(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSc1));
+}
+__device__ __forceinline__ uint64_t ld8_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kSc1));
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)off, 0, kSc1);
+}
+struct StatePair {
+  uint4 lo, hi;
+};
+static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
+
 // One source's step (K1-K4), run by one wavefront.  kOpen: the caller has checked that the step
 // is an open queue without correlated draws, so only the open path is compiled in (fewer
 // registers, a kCap-slot LDS queue).  wg: the slot of the stamps and the statistics copy.
-template <bool kOpen, uint32_t kCap>
+// kH: the carried state is handed off inside the launch (k_sim_fused: sc1 loads and stores).
+template <bool kOpen, uint32_t kCap, bool kH = false>
 __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds) {
   const uint32_t lane = threadIdx.x;
   constexpr uint32_t kSlotMask = kCap - 1;
   stamp(a, wg, lane, 0, __builtin_amdgcn_s_memrealtime());
   const uint64_t t_begin = a.dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const SrcParams pp = a.params[s];
-  const SrcState st = a.state[s];  // dead after the set-up: the end writes a fresh state
+  SrcState st;  // dead after the set-up: the end writes a fresh state
+  if constexpr (kH) {
+    const auto rs = region(a.state + s, sizeof(SrcState));
+    st = __builtin_bit_cast(SrcState, (StatePair{ld16_sc1(rs, 0), ld16_sc1(rs, 16)}));
+  } else {
+    st = a.state[s];
+  }
   SimQueue<kCap> Q{lds, pp, lane};
   Q.rh = 0;
   Q.rn = st.ring_n;
@@ -805,11 +840,21 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     uint64_t rv[kCap / kWave];
     uint4 qv[kCap / kWave];
     const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0;
+    if constexpr (kH) {  // the source's whole reserved region (what lies past rn / qn is dropped)
+      const auto rr = region(gr, kHeapCap * 8u), rq = region(gh, kHeapCap * 16u);
 #pragma unroll
-    for (uint32_t u = 0; u < kCap / kWave; ++u) {
-      const uint32_t k = u * kWave + lane;
-      rv[u] = gr[k < rn ? k : rl];
-      qv[u] = gh[k < qn ? k : ql];
+      for (uint32_t u = 0; u < kCap / kWave; ++u) {
+        const uint32_t k = u * kWave + lane;
+        rv[u] = ld8_sc1(rr, 8u * k);
+        qv[u] = ld16_sc1(rq, 16u * k);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t u = 0; u < kCap / kWave; ++u) {
+        const uint32_t k = u * kWave + lane;
+        rv[u] = gr[k < rn ? k : rl];
+        qv[u] = gh[k < qn ? k : ql];
+      }
     }
     // every load issued before the partition's ballots, which the scheduler would otherwise
     // interleave with them (one HBM round trip per chunk)
@@ -1242,8 +1287,17 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
   {
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     uint4* gh = a.heap + (size_t)s * kHeapCap;
-    for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
-    for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
+    if constexpr (kH) {  // 16-B write-through stores (two ring entries per store)
+      const auto rr = region(gr, kHeapCap * 8u), rq = region(gh, kHeapCap * 16u);
+      for (uint32_t k = lane; 2 * k < Q.rn; k += kWave) {
+        const uint64_t d0 = Q.ring_d(2 * k), d1 = Q.ring_d(2 * k + 1);
+        st16_sc1(rr, 16u * k, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)));
+      }
+      for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) st16_sc1(rq, 16u * k, Q.slot(Q.rn + k));
+    } else {
+      for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
+      for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
+    }
   }
   if (lane == 0) {
     SrcState ns;
@@ -1254,7 +1308,14 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     ns.last_dup = last_dup;
     ns.last_cor = last_cor;
     ns.last_reo = last_reo;
-    a.state[s] = ns;
+    if constexpr (kH) {
+      const auto rs = region(a.state + s, sizeof(SrcState));
+      const StatePair sp = __builtin_bit_cast(StatePair, ns);
+      st16_sc1(rs, 0, sp.lo);
+      st16_sc1(rs, 16, sp.hi);
+    } else {
+      a.state[s] = ns;
+    }
   }
   stamp(a, wg, lane, 4, __builtin_amdgcn_s_memrealtime());
   stamp(a, wg, lane, 5, ((uint64_t)s << 32) | n_batches);
@@ -1297,6 +1358,52 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
 #endif
   if (TGSIM_PRIO && a.order && blockIdx.x < TGSIM_PRIO) __builtin_amdgcn_s_setprio(3);
   sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
+}
+
+// Several consecutive windows in one launch (tgsim_step_n): window k + 1 of a source starts as soon
+// as its window k is done, so the next window's heavy sources fill the CUs that the last dispatch
+// round of this window leaves idle (one launch tail and one launch gap per fused group instead of
+// one per window).  Tickets are claimed in order, window after window, each by a resident
+// workgroup, so the window a ticket waits for is held by a running workgroup: no deadlock.  The
+// wait is bounded (kErrHandoff, then the window runs anyway and the host reports -EIO).
+__global__ __launch_bounds__(kWave) void k_sim_fused(SimArgs a, FusedArgs f) {
+  __shared__ SimLdsT<kHeapCap> lds;
+  uint32_t t = 0;
+  if (threadIdx.x == 0) t = atomicAdd(f.ticket, 1u) - f.ticket_base;
+  t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+  const uint32_t k = t / a.n_src, pos = t - k * a.n_src;
+  if (k >= f.n_win) return;  // (the grid is n_win * n_src)
+  const uint32_t s = a.order ? a.order[pos] : pos;
+  if (k) {
+    const uint32_t need = f.step_base + k;
+    uint32_t late = 0;
+    if (threadIdx.x == 0) {
+      for (uint32_t spin = 0;
+           (int32_t)(__hip_atomic_load(f.done + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - need) < 0;) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spin > (1u << 22)) {
+          late = 1;
+          break;
+        }
+      }
+    }
+    if (__builtin_amdgcn_readfirstlane((int)late) && threadIdx.x == 0) {
+      atomicOr(&a.stats[kStErr], (unsigned long long)kErrHandoff);
+      if (a.err_host) __hip_atomic_store(a.err_host, (uint64_t)kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  const FusedWindow& w = f.w[k];
+  a.off = w.off;
+  a.in = w.in;
+  a.verdict = w.verdict;
+  a.emit = w.emit;
+  a.emit_n = w.emit_n;
+  a.dst_cnt = w.dst_cnt;
+  a.t0_ns = w.t0_ns;
+  a.horizon_ns = w.horizon_ns;
+  sim_source<false, kHeapCap, true>(a, s, t, lds);
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
+  if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Register-only form of an open-queue step (the sparse senders of a gossip flood): no LDS queue.
@@ -2135,6 +2242,68 @@ __global__ __launch_bounds__(256) void k_local_scatter(const tgsim_delivery* emi
   }
 }
 
+// K5 for a fused group (tgsim_step_n): the g windows' histograms are ONE array of g * N counts
+// (window-major), so one scan, one scatter and one per-destination sort cover the whole group, and
+// the sorted output is the windows' deliveries one after the other (the drain order of g
+// tgsim_step calls).  Single-wave workgroups throughout: they fit beside the next group's
+// k_sim_fused waves on a CU whose LDS those fill (no room for a 256- or 1024-thread block), so
+// the delivery of one group runs under the next group's simulation.
+__device__ __forceinline__ uint64_t scan_sum_u64(uint64_t v) {
+#define STEP(C, R) v += dpp64<C, R>(0ull, v);
+  TG_SCAN_STEPS(STEP)
+#undef STEP
+  return v;
+}
+__global__ __launch_bounds__(64) void k_scan_w1(const uint64_t* in, uint64_t n, uint64_t* blk) {
+  const uint64_t base = (uint64_t)blockIdx.x * 1024;
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 16; ++u) {
+    const uint64_t e = base + u * kWave + threadIdx.x;
+    s += e < n ? in[e] : 0ull;
+  }
+  s = wave_sum(s);
+  if (threadIdx.x == 0) blk[blockIdx.x] = s;
+}
+__global__ __launch_bounds__(64) void k_scan_w2(const uint64_t* in, uint64_t n, const uint64_t* blk, uint64_t* out,
+                                                uint64_t* pos, uint64_t* total_out) {
+  const uint32_t lane = threadIdx.x;
+  uint64_t pre = 0;
+  for (uint32_t j = lane; j < blockIdx.x; j += kWave) pre += blk[j];
+  pre = wave_sum(pre);
+  const uint64_t base = (uint64_t)blockIdx.x * 1024;
+  uint64_t x[16];
+#pragma unroll
+  for (uint32_t u = 0; u < 16; ++u) {
+    const uint64_t e = base + u * kWave + lane;
+    x[u] = e < n ? in[e] : 0ull;
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < 16; ++u) {
+    const uint64_t e = base + u * kWave + lane;
+    const uint64_t incl = scan_sum_u64(x[u]);
+    if (e < n) {
+      out[e] = pre + incl - x[u];
+      if (pos) pos[e] = pre + incl - x[u];
+    }
+    pre += readlane64(incl, kWave - 1);
+  }
+  if (blockIdx.x + 1 == gridDim.x && lane == 0) {
+    out[n] = pre;
+    if (total_out) *total_out = pre;
+  }
+}
+__global__ __launch_bounds__(64) void k_local_scatter_group(GroupDeliver g) {
+  const uint32_t w = blockIdx.x / g.n_src, s = blockIdx.x - w * g.n_src;
+  const uint32_t n = g.emit_n[w][s];
+  const tgsim_delivery* base = g.emit[w] + 2 * g.off[w][s] + (uint64_t)kHeapCap * s;
+  unsigned long long* pos = reinterpret_cast<unsigned long long*>(g.pos + (uint64_t)w * g.n_dst);
+  for (uint32_t i = threadIdx.x; i < n; i += kWave) {
+    const tgsim_delivery r = base[i];
+    g.out[atomicAdd(&pos[r.dst], 1ull)] = r;
+  }
+}
+
 // Delivery order inside a destination: (t, src, seq, clone first).
 __device__ __forceinline__ bool rec_lt(uint64_t ta, uint64_t qa, uint32_t ca, uint64_t tb, uint64_t qb, uint32_t cb) {
   return ta != tb ? ta < tb : (qa != qb ? qa < qb : ca < cb);
@@ -2164,6 +2333,15 @@ __device__ __forceinline__ uint32_t wave_rank(const RecKey& k, uint32_t n, uint3
 // buffer and the output (each element's place = its index in its run + its rank in the other
 // run, a binary search), so no scratch memory is needed.  The destination's count is reset to
 // zero for the next step's histogram.
+// A record this wave wrote earlier in the kernel, read from L2 (sc1: not from the CU's L1).
+__device__ __forceinline__ tgsim_delivery load_rec_l2(const tgsim_delivery* p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+  uint64_t w[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) w[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_bit_cast(tgsim_delivery, w);
+}
+
 __device__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_delivery* out, uint32_t lane) {
   if (n <= kWave) {
     tgsim_delivery r;
@@ -2191,18 +2369,20 @@ __device__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_d
     tgsim_delivery* src = in + b;
     tgsim_delivery* dst = out + b;
     for (uint32_t w = kWave; w < n; w <<= 1) {
-      __threadfence();  // device scope: also drops stale vL1D lines of the other buffer
+      // this wave's writes of the previous level have landed in L2; its reads of them bypass the
+      // CU's L1, which may hold a line another wave read before (segments share boundary lines)
+      __builtin_amdgcn_s_waitcnt(0);
       for (uint32_t lo = 0; lo < n; lo += 2 * w) {
         const uint32_t mid = min(lo + w, n), hi = min(lo + 2 * w, n);
         for (uint32_t i = lo + lane; i < hi; i += kWave) {
-          const tgsim_delivery r = src[i];
+          const tgsim_delivery r = load_rec_l2(src + i);
           const RecKey k = rec_key(r);
           const bool inA = i < mid;
           // rank in the other run: A elements count B keys < k, B elements count A keys <= k
           uint32_t a0 = inA ? mid : lo, a1 = inA ? hi : mid;
           while (a0 < a1) {
             const uint32_t m2 = (a0 + a1) >> 1;
-            const RecKey o = rec_key(src[m2]);
+            const RecKey o = rec_key(load_rec_l2(src + m2));
             const bool before = inA ? rec_lt(o.t, o.sq, o.c, k.t, k.sq, k.c)
                                     : !rec_lt(k.t, k.sq, k.c, o.t, o.sq, o.c);
             if (before) a0 = m2 + 1;
@@ -2218,16 +2398,17 @@ __device__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_d
       dst = t;
     }
     if (src != out + b) {
-      __threadfence();  // device scope: also drops stale vL1D lines of the other buffer
-      for (uint32_t i = lane; i < n; i += kWave) out[b + i] = src[i];
+      __builtin_amdgcn_s_waitcnt(0);
+      for (uint32_t i = lane; i < n; i += kWave) out[b + i] = load_rec_l2(src + i);
     }
   }
 }
 
 // One destination per wavefront (segments of tens of records and more: storm).
-__global__ __launch_bounds__(256) void k_dst_sort_wide(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
-                                                       uint32_t n_dst, tgsim_delivery* out) {
-  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6);
+template <uint32_t W>  // wavefronts per workgroup, one destination each
+__global__ __launch_bounds__(64 * W) void k_dst_sort_wide(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
+                                                          uint32_t n_dst, tgsim_delivery* out) {
+  const uint32_t d = blockIdx.x * W + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u;
   if (d >= n_dst) return;
   const uint32_t n = (uint32_t)cnt[d];
@@ -2341,6 +2522,10 @@ __global__ __launch_bounds__(256) void k_metrics_dst(const tgsim_delivery* recs,
 // Host-side launchers.
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
+}
+
+void launch_sim_fused(const SimArgs& a, const FusedArgs& f, hipStream_t st) {
+  hipLaunchKernelGGL(k_sim_fused, dim3(f.n_win * a.n_src), dim3(kWave), 0, st, a, f);
 }
 
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
@@ -2504,7 +2689,27 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
   if (n_hint <= 8ull * n_dst)
     hipLaunchKernelGGL(k_dst_sort_group<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
   else
-    hipLaunchKernelGGL(k_dst_sort_wide, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
+    hipLaunchKernelGGL(k_dst_sort_wide<4>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
+}
+
+void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
+                        tgsim_delivery* out, hipStream_t st) {
+  if (n_dst) hipLaunchKernelGGL(k_dst_sort_wide<1>, dim3(n_dst), dim3(64), 0, st, in, off, cnt, n_dst, out);
+}
+
+void launch_scan_w(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
+                   hipStream_t st, uint64_t* pos) {
+  const uint32_t nb = (uint32_t)((n + 1023) / 1024);
+  if (!nb) {
+    launch_scan(in, out, n, block_sums, total, st, pos);
+    return;
+  }
+  hipLaunchKernelGGL(k_scan_w1, dim3(nb), dim3(64), 0, st, in, n, block_sums);
+  hipLaunchKernelGGL(k_scan_w2, dim3(nb), dim3(64), 0, st, in, n, (const uint64_t*)block_sums, out, pos, total);
+}
+
+void launch_local_scatter_group(const GroupDeliver& g, uint32_t n_win, hipStream_t st) {
+  if (g.n_src && n_win) hipLaunchKernelGGL(k_local_scatter_group, dim3(n_win * g.n_src), dim3(64), 0, st, g);
 }
 
 

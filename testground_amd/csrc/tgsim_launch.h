@@ -25,6 +25,8 @@ struct RouteArgsHost {
 };
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
+// f.n_win consecutive windows of every source in one launch (grid f.n_win * a.n_src)
+void launch_sim_fused(const SimArgs& a, const FusedArgs& f, hipStream_t st);
 // sparse step: k_sim_sparse over every source, then k_sim_list over the ones it deferred
 void launch_sim_sparse(const SimArgs& a, hipStream_t st);
 // no-op above kOrderMax (32768) sources
@@ -75,5 +77,12 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
 // n_hint: about how many records (picks one wavefront per destination or eight).
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                      tgsim_delivery* out, hipStream_t st, uint64_t n_hint);
+// The fused group's K5 (single-wave workgroups, see k_scan_w1): scan of n counts, scatter of the
+// n_win windows' emit regions, one wavefront per (window, destination) segment.
+void launch_scan_w(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
+                   hipStream_t st, uint64_t* pos);
+void launch_local_scatter_group(const GroupDeliver& g, uint32_t n_win, hipStream_t st);
+void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
+                        tgsim_delivery* out, hipStream_t st);
 
 }  // namespace tgsim

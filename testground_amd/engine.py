@@ -156,6 +156,10 @@ class CABIEngine:
     def step(self, n_ticks: int) -> None:
         self._check(self._fn("step")(self._h, n_ticks), "step")
 
+    def step_n(self, n_ticks: int, n_steps: int) -> None:
+        """n_steps windows of n_ticks (tgsim_step_n: generated windows run fused, up to four per launch)."""
+        self._check(self._fn("step_n")(self._h, n_ticks, n_steps), "step_n")
+
     def step_sim(self, n_ticks: int, bounds: Sequence[int], d_out: int, out_cap: int) -> np.ndarray:
         nr = len(bounds) - 1
         b = (C.c_uint32 * len(bounds))(*bounds)
