@@ -1169,7 +1169,7 @@ int deliver_local(Eng* E) {
 // tgsim_step_n's fused path: can the next g windows run in one k_sim_fused launch?  Generated
 // dense windows on an engine that owns every peer, no host packets, no per-window diagnostics.
 bool fusable(Eng* E, uint32_t n_ticks, uint32_t g) {
-  if (g < 2 || E->S != E->N || !E->staged.empty() || E->gen_q.size() < g || E->metrics_on || E->stamps_on ||
+  if (g < 2 || E->S != E->N || !E->staged.empty() || E->gen_q.size() < g || E->metrics_on ||
       E->gossip_on || E->sparse_mode == 1 || E->order_by != 0 || kSpw != 1)
     return false;
   for (uint32_t i = 0; i < g; ++i)
@@ -1204,22 +1204,47 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
   a.order = ordered && E->order_valid ? E->d_order.p : nullptr;
   FusedArgs f{};
   const uint64_t nseg = static_cast<uint64_t>(g) * E->N;  // (window, destination) segments
-  if (E->f_lcnt[p].cap < static_cast<uint64_t>(kFuseMax) * E->N) {
-    HIPCHK(E->f_lcnt[p].ensure(static_cast<uint64_t>(kFuseMax) * E->N));
-    HIPCHK(hipMemsetAsync(E->f_lcnt[p].p, 0, sizeof(uint64_t) * E->f_lcnt[p].cap, E->st));
+  for (auto& lc : E->f_lcnt)
+    if (lc.cap < static_cast<uint64_t>(kFuseMax) * E->N) {
+      HIPCHK(lc.ensure(static_cast<uint64_t>(kFuseMax) * E->N));
+      HIPCHK(hipMemsetAsync(lc.p, 0, sizeof(uint64_t) * lc.cap, E->st));
+    }
+  uint64_t rec_bound = 0, n_max = 0;  // records the group's windows can emit; largest window
+  for (uint32_t i = 0; i < g; ++i) {
+    rec_bound += 2 * win[i].n + static_cast<uint64_t>(kHeapCap) * E->S;
+    n_max = std::max(n_max, win[i].n);
   }
-  uint64_t rec_bound = 0;  // records the group's windows can emit
+  // every buffer set of both parities sized at once (the first group pays the allocations, not a
+  // later one in the middle of a run)
+  for (auto& grp : E->fset)
+    for (uint32_t i = 0; i < static_cast<uint32_t>(E->fuse_max); ++i) {
+      HIPCHK(grp[i].emit.ensure(2 * n_max + static_cast<uint64_t>(kHeapCap) * E->S));
+      HIPCHK(grp[i].emit_n.ensure(E->S));
+    }
+  HIPCHK(E->d_verdict.ensure(n_max ? n_max : 1));
+  for (uint32_t i = 0; i + 1 < static_cast<uint32_t>(E->fuse_max); ++i) HIPCHK(E->f_verdict[i].ensure(n_max ? n_max : 1));
+  {  // the group delivery's scratch, for the largest group
+    const uint64_t segs = static_cast<uint64_t>(E->fuse_max) * E->N;
+    const uint64_t recs = static_cast<uint64_t>(E->fuse_max) * (2 * n_max + static_cast<uint64_t>(kHeapCap) * E->S);
+    HIPCHK(E->d_doff.ensure(segs + 1));
+    HIPCHK(E->d_dpos.ensure(segs));
+    HIPCHK(E->d_dblk.ensure((segs + 1023) / 1024 + 1));
+    HIPCHK(E->d_scatter.ensure(recs));
+    if (E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) HIPCHK(E->d_sorted.ensure(recs));
+  }
   for (uint32_t i = 0; i < g; ++i) {
     Eng::LocalSet& ls = E->fset[p][i];
-    HIPCHK(ls.emit.ensure(2 * win[i].n + static_cast<uint64_t>(kHeapCap) * E->S));
-    HIPCHK(ls.emit_n.ensure(E->S));
-    rec_bound += 2 * win[i].n + static_cast<uint64_t>(kHeapCap) * E->S;
     DevBuf<uint8_t>& vb = i + 1 == g ? E->d_verdict : E->f_verdict[i];
-    HIPCHK(vb.ensure(win[i].n ? win[i].n : 1));
     const uint64_t t0 = (E->now_tick + static_cast<uint64_t>(i) * n_ticks) * E->o.tick_ns;
     f.w[i] = {win[i].off.p, win[i].in.p, vb.p, ls.emit.p, ls.emit_n.p,
               reinterpret_cast<unsigned long long*>(E->f_lcnt[p].p + static_cast<uint64_t>(i) * E->N), t0,
               t0 + n_ticks * E->o.tick_ns + E->o.lookahead_ns};
+  }
+  a.stamps = nullptr;
+  if (E->stamps_on) {  // diagnostics: one stamp row per ticket (window-major)
+    HIPCHK(E->d_stamps.ensure(static_cast<size_t>(g) * E->S * kStampSlots));
+    a.stamps = E->d_stamps.p;
+    E->n_stamp_wg = static_cast<uint64_t>(g) * E->S;
   }
   f.n_win = g;
   f.step_base = E->step_no;

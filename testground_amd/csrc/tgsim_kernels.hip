@@ -1374,6 +1374,7 @@ __global__ __launch_bounds__(kWave) void k_sim_fused(SimArgs a, FusedArgs f) {
   const uint32_t k = t / a.n_src, pos = t - k * a.n_src;
   if (k >= f.n_win) return;  // (the grid is n_win * n_src)
   const uint32_t s = a.order ? a.order[pos] : pos;
+  const uint64_t t_wait = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (k) {
     const uint32_t need = f.step_base + k;
     uint32_t late = 0;
@@ -1401,6 +1402,8 @@ __global__ __launch_bounds__(kWave) void k_sim_fused(SimArgs a, FusedArgs f) {
   a.dst_cnt = w.dst_cnt;
   a.t0_ns = w.t0_ns;
   a.horizon_ns = w.horizon_ns;
+  if (a.stamps && threadIdx.x == 0)  // diagnostics: 10-ns ticks spent waiting for the previous window
+    a.stamps[(size_t)t * kStampSlots + kStampSlots - 1] = __builtin_amdgcn_s_memrealtime() - t_wait;
   sim_source<false, kHeapCap, true>(a, s, t, lds);
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
   if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -26,10 +26,11 @@ def _fused(e):
     return int(e._fn("debug_fused_windows")(e._h))
 
 
-def test_step_n_equals_oracle(make_oracle):
+def test_step_n_equals_oracle(make_oracle, monkeypatch):
     """Storm windows through step_n (10, 3 and 5 per call: fused 4 + 4 + 2, 3, 4 + 1) against the oracle stepping one by one, with
     a reshaping between two calls (configuration applies from the next group's first window)."""
     n, ticks = 600, 300
+    monkeypatch.setenv("TGSIM_FUSE", "4")  # groups of at most four windows (read at engine creation)
     g, c = Engine(n), make_oracle(n)
     for e in (g, c):
         wl.configure_storm(e, n)
