@@ -330,6 +330,8 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_done, d_ticket;    // per-source completion words, ticket counter
   uint32_t step_no = 0, ticket_no = 0;  // windows and tickets issued by fused launches so far
   uint64_t fused_windows = 0;
+  uint32_t fused_wgs = 0;
+  uint32_t prio_heavy = 512;  // TGSIM_PRIO_HEAVY: heaviest sources of a fused launch at wave priority 3 (A/B: 128 +1 %, 512 +7.5 %, 2048 +7 %, 4096 +5 %)  // k_sim_fused's persistent grid (resident workgroups), at the first launch
   int fuse_max = static_cast<int>(kFuseMax);  // TGSIM_FUSE: windows per fused launch (1: never fuse)
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
@@ -1247,6 +1249,7 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
     E->n_stamp_wg = static_cast<uint64_t>(g) * E->S;
   }
   f.n_win = g;
+  f.prio_n = a.order ? E->prio_heavy : 0;
   f.step_base = E->step_no;
   f.ticket_base = E->ticket_no;
   f.ticket = E->d_ticket.p;
@@ -1255,12 +1258,15 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
   HIPCHK(take_event(E, &ev0));
   HIPCHK(take_event(E, &ev1));
   HIPCHK(hipEventRecord(ev0, E->st));
-  launch_sim_fused(a, f, E->st);
+  if (!E->fused_wgs) E->fused_wgs = sim_fused_resident();
+  launch_sim_fused(a, f, E->fused_wgs, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.push_back({ev0, ev1, g});
   E->step_no += g;
-  E->ticket_no += g * E->S;
+  // every workgroup of the persistent grid claims until a claim fails: the counter advances by
+  // the tickets plus one failed claim per workgroup
+  E->ticket_no += g * E->S + std::min(E->fused_wgs, g * E->S);
   E->fused_windows += g;
   if (ordered) {  // the next launch's dispatch order, from the last window's HTB records
     HIPCHK(E->d_order.ensure(E->S));
@@ -1429,6 +1435,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
+  if (const char* ph = getenv("TGSIM_PRIO_HEAVY")) E->prio_heavy = static_cast<uint32_t>(atoi(ph));
   if (const char* fz = getenv("TGSIM_FUSE")) E->fuse_max = std::max(1, std::min(atoi(fz), static_cast<int>(kFuseMax)));
   for (hipEvent_t& ev : E->ev_fgrp) {
     if ((rc = E->hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return bail(rc);

@@ -130,6 +130,7 @@ struct FusedArgs {
   uint32_t ticket_base; // *ticket before this launch (tickets are counted across launches)
   uint32_t* ticket;
   uint32_t* done;       // [S] last completed window of each source (wrapping step counter)
+  uint32_t prio_n;      // tickets at dispatch positions below prio_n run at wave priority 3
 };
 constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
 // Local delivery of a fused group: window w's emit regions, counts and CSR offsets; pos holds the

@@ -796,8 +796,11 @@ static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
 // is an open queue without correlated draws, so only the open path is compiled in (fewer
 // registers, a kCap-slot LDS queue).  wg: the slot of the stamps and the statistics copy.
 // kH: the carried state is handed off inside the launch (k_sim_fused: sc1 loads and stores).
+// kH also claims the workgroup's next ticket (*claim, minus claim_base) before the write-back, so
+// the atomic's round trip overlaps the stores; it is returned (0 otherwise).
 template <bool kOpen, uint32_t kCap, bool kH = false>
-__device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds) {
+__device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
+                                               uint32_t* claim = nullptr, uint32_t claim_base = 0) {
   const uint32_t lane = threadIdx.x;
   constexpr uint32_t kSlotMask = kCap - 1;
   stamp(a, wg, lane, 0, __builtin_amdgcn_s_memrealtime());
@@ -840,8 +843,8 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     uint64_t rv[kCap / kWave];
     uint4 qv[kCap / kWave];
     const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0;
-    if constexpr (kH) {  // the source's whole reserved region (what lies past rn / qn is dropped)
-      const auto rr = region(gr, kHeapCap * 8u), rq = region(gh, kHeapCap * 16u);
+    if constexpr (kH) {  // regions of exactly rn / qn entries: the loads past them return 0 with no memory access
+      const auto rr = region(gr, 8u * rn), rq = region(gh, 16u * qn);
 #pragma unroll
       for (uint32_t u = 0; u < kCap / kWave; ++u) {
         const uint32_t k = u * kWave + lane;
@@ -1283,6 +1286,10 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
     if (lane == 0) a.dur[s] = (uint32_t)(t_end - t_begin);
   }
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
+  uint32_t next_ticket = 0;
+  if constexpr (kH) {
+    if (lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
+  }
   // ---- write back the compacted ring, the sorted queue and the state
   {
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
@@ -1346,6 +1353,7 @@ __device__ __forceinline__ void sim_source(const SimArgs& a, const uint32_t s, c
         __hip_atomic_store(a.err_host, (uint64_t)kErrTimeOverflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)next_ticket);
 }
 
 __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
@@ -1363,50 +1371,63 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
 // Several consecutive windows in one launch (tgsim_step_n): window k + 1 of a source starts as soon
 // as its window k is done, so the next window's heavy sources fill the CUs that the last dispatch
 // round of this window leaves idle (one launch tail and one launch gap per fused group instead of
-// one per window).  Tickets are claimed in order, window after window, each by a resident
-// workgroup, so the window a ticket waits for is held by a running workgroup: no deadlock.  The
-// wait is bounded (kErrHandoff, then the window runs anyway and the host reports -EIO).
-__global__ __launch_bounds__(kWave) void k_sim_fused(SimArgs a, FusedArgs f) {
+// one per window).  Persistent: the grid is what fits on the chip at once, and each workgroup takes
+// tickets in order until none is left (its next ticket claimed during the write-back of the
+// current one), so no slot waits for a workgroup dispatch between two sources.  Every claimed
+// ticket is held by a resident workgroup and waits only for a lower ticket (its source's previous
+// window), so the lowest unfinished ticket can always run: no deadlock.  The wait is bounded
+// anyway (kErrHandoff, then the window runs and the host reports -EIO).
+__global__ __launch_bounds__(kWave, 3) void k_sim_fused(SimArgs a0, FusedArgs f) {
   __shared__ SimLdsT<kHeapCap> lds;
+  const uint32_t total = f.n_win * a0.n_src;
   uint32_t t = 0;
   if (threadIdx.x == 0) t = atomicAdd(f.ticket, 1u) - f.ticket_base;
   t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-  const uint32_t k = t / a.n_src, pos = t - k * a.n_src;
-  if (k >= f.n_win) return;  // (the grid is n_win * n_src)
-  const uint32_t s = a.order ? a.order[pos] : pos;
-  const uint64_t t_wait = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  if (k) {
-    const uint32_t need = f.step_base + k;
-    uint32_t late = 0;
-    if (threadIdx.x == 0) {
-      for (uint32_t spin = 0;
-           (int32_t)(__hip_atomic_load(f.done + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - need) < 0;) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spin > (1u << 22)) {
-          late = 1;
-          break;
+  while (t < total) {
+    const uint32_t k = t / a0.n_src, pos = t - k * a0.n_src;
+    const uint32_t s = a0.order ? a0.order[pos] : pos;
+    // the heaviest sources (first in dispatch order) chain their windows through the launch: their
+    // waves issue first on their SIMDs, so the chain is not the launch's critical path
+    if (pos < f.prio_n) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);
+    const uint64_t t_wait = a0.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    if (k) {
+      const uint32_t need = f.step_base + k;
+      uint32_t late = 0;
+      if (threadIdx.x == 0) {
+        for (uint32_t spin = 0;
+             (int32_t)(__hip_atomic_load(f.done + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - need) < 0;) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spin > (1u << 22)) {
+            late = 1;
+            break;
+          }
         }
       }
+      if (__builtin_amdgcn_readfirstlane((int)late) && threadIdx.x == 0) {
+        atomicOr(&a0.stats[kStErr], (unsigned long long)kErrHandoff);
+        if (a0.err_host)
+          __hip_atomic_store(a0.err_host, (uint64_t)kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
-    if (__builtin_amdgcn_readfirstlane((int)late) && threadIdx.x == 0) {
-      atomicOr(&a.stats[kStErr], (unsigned long long)kErrHandoff);
-      if (a.err_host) __hip_atomic_store(a.err_host, (uint64_t)kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (a0.stamps && threadIdx.x == 0)  // diagnostics: 10-ns ticks spent waiting for the previous window
+      a0.stamps[(size_t)t * kStampSlots + kStampSlots - 1] = __builtin_amdgcn_s_memrealtime() - t_wait;
+    SimArgs a = a0;
+    const FusedWindow& w = f.w[k];
+    a.off = w.off;
+    a.in = w.in;
+    a.verdict = w.verdict;
+    a.emit = w.emit;
+    a.emit_n = w.emit_n;
+    a.dst_cnt = w.dst_cnt;
+    a.t0_ns = w.t0_ns;
+    a.horizon_ns = w.horizon_ns;
+    const uint32_t next = sim_source<false, kHeapCap, true>(a, s, t, lds, f.ticket, f.ticket_base);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
+    if (threadIdx.x == 0)
+      __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = next;
   }
-  const FusedWindow& w = f.w[k];
-  a.off = w.off;
-  a.in = w.in;
-  a.verdict = w.verdict;
-  a.emit = w.emit;
-  a.emit_n = w.emit_n;
-  a.dst_cnt = w.dst_cnt;
-  a.t0_ns = w.t0_ns;
-  a.horizon_ns = w.horizon_ns;
-  if (a.stamps && threadIdx.x == 0)  // diagnostics: 10-ns ticks spent waiting for the previous window
-    a.stamps[(size_t)t * kStampSlots + kStampSlots - 1] = __builtin_amdgcn_s_memrealtime() - t_wait;
-  sim_source<false, kHeapCap, true>(a, s, t, lds);
-  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
-  if (threadIdx.x == 0) __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Register-only form of an open-queue step (the sparse senders of a gossip flood): no LDS queue.
@@ -2527,8 +2548,18 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
 }
 
-void launch_sim_fused(const SimArgs& a, const FusedArgs& f, hipStream_t st) {
-  hipLaunchKernelGGL(k_sim_fused, dim3(f.n_win * a.n_src), dim3(kWave), 0, st, a, f);
+void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st) {
+  const uint32_t total = f.n_win * a.n_src;
+  hipLaunchKernelGGL(k_sim_fused, dim3(n_wg < total ? n_wg : total), dim3(kWave), 0, st, a, f);
+}
+
+uint32_t sim_fused_resident() {
+  int dev = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sim_fused, kWave, 0) != hipSuccess || per_cu <= 0)
+    return 2048;
+  return (uint32_t)(per_cu * cus);
 }
 
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {

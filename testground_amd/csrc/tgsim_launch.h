@@ -25,8 +25,10 @@ struct RouteArgsHost {
 };
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
-// f.n_win consecutive windows of every source in one launch (grid f.n_win * a.n_src)
-void launch_sim_fused(const SimArgs& a, const FusedArgs& f, hipStream_t st);
+// f.n_win consecutive windows of every source in one persistent launch of n_wg workgroups
+void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st);
+// workgroups of k_sim_fused resident on the device at once (its grid)
+uint32_t sim_fused_resident();
 // sparse step: k_sim_sparse over every source, then k_sim_list over the ones it deferred
 void launch_sim_sparse(const SimArgs& a, hipStream_t st);
 // no-op above kOrderMax (32768) sources
