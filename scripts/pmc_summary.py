@@ -15,8 +15,9 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 
 root, steps = sys.argv[1], int(sys.argv[2])
+FUSE = 8  # bench.py's storm windows run through tgsim_step_n: groups of at most 8 per k_sim_fused dispatch
 vals = defaultdict(dict)
-FIRST = ("k_sim(", "k_sim_sparse(")  # one of these opens every step; k_sim_list joins the sparse step
+FIRST = ("k_sim(", "k_sim_sparse(", "k_sim_fused(")  # one opens every dispatch group; k_sim_list joins the sparse one
 for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
     per = defaultdict(lambda: defaultdict(float))
     name = {}
@@ -24,17 +25,20 @@ for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
         if any(k in r["Kernel_Name"] for k in FIRST + ("k_sim_list(",)):
             per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
             name[int(r["Dispatch_Id"])] = r["Kernel_Name"]
-    step = []  # counters summed per step, in dispatch order
+    step = []  # counters summed per dispatch group, in dispatch order, with its window count
     for i in sorted(per):
         if any(k in name[i] for k in FIRST) or not step:
-            step.append(defaultdict(float))
+            step.append([defaultdict(float), "k_sim_fused(" in name[i]])
         for k, v in per[i].items():
-            step[-1][k] += v
-    for sv in step[-steps:]:
+            step[-1][0][k] += v
+    # the timed windows: groups of FUSE, then the remainder (tgsim_step_n); a group of w windows
+    # counts w times, with 1/w of its counters each
+    groups = [FUSE] * (steps // FUSE) + ([steps % FUSE] if steps % FUSE else [])
+    for (sv, _), w in zip(reversed(step), reversed(groups)):
         for k, v in sv.items():
-            vals[k].setdefault("v", []).append(v)
+            vals[k].setdefault("v", []).extend([v / w] * w)
 avg = {k: sum(d["v"]) / len(d["v"]) for k, d in vals.items()}
-out = {"kernel": "tgsim::k_sim (dense steps) | k_sim_sparse + k_sim_list (sparse steps), per step", "counters_avg_per_launch": avg,
+out = {"kernel": "tgsim::k_sim | k_sim_fused (dense windows) | k_sim_sparse + k_sim_list (sparse windows), per window", "counters_avg_per_launch": avg,
        "hbm_bytes_per_launch": (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)) * 1024
        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg else None,
        "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 64 B per 128 B request)",

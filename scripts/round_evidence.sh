@@ -24,8 +24,8 @@ rm -rf $O/pmc && mkdir -p $O/pmc
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $O/pmc/p$i -o run -- python3 bench.py $B --no-cpu --steps 5 --warmup 1 > $O/pmc/p$i.log 2>&1 || { tail $O/pmc/p$i.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $O/pmc/p$i -o run -- python3 bench.py $B --no-cpu --steps 8 --warmup 8 > $O/pmc/p$i.log 2>&1 || { tail $O/pmc/p$i.log; exit 1; }
   echo "pmc pass $i ok"
 done
 LAM=$(python -c "import json; print(json.load(open('$O/bench.json'))['config']['lambda_per_tick'])")
-python scripts/pmc_summary.py $O/pmc 5 10000 $LAM 2000 $SHAPES > $O/pmc_k_sim.json && cat $O/pmc_k_sim.json
+python scripts/pmc_summary.py $O/pmc 8 10000 $LAM 2000 $SHAPES > $O/pmc_k_sim.json && cat $O/pmc_k_sim.json
