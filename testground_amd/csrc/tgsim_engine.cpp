@@ -332,7 +332,7 @@ struct tgsim_engine_s {
   uint64_t fused_windows = 0;
   uint32_t fused_wgs = 0;
   uint32_t prio_heavy = 512;  // TGSIM_PRIO_HEAVY: heaviest sources of a fused launch at wave priority 3 (A/B: 128 +1 %, 512 +7.5 %, 2048 +7 %, 4096 +5 %)  // k_sim_fused's persistent grid (resident workgroups), at the first launch
-  int fuse_max = static_cast<int>(kFuseMax);  // TGSIM_FUSE: windows per fused launch (1: never fuse)
+  int fuse_max = 8;  // TGSIM_FUSE: windows per fused launch, up to kFuseMax (1: never fuse; A/B at 30 windows: 4 34.8, 8 36.3, 16 36.3 G pkt/s)
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
 
