@@ -416,7 +416,9 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
 
     def run_steps(n):
         if stepper is not None and workload == "storm":  # pre-generated: simulate one step ahead
-            stepper.run(n, window)
+            # slotted exchange: groups of up to four windows per launch and per all-to-all (A/B at one
+            # rank: 1 27.5, 4 30.4, 8 27.7-28.6 G pkt/s: larger groups lengthen the pipeline drain)
+            stepper.run(n, window, fuse=1 if a.exact_exchange else int(os.environ.get("TGSIM_FUSE", "4")))
         elif workload == "storm":  # pre-generated windows, up to four per launch (tgsim_step_n)
             eng.step_n(window, n)
         else:

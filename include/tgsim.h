@@ -254,6 +254,16 @@ int tgsim_step_sim_counts(void* engine, uint64_t* rank_counts);
 int tgsim_step_sim_launch_slotted(void* engine, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* rank_bounds,
                                   void* d_out, uint64_t slot_cap, void* routed_event);
 int tgsim_step_sim_release(void* engine);
+/* Fused form of the slotted step (n_win generated windows in one launch, tgsim_step_n): d_out holds
+ * n_ranks x n_win chunks of (slot_cap + 1) records, rank-major (chunk r * n_win + w: window w's
+ * records for rank r behind its count header), so one all-to-all moves the whole group; counts as
+ * ONE launched step for _release.  -EINVAL when the next n_win windows are not fusable. */
+int tgsim_step_sim_launch_slotted_n(void* engine, uint32_t n_ticks, uint32_t n_win, uint32_t n_ranks,
+                                    const uint32_t* rank_bounds, void* d_out, uint64_t slot_cap, void* routed_event);
+/* tgsim_deliver_slotted_async of a fused group's exchange output (n_ranks x n_win chunks, source-rank
+ * major): the windows' deliveries are appended in window order. */
+int tgsim_deliver_slotted_n_async(void* engine, const void* d_in, uint32_t n_ranks, uint32_t n_win, uint64_t slot_cap,
+                                  void* wait_event);
 /* Phase 2: sorts the records addressed to this shard (DEVICE memory, n records) into the
  * delivery order and appends them to the drain buffer. */
 int tgsim_deliver(void* engine, const void* d_in, size_t n);

@@ -125,7 +125,7 @@ EXPORTS = [
     "tgsim_submit", "tgsim_gen_storm", "tgsim_step", "tgsim_step_sim", "tgsim_deliver",
     "tgsim_deliver_async", "tgsim_wait_event", "tgsim_sync", "tgsim_step_sim_launch", "tgsim_step_sim_finish",
     "tgsim_step_sim_counts", "tgsim_delivery_event", "tgsim_step_sim_launch_slotted", "tgsim_step_sim_release",
-    "tgsim_deliver_slotted_async",
+    "tgsim_deliver_slotted_async", "tgsim_step_sim_launch_slotted_n", "tgsim_deliver_slotted_n_async",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
     "tgsim_debug_fused_windows", "tgsim_step_n",
@@ -165,6 +165,9 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("delivery_event", C.c_int, vp, vp)
     f("step_sim_launch_slotted", C.c_int, vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), vp, C.c_uint64, vp)
     f("step_sim_release", C.c_int, vp)
+    f("step_sim_launch_slotted_n", C.c_int, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), vp,
+      C.c_uint64, vp)
+    f("deliver_slotted_n_async", C.c_int, vp, vp, C.c_uint32, C.c_uint32, C.c_uint64, vp)
     f("deliver_slotted_async", C.c_int, vp, vp, C.c_uint32, C.c_uint64, vp)
     f("deliver", C.c_int, vp, vp, C.c_size_t)
     f("deliver_async", C.c_int, vp, vp, C.c_size_t, vp)

@@ -331,6 +331,7 @@ struct tgsim_engine_s {
   uint32_t step_no = 0, ticket_no = 0;  // windows and tickets issued by fused launches so far
   uint64_t fused_windows = 0;
   uint32_t fused_wgs = 0;
+  bool persist_routed = false;  // TGSIM_FUSED_PERSIST: persistent grid for sharded (routed) groups too
   uint32_t prio_heavy = 512;  // TGSIM_PRIO_HEAVY: heaviest sources of a fused launch at wave priority 3 (A/B: 128 +1 %, 512 +7.5 %, 2048 +7 %, 4096 +5 %)  // k_sim_fused's persistent grid (resident workgroups), at the first launch
   int fuse_max = 8;  // TGSIM_FUSE: windows per fused launch, up to kFuseMax (1: never fuse; A/B at 30 windows: 4 34.8, 8 36.3, 16 36.3 G pkt/s)
   DevBuf<uint64_t> d_stamps;
@@ -1055,19 +1056,30 @@ int delivery_out(Eng* E, uint64_t n, tgsim_delivery** out, hipStream_t sq) {
 // records come from tgsim_step_sim, which completed them before returning), only for `wait` (the
 // producer of d_in, e.g. the collective).
 // check: read the record count back and reject records addressed to other shards.
-int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool check, uint64_t slot = 0) {
+// n_win > 1: the slotted input of a fused group (chunk c = source rank * n_win + window): the
+// records are sorted per (window, destination) segment, so the output is the windows' deliveries
+// in window order, in single-wave workgroups (beside the next group's k_sim_fused).
+int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool check, uint64_t slot = 0,
+            uint32_t n_win = 1) {
   const uint32_t nd = E->S;  // destinations owned by this shard
+  const uint64_t nseg = static_cast<uint64_t>(n_win) * nd;
   hipStream_t sq = E->dst_st;
   if (wait) HIPCHK(hipStreamWaitEvent(sq, wait, 0));
-  if (E->d_dcnt.cap < nd) {
-    HIPCHK(E->d_dcnt.ensure(nd));
+  if (E->d_dcnt.cap < nseg) {
+    HIPCHK(E->d_dcnt.ensure(nseg));
     HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, sq));
   }
-  HIPCHK(E->d_dpos.ensure(nd));
-  launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq, slot);
+  HIPCHK(E->d_dpos.ensure(nseg));
+  launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq, slot, n_win);
   HIPCHK(hipGetLastError());
   int rc = 0;
-  if (!check) {  // nothing on the host needs the count
+  if (n_win > 1) {
+    HIPCHK(E->d_doff.ensure(nseg + 1));
+    HIPCHK(E->d_dblk.ensure((nseg + 1023) / 1024 + 1));
+    HIPCHK(E->d_dtot.ensure(1));
+    launch_scan_w(E->d_dcnt.p, E->d_doff.p, nseg, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
+    HIPCHK(hipGetLastError());
+  } else if (!check) {  // nothing on the host needs the count
     HIPCHK(E->d_doff.ensure(nd + 1));
     HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
     HIPCHK(E->d_dtot.ensure(1));
@@ -1081,7 +1093,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
                                    static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq, slot);
+  launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq, slot, n_win);
   HIPCHK(hipGetLastError());
   if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
     if (slot) launch_gossip_recv_dev(gossip_args(E, 0, 0), E->d_scatter.p, E->d_dtot.p, sq);
@@ -1097,7 +1109,8 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   tgsim_delivery* dst = nullptr;
   rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq, n);
+  if (n_win > 1) launch_dst_sort_w1(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, static_cast<uint32_t>(nseg), dst, sq);
+  else launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq, n);
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
@@ -1170,8 +1183,8 @@ int deliver_local(Eng* E) {
 
 // tgsim_step_n's fused path: can the next g windows run in one k_sim_fused launch?  Generated
 // dense windows on an engine that owns every peer, no host packets, no per-window diagnostics.
-bool fusable(Eng* E, uint32_t n_ticks, uint32_t g) {
-  if (g < 2 || E->S != E->N || !E->staged.empty() || E->gen_q.size() < g || E->metrics_on ||
+bool fusable(Eng* E, uint32_t n_ticks, uint32_t g, bool routed = false) {
+  if (g < 2 || (E->S != E->N && !routed) || !E->staged.empty() || E->gen_q.size() < g || E->metrics_on ||
       E->gossip_on || E->sparse_mode == 1 || E->order_by != 0 || kSpw != 1)
     return false;
   for (uint32_t i = 0; i < g; ++i)
@@ -1181,7 +1194,15 @@ bool fusable(Eng* E, uint32_t n_ticks, uint32_t g) {
 
 // g consecutive windows in one k_sim_fused launch, then the g local deliveries on the delivery
 // stream (beside the next group's launch, which writes the other parity's buffer sets).
-int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
+struct GroupRoute {  // a sharded group: the windows' records routed into slotted chunks
+  uint32_t n_ranks;
+  const uint32_t* bounds;
+  tgsim_delivery* out;  // n_ranks x g chunks of (slot_cap + 1) records, rank-major
+  uint64_t slot_cap;
+  hipEvent_t routed;
+};
+
+int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = nullptr) {
   int rc = check_sim_error(E);
   if (rc) return rc;
   rc = harvest_timing(E, false);
@@ -1218,14 +1239,15 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
   }
   // every buffer set of both parities sized at once (the first group pays the allocations, not a
   // later one in the middle of a run)
+  const uint32_t n_sets = std::max(static_cast<uint32_t>(E->fuse_max), g);
   for (auto& grp : E->fset)
-    for (uint32_t i = 0; i < static_cast<uint32_t>(E->fuse_max); ++i) {
+    for (uint32_t i = 0; i < n_sets; ++i) {
       HIPCHK(grp[i].emit.ensure(2 * n_max + static_cast<uint64_t>(kHeapCap) * E->S));
       HIPCHK(grp[i].emit_n.ensure(E->S));
     }
   HIPCHK(E->d_verdict.ensure(n_max ? n_max : 1));
-  for (uint32_t i = 0; i + 1 < static_cast<uint32_t>(E->fuse_max); ++i) HIPCHK(E->f_verdict[i].ensure(n_max ? n_max : 1));
-  {  // the group delivery's scratch, for the largest group
+  for (uint32_t i = 0; i + 1 < n_sets; ++i) HIPCHK(E->f_verdict[i].ensure(n_max ? n_max : 1));
+  if (!gr) {  // the group delivery's scratch, for the largest group
     const uint64_t segs = static_cast<uint64_t>(E->fuse_max) * E->N;
     const uint64_t recs = static_cast<uint64_t>(E->fuse_max) * (2 * n_max + static_cast<uint64_t>(kHeapCap) * E->S);
     HIPCHK(E->d_doff.ensure(segs + 1));
@@ -1239,8 +1261,8 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
     DevBuf<uint8_t>& vb = i + 1 == g ? E->d_verdict : E->f_verdict[i];
     const uint64_t t0 = (E->now_tick + static_cast<uint64_t>(i) * n_ticks) * E->o.tick_ns;
     f.w[i] = {win[i].off.p, win[i].in.p, vb.p, ls.emit.p, ls.emit_n.p,
-              reinterpret_cast<unsigned long long*>(E->f_lcnt[p].p + static_cast<uint64_t>(i) * E->N), t0,
-              t0 + n_ticks * E->o.tick_ns + E->o.lookahead_ns};
+              gr ? nullptr : reinterpret_cast<unsigned long long*>(E->f_lcnt[p].p + static_cast<uint64_t>(i) * E->N),
+              t0, t0 + n_ticks * E->o.tick_ns + E->o.lookahead_ns};
   }
   a.stamps = nullptr;
   if (E->stamps_on) {  // diagnostics: one stamp row per ticket (window-major)
@@ -1259,14 +1281,17 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
   HIPCHK(take_event(E, &ev1));
   HIPCHK(hipEventRecord(ev0, E->st));
   if (!E->fused_wgs) E->fused_wgs = sim_fused_resident();
+  // a sharded group's exchange (RCCL) and deliveries need CU slots while the next group simulates:
+  // there the workgroups turn over (TGSIM_FUSED_PERSIST=1 forces the persistent grid)
+  f.persistent = gr ? (E->persist_routed ? 1u : 0u) : 1u;
   launch_sim_fused(a, f, E->fused_wgs, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.push_back({ev0, ev1, g});
   E->step_no += g;
   // every workgroup of the persistent grid claims until a claim fails: the counter advances by
-  // the tickets plus one failed claim per workgroup
-  E->ticket_no += g * E->S + std::min(E->fused_wgs, g * E->S);
+  // the tickets plus one failed claim per workgroup (one claim per ticket otherwise)
+  E->ticket_no += g * E->S + (f.persistent ? std::min(E->fused_wgs, g * E->S) : 0u);
   E->fused_windows += g;
   if (ordered) {  // the next launch's dispatch order, from the last window's HTB records
     HIPCHK(E->d_order.ensure(E->S));
@@ -1274,6 +1299,51 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
     HIPCHK(hipGetLastError());
     E->order_valid = true;
   }
+  if (gr) {  // sharded: each window's records into its (rank, window) chunks, on the routing stream
+    hipStream_t rs = E->rt_st;
+    HIPCHK(hipEventRecord(E->ev_sim, E->st));
+    HIPCHK(hipStreamWaitEvent(rs, E->ev_sim, 0));
+    const uint64_t m = static_cast<uint64_t>(gr->n_ranks) * E->S;
+    HIPCHK(E->d_rcnt.ensure(m));
+    HIPCHK(E->d_rpos.ensure(m + 1));
+    HIPCHK(E->d_rblk.ensure((m + 1023) / 1024 + 1));
+    HIPCHK(E->d_rtot.ensure(1));
+    const uint32_t k = (E->route_head + E->route_n) % Eng::kRouteSlots;
+    E->route_seq[k] = ++E->route_next_seq;
+    for (uint32_t i = 0; i < g; ++i) {
+      RouteArgsHost h;
+      memset(&h, 0, sizeof h);
+      h.emit = E->fset[p][i].emit.p;
+      h.emit_n = E->fset[p][i].emit_n.p;
+      h.off = win[i].off.p;
+      h.n_src = E->S;
+      h.n_ranks = gr->n_ranks;
+      for (uint32_t r = 0; r <= gr->n_ranks && r < 9; ++r) h.bounds[r] = gr->bounds[r];
+      h.cnt = E->d_rcnt.p;
+      h.pos = E->d_rpos.p;
+      h.out = gr->out + static_cast<uint64_t>(i) * (gr->slot_cap + 1);
+      h.out_cap = static_cast<uint64_t>(gr->n_ranks) * g * (gr->slot_cap + 1);
+      h.slot_cap = gr->slot_cap;
+      h.chunk_stride = static_cast<uint64_t>(g) * (gr->slot_cap + 1);
+      h.waves_per_block = 1;  // beside the next group's k_sim_fused (see k_scan_w1)
+      launch_route(h, 0, rs);
+      HIPCHK(hipGetLastError());
+      launch_scan_w(E->d_rcnt.p, E->d_rpos.p, m, E->d_rblk.p, E->d_rtot.p, rs, nullptr);
+      HIPCHK(hipGetLastError());
+      launch_route(h, 1, rs);
+      HIPCHK(hipGetLastError());
+      launch_route_edges(E->d_rpos.p, E->S, gr->n_ranks, E->h_edges + 16 * k, E->route_seq[k], rs, h.out,
+                         gr->slot_cap, E->d_xerr, h.chunk_stride);
+      HIPCHK(hipGetLastError());
+    }
+    if (gr->routed) HIPCHK(hipEventRecord(gr->routed, rs));
+    HIPCHK(hipEventRecord(E->ev_route[k], rs));
+    HIPCHK(hipEventRecord(E->ev_rt, rs));
+    HIPCHK(hipEventRecord(E->ev_fgrp[p], rs));  // the last reader of buffer set p
+    E->route_ranks[k] = gr->n_ranks;
+    E->route_cap[k] = static_cast<size_t>(gr->n_ranks) * g * (gr->slot_cap + 1);
+    E->route_n++;
+  } else {
   // the group's deliveries, beside the next launch: one scan over the (window, destination)
   // counts, one scatter of every window's emit regions, one sort per segment; the sorted output is
   // window 0's deliveries, then window 1's, ... (the drain order of g tgsim_step calls)
@@ -1313,6 +1383,7 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(E->ev_fgrp[p], sq));
   HIPCHK(hipEventRecord(E->ev_dst, E->dst_st));
+  }
   E->fgrp = p ^ 1;
   // the last window's input stays the engine's current input (as after tgsim_step); the replaced
   // buffers and the other windows go back to the free list (a generation waits for ev_dst first)
@@ -1435,6 +1506,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
+  if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) E->persist_routed = atoi(fp) != 0;
   if (const char* ph = getenv("TGSIM_PRIO_HEAVY")) E->prio_heavy = static_cast<uint32_t>(atoi(ph));
   if (const char* fz = getenv("TGSIM_FUSE")) E->fuse_max = std::max(1, std::min(atoi(fz), static_cast<int>(kFuseMax)));
   for (hipEvent_t& ev : E->ev_fgrp) {
@@ -1797,6 +1869,33 @@ int tgsim_step_sim_launch_slotted(void* e, uint32_t n_ticks, uint32_t n_ranks, c
   if (rc) return rc;
   return route_launch(E, n_ranks, bounds, static_cast<tgsim_delivery*>(d_out), n_ranks * (slot_cap + 1), slot_cap,
                       static_cast<hipEvent_t>(routed_event));
+}
+
+int tgsim_step_sim_launch_slotted_n(void* e, uint32_t n_ticks, uint32_t n_win, uint32_t n_ranks,
+                                    const uint32_t* bounds, void* d_out, uint64_t slot_cap, void* routed_event) {
+  Eng* E = as_eng(e);
+  if (!E || n_ticks == 0 || n_win == 0 || n_win > kFuseMax || n_ranks == 0 || n_ranks > 8 || !bounds || !d_out ||
+      slot_cap == 0)
+    return -EINVAL;
+  if (n_win == 1)
+    return tgsim_step_sim_launch_slotted(e, n_ticks, n_ranks, bounds, d_out, slot_cap, routed_event);
+  if (bounds[0] != 0 || bounds[n_ranks] != E->N) return E->fail(-EINVAL, "rank bounds must cover [0, n_peers)");
+  if (E->route_n == Eng::kRouteSlots) return E->fail(-EBUSY, "two launched steps are not released yet");
+  HIPCHK(hipSetDevice(E->dev));
+  if (!fusable(E, n_ticks, n_win, true))
+    return E->fail(-EINVAL, "step_sim_launch_slotted_n: the next %u windows are not generated dense windows of %u ticks",
+                   n_win, n_ticks);
+  const GroupRoute gr{n_ranks, bounds, static_cast<tgsim_delivery*>(d_out), slot_cap, static_cast<hipEvent_t>(routed_event)};
+  return step_fused(E, n_ticks, n_win, &gr);
+}
+
+int tgsim_deliver_slotted_n_async(void* e, const void* d_in, uint32_t n_ranks, uint32_t n_win, uint64_t slot_cap,
+                                  void* wait_event) {
+  Eng* E = as_eng(e);
+  if (!E || !d_in || n_ranks == 0 || n_ranks > 8 || n_win == 0 || n_win > kFuseMax || slot_cap == 0) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  return deliver(E, static_cast<const tgsim_delivery*>(d_in), static_cast<uint64_t>(n_ranks) * n_win * (slot_cap + 1),
+                 static_cast<hipEvent_t>(wait_event), false, slot_cap, n_win);
 }
 
 int tgsim_step_sim_release(void* e) {

@@ -131,6 +131,8 @@ struct FusedArgs {
   uint32_t* ticket;
   uint32_t* done;       // [S] last completed window of each source (wrapping step counter)
   uint32_t prio_n;      // tickets at dispatch positions below prio_n run at wave priority 3
+  uint32_t persistent;  // 1: a grid of resident workgroups claims tickets until none is left; 0: one
+                        // workgroup per ticket (the slots turn over, so an exchange can be dispatched)
 };
 constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
 // Local delivery of a fused group: window w's emit regions, counts and CSR offsets; pos holds the

@@ -1288,7 +1288,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   uint32_t next_ticket = 0;
   if constexpr (kH) {
-    if (lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
+    if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
   }
   // ---- write back the compacted ring, the sorted queue and the state
   {
@@ -1422,10 +1422,12 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused(SimArgs a0, FusedArgs f)
     a.dst_cnt = w.dst_cnt;
     a.t0_ns = w.t0_ns;
     a.horizon_ns = w.horizon_ns;
-    const uint32_t next = sim_source<false, kHeapCap, true>(a, s, t, lds, f.ticket, f.ticket_base);
+    const uint32_t next = sim_source<false, kHeapCap, true>(a, s, t, lds, f.persistent ? f.ticket : nullptr,
+                                                            f.ticket_base);
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
     if (threadIdx.x == 0)
       __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!f.persistent) break;  // one ticket per workgroup: the dispatcher interleaves other streams' work
     t = next;
   }
 }
@@ -2125,7 +2127,9 @@ struct RouteArgs {
   const uint64_t* pos;           // exclusive scan of cnt
   tgsim_delivery* out;
   uint64_t out_cap;              // records beyond it are not written (the host reports -ENOSPC)
-  uint64_t slot_cap;             // 0: flat, rank-major; else rank r's records at out[r * (slot_cap + 1) + 1 ..]
+  uint64_t slot_cap;             // 0: flat, rank-major; else rank r's records at out[r * stride + 1 ..]
+  uint64_t stride;               // slotted: records from one rank's chunk to the next (slot_cap + 1, or
+                                 // n_win * (slot_cap + 1) for a fused group's window)
 };
 
 __device__ __forceinline__ uint32_t rank_of(const RouteArgs& a, uint32_t dst) {
@@ -2134,10 +2138,11 @@ __device__ __forceinline__ uint32_t rank_of(const RouteArgs& a, uint32_t dst) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_route_count(RouteArgs a) {
+template <uint32_t W>  // wavefronts per workgroup, one source each
+__global__ __launch_bounds__(64 * W) void k_route_count(RouteArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nw = gridDim.x * 4;
-  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < a.n_src; s += nw) {
+  const uint32_t nw = gridDim.x * W;
+  for (uint32_t s = blockIdx.x * W + (threadIdx.x >> 6); s < a.n_src; s += nw) {
     const uint32_t n = a.emit_n[s];
     if (a.n_ranks == 1) {
       if (lane == 0) a.cnt[s] = n;
@@ -2160,10 +2165,11 @@ __global__ __launch_bounds__(256) void k_route_count(RouteArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
+template <uint32_t W>
+__global__ __launch_bounds__(64 * W) void k_route_scatter(RouteArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nw = gridDim.x * 4;
-  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < a.n_src; s += nw) {
+  const uint32_t nw = gridDim.x * W;
+  for (uint32_t s = blockIdx.x * W + (threadIdx.x >> 6); s < a.n_src; s += nw) {
     const uint32_t n = a.emit_n[s];
     const tgsim_delivery* base = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
     uint64_t run[8], edge[8];
@@ -2188,7 +2194,7 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
           const uint64_t p = run[q] + __popcll(m & below);
           if (a.slot_cap) {
             const uint64_t j = p - edge[q];
-            if (j < a.slot_cap) a.out[q * (a.slot_cap + 1) + 1 + j] = r;
+            if (j < a.slot_cap) a.out[q * a.stride + 1 + j] = r;
           } else if (p < a.out_cap) {
             a.out[p] = r;
           }
@@ -2205,14 +2211,14 @@ __global__ __launch_bounds__(256) void k_route_scatter(RouteArgs a) {
 // (system-scope release): the host polls that word instead of synchronizing on an event, which
 // would also wait for the next step's k_sim queued behind this kernel.
 __global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
-                              tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow) {
+                              tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow, uint64_t stride) {
   const uint32_t r = threadIdx.x;
   if (r <= n_ranks) slot[r] = pos[(size_t)r * n_src];
   if (slot_cap && r < n_ranks) {  // slotted output: each rank's chunk starts with its record count
     const uint64_t c = pos[(size_t)(r + 1) * n_src] - pos[(size_t)r * n_src];
     tgsim_delivery h = {};
     h.t_ns = c < slot_cap ? c : slot_cap;
-    out[r * (slot_cap + 1)] = h;
+    out[r * stride] = h;
     if (c > slot_cap) *overflow = 1u;  // sticky, in pinned host memory: the host fails with -ENOSPC
   }
   __threadfence_system();
@@ -2231,23 +2237,30 @@ __device__ __forceinline__ bool slot_empty(const tgsim_delivery* in, uint64_t i,
   const uint64_t r = i / (slot + 1), j = i - r * (slot + 1);
   return j == 0 || j > in[r * (slot + 1)].t_ns;
 }
+// Histogram / cursor index of record i: its destination, in its window's segment block when the
+// slotted input is a fused group's (chunk c = rank * n_win + window).
+__device__ __forceinline__ uint64_t seg_of(uint64_t i, uint64_t slot, uint32_t n_win, uint32_t n_dst, uint32_t d) {
+  if (n_win <= 1) return d;
+  return (uint64_t)((i / (slot + 1)) % n_win) * n_dst + d;
+}
 
 __global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
-                           uint64_t slot) {
+                           uint64_t slot, uint32_t n_win) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || slot_empty(in, i, slot)) return;
   const uint32_t d = in[i].dst - dst_begin;
-  if (d < n_dst) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[d]), 1ull);
+  if (d < n_dst) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[seg_of(i, slot, n_win, n_dst, d)]), 1ull);
 }
 
 // Flat input (records received from every shard): pos[] starts as the exclusive scan of counts.
 __global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst,
-                              uint64_t* pos, tgsim_delivery* out, uint64_t slot) {
+                              uint64_t* pos, tgsim_delivery* out, uint64_t slot, uint32_t n_win) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || slot_empty(in, i, slot)) return;
   const tgsim_delivery r = in[i];
   const uint32_t d = r.dst - dst_begin;
-  if (d < n_dst) out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[d]), 1ull)] = r;
+  if (d < n_dst)
+    out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[seg_of(i, slot, n_win, n_dst, d)]), 1ull)] = r;
 }
 
 // Single shard: straight from k_sim's per-source emit regions (counts were taken by k_sim).
@@ -2550,7 +2563,7 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
 
 void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st) {
   const uint32_t total = f.n_win * a.n_src;
-  hipLaunchKernelGGL(k_sim_fused, dim3(n_wg < total ? n_wg : total), dim3(kWave), 0, st, a, f);
+  hipLaunchKernelGGL(k_sim_fused, dim3(f.persistent && n_wg < total ? n_wg : total), dim3(kWave), 0, st, a, f);
 }
 
 uint32_t sim_fused_resident() {
@@ -2668,9 +2681,9 @@ void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_
 }
 
 void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
-                        hipStream_t st, tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow) {
+                        hipStream_t st, tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow, uint64_t chunk_stride) {
   hipLaunchKernelGGL(k_route_edges, dim3(1), dim3(64), 0, st, pos, n_src, n_ranks, slot, seq, out, slot_cap,
-                     overflow);
+                     overflow, chunk_stride ? chunk_stride : slot_cap + 1);
 }
 
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
@@ -2686,25 +2699,34 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
   a.out = h.out;
   a.out_cap = h.out_cap;
   a.slot_cap = h.slot_cap;
+  a.stride = h.chunk_stride ? h.chunk_stride : h.slot_cap + 1;
+  if (h.waves_per_block == 1) {  // one wave per source, single-wave workgroups
+    const uint32_t grid = h.n_src ? h.n_src : 1;
+    if (phase == 0) hipLaunchKernelGGL(k_route_count<1>, dim3(grid), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_route_scatter<1>, dim3(grid), dim3(64), 0, st, a);
+    return;
+  }
   uint32_t grid = (h.n_src + 3) / 4;
   if (grid > 4096) grid = 4096;
   if (grid == 0) grid = 1;
-  if (phase == 0) hipLaunchKernelGGL(k_route_count, dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(k_route_scatter, dim3(grid), dim3(256), 0, st, a);
+  if (phase == 0) hipLaunchKernelGGL(k_route_count<4>, dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(k_route_scatter<4>, dim3(grid), dim3(256), 0, st, a);
 }
 
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
-                     hipStream_t st, uint64_t slot) {
+                     hipStream_t st, uint64_t slot, uint32_t n_win) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, n_dst, cnt,
-                     slot);
+  const uint32_t b = n_win > 1 ? 64u : 256u;  // a fused group's: single-wave workgroups
+  hipLaunchKernelGGL(k_dst_hist, dim3((uint32_t)((n + b - 1) / b)), dim3(b), 0, st, in, n, dst_begin, n_dst, cnt,
+                     slot, n_win);
 }
 
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
-                        tgsim_delivery* out, hipStream_t st, uint64_t slot) {
+                        tgsim_delivery* out, hipStream_t st, uint64_t slot, uint32_t n_win) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, n, dst_begin, n_dst,
-                     pos, out, slot);
+  const uint32_t b = n_win > 1 ? 64u : 256u;
+  hipLaunchKernelGGL(k_dst_scatter, dim3((uint32_t)((n + b - 1) / b)), dim3(b), 0, st, in, n, dst_begin, n_dst,
+                     pos, out, slot, n_win);
 }
 
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,

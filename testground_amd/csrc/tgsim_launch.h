@@ -22,6 +22,8 @@ struct RouteArgsHost {
   tgsim_delivery* out;
   uint64_t out_cap;
   uint64_t slot_cap;  // 0: flat; else per-rank chunks of a count header + slot_cap records
+  uint64_t chunk_stride;      // slotted: records from one rank's chunk to the next (0: slot_cap + 1)
+  uint32_t waves_per_block;   // 0 or 4: 256-thread blocks; 1: single-wave workgroups
 };
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st);
@@ -66,12 +68,14 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
 // when a rank's count exceeds slot_cap.
 void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
                         hipStream_t st, tgsim_delivery* out = nullptr, uint64_t slot_cap = 0,
-                        uint32_t* overflow = nullptr);
-// slot != 0: slotted input of n = ranks * (slot + 1) records (see launch_route_edges)
+                        uint32_t* overflow = nullptr, uint64_t chunk_stride = 0);
+// slot != 0: slotted input of n = chunks * (slot + 1) records (see launch_route_edges); with
+// n_win > 1 chunk c holds window c % n_win, counted into cnt[(c % n_win) * n_dst + d] (a fused
+// group: rank-major chunks, window-minor), in single-wave workgroups
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
-                     hipStream_t st, uint64_t slot = 0);
+                     hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
-                        tgsim_delivery* out, hipStream_t st, uint64_t slot = 0);
+                        tgsim_delivery* out, hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st);
 // Orders each destination's records; resets cnt[] to zero for the next histogram.

@@ -203,6 +203,20 @@ class CABIEngine:
         """Retires the oldest launched slotted step without waiting for it."""
         self._check(self._fn("step_sim_release")(self._h), "step_sim_release")
 
+    def step_sim_launch_slotted_n(self, n_ticks: int, n_win: int, bounds: Sequence[int], d_out: int, slot_cap: int,
+                                  routed_event: int = 0) -> None:
+        """Fused slotted group: n_win generated windows in one launch; d_out holds n_ranks x n_win
+        chunks of (slot_cap + 1) records (rank-major), one launched step for step_sim_release."""
+        b = (C.c_uint32 * len(bounds))(*bounds)
+        self._check(self._fn("step_sim_launch_slotted_n")(self._h, n_ticks, n_win, len(bounds) - 1, b,
+                                                           C.c_void_p(d_out), slot_cap,
+                                                           C.c_void_p(routed_event or None)),
+                    "step_sim_launch_slotted_n")
+
+    def deliver_slotted_n_async(self, d_in: int, n_ranks: int, n_win: int, slot_cap: int, wait_event: int = 0) -> None:
+        self._check(self._fn("deliver_slotted_n_async")(self._h, C.c_void_p(d_in), n_ranks, n_win, slot_cap,
+                                                         C.c_void_p(wait_event or None)), "deliver_slotted_n_async")
+
     def deliver_slotted_async(self, d_in: int, n_ranks: int, slot_cap: int, wait_event: int = 0) -> None:
         self._check(self._fn("deliver_slotted_async")(self._h, C.c_void_p(d_in), n_ranks, slot_cap,
                                                        C.c_void_p(wait_event or None)), "deliver_slotted_async")

@@ -157,21 +157,27 @@ class ShardedStepper:
             evs[j] = ev
         return ev
 
-    def _launch_slotted(self, n_ticks: int):
+    def _launch_slotted(self, n_ticks: int, n_win: int = 1):
+        """One launched step: a window, or a fused group of n_win windows (tgsim_step_sim_launch_slotted_n:
+        rank-major chunks, window-minor, all moved by one all-to-all)."""
         k = self._k
         self._k += 1
         j = k % 3
         n_r = len(self.bounds) - 1
-        out = self._buf(self._out, j, n_r * (self.slot_cap + 1) * REC)
+        out = self._buf(self._out, j, n_r * n_win * (self.slot_cap + 1) * REC)
         if self._ev[j] is not None:  # an earlier exchange still reads out[j]
             self.engine.wait_event(self._ev[j].cuda_event)
         routed = self._event(self._routed, j)
-        self.engine.step_sim_launch_slotted(n_ticks, self.bounds, out.data_ptr(), self.slot_cap, routed.cuda_event)
-        return k, out
+        if n_win > 1:
+            self.engine.step_sim_launch_slotted_n(n_ticks, n_win, self.bounds, out.data_ptr(), self.slot_cap,
+                                                  routed.cuda_event)
+        else:
+            self.engine.step_sim_launch_slotted(n_ticks, self.bounds, out.data_ptr(), self.slot_cap, routed.cuda_event)
+        return k, out, n_win
 
-    def _exchange_slotted(self, k: int, out: torch.Tensor) -> None:
+    def _exchange_slotted(self, k: int, out: torch.Tensor, n_win: int = 1) -> None:
         n_r = len(self.bounds) - 1
-        size = n_r * (self.slot_cap + 1) * REC
+        size = n_r * n_win * (self.slot_cap + 1) * REC
         i = k % 2
         with torch.cuda.stream(self._xs):
             cur = torch.cuda.current_stream(self.device)
@@ -181,9 +187,12 @@ class ShardedStepper:
             if self._in[i] is not None and self._in[i].numel() < size and self._dev[i] is not None:
                 self._dev[i].synchronize()  # growing: the old block returns to the allocator
             inb = self._buf(self._in, i, size)
-            self.exchanged_records += n_r * (self.slot_cap + 1)
+            self.exchanged_records += n_r * n_win * (self.slot_cap + 1)
             dist.all_to_all_single(inb[:size], out[:size], group=self.group)
-            self.engine.deliver_slotted_async(inb.data_ptr(), n_r, self.slot_cap, self._exchanged(k))
+            if n_win > 1:
+                self.engine.deliver_slotted_n_async(inb.data_ptr(), n_r, n_win, self.slot_cap, self._exchanged(k))
+            else:
+                self.engine.deliver_slotted_async(inb.data_ptr(), n_r, self.slot_cap, self._exchanged(k))
             self._mark_delivery(i)
 
     def step(self, n_ticks: int, between: Optional[Callable[[], object]] = None) -> int:
@@ -200,21 +209,24 @@ class ShardedStepper:
             return self.engine.step_sim_counts()
         return self.engine.step_sim_finish()
 
-    def run(self, n_steps: int, n_ticks: int) -> int:
+    def run(self, n_steps: int, n_ticks: int, fuse: int = 1) -> int:
         """n_steps windows with the simulation two steps ahead of the exchange: while the host
         exchanges step k, the engine's simulate stream already holds steps k+1 and k+2, so it never
         idles on the host.  Only for steps with no host-side change between them (pre-generated
         traffic, no reshaping, no receipts feeding generation); the results are identical to
         n_steps calls of step().  Returns the records delivered to this rank, or -1 in slotted
-        mode (the host never reads a count there)."""
+        mode (the host never reads a count there).  fuse > 1 (slotted mode): groups of up to `fuse`
+        generated windows per launch and per all-to-all."""
         if self.slot_cap and self.device.type == "cuda":
-            pend = [self._launch_slotted(n_ticks) for _ in range(min(2, n_steps))]
-            for s in range(n_steps):
-                k, out = pend.pop(0)
+            groups = [fuse] * (n_steps // fuse) + ([n_steps % fuse] if n_steps % fuse else []) if fuse > 1 \
+                else [1] * n_steps
+            pend = [self._launch_slotted(n_ticks, w) for w in groups[:2]]
+            for s in range(len(groups)):
+                k, out, w = pend.pop(0)
                 self.engine.step_sim_release()
-                if s + 2 < n_steps:
-                    pend.append(self._launch_slotted(n_ticks))
-                self._exchange_slotted(k, out)
+                if s + 2 < len(groups):
+                    pend.append(self._launch_slotted(n_ticks, groups[s + 2]))
+                self._exchange_slotted(k, out, w)
             return -1  # the host never read a count
         total = 0
         pend = [self._launch(n_ticks) for _ in range(min(2, n_steps))]

@@ -79,3 +79,90 @@ def test_step_n_falls_back_when_not_fusable(make_oracle):
         e.step_n(ticks, 2)
     assert _fused(g) == 0
     assert_same(g, c, "sparse windows through step_n")
+
+
+def test_three_shards_fused_slotted_exchange_equal_one():
+    """The fused slotted layout (tgsim_step_sim_launch_slotted_n: rank-major chunks, window-minor;
+    tgsim_deliver_slotted_n_async) over three shards on one GPU, the chunks swapped by hand as the
+    fixed-size all-to-all would: three fused windows deliver exactly what one engine delivers over
+    three tgsim_step calls, window after window."""
+    import torch
+
+    n, bounds, ticks, g = 600, [0, 150, 420, 600], 400, 3
+    ref = Engine(n)
+    shards = [Engine(n, shard=(bounds[r], bounds[r + 1])) for r in range(3)]
+    for e in [ref] + shards:
+        wl.configure_storm(e, n)
+        for _ in range(g):
+            e.gen_storm(0.5, ticks)
+    want = []
+    for _ in range(g):
+        ref.step(ticks)
+        want.append(ref.drain())
+    want = np.concatenate(want)
+    cap = 40_000
+    chunk = (cap + 1) * 24
+    bufs = []
+    for r, s in enumerate(shards):
+        buf = torch.zeros(3 * g * chunk, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        s.step_sim_launch_slotted_n(ticks, g, bounds, buf.data_ptr(), cap)
+        s.step_sim_release()
+        s.sync()
+        assert _fused(s) == g
+        bufs.append(buf)
+    for k, s in enumerate(shards):  # rank k receives chunks [k * g, (k + 1) * g) of every sender
+        inbound = torch.cat([b[k * g * chunk:(k + 1) * g * chunk] for b in bufs])
+        torch.cuda.synchronize()
+        s.deliver_slotted_n_async(inbound.data_ptr(), 3, g, cap)
+        s.sync()
+    # each shard's drain is its destinations' deliveries window after window; the single engine's is
+    # every destination's, window after window
+    got = [s.drain() for s in shards]
+    for r in range(3):
+        lo, hi = bounds[r], bounds[r + 1]
+        mine = want[(want["dst"] >= lo) & (want["dst"] < hi)]
+        assert len(got[r]) == len(mine) > 1000
+        assert (got[r] == mine).all()
+    s_ref = ref.stats()
+    tot = [s.stats() for s in shards]
+    assert sum(t["offered"] for t in tot) == s_ref["offered"]
+    assert sum(t["scheduled"] for t in tot) == s_ref["scheduled"]
+
+
+def test_stepper_fused_slotted_run_equals_step():
+    """ShardedStepper.run(fuse=4) through RCCL at one rank: groups of four windows per launch and per
+    all-to-all, the same deliveries and statistics as the single-engine steps."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from testground_amd.shard import ShardedStepper, init_rccl
+
+    torch.cuda.init()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29534")
+    init_rccl(torch.device("cuda", 0), rank=0, world_size=1)
+    try:
+        n, steps = 2000, 10
+        ref, sh = Engine(n), Engine(n)
+        for e in (ref, sh):
+            wl.configure_storm(e, n)
+        for _ in range(steps):
+            sh.gen_storm(0.5, 1000)
+        st = ShardedStepper(sh, [0, n], device="cuda:0", slot_cap=400_000)
+        assert st.run(steps, 1000, fuse=4) == -1
+        assert _fused(sh) == steps  # 4 + 4 + 2
+        want = []
+        for _ in range(steps):
+            ref.gen_storm(0.5, 1000)
+            ref.step(1000)
+            want.append(ref.drain())
+        want = np.concatenate(want)
+        got = sh.drain()
+        assert len(got) == len(want) > 10_000 and (got == want).all()
+        s, r = sh.stats(), ref.stats()
+        assert (s["offered"], s["scheduled"], s["by_verdict"]) == (r["offered"], r["scheduled"], r["by_verdict"])
+    finally:
+        dist.destroy_process_group()
