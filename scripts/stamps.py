@@ -97,6 +97,15 @@ dec = np.array_split(np.arange(len(st)), 10)
 print("  duration by dispatch decile (mean us):", [round(float(tot[d].mean()), 1) for d in dec])
 print("  start by dispatch decile (mean us):   ", [round(float(start[d].mean()), 1) for d in dec])
 print("  end by dispatch decile (max us):      ", [round(float(end[d].max()), 1) for d in dec])
+if shapes:  # per bandwidth class: phase times and profile cycles per batch
+    bwc = np.array([shapes[i].Bandwidth for i in src_of]) / 1e6
+    for c in np.unique(bwc):
+        m = bwc == c
+        line = (f"  bw {c:6.0f} Mbit/s: {m.sum():5d} srcs, total {tot[m].mean():6.1f} us (load {ph[m, 0].mean():5.2f}, "
+                f"batches {ph[m, 1].mean():6.2f}, end {ph[m, 2].mean():5.2f}, wb {ph[m, 3].mean():5.2f}); per batch: "
+                + ", ".join(f"{v} {np.mean(pf[m, k] / nb[m]):.0f}" for k, v in names.items()) +
+                f"; windows {np.mean(pf[m, 3] / nb[m]):.2f}, fullq {np.mean(pf[m, 2] / nb[m]):.2f}")
+        print(line)
 if shapes:
     lat = np.array([shapes[i].Latency for i in src_of]) / 1e6
     jit = np.array([shapes[i].Jitter for i in src_of]) / 1e6

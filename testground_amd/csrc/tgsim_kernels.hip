@@ -2748,7 +2748,11 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
   // n_hint bounds the step's records (offered packets or the exact count).  Measured at the 1M-peer
   // flood's peak (up to ~20 records per destination): groups of 16 lanes 0.77 ms, of 32 3.8 ms
   // (the in-group shuffles), the wavefront per destination 1.4 ms
-  if (n_hint <= 8ull * n_dst)
+  static const uint64_t group_max = [] {  // TGSIM_SORT_GROUP_MAX: average records per destination
+    const char* v = getenv("TGSIM_SORT_GROUP_MAX");
+    return v ? (uint64_t)atoll(v) : 8ull;
+  }();
+  if (n_hint <= group_max * n_dst)
     hipLaunchKernelGGL(k_dst_sort_group<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
   else
     hipLaunchKernelGGL(k_dst_sort_wide<4>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
