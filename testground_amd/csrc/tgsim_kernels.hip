@@ -23,11 +23,8 @@ __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, ui
   // the round keys are derived from the key at every call (2 SALU per round): hoisted out of the
   // simulate loop they held 20 SGPRs and came back as spill reloads (v_readlane) at every draw
   __asm__ volatile("" : "+s"(k0), "+s"(k1));
-#ifndef TGSIM_PHILOX_ROUNDS
-#define TGSIM_PHILOX_ROUNDS 10  // (timing experiments only may lower it: the draws then differ)
-#endif
 #pragma unroll
-  for (int i = 0; i < TGSIM_PHILOX_ROUNDS; ++i) {
+  for (int i = 0; i < 10; ++i) {
     // one v_mad_u64_u32 per product instead of a v_mul_hi_u32 + v_mul_lo_u32 pair
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
@@ -948,7 +945,8 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     const InRec r = rec;
     idx += kWave;
     rec = rec2;
-    rec2 = a.in[idx + kWave < send ? idx + kWave : last_in];  // in flight two batches ahead
+    // in flight two batches ahead (three: no gain, A/B round 2)
+    rec2 = a.in[idx + kWave < send ? idx + kWave : last_in];
     if (v_pend) a.verdict[v_idx] = (uint8_t)v_out;
     const uint64_t T = a.t0_ns + (uint64_t)r.tick * a.tick_ns;
     const uint32_t len = r.len & 0xFFFFu;
@@ -1694,9 +1692,6 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
   const uint64_t t_bytes = wave_sum(bytes);
   const bool err = __ballot(perr != 0) != 0;
   unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
-#ifdef TGSIM_EXP_NOSTATS  // timing experiment only: the statistics go missing
-  if (s < kStatCopies) return;
-#endif
   if (lane < 8 && vcnt) atomicAdd(&sc[kStVerdict0 + lane], (unsigned long long)vcnt);
   if (lane == 0) {
     const uint64_t qb = 16ull * qn + 8ull * rn + 16ull * wpos + 8ull * rn_new;
