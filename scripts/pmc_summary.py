@@ -33,7 +33,8 @@ for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
             step[-1][0][k] += v
     # the timed windows: groups of FUSE, then the remainder (tgsim_step_n); a group of w windows
     # counts w times, with 1/w of its counters each
-    groups = [FUSE] * (steps // FUSE) + ([steps % FUSE] if steps % FUSE else [])
+    fused = any(f for _, f in step)  # per-window dispatches otherwise (sparse steps, gossip)
+    groups = [FUSE] * (steps // FUSE) + ([steps % FUSE] if steps % FUSE else []) if fused else [1] * steps
     for (sv, _), w in zip(reversed(step), reversed(groups)):
         for k, v in sv.items():
             vals[k].setdefault("v", []).extend([v / w] * w)

@@ -24,7 +24,8 @@ for r in rows:
 
 # the timed windows: tgsim_step_n(n) runs groups of fuse windows, then the remainder (a lone
 # window unfused); matched to the last dispatch groups
-groups = [fuse] * (n // fuse) + ([n % fuse] if n % fuse else [])
+fused = any("k_sim_fused" in d["kernels"] for d in disp)  # per-window dispatches otherwise
+groups = [fuse] * (n // fuse) + ([n % fuse] if n % fuse else []) if fused else [1] * n
 timed = [(d, w) for d, w in zip(reversed(disp), reversed(groups))]
 ms = sum(d["ms"] for d, _ in timed)
 wins = sum(w for _, w in timed)
