@@ -1280,7 +1280,10 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   HIPCHK(take_event(E, &ev0));
   HIPCHK(take_event(E, &ev1));
   HIPCHK(hipEventRecord(ev0, E->st));
-  if (!E->fused_wgs) E->fused_wgs = sim_fused_resident();
+  if (!E->fused_wgs) {
+    E->fused_wgs = sim_fused_resident();
+    if (const char* w = getenv("TGSIM_FUSED_WGS")) E->fused_wgs = static_cast<uint32_t>(std::max(1, atoi(w)));
+  }
   // a sharded group's exchange (RCCL) and deliveries need CU slots while the next group simulates:
   // there the workgroups turn over (TGSIM_FUSED_PERSIST=1 forces the persistent grid)
   f.persistent = gr ? (E->persist_routed ? 1u : 0u) : 1u;
