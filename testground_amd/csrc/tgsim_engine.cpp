@@ -1347,45 +1347,45 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
     E->route_cap[k] = static_cast<size_t>(gr->n_ranks) * g * (gr->slot_cap + 1);
     E->route_n++;
   } else {
-  // the group's deliveries, beside the next launch: one scan over the (window, destination)
-  // counts, one scatter of every window's emit regions, one sort per segment; the sorted output is
-  // window 0's deliveries, then window 1's, ... (the drain order of g tgsim_step calls)
-  hipStream_t sq = E->dst_st;
-  HIPCHK(hipEventRecord(E->ev_sim, E->st));
-  HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
-  HIPCHK(E->d_doff.ensure(nseg + 1));
-  HIPCHK(E->d_dpos.ensure(nseg));
-  HIPCHK(E->d_dblk.ensure((nseg + 1023) / 1024 + 1));
-  HIPCHK(E->d_dtot.ensure(1));
-  launch_scan_w(E->f_lcnt[p].p, E->d_doff.p, nseg, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
-  HIPCHK(hipGetLastError());
-  uint64_t n_rec = rec_bound;
-  if (!(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES)) {
-    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
-    HIPCHK(hipStreamSynchronize(sq));
-    n_rec = E->h_dtot;
-  }
-  HIPCHK(E->d_scatter.ensure(n_rec ? n_rec : 1));
-  GroupDeliver gd{};
-  for (uint32_t i = 0; i < g; ++i) {
-    gd.emit[i] = E->fset[p][i].emit.p;
-    gd.emit_n[i] = E->fset[p][i].emit_n.p;
-    gd.off[i] = win[i].off.p;
-  }
-  gd.n_src = E->S;
-  gd.n_dst = E->N;
-  gd.pos = E->d_dpos.p;
-  gd.out = E->d_scatter.p;
-  launch_local_scatter_group(gd, g, sq);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(E->ev_recv, sq));
-  tgsim_delivery* dst = nullptr;
-  rc = delivery_out(E, n_rec, &dst, sq);
-  if (rc) return rc;
-  launch_dst_sort_w1(E->d_scatter.p, E->d_doff.p, E->f_lcnt[p].p, static_cast<uint32_t>(nseg), dst, sq);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(E->ev_fgrp[p], sq));
-  HIPCHK(hipEventRecord(E->ev_dst, E->dst_st));
+    // the group's deliveries, beside the next launch: one scan over the (window, destination)
+    // counts, one scatter of every window's emit regions, one sort per segment; the sorted output is
+    // window 0's deliveries, then window 1's, ... (the drain order of g tgsim_step calls)
+    hipStream_t sq = E->dst_st;
+    HIPCHK(hipEventRecord(E->ev_sim, E->st));
+    HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+    HIPCHK(E->d_doff.ensure(nseg + 1));
+    HIPCHK(E->d_dpos.ensure(nseg));
+    HIPCHK(E->d_dblk.ensure((nseg + 1023) / 1024 + 1));
+    HIPCHK(E->d_dtot.ensure(1));
+    launch_scan_w(E->f_lcnt[p].p, E->d_doff.p, nseg, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
+    HIPCHK(hipGetLastError());
+    uint64_t n_rec = rec_bound;
+    if (!(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES)) {
+      HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
+      HIPCHK(hipStreamSynchronize(sq));
+      n_rec = E->h_dtot;
+    }
+    HIPCHK(E->d_scatter.ensure(n_rec ? n_rec : 1));
+    GroupDeliver gd{};
+    for (uint32_t i = 0; i < g; ++i) {
+      gd.emit[i] = E->fset[p][i].emit.p;
+      gd.emit_n[i] = E->fset[p][i].emit_n.p;
+      gd.off[i] = win[i].off.p;
+    }
+    gd.n_src = E->S;
+    gd.n_dst = E->N;
+    gd.pos = E->d_dpos.p;
+    gd.out = E->d_scatter.p;
+    launch_local_scatter_group(gd, g, sq);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(E->ev_recv, sq));
+    tgsim_delivery* dst = nullptr;
+    rc = delivery_out(E, n_rec, &dst, sq);
+    if (rc) return rc;
+    launch_dst_sort_w1(E->d_scatter.p, E->d_doff.p, E->f_lcnt[p].p, static_cast<uint32_t>(nseg), dst, sq);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(E->ev_fgrp[p], sq));
+    HIPCHK(hipEventRecord(E->ev_dst, E->dst_st));
   }
   E->fgrp = p ^ 1;
   // the last window's input stays the engine's current input (as after tgsim_step); the replaced
