@@ -113,7 +113,7 @@ constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (T
 // t % S-th source in dispatch order.  A source's window k > 0 starts once its window k - 1 has
 // stored done[s] = step_base + k (the hand-off); the windows differ only in these
 // per-window fields.
-constexpr uint32_t kFuseMax = 16;
+constexpr uint32_t kFuseMax = 8;
 struct FusedWindow {
   const uint64_t* off;
   const InRec* in;

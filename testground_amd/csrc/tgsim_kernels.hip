@@ -1378,7 +1378,11 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
 // ticket is held by a resident workgroup and waits only for a lower ticket (its source's previous
 // window), so the lowest unfinished ticket can always run: no deadlock.  The wait is bounded
 // anyway (kErrHandoff, then the window runs and the host reports -EIO).
-__global__ __launch_bounds__(kWave, 3) void k_sim_fused(SimArgs a0, FusedArgs f) {
+struct FusedSim {
+  SimArgs w[kFuseMax];  // window k's arguments (tables and state shared, step fields its own)
+};
+__global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f) {
+  const SimArgs& a0 = fs.w[0];
   __shared__ SimLdsT<kHeapCap> lds;
   const uint32_t total = f.n_win * a0.n_src;
   uint32_t t = 0;
@@ -1413,16 +1417,13 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused(SimArgs a0, FusedArgs f)
     }
     if (a0.stamps && threadIdx.x == 0)  // diagnostics: 10-ns ticks spent waiting for the previous window
       a0.stamps[(size_t)t * kStampSlots + kStampSlots - 1] = __builtin_amdgcn_s_memrealtime() - t_wait;
-    SimArgs a = a0;
-    const FusedWindow& w = f.w[k];
-    a.off = w.off;
-    a.in = w.in;
-    a.verdict = w.verdict;
-    a.emit = w.emit;
-    a.emit_n = w.emit_n;
-    a.dst_cnt = w.dst_cnt;
-    a.t0_ns = w.t0_ns;
-    a.horizon_ns = w.horizon_ns;
+    // window k's arguments read in place in the kernel-argument segment (scalar loads of invariant
+    // memory: re-read when needed instead of held in spilled SGPRs)
+    using KernargSimArgs = __attribute__((address_space(4))) const SimArgs;
+    const KernargSimArgs* ka =
+        (KernargSimArgs*)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                          k * sizeof(SimArgs));
+    const SimArgs& a = *(const SimArgs*)ka;
     const uint32_t next = sim_source<false, kHeapCap, true>(a, s, t, lds, f.persistent ? f.ticket : nullptr,
                                                             f.ticket_base);
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
@@ -2564,7 +2565,21 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
 
 void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st) {
   const uint32_t total = f.n_win * a.n_src;
-  hipLaunchKernelGGL(k_sim_fused, dim3(f.persistent && n_wg < total ? n_wg : total), dim3(kWave), 0, st, a, f);
+  FusedSim fs;
+  for (uint32_t k = 0; k < kFuseMax; ++k) {
+    fs.w[k] = a;
+    if (k >= f.n_win) continue;
+    const FusedWindow& w = f.w[k];
+    fs.w[k].off = w.off;
+    fs.w[k].in = w.in;
+    fs.w[k].verdict = w.verdict;
+    fs.w[k].emit = w.emit;
+    fs.w[k].emit_n = w.emit_n;
+    fs.w[k].dst_cnt = w.dst_cnt;
+    fs.w[k].t0_ns = w.t0_ns;
+    fs.w[k].horizon_ns = w.horizon_ns;
+  }
+  hipLaunchKernelGGL(k_sim_fused, dim3(f.persistent && n_wg < total ? n_wg : total), dim3(kWave), 0, st, fs, f);
 }
 
 uint32_t sim_fused_resident() {
