@@ -523,7 +523,7 @@ def test_sparse_and_dense_kernels_agree(make_oracle, monkeypatch, mode):
     bit-exact with the oracle either way, on a mix of sparse and dense, correlated and plain
     senders."""
     monkeypatch.setenv("TGSIM_SPARSE", mode)
-    n = 200
+    n = 201
     rng = np.random.default_rng(41)
     g, c = both(make_oracle, n, queue_limit=300, lookahead_ns=200_000)
     shapes = wl.storm_shapes(n, 3)
@@ -556,3 +556,41 @@ def test_sparse_and_dense_kernels_agree(make_oracle, monkeypatch, mode):
         g.step(3000)
         c.step(3000)
         assert_same(g, c, f"mode {mode} step {step}")
+
+
+def test_sparse_long_queues(make_oracle, monkeypatch):
+    """Sparse windows whose netem queues grow to 300-600 items (30-60 ms of latency, 2-ms windows of
+    ~20 packets): k_sim_sparse serves them from registers while they fit (256 queued items), then
+    defers them to k_sim_list; bit-exact with the oracle window by window."""
+    monkeypatch.setenv("TGSIM_SPARSE", "1")
+    n = 65
+    rng = np.random.default_rng(7)
+    g, c = both(make_oracle, n)
+    for i in range(n):
+        s = nw.LinkShape(Latency=int(rng.integers(30, 61)) * nw.Millisecond, Jitter=int(rng.integers(0, 3)) * nw.Millisecond,
+                         Bandwidth=1 << 30, Loss=1.0, Duplicate=2.0, Corrupt=1.0)
+        for e in (g, c):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=s))
+    seq = np.zeros(n, dtype=np.uint32)
+    for step in range(40):
+        m = 20 * n
+        src = rng.integers(0, n, m)
+        pk = np.zeros(m, dtype=abi.PKT_DTYPE)
+        pk["src"] = src
+        pk["dst"] = (src + 1 + rng.integers(0, n - 1, m)) % n
+        pk["len"] = rng.integers(40, 1500, m)
+        pk["tick"] = rng.integers(0, 2000, m)
+        order = np.lexsort((pk["tick"], src))
+        counts = np.bincount(src, minlength=n)
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        sq = np.empty(m, dtype=np.uint32)
+        sq[order] = np.arange(m) - starts[src[order]] + seq[src[order]]
+        seq += counts.astype(np.uint32)
+        pk["seq"] = sq
+        g.submit(pk)
+        c.submit(pk)
+        g.step(2000)
+        c.step(2000)
+        assert_same(g, c, f"step {step}")
+    # the queues did grow past the 128 items held in registers (state bytes: ~16 B x 2 per item)
+    assert g.stats()["queue_state_bytes"] > 40 * n * 32 * 128 // 2
