@@ -79,3 +79,41 @@ def test_gossip_1m_sparse_equals_dense(monkeypatch):
     assert sum(by.values()) == st["offered"] + st["cloned"]
     assert by["scheduled"] > 0.98 * st["offered"] and st["scheduled"] > 0
     assert set(k for k, x in by.items() if x) <= {"scheduled", "loss"}, by
+
+
+def test_epochs_100k_two_shards_equal_one():
+    """C5 at full size (configs[4]: 100,000 instances, 10 % reshaped per 1,000-tick epoch): one
+    engine and two uneven shards whose records are exchanged by hand (the all-to-all's data
+    movement) agree bit for bit, epoch after epoch — verdicts, every delivery, the offered and
+    scheduled counts — and each shard's barrier releases with its own peers' signals."""
+    from test_gpu_parity import _manual_sharded_step
+
+    n, bounds = 100_000, [0, 40_000, 100_000]
+    ref = Engine(n)
+    shards = [Engine(n, shard=(bounds[r], bounds[r + 1])) for r in range(2)]
+    for e in [ref] + shards:
+        wl.configure_storm(e, n)
+    for k in range(4):
+        wl.run_epoch(ref, n, k, n)
+        for e in shards:
+            if k:
+                wl.epoch_reshape(e, n, k)
+            e.gen_storm(wl.EPOCH_LAMBDA, wl.EPOCH_TICKS)
+        _manual_sharded_step(shards, bounds, wl.EPOCH_TICKS)
+        state, rnd = wl.epoch_state(k)
+        for r, e in enumerate(shards):
+            e.signal_async(state, bounds[r + 1] - bounds[r])
+            assert e.barrier_poll(state, rnd * (bounds[r + 1] - bounds[r]))
+        v_ref = ref.verdicts()
+        v_sh = np.concatenate([e.verdicts() for e in shards])
+        assert len(v_ref) > 15_000_000 and np.array_equal(v_sh, v_ref), f"epoch {k}: verdicts differ"
+        d_ref = ref.drain()
+        d_sh = np.concatenate([e.drain() for e in shards])
+        assert len(d_sh) == len(d_ref) > 100_000, f"epoch {k}"
+        assert np.array_equal(d_sh.view(np.uint8), d_ref.view(np.uint8)), f"epoch {k}: deliveries differ"
+        assert _ordered(d_ref)
+        print(f"epoch {k}: {len(v_ref)} packets, {len(d_ref)} deliveries", flush=True)
+    s_ref, s_sh = ref.stats(), [e.stats() for e in shards]
+    for key in ("offered", "scheduled", "cloned", "corrupted", "bytes_scheduled"):
+        assert sum(s[key] for s in s_sh) == s_ref[key], key
+    assert ref.barrier_poll(wl.epoch_state(3)[0], n)
