@@ -18,8 +18,11 @@ runs the epoch and passes the `epoch-k` barrier (counters summed over ranks on t
 
 Launch: N = 1 runs directly.  `--gpus N` with N > 1 and no WORLD_SIZE in the environment starts N
 ranks itself (torch.distributed.run, one process per GPU) from this parent, which never touches
-the GPU; under an external launcher WORLD_SIZE must equal --gpus.  Every rank owns --peers
-instances (weak scaling); cross-shard deliveries are exchanged with all_to_all_single (RCCL).
+the GPU; under an external launcher WORLD_SIZE must equal --gpus.  The storm headline is
+BASELINE.json configs[2] at every N: 10,000 instances in total, split over the ranks (strong
+scaling); at N > 1 the line also carries `weak_per_gpu`, the same storm with 10,000 instances per
+rank.  The 1M-peer gossip is 1,000,000 peers in total at every N.  Cross-shard deliveries are
+exchanged by the engine's RCCL all-to-all.
 """
 import argparse
 import ctypes
@@ -54,7 +57,9 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; gossip: 0)")
     p.add_argument("--workload", default="storm", choices=["storm", "gossip", "epochs", "bridge"])
     p.add_argument("--peers", type=int, default=0,
-                   help="instances per GPU (default: storm 10,000; gossip 125,000; epochs 100,000)")
+                   help="storm: instances in total, split over the GPUs (configs[2]; at N > 1 a second run with "
+                        "this many per GPU is reported as weak_per_gpu); gossip/epochs/bridge: instances per GPU "
+                        "(default: storm 10,000; gossip 125,000; epochs 100,000)")
     p.add_argument("--floods", type=int, default=64, help="gossip: flood messages")
     p.add_argument("--flood-gap", type=int, default=1000, help="gossip: ticks between flood starts")
     p.add_argument("--lam", type=float, default=None,
@@ -220,8 +225,9 @@ def load_pmc(workload, window, peers, lam, shapes="storm"):
     src.update({k: pmc.get(k) for k in ("kernel_sha16", "commit", "peers", "lam", "window")})
     if pmc.get("kernel_sha16") != src["kernel_sha16_now"]:
         return None, dict(src, status="stale: collected on another k_sim source")
-    if (pmc.get("window") != window or pmc.get("peers") != peers or pmc.get("lam", lam) != lam
-            or pmc.get("shapes", "storm") != shapes):
+    want_shapes = shapes if workload == "storm" else workload  # gossip/epochs have their own shapes
+    if (pmc.get("window") != window or pmc.get("peers") != peers
+            or (workload != "gossip" and pmc.get("lam", lam) != lam) or pmc.get("shapes", "storm") != want_shapes):
         return None, dict(src, status="other configuration")
     return pmc.get("hbm_bytes_per_launch"), dict(src, status="matches this kernel and configuration")
 
@@ -343,10 +349,31 @@ def cpu_bridge_baseline(n, window, seconds):
                       f"{steps} windows of {len(items)} sends ({el:.1f} s, including the fill of the first windows)"}
 
 
-def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, local, dist, want_cpu):
-    """Builds one engine shard of `peers` sources on this rank, brings the workload to its timed
-    state, times `steps` steps (barrier + synchronize on both sides, max over ranks) and returns the
-    rank-0 result object (None on the other ranks)."""
+def shard_bounds(peers, world, split):
+    """(instances in total, contiguous source ranges of the ranks): `peers` per rank, or with split
+    `peers` in total, split evenly (contiguous source partition)."""
+    total = peers if split else peers * world
+    return total, [r * total // world for r in range(world)] + [total]
+
+
+def headline_plan(a, world):
+    """What the default line measures at this world size (bench.py --launch-check prints it)."""
+    total, bounds = shard_bounds(a.peers, world, a.workload == "storm")
+    plan = {"workload": a.workload, "peers_total": total, "bounds": bounds,
+            "scaling": "strong" if a.workload == "storm" and world > 1 else "weak"}
+    if a.workload == "storm" and world > 1:
+        plan["weak_per_gpu_peers_total"] = shard_bounds(a.peers, world, False)[0]
+    if a.workload == "storm" and not a.no_1m:
+        plan["at_1M_peers_total"] = shard_bounds(a.gossip_1m_peers, world, True)[0]
+    return plan
+
+
+def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, local, dist, want_cpu,
+                 split=False):
+    """Builds one engine shard on this rank, brings the workload to its timed state, times `steps`
+    steps (barrier + synchronize on both sides, max over ranks) and returns the rank-0 result object
+    (None on the other ranks).  `peers` instances per rank (weak scaling), or with split=True
+    `peers` instances in total, split evenly over the ranks (strong scaling)."""
     import numpy as np
     import torch
 
@@ -355,8 +382,9 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     from testground_amd.network import configs_array
 
     sharded = dist is not None
-    peers_total = peers * world
-    lo, hi = rank * peers, (rank + 1) * peers
+    peers_total, bounds = shard_bounds(peers, world, split)
+    lo, hi = bounds[rank], bounds[rank + 1]
+    peers = hi - lo  # this rank's sources
     kw = dict(lookahead_ns=workloads.GOSSIP_MIN_LAT) if workload == "gossip" else {}
     eng = Engine(peers_total, shard=(lo, hi), device=local, flags=abi.OPT_DISCARD_DELIVERIES,
                  queue_limit=a.queue_limit, **kw)
@@ -367,7 +395,6 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         workloads.configure_storm(eng, peers_total, open_links=a.shapes == "open")
     else:
         eng.configure_batch(np.arange(peers_total), configs_array(np.full(peers_total, 5_000_000), routing_policy=2))
-    bounds = [r * peers for r in range(world)] + [peers_total]
     stepper = None
     if sharded:
         from testground_amd.shard import ShardedStepper
@@ -416,10 +443,11 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
 
     def run_steps(n):
         if stepper is not None and workload == "storm":  # pre-generated: simulate one step ahead
-            # slotted exchange: groups of up to four windows per launch and per all-to-all (A/B at one
-            # rank: 1 27.5, 4 30.4, 8 27.7-28.6 G pkt/s: larger groups lengthen the pipeline drain)
-            stepper.run(n, window, fuse=1 if a.exact_exchange else int(os.environ.get("TGSIM_FUSE", "4")))
-        elif workload == "storm":  # pre-generated windows, up to four per launch (tgsim_step_n)
+            # slotted exchange: groups of TGSIM_SHARD_FUSE (4) windows per launch and per all-to-all
+            # (A/B at one rank: 1 27.5, 4 30.4, 8 27.7-28.6 G pkt/s: larger groups lengthen the
+            # pipeline drain); TGSIM_FUSE is the single engine's group size (default 8, tgsim_step_n)
+            stepper.run(n, window, fuse=1 if a.exact_exchange else int(os.environ.get("TGSIM_SHARD_FUSE", "4")))
+        elif workload == "storm":  # pre-generated windows, up to TGSIM_FUSE (8) per launch (tgsim_step_n)
             eng.step_n(window, n)
         else:
             for _ in range(n):
@@ -492,14 +520,14 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         "warmup": warmup,
         "ms_per_step": el * 1e3 / steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if split and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
         "data": f"synthetic (device-generated {workload} traffic, Philox-keyed)",
         "config": dict({"workload": WORKLOAD_NAMES["storm_open" if workload == "storm" and a.shapes == "open"
                                                    else workload],
-                        "peers_per_gpu": peers, "peers_total": peers_total, "lambda_per_tick": lam,
-                        "tick_ns": 1000, "window_ticks": window, "settle_sim_ms": settle * window / 1000,
+                        "peers_per_gpu": peers, "peers_total": peers_total,
+                        **({} if workload == "gossip" else {"lambda_per_tick": lam}), "tick_ns": 1000, "window_ticks": window, "settle_sim_ms": settle * window / 1000,
                         "shapes": a.shapes if workload == "storm" else workload,
                         "queue_limit": a.queue_limit or 1000, "packets_per_step": offered_all / steps,
                         "parallelism": f"peer-sharded x{world}" + (" (RCCL exchange path)" if sharded else ""),
@@ -545,7 +573,8 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.launch_check:
         line = json.dumps({"rank": rank, "world": world, "local_rank": local, "gpus": a.gpus,
-                           "launched_by_bench": os.environ.get("TGSIM_BENCH_LAUNCHED") == "1"})
+                           "launched_by_bench": os.environ.get("TGSIM_BENCH_LAUNCHED") == "1",
+                           "headline": headline_plan(a, world)})
         os.write(1, (line + "\n").encode())  # one write: the ranks share the pipe
         return
     # the one JSON line goes to the original stdout; everything else (RCCL's version banner, library
@@ -568,12 +597,20 @@ def main(argv=None):
     if a.workload == "bridge":
         res = run_bridge(a, world, rank, local, dist, want_cpu=not a.no_cpu)
     else:
+        # storm (configs[2]: "10k instances, 1/2/4/8 GPUs"): the headline is --peers instances in
+        # total, split over the ranks; the weak-scaling run (--peers per GPU) rides along at N > 1
         res = run_workload(a, a.workload, a.peers, a.steps, a.warmup, a.window, a.lam, world, rank, local, dist,
-                           want_cpu=not a.no_cpu)
+                           want_cpu=not a.no_cpu, split=a.workload == "storm")
+        if a.workload == "storm" and world > 1:
+            w = run_workload(a, "storm", a.peers, a.steps, a.warmup, a.window, a.lam, world, rank, local, dist,
+                             want_cpu=False)
+            if res is not None:
+                res["weak_per_gpu"] = {k: w[k] for k in ("value", "unit", "ms_per_step", "steps", "scaling", "config",
+                                                         "scheduled_per_s", "roofline")}
     if a.workload == "storm" and not a.no_1m:
         # the 1M-peer half of the metric: C4 gossip over 1M peers in total, split over the ranks
-        g = run_workload(a, "gossip", a.gossip_1m_peers // world, 70, 0, 5000, a.lam, world, rank, local, dist,
-                         want_cpu=not a.no_cpu)
+        g = run_workload(a, "gossip", a.gossip_1m_peers, 70, 0, 5000, a.lam, world, rank, local, dist,
+                         want_cpu=not a.no_cpu, split=True)
         if res is not None:
             res["at_1M_peers"] = {k: g[k] for k in ("value", "unit", "ms_per_step", "steps", "config",
                                                     "scheduled_per_s", "verdict_mix", "setup_s", "roofline",

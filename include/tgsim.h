@@ -203,6 +203,12 @@ int tgsim_configure(void* engine, uint32_t peer, const tgsim_config* cfg);
  * rcs[i] (optional) receives each call's return code; returns the number of failed calls. */
 int64_t tgsim_configure_batch(void* engine, const uint32_t* peers, const tgsim_config* cfgs, size_t n,
                               int32_t* rcs);
+/* How many times `peer`'s data link has been removed so far: a disconnect (Enable=false,
+ * docker_network.go:65-75) or a re-addressing reconnect (:77-88; k8s_network.go:130-155).  A caller
+ * that holds state about packets in flight (the packet bridge) compares it before and after a
+ * tgsim_configure: a changed value means every packet queued by the peer, or towards it, is gone
+ * (tgsim_stats_t.flushed / lost_in_flight) and will never be delivered. */
+int64_t tgsim_link_generation(void* engine, uint32_t peer);
 
 /* ---- data path ---------------------------------------------------------------------------- */
 int tgsim_submit(void* engine, const tgsim_pkt* pkts, size_t n);
@@ -218,7 +224,7 @@ int tgsim_gen_storm(void* engine, double lambda, uint32_t n_ticks);
 int tgsim_step(void* engine, uint32_t n_ticks);
 /* n_steps consecutive tgsim_step(engine, n_ticks) calls, with identical results (verdicts then
  * refer to the last window).  Windows of generated traffic (tgsim_gen_storm) on an engine that owns
- * every peer run up to four per launch: a source's next window starts as soon as its previous one
+ * every peer run up to kFuseMax = 8 per launch (TGSIM_FUSE, default 8): a source's next window starts as soon as its previous one
  * is done, so one window's slowest sources overlap the next window's first ones (no launch tail or
  * gap between the windows of a group).  A source whose previous window does not complete in time
  * (a hardware fault) is reported as -EIO. */
@@ -379,6 +385,11 @@ int64_t tgsim_bridge_step(void* bridge);
 int64_t tgsim_bridge_recv(void* bridge, uint32_t peer, tgsim_msg* msgs, size_t max, uint8_t* data, size_t cap);
 int64_t tgsim_bridge_pending(void* bridge, uint32_t peer); /* deliveries queued (UINT32_MAX: all) */
 int64_t tgsim_bridge_in_flight(void* bridge);              /* datagrams sent, not yet resolved  */
+/* peer's data link was removed by the last tgsim_configure (tgsim_link_generation changed): every
+ * datagram already handed to the engine that was sent by peer or addressed to it is resolved as
+ * lost, since the engine flushes or purges it without a delivery.  Datagrams not yet handed to the
+ * engine (due in a later window) are kept.  Returns how many were resolved. */
+int64_t tgsim_bridge_link_removed(void* bridge, uint32_t peer);
 uint64_t tgsim_bridge_now_tick(void* bridge);              /* start of the next window          */
 /* UDP front end: one socket on 127.0.0.1 receives every instance's datagrams (a 4-byte big-endian
  * destination header, then the payload) from the instance's registered address; pump() moves what

@@ -202,6 +202,7 @@ typedef struct {
     uint8_t* ip6_set;   /* the link carries an IPv6 address (cfg.IPv6 was given at connect) */
     uint8_t (*ip6)[16];
     uint8_t* k8s_init;  /* K8sNetwork.initialized, per instance (k8s_network.go:119-125) */
+    uint32_t* link_gen; /* data links removed per instance (tgsim_link_generation) */
     uint32_t key[2];
     uint64_t now_tick;
     offered* off;
@@ -313,6 +314,7 @@ int tgo_create(const tgsim_opts* opts, void** out) {
     o->ip6_set = (uint8_t*)calloc(o->o.n_peers, 1);
     o->ip6 = calloc(o->o.n_peers, 16);
     o->k8s_init = (uint8_t*)calloc(o->o.n_peers, 1);
+    o->link_gen = (uint32_t*)calloc(o->o.n_peers, sizeof(uint32_t));
     for (uint32_t i = 0; i < o->o.n_peers; ++i) o->ip[i] = o->o.subnet_base + 2 + i;
     o->gen_seq = (uint32_t*)calloc(o->nsrc, sizeof(uint32_t));
     o->metrics_on = (o->o.flags & TGSIM_OPT_METRICS) != 0;
@@ -340,7 +342,7 @@ void tgo_destroy(void* p) {
     for (size_t i = 0; i < o->gq_n; ++i) free(o->gq[i].pk);
     free(o->gq);
     free(o->src); free(o->enabled); free(o->ip); free(o->off); free(o->verdicts);
-    free(o->ip6_set); free(o->ip6); free(o->k8s_init);
+    free(o->ip6_set); free(o->ip6); free(o->k8s_init); free(o->link_gen);
     free(o->out); free(o->step_out); free(o->gen_seq); free(o->g_first); free(o->g_fwd);
     free(o->m_src); free(o->m_dst);
     free(o);
@@ -391,6 +393,7 @@ static int add_rules(oracle* o, source* S, const tgsim_rule* rules, uint32_t n) 
  * packet still waiting in some sender's netem queue towards it will leave into a missing port. */
 static void link_down(oracle* o, uint32_t peer) {
     o->enabled[peer] = 0;
+    o->link_gen[peer]++;
     if (peer >= o->o.shard_begin && peer < o->o.shard_end) {
         source* S = &o->src[peer - o->o.shard_begin];
         o->st.flushed += S->heap_n + S->ring_n;
@@ -450,6 +453,12 @@ static void routing_policy(oracle* o, uint32_t peer, uint8_t policy) { /* route.
 
 static int ipv4_differs(const oracle* o, uint32_t peer, const tgsim_config* cfg) {
     return cfg->has_ipv4 && cfg->ipv4 != o->ip[peer];
+}
+
+int64_t tgo_link_generation(void* p, uint32_t peer) {
+    oracle* o = (oracle*)p;
+    if (!o || peer >= o->o.n_peers) return -EINVAL;
+    return o->link_gen[peer];
 }
 
 int tgo_configure(void* p, uint32_t peer, const tgsim_config* cfg) {

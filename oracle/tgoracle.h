@@ -31,6 +31,7 @@ void tgo_destroy(void* o);
 const char* tgo_last_error(const void* o);
 int tgo_configure(void* o, uint32_t peer, const tgsim_config* cfg);
 int64_t tgo_configure_batch(void* o, const uint32_t* peers, const tgsim_config* cfgs, size_t n, int32_t* rcs);
+int64_t tgo_link_generation(void* o, uint32_t peer);
 int tgo_submit(void* o, const tgsim_pkt* pkts, size_t n);
 int tgo_gen_storm(void* o, double lambda, uint32_t n_ticks);
 int tgo_step(void* o, uint32_t n_ticks);

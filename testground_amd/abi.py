@@ -121,7 +121,7 @@ assert C.sizeof(Gossip) == 24 and C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56
 # Every symbol include/tgsim.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "tgsim_create", "tgsim_destroy", "tgsim_last_error", "tgsim_abi_version", "tgsim_configure",
-    "tgsim_configure_batch",
+    "tgsim_configure_batch", "tgsim_link_generation",
     "tgsim_submit", "tgsim_gen_storm", "tgsim_step", "tgsim_step_sim", "tgsim_deliver",
     "tgsim_deliver_async", "tgsim_wait_event", "tgsim_sync", "tgsim_step_sim_launch", "tgsim_step_sim_finish",
     "tgsim_step_sim_counts", "tgsim_delivery_event", "tgsim_step_sim_launch_slotted", "tgsim_step_sim_release",
@@ -132,6 +132,7 @@ EXPORTS = [
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
     "tgsim_bridge_create", "tgsim_bridge_destroy", "tgsim_bridge_send", "tgsim_bridge_step",
     "tgsim_bridge_recv", "tgsim_bridge_pending", "tgsim_bridge_in_flight", "tgsim_bridge_now_tick",
+    "tgsim_bridge_link_removed",
     "tgsim_udp_front_create", "tgsim_udp_front_port", "tgsim_udp_front_register",
     "tgsim_udp_front_pump", "tgsim_udp_front_destroy",
 ]
@@ -153,6 +154,7 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("last_error", C.c_char_p, vp)
     f("configure", C.c_int, vp, C.c_uint32, C.POINTER(Config))
     f("configure_batch", C.c_int64, vp, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+    f("link_generation", C.c_int64, vp, C.c_uint32)
     f("submit", C.c_int, vp, C.c_void_p, C.c_size_t)
     f("gen_storm", C.c_int, vp, C.c_double, C.c_uint32)
     f("step", C.c_int, vp, C.c_uint32)

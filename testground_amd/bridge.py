@@ -68,6 +68,7 @@ class PacketBridge:
         self._pending: List[Tuple[int, int, int, int, int]] = []  # src, dst, seq, len, absolute tick
         self._payload: Dict[Tuple[int, int], bytes] = {}  # (src, seq) -> bytes, until delivered or dropped
         self._copies: Dict[Tuple[int, int], int] = {}     # deliveries still possible per packet
+        self._dst: Dict[Tuple[int, int], int] = {}        # destination of each packet in flight
         self.inbox: List[Deque[Tuple[int, int, int, bytes, int]]] = [deque() for _ in range(n_peers)]
         self.verdicts: List[np.ndarray] = []
 
@@ -88,6 +89,7 @@ class PacketBridge:
         self._seq[src] += 1
         self._pending.append((src, dst, seq, len(data) + IP_UDP_HEADER, t))
         self._payload[(src, seq)] = bytes(data)
+        self._dst[(src, seq)] = dst
         return seq
 
     def step(self) -> int:
@@ -112,6 +114,7 @@ class PacketBridge:
                 self._copies[(src, seq)] = n
             else:  # dropped, filtered or queue-full: no copy will ever arrive
                 self._payload.pop((src, seq), None)
+                self._dst.pop((src, seq), None)
         d = self.engine.drain()
         for r in d:
             src, seq, flags = int(r["src"]), int(r["seq"]), int(r["flags"])
@@ -126,7 +129,20 @@ class PacketBridge:
             else:
                 del self._copies[(src, seq)]
                 del self._payload[(src, seq)]
+                del self._dst[(src, seq)]
         return len(d)
+
+    def link_removed(self, peer: int) -> int:
+        """peer's data link was removed (engine.link_generation changed after a ConfigureNetwork):
+        the packets already handed to the engine that peer sent, or that were addressed to it, are
+        flushed or purged by the engine without a delivery (docker_network.go:65-88), so they are
+        resolved as lost here.  Packets due in a later window stay queued.  Returns the count."""
+        gone = [k for k in self._copies if k[0] == peer or self._dst[k] == peer]
+        for k in gone:
+            del self._copies[k]
+            del self._payload[k]
+            del self._dst[k]
+        return len(gone)
 
     def recv(self, peer: int) -> List[Tuple[int, int, int, bytes, int]]:
         """Everything delivered to peer so far: (t_ns, src, seq, payload, flags), in delivery order."""
@@ -165,6 +181,7 @@ def _declare_bridge(lib: C.CDLL) -> None:
             ("tgsim_bridge_pending", C.c_int64, [vp, C.c_uint32]),
             ("tgsim_bridge_in_flight", C.c_int64, [vp]),
             ("tgsim_bridge_now_tick", C.c_uint64, [vp]),
+            ("tgsim_bridge_link_removed", C.c_int64, [vp, C.c_uint32]),
             ("tgsim_udp_front_create", C.c_int, [vp, C.c_uint16, C.POINTER(vp)]),
             ("tgsim_udp_front_port", C.c_int, [vp]),
             ("tgsim_udp_front_register", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint16]),
@@ -271,6 +288,9 @@ class NativeBridge:
 
     def in_flight(self) -> int:
         return self._chk(self._lib.tgsim_bridge_in_flight(self._h), "tgsim_bridge_in_flight")
+
+    def link_removed(self, peer: int) -> int:
+        return self._chk(self._lib.tgsim_bridge_link_removed(self._h, peer), "tgsim_bridge_link_removed")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -52,7 +52,7 @@ struct Rec {
   uint32_t len;
   uint64_t off;
   uint32_t copies;     // deliveries still to come (0: not yet stepped)
-  uint32_t src, seq;
+  uint32_t src, seq, dst;
 };
 
 struct Msg {
@@ -238,7 +238,7 @@ int64_t tgsim_bridge_send(void* b, size_t n, const uint32_t* src, const uint32_t
       rid = static_cast<uint32_t>(B->recs.size());
       B->recs.emplace_back();
     }
-    B->recs[rid] = Rec{B->cur_chunk, len, base + (off[i] - off[0]), 0, s, seq};
+    B->recs[rid] = Rec{B->cur_chunk, len, base + (off[i] - off[0]), 0, s, seq, dst[i]};
     SeqWindow& w = B->seqwin[s];
     if (w.ids.empty()) w.base = seq;
     w.ids.push_back(rid);
@@ -370,6 +370,24 @@ int64_t tgsim_bridge_pending(void* b, uint32_t peer) {
 int64_t tgsim_bridge_in_flight(void* b) {
   Br* B = static_cast<Br*>(b);
   return B ? static_cast<int64_t>(B->in_flight) : -EINVAL;
+}
+
+int64_t tgsim_bridge_link_removed(void* b, uint32_t peer) {
+  Br* B = static_cast<Br*>(b);
+  if (!B || peer >= B->n) return -EINVAL;
+  // records awaiting a delivery (copies > 0) were handed to the engine and given a SCHEDULED
+  // verdict; the engine's flush (sender side) and purge (destination side) drop them silently
+  int64_t k = 0;
+  for (uint32_t rid = 0; rid < B->recs.size(); ++rid) {
+    Rec& r = B->recs[rid];
+    if (r.copies == 0 || (r.src != peer && r.dst != peer)) continue;
+    r.copies = 0;
+    const uint32_t ch = r.chunk;
+    resolve(B, rid);
+    chunk_release(B, ch);
+    ++k;
+  }
+  return k;
 }
 
 uint64_t tgsim_bridge_now_tick(void* b) {

@@ -246,6 +246,7 @@ struct tgsim_engine_s {
   std::vector<std::array<uint8_t, 16>> ip6;
   std::vector<uint8_t> k8s_init;                // K8sNetwork.initialized (k8s_network.go:119-125)
   std::vector<uint8_t> gone;                    // link removed since the last step (purge pending)
+  std::vector<uint32_t> link_gen;               // per peer: data links removed so far (tgsim_link_generation)
   bool any_gone = false;
   DevBuf<uint8_t> d_gone;
   std::vector<HostSrc> src;
@@ -403,6 +404,7 @@ void link_down(Eng* E, uint32_t peer) {
   }
   E->gone[peer] = 1;
   E->any_gone = true;
+  E->link_gen[peer]++;
   if (owns(E, peer)) {
     HostSrc& h = E->src[peer - E->o.shard_begin];
     h.patch_mask |= 16u;
@@ -670,7 +672,7 @@ int stage_host_input(Eng* E, uint32_t n_ticks) {
 }
 
 // Device exclusive scan of cnt[0..n) into off[0..n] (off[n] = total); returns total on host.
-int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev);
+int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev, const char* what);
 
 // Device exclusive scan of cnt[0..n) into off[0..n] (off[n] = total); returns total on host.  The
 // total (and *flag, when given) reach the host through pinned words the device publishes behind a
@@ -688,7 +690,7 @@ int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uin
   launch_publish(tot.p, flag, E->dm_pub, ++E->pub_seq, sq);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(E->ev_pub, sq));
-  int rc = wait_published(E, &E->h_pub[2], E->pub_seq, E->ev_pub);
+  int rc = wait_published(E, &E->h_pub[2], E->pub_seq, E->ev_pub, "traffic generation (scan total)");
   if (rc) return rc;
   *total = __atomic_load_n(&E->h_pub[0], __ATOMIC_ACQUIRE);
   if (flag_out) *flag_out = static_cast<uint32_t>(__atomic_load_n(&E->h_pub[1], __ATOMIC_ACQUIRE));
@@ -960,14 +962,14 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
 
 // Spins until the device publishes `want` into the pinned word (kernels release it at system
 // scope); `ev`, recorded after the publishing kernel, tells a fault from a slow step.
-int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev) {
+int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev, const char* what) {
   for (uint32_t it = 1;; ++it) {
     if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == want) return 0;
     if ((it & 255) == 0) {
       const hipError_t q = hipEventQuery(ev);
       if (q == hipSuccess) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == want) return 0;
-        return E->fail(-EIO, "route: step finished without publishing its edges");
+        return E->fail(-EIO, "%s: the device finished without publishing its result", what);
       }
       if (q != hipErrorNotReady) HIPCHK(q);
       std::this_thread::yield();
@@ -983,7 +985,7 @@ int route_finish(Eng* E, uint64_t* counts, bool wait_deliveries = true) {
   const uint32_t k = E->route_head;
   E->route_head = (k + 1) % Eng::kRouteSlots;
   E->route_n--;
-  int rc = wait_published(E, &E->h_edges[16 * k + 15], E->route_seq[k], E->ev_route[k]);
+  int rc = wait_published(E, &E->h_edges[16 * k + 15], E->route_seq[k], E->ev_route[k], "route (per-rank edges)");
   if (rc) return rc;
   if (wait_deliveries) HIPCHK(hipEventSynchronize(E->ev_dst));
   const uint32_t n_ranks = E->route_ranks[k];
@@ -1521,6 +1523,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->ip6.resize(E->N);
   E->k8s_init.assign(E->N, 0);
   E->gone.assign(E->N, 0);
+  E->link_gen.assign(E->N, 0);
   E->ip.resize(E->N);
   for (uint32_t i = 0; i < E->N; ++i) E->ip[i] = E->o.subnet_base + 2 + i;
   E->src.resize(E->S);
@@ -2017,6 +2020,12 @@ int tgsim_step_n(void* e, uint32_t n_ticks, uint32_t n_steps) {
   return 0;
 }
 
+int64_t tgsim_link_generation(void* e, uint32_t peer) {
+  Eng* E = as_eng(e);
+  if (!E || peer >= E->N) return -EINVAL;
+  return E->link_gen[peer];
+}
+
 int64_t tgsim_drain(void* e, tgsim_delivery* out, size_t cap) {
   Eng* E = as_eng(e);
   if (!E || (!out && cap)) return -EINVAL;
@@ -2107,7 +2116,7 @@ int tgsim_signal_async(void* e, uint32_t state, uint32_t n) {
 // Waits until every signal issued so far has landed in the pinned words (no device call).
 static int signals_landed(Eng* E) {
   if (!E->sig_seq) return 0;
-  return wait_published(E, &E->h_sig[1], E->sig_seq, E->ev_sig);
+  return wait_published(E, &E->h_sig[1], E->sig_seq, E->ev_sig, "sync signal");
 }
 
 int64_t tgsim_signal(void* e, uint32_t state, uint32_t n) {

@@ -73,6 +73,7 @@ class CABIEngine:
         o.subnet_base = subnet_base
         o.device = device
         self.n_peers = n_peers
+        self.subnet_base = subnet_base or (16 << 24)  # the engine's default data network, 16.0.0.0
         self.shard = (shard[0], shard[1] if shard[1] else n_peers) if shard != (0, 0) else (0, n_peers)
         self.tick_ns = tick_ns
         h = C.c_void_p()
@@ -130,6 +131,10 @@ class CABIEngine:
             i = int(np.nonzero(rcs)[0][0])
             self._check(int(rcs[i]), f"configure_batch: peer {int(peers[i])} (and {failed - 1} more)")
 
+    def link_generation(self, peer: int) -> int:
+        """How many times peer's data link has been removed (disconnect or re-addressing)."""
+        return self._check(self._fn("link_generation")(self._h, peer), "link_generation")
+
     # -- data path -----------------------------------------------------------------------------
     def submit(self, pkts: np.ndarray) -> None:
         pkts = np.ascontiguousarray(pkts, dtype=abi.PKT_DTYPE)
@@ -157,7 +162,7 @@ class CABIEngine:
         self._check(self._fn("step")(self._h, n_ticks), "step")
 
     def step_n(self, n_ticks: int, n_steps: int) -> None:
-        """n_steps windows of n_ticks (tgsim_step_n: generated windows run fused, up to four per launch)."""
+        """n_steps windows of n_ticks (tgsim_step_n: generated windows run fused, up to eight per launch)."""
         self._check(self._fn("step_n")(self._h, n_ticks, n_steps), "step_n")
 
     def step_sim(self, n_ticks: int, bounds: Sequence[int], d_out: int, out_cap: int) -> np.ndarray:

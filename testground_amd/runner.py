@@ -39,7 +39,7 @@ import time
 from typing import Callable, Dict, List, Optional, Tuple
 
 from .bridge import NativeBridge, PacketBridge
-from .engine import LIB_PATH
+from .engine import LIB_PATH, EngineError
 from .sidecar import Context, NetClient, SimReactor, SyncClient, handler
 
 OUTCOME_UNKNOWN = "unknown"     # pkg/task/task.go:25-28
@@ -141,11 +141,17 @@ class LocalSimRunnerCfg:
 
 
 def _make_bridge(engine, n: int, cfg):
-    """The native bridge (libtgsim's tgsim_bridge_*) whenever the library loads: always with the HIP
-    engine, which needs it anyway; the Python PacketBridge only for an engine_factory engine on a
-    host where libtgsim.so has not been built."""
-    if cfg.engine_factory is None or LIB_PATH.exists():
+    """The native bridge (libtgsim's tgsim_bridge_*): always with the HIP engine, which needs the
+    library anyway (a failure to load it is the run's failure).  An engine_factory engine (the
+    oracle in the CPU tests) falls back to the Python PacketBridge when libtgsim.so is absent or
+    cannot be loaded on this host (no HIP runtime)."""
+    if cfg.engine_factory is None:
         return NativeBridge(engine, n, cfg.window_ticks, cfg.tick_ns)
+    if LIB_PATH.exists():
+        try:
+            return NativeBridge(engine, n, cfg.window_ticks, cfg.tick_ns)
+        except (OSError, AttributeError, EngineError):
+            pass
     return PacketBridge(engine, n, cfg.window_ticks, cfg.tick_ns)
 
 
@@ -411,6 +417,7 @@ class LocalSimRunner:
         reactor = SimReactor(engine, n)
         sync_client = reactor.Client
         bridge = _make_bridge(engine, n, cfg)
+        reactor.on_link_removed(bridge.link_removed)
         clock = _Clock(bridge, reactor.lock, n, run_ctx, cfg.max_sim_ns)
         run_dir = os.path.join(self._outputs_dir(cfg), job.TestPlan, job.RunID)
         threads: List[threading.Thread] = []
@@ -505,8 +512,8 @@ class LocalSimRunner:
             return (HEALTH_OK, d) if os.path.isdir(d) else (HEALTH_FAILED, f"{d} does not exist")
 
         def library():
-            if cfg.engine_factory is not None:  # the run will not load libtgsim.so
-                return HEALTH_OMITTED, "engine_factory configured"
+            if cfg.engine_factory is not None:  # the run falls back to the Python bridge without it
+                return HEALTH_OMITTED, "engine_factory configured (libtgsim.so optional)"
             from .engine import load_library
             try:
                 load_library()

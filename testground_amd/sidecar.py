@@ -252,10 +252,14 @@ class SimNetwork(Network):
     applies DockerNetwork.ConfigureNetwork's order of operations and errors (docker_network.go:51-148);
     the config is copied into engine state and never mutated (sidecar_test.go:91-92)."""
 
-    def __init__(self, engine, peer: int, lock: threading.Lock):
+    def __init__(self, engine, peer: int, lock: threading.Lock,
+                 on_link_removed: Optional[Callable[[int], None]] = None):
         self.engine = engine
         self.peer = peer
         self.lock = lock
+        # called (under the lock) when a config removed the data link: the packet bridge then
+        # resolves the packets the engine flushed or purged with it (tgsim_bridge_link_removed)
+        self.on_link_removed = on_link_removed
         self.active: Dict[str, bool] = {DEFAULT_DATA_NETWORK: True}
         self.closed = False
 
@@ -263,7 +267,10 @@ class SimNetwork(Network):
         if self.closed:
             raise RuntimeError("network is closed")
         with self.lock:
+            gen = self.engine.link_generation(self.peer) if self.on_link_removed else 0
             self.engine.configure(self.peer, cfg)
+            if self.on_link_removed and self.engine.link_generation(self.peer) != gen:
+                self.on_link_removed(self.peer)
         self.active[cfg.Network] = bool(cfg.Enable)
 
     def ListActive(self) -> List[str]:
@@ -366,6 +373,11 @@ class SimReactor(Reactor):
             t = threading.Thread(target=run, args=(p,), daemon=True)
             t.start()
             self.threads.append(t)
+
+    def on_link_removed(self, fn: Callable[[int], None]) -> None:
+        """Routes every instance's link removals to fn (the runner's packet bridge)."""
+        for nw in self.networks:
+            nw.on_link_removed = fn
 
     def net_client(self, peer: int) -> NetClient:
         import ipaddress

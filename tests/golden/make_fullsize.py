@@ -1,0 +1,143 @@
+"""Full-size golden digests of BASELINE.json configs[2..4], generated with the CPU oracle.
+
+At BASELINE's full sizes the delivered records run to hundreds of megabytes per window, too much to
+commit; what is committed (tests/golden/fullsize_<config>.json, a few tens of KB each) is, per window,
+the SHA-256 of the verdict bytes, the SHA-256 of the drain-ordered delivery records, their counts
+and the engine statistics.  The oracle (oracle/tgoracle.c, single thread) runs each configuration
+exactly as the bench drives the HIP engine (bench.py run_workload), through the same driver
+functions below, so tests/test_gpu_fullsize_digests.py can run the HIP path the bench runs and
+compare digest by digest:
+
+  c3  storm, 10,000 instances, lambda 0.5, 2,000-tick windows (configs[2]): the bench's 120 ms
+      settle as 60 single windows (k_sim), then two groups of eight generated windows in one
+      tgsim_step_n call each (k_sim_fused, one digest per group: its deliveries in window order,
+      the last window's verdicts, the statistics);
+  c4  gossip flood, 1,000,000 peers, 64 floods 1,000 ticks apart, degree 8, 1 KiB, 5,000-tick
+      windows (configs[3]): two empty windows, then the 70 windows the bench times;
+  c5  epochs, 100,000 instances, lambda 0.2, 1,000-tick epochs, 10 % reshaped per epoch and a
+      barrier per epoch (configs[4]): six epochs.
+
+    python tests/golden/make_fullsize.py [--only c3,c4,c5]   # rewrites the entries it runs
+
+The oracle takes about 1 min (c5), 1-2 min (c3) and a few minutes (c4) on one core here.
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+
+from testground_amd import workloads as wl  # noqa: E402
+
+HERE = Path(__file__).resolve().parent
+
+STAT_KEYS = ("offered", "scheduled", "cloned", "corrupted", "bytes_scheduled", "now_tick", "queue_state_bytes",
+             "flushed", "lost_in_flight")
+
+# configs[2..4] as the bench runs them (bench.py parse/run_workload)
+C3 = dict(peers=10_000, lam=0.5, window=2000, settle=60, groups=2, group=8)
+C4 = dict(peers=1_000_000, floods=64, gap=1000, degree=8, msg_len=1024, window=5000, empty=2, windows=70)
+C5 = dict(peers=100_000, epochs=6)
+
+
+def stats_list(st):
+    return [int(st[k]) for k in STAT_KEYS] + [int(st["by_verdict"][k]) for k in sorted(st["by_verdict"])]
+
+
+def digest(eng):
+    """One digest entry for the engine's last step: verdicts, every pending delivery (drain order),
+    statistics."""
+    v = eng.verdicts()
+    d = eng.drain()
+    return {"n_verdicts": int(len(v)), "verdicts": hashlib.sha256(v.tobytes()).hexdigest(),
+            "n_deliveries": int(len(d)), "deliveries": hashlib.sha256(d.tobytes()).hexdigest(),
+            "stats": stats_list(eng.stats())}
+
+
+def run_c3(eng, sink):
+    c = C3
+    wl.configure_storm(eng, c["peers"])
+    for k in range(c["settle"]):
+        eng.gen_storm(c["lam"], c["window"])
+        eng.step(c["window"])
+        sink(f"window {k}", digest(eng))
+    for g in range(c["groups"]):
+        for _ in range(c["group"]):
+            eng.gen_storm(c["lam"], c["window"])
+        eng.step_n(c["window"], c["group"])
+        sink(f"fused group {g}", digest(eng))
+
+
+def run_c4(eng, sink):
+    c = C4
+    wl.configure_gossip(eng, c["peers"])
+    for _ in range(c["empty"]):
+        eng.step(c["window"])
+    eng.drain()
+    eng.gossip_init(n_floods=c["floods"], degree=c["degree"], msg_len=c["msg_len"], start_gap_ticks=c["gap"])
+    for k in range(c["windows"]):
+        eng.gen_gossip(c["window"])
+        eng.step(c["window"])
+        sink(f"window {k}", digest(eng))
+    sink("reached", {"reached": [int(x) for x in eng.gossip_reached()]})
+
+
+def run_c5(eng, sink):
+    c = C5
+    wl.configure_storm(eng, c["peers"])
+    for k in range(c["epochs"]):
+        wl.run_epoch(eng, c["peers"], k, c["peers"])
+        sink(f"epoch {k}", digest(eng))
+
+
+RUNS = {"c3": (run_c3, C3, {}), "c4": (run_c4, C4, {"lookahead_ns": wl.GOSSIP_MIN_LAT}), "c5": (run_c5, C5, {})}
+
+
+def engine_kwargs(name):
+    return dict(RUNS[name][2])
+
+
+def fixture(name):
+    return HERE / f"fullsize_{name}.json"
+
+
+def load(name):
+    return json.loads(fixture(name).read_text())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="c3,c4,c5")
+    a = ap.parse_args()
+    from testground_amd import abi
+    from testground_amd.build import build_oracle
+    from testground_amd.engine import CABIEngine
+
+    lib = ctypes.CDLL(str(build_oracle()))
+    abi.declare(lib, "tgo_")
+    for name in a.only.split(","):
+        fn, cfg, kw = RUNS[name]
+        eng = CABIEngine(lib, "tgo_", cfg["peers"], **kw)
+        entries = []
+        t0 = time.perf_counter()
+
+        def sink(label, d):
+            entries.append(dict(label=label, **d))
+            print(f"{name} {label} {d.get('n_verdicts', '')} {d.get('n_deliveries', '')} "
+                  f"{time.perf_counter() - t0:.0f}s", flush=True)
+
+        fn(eng, sink)
+        eng.close()
+        fx = {"config": cfg, "engine": kw, "oracle_seconds": round(time.perf_counter() - t0, 1), "entries": entries}
+        fixture(name).write_text(json.dumps(fx, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()

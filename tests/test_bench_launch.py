@@ -2,7 +2,6 @@
 command it builds, and a real two-rank launch on CPU that stops before any GPU call."""
 import json
 import os
-import re
 import subprocess
 import sys
 from pathlib import Path
@@ -33,9 +32,15 @@ def test_two_ranks_spawned_on_cpu():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--launch-check"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(x) for x in re.findall(r"\{[^{}]*\}", r.stdout)]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert sorted(x["rank"] for x in lines) == [0, 1]
     assert all(x["world"] == 2 and x["gpus"] == 2 and x["launched_by_bench"] for x in lines)
+    # the headline at N = 2 is BASELINE configs[2] itself: 10,000 instances in total, split over the
+    # ranks; the weak-scaling run and the 1M-peer flood ride along
+    for x in lines:
+        h = x["headline"]
+        assert h["peers_total"] == 10_000 and h["bounds"] == [0, 5000, 10_000] and h["scaling"] == "strong"
+        assert h["weak_per_gpu_peers_total"] == 20_000 and h["at_1M_peers_total"] == 1_000_000
 
 
 def test_world_mismatch_fails():

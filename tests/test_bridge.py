@@ -260,3 +260,62 @@ def test_native_bridge_gpu_equals_oracle(make_oracle):
         assert bn.step() == bp.step()
     for peer in range(n):
         assert bn.recv(peer) == bp.recv(peer)
+
+
+@native
+def test_bridge_link_removal_resolves_queued_packets(make_oracle):
+    """a scheduled datagram can vanish inside the engine when a link goes away: its
+    sender is disconnected (the netem queue is flushed, docker_network.go:65-75) or its destination
+    is re-addressed (in-flight packets find no port, :77-88).  The sidecar's SimNetwork sees the
+    engine's link generation change and tells the bridge, which resolves exactly those datagrams:
+    after draining, nothing is left in flight, on the C++ bridge and on the Python one, and both
+    delivered the same datagrams."""
+    import ipaddress
+
+    from testground_amd.bridge import NativeBridge
+    from testground_amd.sidecar import Context, SimNetwork
+    import threading
+
+    n = 6
+    shape = nw.LinkShape(Latency=20 * nw.Millisecond, Jitter=5 * nw.Millisecond, Loss=5.0, Duplicate=20.0,
+                         Bandwidth=10**7)
+    engines = [make_oracle(n, lookahead_ns=WINDOW * 1000, queue_limit=256) for _ in range(2)]
+    for e in engines:
+        for i in range(n):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=shape))
+    bp, bn = PacketBridge(engines[0], n, WINDOW), NativeBridge(engines[1], n, WINDOW)
+    nets = [[SimNetwork(e, p, threading.Lock(), on_link_removed=b.link_removed) for p in range(n)]
+            for e, b in ((engines[0], bp), (engines[1], bn))]
+    rng = np.random.default_rng(3)
+    ctx = Context()
+    for w in range(16):
+        k = 60
+        src = rng.integers(0, n, k)
+        dst = (src + 1 + rng.integers(0, n - 1, k)) % n
+        off = np.concatenate([[0], np.cumsum(rng.integers(1, 300, k))]).astype(np.uint64)
+        data = rng.bytes(int(off[-1]))
+        ticks = bp.now_tick + rng.integers(0, 3 * WINDOW, k)
+        bn.send_many(src, dst, data, off, ticks)
+        for i, (s, d) in enumerate(zip(src, dst)):
+            bp.send(int(s), int(d), data[int(off[i]):int(off[i + 1])], at_tick=int(ticks[i]))
+        if w == 6:  # peer 2 disconnects with its queue full of traffic
+            for ns in nets:
+                ns[2].ConfigureNetwork(ctx, nw.Config(Network="default", Enable=False))
+        if w == 9:  # peer 4 moves to a new address while traffic towards it is queued everywhere
+            ip = (str(ipaddress.IPv4Address((16 << 24) + 0x100 + 4)), 8)
+            for ns in nets:
+                ns[4].ConfigureNetwork(ctx, nw.Config(Network="default", Enable=True, IPv4=ip, Default=shape))
+        if w == 12:  # peer 2 comes back
+            for ns in nets:
+                ns[2].ConfigureNetwork(ctx, nw.Config(Network="default", Enable=True, Default=shape))
+        assert bp.step() == bn.step()
+    for _ in range(40):
+        bp.step()
+        bn.step()
+    for e in engines:
+        st = e.stats()
+        assert st["flushed"] > 0 and st["lost_in_flight"] > 0, st  # the scenario removed queued packets
+        assert e.link_generation(2) == 1 and e.link_generation(4) == 1 and e.link_generation(0) == 0
+    for peer in range(n):
+        assert bp.recv(peer) == bn.recv(peer)
+    assert bp.in_flight() == bn.in_flight() == 0

@@ -43,3 +43,27 @@ def test_engine_reproduces_golden(name):
 
     case, _ = make_golden.load(name)
     _check(Engine(case["n"], queue_limit=case["queue_limit"], lookahead_ns=case["lookahead_ns"]), name)
+
+
+def test_oracle_reproduces_fullsize_c5_prefix(make_oracle):
+    """The committed full-size digests (tests/golden/fullsize_*.json, checked against the HIP engine
+    by tests/test_gpu_fullsize_digests.py) still describe the current oracle: its first two C5
+    epochs at 100,000 instances (about 40 M packets) reproduce their digests."""
+    import make_fullsize as mf
+
+    fx = mf.load("c5")
+    entries = iter(fx["entries"][:2])
+
+    class Stop(Exception):
+        pass
+
+    def sink(label, got):
+        want = next(entries, None)
+        if want is None:
+            raise Stop
+        assert want["label"] == label
+        for key in ("n_verdicts", "verdicts", "n_deliveries", "deliveries", "stats"):
+            assert got[key] == want[key], f"c5 {label}: {key}"
+
+    with pytest.raises(Stop):
+        mf.run_c5(make_oracle(mf.C5["peers"]), sink)
