@@ -43,9 +43,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 
 # Algorithmic HBM bytes of k_sim: per offered packet 16 B record read + 1 B verdict
 # write; per scheduled record 24 B delivery write; per source 64 B params + 32 B state read + 32 B
-# state write + 16 B CSR offsets + 4 B emit count; plus the netem queue state each source carries
-# across steps (16 B per queued item, 8 B per departing item, loaded at step start and stored at
-# step end: the engine's queue_state_bytes counter).
+# state write + 16 B CSR offsets + 4 B emit count; plus the netem queue state the kernel actually
+# carries between windows through HBM (16 B per queued item, 8 B per departing item, loaded and
+# stored once per fused group: tgsim_debug_carry_bytes), reported apart as carry_bytes.  The r02
+# basis charged the per-window model of that carry (queue_state_bytes: a load and a store at every
+# window), which rewards re-streaming; it is kept as frac_modeled_restream.
 B_OFFERED, B_SCHEDULED, B_SOURCE = 17, 24, 148
 REC = 24  # sizeof(tgsim_delivery), the record an exchange moves
 
@@ -396,9 +398,9 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     else:
         eng.configure_batch(np.arange(peers_total), configs_array(np.full(peers_total, 5_000_000), routing_policy=2))
     stepper = None
-    if sharded:
-        from testground_amd.shard import ShardedStepper
-        stepper = ShardedStepper(eng, bounds, device=f"cuda:{local}")
+    if sharded:  # the engine's own RCCL exchange (tgsim_comm_*), as a Go host would drive it
+        from testground_amd.shard import CommStepper
+        stepper = CommStepper(eng, bounds, device=f"cuda:{local}")
     step = eng.step if stepper is None else stepper.step
     epoch = [0]
 
@@ -442,29 +444,29 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
             eng.gen_storm(lam, window)  # inputs resident in HBM before the timed region
 
     def run_steps(n):
-        if stepper is not None and workload == "storm":  # pre-generated: simulate one step ahead
+        if stepper is not None and workload == "storm" and a.exact_exchange:
+            for _ in range(n):
+                stepper.step(window)
+        elif stepper is not None and workload == "storm":  # pre-generated: simulate one step ahead
             # slotted exchange: groups of TGSIM_SHARD_FUSE (4) windows per launch and per all-to-all
             # (A/B at one rank: 1 27.5, 4 30.4, 8 27.7-28.6 G pkt/s: larger groups lengthen the
             # pipeline drain); TGSIM_FUSE is the single engine's group size (default 8, tgsim_step_n)
-            stepper.run(n, window, fuse=1 if a.exact_exchange else int(os.environ.get("TGSIM_SHARD_FUSE", "4")))
+            stepper.run(n, window, fuse=int(os.environ.get("TGSIM_SHARD_FUSE", "4")))
         elif workload == "storm":  # pre-generated windows, up to TGSIM_FUSE (8) per launch (tgsim_step_n)
             eng.step_n(window, n)
         else:
             for _ in range(n):
                 one_step()
 
-    if stepper is not None and workload == "storm" and not a.exact_exchange:
-        # fixed-size exchange for the pipelined run: per-rank chunks sized from the largest count
-        # the settle steps exchanged (max over ranks) plus a margin; an overflow fails the run
-        m = torch.tensor([stepper.max_count], dtype=torch.int64, device=f"cuda:{local}")
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        stepper.slot_cap = int(int(m.item()) * 1.25) + 4096
+    # the pipelined run's fixed-size chunks are sized by the engine from the largest per-rank count
+    # the settle windows exchanged (max over ranks, x1.25 + 4096); an overflow fails the run
     run_steps(warmup)
     eng.drain()
     setup_s = time.perf_counter() - t_setup
     s0 = eng.stats()
     x0 = stepper.exchanged_records if stepper is not None else 0
     eng.sim_kernel_ms(reset=True)
+    c0 = eng.carry_bytes()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -502,13 +504,18 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
                  "reached_min_frac": float(reached.min()) / peers_total,
                  "sim_ms_covered": (warmup + steps) * window / 1000}
     qbytes = s1["queue_state_bytes"] - s0["queue_state_bytes"]
+    carry = eng.carry_bytes() - c0
     slot_cap = stepper.slot_cap if stepper is not None else None
     eng.close()
     del eng, stepper
     if rank != 0:
         return None
-    per_launch = (B_OFFERED * offered + B_SCHEDULED * scheduled + qbytes) / max(1, steps) + B_SOURCE * peers
-    achieved = per_launch / (sim_ms * 1e-3) / 1e9 if sim_ms > 0 else None
+    base = (B_OFFERED * offered + B_SCHEDULED * scheduled) / max(1, steps) + B_SOURCE * peers
+    carry_w, model_w = carry / max(1, steps), qbytes / max(1, steps)
+    per_launch = base + carry_w
+    gbs = (lambda b: b / (sim_ms * 1e-3) / 1e9) if sim_ms > 0 else (lambda b: None)
+    achieved = gbs(per_launch)
+    frac_of = lambda b: (gbs(b) / HBM_PEAK_GBS) if sim_ms > 0 else None  # noqa: E731
     traffic, traffic_src = load_pmc(workload, window, peers, lam, a.shapes)
     tot_v = max(1.0, float(verd_all.sum()))
     res = {
@@ -543,7 +550,10 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
                      "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": per_launch, "kernel_ms_avg": sim_ms, "launches": n_launch,
+                     "algorithmic_bytes_per_launch": per_launch, "carry_bytes": carry_w,
+                     "frac_without_carry": frac_of(base), "queue_state_bytes_modeled": model_w,
+                     "frac_modeled_restream": frac_of(base + model_w),
+                     "kernel_ms_avg": sim_ms, "launches": n_launch,
                      "per": "window (one step of --window ticks; a fused dispatch counts each of its windows)"},
         "cpu_baseline": None,
     }

@@ -299,6 +299,52 @@ int64_t tgsim_pending_deliveries(void* engine);
 int64_t tgsim_verdicts(void* engine, uint8_t* out, size_t cap);
 int tgsim_stats(void* engine, tgsim_stats_t* out);
 
+/* ---- RCCL exchange owned by the engine ---------------------------------- */
+/* Replaces the cross-host delivery of the reference (weave CNI between k8s nodes,
+ * pkg/sidecar/k8s_network.go:266-314): peers are partitioned over one engine per GPU (one process
+ * per GPU), and scheduled records reach their destination's engine over RCCL (xGMI).  The engine
+ * owns the communicator, its exchange stream and every buffer; a host only calls these functions
+ * (INTEGRATION.md shows the Go loop).  librccl.so.1 is loaded on first use. */
+#define TGSIM_COMM_ID_BYTES 128
+/* A fresh communicator id (ncclGetUniqueId, 128 bytes into out_id).  One rank creates it and the
+ * host hands it to every rank (the Go runner: through the sync service). */
+int tgsim_comm_id(void* out_id);
+/* Joins `engine` to the run's exchange as `rank` of `nranks` (<= 8) engines, one per GPU.  The
+ * shards (tgsim_opts shard_begin/shard_end) must be contiguous in rank order and cover every peer;
+ * they are gathered here.  Collective: every rank calls it with the same id. */
+int tgsim_comm_init(void* engine, const void* id, int rank, int nranks);
+/* One window on every rank (collective): simulate the owned sources, route the scheduled records
+ * by destination shard, exchange the per-rank counts and then the records (grouped send/recv; the
+ * own shard's records never leave the GPU), deliver them beside the next window's simulation.  The
+ * host waits for this window's routing (one pinned-word poll) and for the count exchange: the
+ * closed-loop form (gossip forwards, epoch reshaping) of tgsim_step. */
+int tgsim_comm_step(void* engine, uint32_t n_ticks);
+/* tgsim_comm_step in two halves: _launch enqueues the window's simulation and routing and returns,
+ * so the host can stage the next window's ConfigureNetwork calls (they take effect at the next
+ * launch) while the window simulates; _finish exchanges and delivers it. */
+int tgsim_comm_launch(void* engine, uint32_t n_ticks);
+int tgsim_comm_finish(void* engine);
+/* n_steps pre-generated windows (tgsim_gen_storm) with the simulation two launches ahead of the
+ * exchange, in groups of up to `fuse` (<= 8) windows per launch and per exchange, each rank's
+ * records in fixed chunks of slot_cap records behind a count header (0: the largest per-rank count
+ * of the earlier tgsim_comm_step windows, max over ranks, x 1.25 + 4096; without such windows the
+ * bound of what one window can emit).  The host never waits for
+ * the device.  A chunk that would overflow fails the run with -ENOSPC (nothing is lost silently). */
+int tgsim_comm_run(void* engine, uint32_t n_ticks, uint32_t n_steps, uint32_t fuse, uint64_t slot_cap);
+/* SignalAndWait over the shards (sync-service Barrier, sidecar_handler.go:40-44): the counts of
+ * `state` are summed over the ranks by an all-reduce of the device counter tables; returns 1 when
+ * the sum >= target, else 0.  Collective. */
+int tgsim_comm_barrier(void* engine, uint32_t state, uint64_t target);
+typedef struct {
+    int32_t rank, nranks;
+    uint64_t exchanged_records; /* records (slotted: record slots) this rank has sent, self included */
+    uint64_t max_rank_count;    /* largest per-rank count a tgsim_comm_step window routed here */
+    uint64_t slot_cap;          /* chunk capacity of the last tgsim_comm_run                    */
+    uint32_t bounds[9];         /* rank r owns peers [bounds[r], bounds[r + 1])                 */
+    uint32_t _pad;
+} tgsim_comm_info_t;
+int tgsim_comm_info(void* engine, tgsim_comm_info_t* out);
+
 /* ---- gossip workload (C4) ------------------------------------------------------------------ */
 /* Arms the gossip driver: resets the per-peer receipt state of this shard and schedules the
  * floods whose origin it owns.  Requires lookahead_ns >= the window of every later step and
@@ -410,6 +456,11 @@ void* tgsim_stream(void* engine);
  * workgroup (s_memrealtime at its phase boundaries, batch count, HW_ID, queue sizes); copies them
  * for the last step and returns the word count (0 when disabled). */
 int64_t tgsim_debug_stamps(void* engine, uint64_t* out, size_t cap);
+/* Diagnostics: HBM bytes the simulate kernels actually moved carrying netem queues and departure
+ * rings between windows since the engine was created (loads + stores).  tgsim_stats_t's
+ * queue_state_bytes models one load and one store per window; a fused group (tgsim_step_n) keeps
+ * each source's queue in LDS across its windows and moves it once per group. */
+int64_t tgsim_debug_carry_bytes(void* engine);
 /* Diagnostics: windows simulated by fused launches (tgsim_step_n) since the engine was created. */
 int64_t tgsim_debug_fused_windows(void* engine);
 

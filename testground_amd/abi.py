@@ -104,6 +104,14 @@ class Gossip(C.Structure):
     ]
 
 
+class CommInfo(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("nranks", C.c_int32), ("exchanged_records", C.c_uint64),
+                ("max_rank_count", C.c_uint64), ("slot_cap", C.c_uint64), ("bounds", C.c_uint32 * 9),
+                ("_pad", C.c_uint32)]
+
+
+COMM_ID_BYTES = 128
+
 PKT_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"), ("len", "<u2"), ("tick", "<u2")])
 DELIVERY_DTYPE = np.dtype([("t_ns", "<u8"), ("src", "<u4"), ("dst", "<u4"), ("seq", "<u4"),
                            ("len", "<u2"), ("flags", "<u2")])
@@ -116,7 +124,7 @@ CONFIG_DTYPE = np.dtype([("network", "<u8"), ("enable", "u1"), ("routing_policy"
                          ("n_rules", "<u4"), ("_pad2", "<u4"), ("ipv6", "u1", (16,))])
 assert SHAPE_DTYPE.itemsize == 56 and CONFIG_DTYPE.itemsize == 104
 assert PKT_DTYPE.itemsize == 16 and DELIVERY_DTYPE.itemsize == 24
-assert C.sizeof(Gossip) == 24 and C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56 and C.sizeof(Config) == 104
+assert C.sizeof(CommInfo) == 72 and C.sizeof(Gossip) == 24 and C.sizeof(Opts) == 56 and C.sizeof(Shape) == 56 and C.sizeof(Config) == 104
 
 # Every symbol include/tgsim.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -128,8 +136,9 @@ EXPORTS = [
     "tgsim_deliver_slotted_async", "tgsim_step_sim_launch_slotted_n", "tgsim_deliver_slotted_n_async",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
-    "tgsim_debug_fused_windows", "tgsim_step_n",
+    "tgsim_debug_fused_windows", "tgsim_debug_carry_bytes", "tgsim_step_n",
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
+    "tgsim_comm_id", "tgsim_comm_init", "tgsim_comm_step", "tgsim_comm_launch", "tgsim_comm_finish", "tgsim_comm_run", "tgsim_comm_barrier", "tgsim_comm_info",
     "tgsim_bridge_create", "tgsim_bridge_destroy", "tgsim_bridge_send", "tgsim_bridge_step",
     "tgsim_bridge_recv", "tgsim_bridge_pending", "tgsim_bridge_in_flight", "tgsim_bridge_now_tick",
     "tgsim_bridge_link_removed",
@@ -188,9 +197,18 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("stream", vp, vp)
     f("debug_stamps", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("debug_fused_windows", C.c_int64, vp)
+    f("debug_carry_bytes", C.c_int64, vp)
     f("abi_version", C.c_uint32)
     f("gossip_init", C.c_int, vp, C.POINTER(Gossip))
     f("gen_gossip", C.c_int, vp, C.c_uint32)
     f("gossip_reached", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("offered", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("metrics", C.c_int64, vp, C.c_uint32, C.c_void_p, C.c_size_t)
+    f("comm_id", C.c_int, vp)
+    f("comm_init", C.c_int, vp, vp, C.c_int, C.c_int)
+    f("comm_step", C.c_int, vp, C.c_uint32)
+    f("comm_launch", C.c_int, vp, C.c_uint32)
+    f("comm_finish", C.c_int, vp)
+    f("comm_run", C.c_int, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64)
+    f("comm_barrier", C.c_int, vp, C.c_uint32, C.c_uint64)
+    f("comm_info", C.c_int, vp, C.POINTER(CommInfo))

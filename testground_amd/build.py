@@ -13,7 +13,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libtgsim.so"
-SOURCES = [CSRC / "tgsim_kernels.hip", CSRC / "tgsim_engine.cpp", CSRC / "tgsim_bridge.cpp"]
+SOURCES = [CSRC / "tgsim_kernels.hip", CSRC / "tgsim_engine.cpp", CSRC / "tgsim_bridge.cpp", CSRC / "tgsim_comm.cpp"]
 HEADERS = [CSRC / "tgsim_internal.h", CSRC / "tgsim_launch.h", ROOT / "include" / "tgsim.h"]
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "build" / "libtgoracle.so"

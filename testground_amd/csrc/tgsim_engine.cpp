@@ -328,11 +328,13 @@ struct tgsim_engine_s {
   hipEvent_t ev_fgrp[2] = {};
   uint32_t fgrp = 0;                    // parity of the next fused group
   DevBuf<uint8_t> f_verdict[kFuseMax];  // verdicts of a group's windows but the last (discarded)
-  DevBuf<uint32_t> d_done, d_ticket;    // per-source completion words, ticket counter
-  uint32_t step_no = 0, ticket_no = 0;  // windows and tickets issued by fused launches so far
+  DevBuf<uint32_t> d_ticket;            // ticket counter of the fused launches
+  uint32_t ticket_no = 0;               // tickets issued by fused launches so far
   uint64_t fused_windows = 0;
   uint32_t fused_wgs = 0;
   bool persist_routed = false;  // TGSIM_FUSED_PERSIST: persistent grid for sharded (routed) groups too
+  bool persist_env = false;     // TGSIM_FUSED_PERSIST was set (the comm layer keeps its choice)
+  CommSlot comm{};              // tgsim_comm_init's exchange state (tgsim_comm.cpp)
   uint32_t prio_heavy = 512;  // TGSIM_PRIO_HEAVY: heaviest sources of a fused launch at wave priority 3 (A/B: 128 +1 %, 512 +7.5 %, 2048 +7 %, 4096 +5 %)  // k_sim_fused's persistent grid (resident workgroups), at the first launch
   int fuse_max = 8;  // TGSIM_FUSE: windows per fused launch, up to kFuseMax (1: never fuse; A/B at 30 windows: 4 34.8, 8 36.3, 16 36.3 G pkt/s)
   DevBuf<uint64_t> d_stamps;
@@ -734,8 +736,6 @@ int harvest_timing(Eng* E, bool wait) {
 int check_sim_error(Eng* E) {
   const uint64_t herr = E->h_err ? __atomic_load_n(E->h_err, __ATOMIC_RELAXED) : 0;
   if (herr & kErrTimeOverflow) return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
-  if (herr & kErrHandoff)
-    return E->fail(-EIO, "fused step: a source's previous window did not complete (hand-off timed out)");
   if (E->h_xerr && __atomic_load_n(E->h_xerr, __ATOMIC_RELAXED))
     return E->fail(-ENOSPC, "exchange: a step's records for one rank exceed the slot capacity");
   return 0;
@@ -1217,12 +1217,10 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   E->gen_q.erase(E->gen_q.begin(), E->gen_q.begin() + g);
   E->gen_q_ticks -= static_cast<uint64_t>(g) * n_ticks;
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_fgrp[p], 0));  // the deliveries that last read set p
-  if (E->d_done.cap < E->S) {
-    HIPCHK(E->d_done.ensure(E->S));
-    HIPCHK(hipMemsetAsync(E->d_done.p, 0, sizeof(uint32_t) * E->d_done.cap, E->st));
+  if (!E->d_ticket.cap) {
     HIPCHK(E->d_ticket.ensure(1));
     HIPCHK(hipMemsetAsync(E->d_ticket.p, 0, sizeof(uint32_t), E->st));
-    E->step_no = E->ticket_no = 0;
+    E->ticket_no = 0;
   }
   SimArgs a = base_sim_args(E);
   const bool ordered = E->S <= kOrderMaxSources;
@@ -1267,17 +1265,15 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
               t0, t0 + n_ticks * E->o.tick_ns + E->o.lookahead_ns};
   }
   a.stamps = nullptr;
-  if (E->stamps_on) {  // diagnostics: one stamp row per ticket (window-major)
+  if (E->stamps_on) {  // diagnostics: one stamp row per (window, dispatch position), window-major
     HIPCHK(E->d_stamps.ensure(static_cast<size_t>(g) * E->S * kStampSlots));
     a.stamps = E->d_stamps.p;
     E->n_stamp_wg = static_cast<uint64_t>(g) * E->S;
   }
   f.n_win = g;
   f.prio_n = a.order ? E->prio_heavy : 0;
-  f.step_base = E->step_no;
   f.ticket_base = E->ticket_no;
   f.ticket = E->d_ticket.p;
-  f.done = E->d_done.p;
   hipEvent_t ev0, ev1;
   HIPCHK(take_event(E, &ev0));
   HIPCHK(take_event(E, &ev1));
@@ -1293,10 +1289,9 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.push_back({ev0, ev1, g});
-  E->step_no += g;
-  // every workgroup of the persistent grid claims until a claim fails: the counter advances by
-  // the tickets plus one failed claim per workgroup (one claim per ticket otherwise)
-  E->ticket_no += g * E->S + (f.persistent ? std::min(E->fused_wgs, g * E->S) : 0u);
+  // one ticket per source; every workgroup of the persistent grid claims until a claim fails, so the
+  // counter advances by the tickets plus one failed claim per workgroup (one claim per ticket otherwise)
+  E->ticket_no += E->S + (f.persistent ? std::min(E->fused_wgs, E->S) : 0u);
   E->fused_windows += g;
   if (ordered) {  // the next launch's dispatch order, from the last window's HTB records
     HIPCHK(E->d_order.ensure(E->S));
@@ -1405,6 +1400,24 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
 
 Eng* as_eng(void* e) { return static_cast<Eng*>(e); }
 
+}  // namespace
+
+namespace tgsim {
+CommSlot* engine_comm_slot(void* e) { return e ? &as_eng(e)->comm : nullptr; }
+int engine_device(void* e) { return as_eng(e)->dev; }
+uint32_t engine_peers(void* e) { return as_eng(e)->N; }
+void engine_shard(void* e, uint32_t* begin, uint32_t* end) {
+  *begin = as_eng(e)->o.shard_begin;
+  *end = as_eng(e)->o.shard_end;
+}
+int engine_fail(void* e, int code, const char* msg) { return as_eng(e)->fail(code, "%s", msg); }
+void engine_persist_routed(void* e, bool on) {
+  if (!as_eng(e)->persist_env) as_eng(e)->persist_routed = on;
+}
+}  // namespace tgsim
+
+namespace {
+
 
 }  // namespace
 
@@ -1511,7 +1524,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
-  if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) E->persist_routed = atoi(fp) != 0;
+  if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) {
+    E->persist_routed = atoi(fp) != 0;
+    E->persist_env = true;
+  }
   if (const char* ph = getenv("TGSIM_PRIO_HEAVY")) E->prio_heavy = static_cast<uint32_t>(atoi(ph));
   if (const char* fz = getenv("TGSIM_FUSE")) E->fuse_max = std::max(1, std::min(atoi(fz), static_cast<int>(kFuseMax)));
   for (hipEvent_t& ev : E->ev_fgrp) {
@@ -1591,6 +1607,8 @@ void tgsim_destroy(void* e) {
   if (E->dst_st) (void)hipStreamSynchronize(E->dst_st);
   if (E->rt_st) (void)hipStreamSynchronize(E->rt_st);
   if (E->sy_st) (void)hipStreamSynchronize(E->sy_st);
+  // the exchange layer after the engine's streams (deliveries read its buffers), before their destruction
+  if (E->comm.free_fn) E->comm.free_fn(E->comm.state);
   E->d_sync.release(); E->d_gone.release();
   if (E->h_mirror) (void)hipHostFree(E->h_mirror);
   if (E->h_sig) (void)hipHostFree(E->h_sig);
@@ -1616,7 +1634,7 @@ void tgsim_destroy(void* e) {
     for (auto& ls : grp) { ls.emit.release(); ls.emit_n.release(); }
   for (auto& v : E->f_lcnt) v.release();
   for (auto& v : E->f_verdict) v.release();
-  E->d_done.release(); E->d_ticket.release();
+  E->d_ticket.release();
   for (hipEvent_t ev : E->ev_fgrp)
     if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
@@ -2185,6 +2203,19 @@ int64_t tgsim_debug_stamps(void* e, uint64_t* out, size_t cap) {
     if (rc) return rc;
     HIPCHK(hipMemcpy(out, E->d_stamps.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   }
+  return static_cast<int64_t>(n);
+}
+
+int64_t tgsim_debug_carry_bytes(void* e) {
+  Eng* E = as_eng(e);
+  if (!E) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
+  std::vector<unsigned long long> all(static_cast<size_t>(kStSlots) * kStatCopies);
+  HIPCHK(hipMemcpy(all.data(), E->d_stats.p, sizeof(unsigned long long) * all.size(), hipMemcpyDeviceToHost));
+  unsigned long long n = 0;
+  for (uint32_t c = 0; c < kStatCopies; ++c) n += all[static_cast<size_t>(c) * kStSlots + kStCarry];
   return static_cast<int64_t>(n);
 }
 

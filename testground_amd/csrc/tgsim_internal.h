@@ -73,7 +73,9 @@ struct CfgPatch {
 
 enum StatSlot {
   kStOffered = 0, kStScheduled, kStCloned, kStCorrupted, kStVerdict0,  // 4..11 verdicts
-  kStBytes = 12, kStErr = 13, kStQueue = 14, kStLost = 15, kStFlushed = 16, kStSlots = 20
+  kStBytes = 12, kStErr = 13, kStQueue = 14, kStLost = 15, kStFlushed = 16,
+  kStCarry = 17,  // queue state bytes the simulate kernels actually moved (a fused group: once per group)
+  kStSlots = 20
 };
 // Counters are spread over kStatCopies copies (workgroup w adds into copy w % kStatCopies) so that
 // a million one-source workgroups do not serialize on 16 addresses; readers sum the copies.  The
@@ -109,10 +111,9 @@ struct SimArgs {
 };
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 
-// Fused launch of up to kFuseMax consecutive windows (k_sim_fused): ticket t -> window t / S, the
-// t % S-th source in dispatch order.  A source's window k > 0 starts once its window k - 1 has
-// stored done[s] = step_base + k (the hand-off); the windows differ only in these
-// per-window fields.
+// Fused launch of up to kFuseMax consecutive windows (k_sim_fused), source-major: ticket t -> the
+// t-th source in dispatch order, whose windows one wavefront runs back to back;
+// the windows differ only in these per-window fields.
 constexpr uint32_t kFuseMax = 8;
 struct FusedWindow {
   const uint64_t* off;
@@ -126,15 +127,12 @@ struct FusedWindow {
 struct FusedArgs {
   FusedWindow w[kFuseMax];
   uint32_t n_win;
-  uint32_t step_base;   // done[] value that window 0's predecessors have reached
   uint32_t ticket_base; // *ticket before this launch (tickets are counted across launches)
   uint32_t* ticket;
-  uint32_t* done;       // [S] last completed window of each source (wrapping step counter)
   uint32_t prio_n;      // tickets at dispatch positions below prio_n run at wave priority 3
   uint32_t persistent;  // 1: a grid of resident workgroups claims tickets until none is left; 0: one
                         // workgroup per ticket (the slots turn over, so an exchange can be dispatched)
 };
-constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
 // Local delivery of a fused group: window w's emit regions, counts and CSR offsets; pos holds the
 // scatter cursors of the g * n_dst (window, destination) segments.
 struct GroupDeliver {
@@ -173,5 +171,18 @@ struct GossipArgs {
   uint32_t n_floods, degree, msg_len, n_ticks;
   uint64_t tick_ns, win0;   // window start (absolute tick)
 };
+
+// Engine hooks of the RCCL exchange layer (tgsim_comm.cpp), which drives the engine through the
+// public ABI and keeps its own state in the engine's comm slot (freed by tgsim_destroy).
+struct CommSlot {
+  void* state;
+  void (*free_fn)(void*);
+};
+CommSlot* engine_comm_slot(void* engine);
+int engine_device(void* engine);
+uint32_t engine_peers(void* engine);
+void engine_shard(void* engine, uint32_t* begin, uint32_t* end);
+int engine_fail(void* engine, int code, const char* msg);
+void engine_persist_routed(void* engine, bool on);  // unless TGSIM_FUSED_PERSIST was set
 
 }  // namespace tgsim

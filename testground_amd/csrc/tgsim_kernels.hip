@@ -765,60 +765,65 @@ __device__ __forceinline__ uint4 make_item(uint64_t e, uint32_t len, uint32_t fl
 }
 
 // ---------------------------------------------------------------------------------------------
-// Hand-off of a source's carried state (netem queue, departure ring, SrcState) between the windows
-// of one fused launch (k_sim_fused): window k+1 of a source may run on another CU or XCD than
-// window k, inside the same kernel, where neither the L1s nor the per-XCD L2s are coherent.  The
-// producer writes every handed-off byte with write-through (sc1) stores, drains them
-// (vmcnt(0)), then one lane stores the source's completion word (sc1); the consumer polls that word
-// with sc1 loads and reads every handed-off byte with L1-bypassing sc1 buffer loads
-// (MI355X_MICROARCH.md, "Valid forms", first row of the hand-off table).
+// The carried netem queue and departure ring move between HBM and LDS with bounded buffer loads
+// and stores: the resource covers exactly the live entries, so a lane past the end reads 0 without
+// touching memory (one load instruction per 64 slots, no per-lane bounds branch).
 using v4u = unsigned int __attribute__((ext_vector_type(4)));
-using v2u = unsigned int __attribute__((ext_vector_type(2)));
-constexpr int kSc1 = 16;  // buffer cache-policy bit SC1 (gfx940+)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t region(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
-__device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSc1));
+__device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
-__device__ __forceinline__ uint64_t ld8_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kSc1));
+__device__ __forceinline__ uint64_t ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
 }
-__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)off, 0, kSc1);
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)off, 0, 0);
 }
-struct StatePair {
-  uint4 lo, hi;
+
+// What a source carries from one window to the next when both run in the same wavefront
+// (k_sim_fused runs each source's windows back to back: the queue stays in LDS, only these
+// wave-uniform scalars pass from one sim_source call to the next).
+struct SrcCarry {
+  uint32_t rh, rn, qn, pn, fn;
+  uint64_t tat;
+  uint32_t last_dup, last_cor, last_reo;
 };
-static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
+constexpr uint32_t kPhLoad = 1, kPhStore = 2;  // sim_source phases: queue from HBM / back to HBM
 
 // One source's step (K1-K4), run by one wavefront.  kOpen: the caller has checked that the step
 // is an open queue without correlated draws, so only the open path is compiled in (fewer
 // registers, a kCap-slot LDS queue).  wg: the slot of the stamps and the statistics copy.
-// kH: the carried state is handed off inside the launch (k_sim_fused: sc1 loads and stores).
-// kH also claims the workgroup's next ticket (*claim, minus claim_base) before the write-back, so
-// the atomic's round trip overlaps the stores; it is returned (0 otherwise).
-template <bool kOpen, uint32_t kCap, bool kH = false>
+// ph & kPhLoad: the queue, ring and SrcState come from HBM; otherwise from *carry, with the queue
+// still in LDS from the source's previous window.  ph & kPhStore: they go back to HBM at the end;
+// otherwise into *carry.  *claim (when given) is the workgroup's next ticket, claimed before the
+// write-back so that the atomic's round trip overlaps the stores; returned minus claim_base.
+template <bool kOpen, uint32_t kCap>
 __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
-                                               uint32_t* claim = nullptr, uint32_t claim_base = 0) {
+                                               uint32_t* claim = nullptr, uint32_t claim_base = 0,
+                                               SrcCarry* carry = nullptr, uint32_t ph = kPhLoad | kPhStore) {
   const uint32_t lane = threadIdx.x;
   constexpr uint32_t kSlotMask = kCap - 1;
   stamp(a, wg, lane, 0, __builtin_amdgcn_s_memrealtime());
   const uint64_t t_begin = a.dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const SrcParams pp = a.params[s];
+  const bool load = (ph & kPhLoad) != 0;
   SrcState st;  // dead after the set-up: the end writes a fresh state
-  if constexpr (kH) {
-    const auto rs = region(a.state + s, sizeof(SrcState));
-    st = __builtin_bit_cast(SrcState, (StatePair{ld16_sc1(rs, 0), ld16_sc1(rs, 16)}));
-  } else {
+  if (load) {
     st = a.state[s];
+  } else {
+    st.tat = carry->tat;
+    st.last_dup = carry->last_dup;
+    st.last_cor = carry->last_cor;
+    st.last_reo = carry->last_reo;
   }
   SimQueue<kCap> Q{lds, pp, lane};
-  Q.rh = 0;
-  Q.rn = st.ring_n;
-  Q.qn = st.near_n;
-  Q.pn = st.heap_n - st.near_n;  // the whole pool until the load below splits it
-  Q.fn = 0;
+  Q.rh = load ? 0 : carry->rh;
+  Q.rn = load ? st.ring_n : carry->rn;
+  Q.qn = load ? st.near_n : carry->qn;
+  Q.pn = load ? st.heap_n - st.near_n : carry->pn;  // on a load: the whole pool until it is split
+  Q.fn = load ? 0 : carry->fn;
   Q.H = a.horizon_ns;
   Q.tat = st.tat;
   Q.src = a.shard_begin + s;
@@ -832,32 +837,22 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   uint64_t* pf = Q.pf;
 #endif
   // ---- load the departure ring (compacted) and the sorted eligibility queue into LDS
-  {
+  if (load) {
     const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     const uint4* gh = a.heap + (size_t)s * kHeapCap;
     const uint32_t rn = Q.rn, qn = Q.qn + Q.pn;
     // every load of the ring and the queue in flight before the first LDS write (one HBM
-    // latency instead of one per 256 slots)
-    // (branch-free: a lane past the end re-reads the last entry, the same line as its neighbours,
-    // and drops it; a conditional load made the compiler wait for each chunk inside its branch)
+    // latency instead of one per 256 slots); regions of exactly rn / qn entries, so the loads
+    // past them return 0 with no memory access (branch-free: a conditional load made the compiler
+    // wait for each chunk inside its branch)
     uint64_t rv[kCap / kWave];
     uint4 qv[kCap / kWave];
-    const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0;
-    if constexpr (kH) {  // regions of exactly rn / qn entries: the loads past them return 0 with no memory access
-      const auto rr = region(gr, 8u * rn), rq = region(gh, 16u * qn);
+    const auto rr = region(gr, 8u * rn), rq = region(gh, 16u * qn);
 #pragma unroll
-      for (uint32_t u = 0; u < kCap / kWave; ++u) {
-        const uint32_t k = u * kWave + lane;
-        rv[u] = ld8_sc1(rr, 8u * k);
-        qv[u] = ld16_sc1(rq, 16u * k);
-      }
-    } else {
-#pragma unroll
-      for (uint32_t u = 0; u < kCap / kWave; ++u) {
-        const uint32_t k = u * kWave + lane;
-        rv[u] = gr[k < rn ? k : rl];
-        qv[u] = gh[k < qn ? k : ql];
-      }
+    for (uint32_t u = 0; u < kCap / kWave; ++u) {
+      const uint32_t k = u * kWave + lane;
+      rv[u] = ld8(rr, 8u * k);
+      qv[u] = ld16(rq, 16u * k);
     }
     // every load issued before the partition's ballots, which the scheduler would otherwise
     // interleave with them (one HBM round trip per chunk)
@@ -883,6 +878,38 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     }
     Q.pn = cs;
     Q.fn = cf;
+  } else if (Q.fn) {
+    // the previous window's far pool holds every item with e >= its horizon; the ones below this
+    // window's horizon join the soon pool (placed right behind it, the rest behind them; neither
+    // part has an order): read all, then write, in one pass of registers
+    const uint32_t b = Q.rn + Q.qn + Q.pn, nf = Q.fn;
+    uint4 fv[kCap / kWave];
+#pragma unroll
+    for (uint32_t u = 0; u < kCap / kWave; ++u) {
+      const uint32_t k = u * kWave + lane;
+      fv[u] = k < nf ? Q.slot(b + k) : make_uint4(0, 0, 0, 0);
+    }
+    wave_lds_sync();
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t ns = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kCap / kWave; ++u)
+      ns += ballot_count(u * kWave + lane < nf && (w0_of(fv[u]) & kEMask) < Q.H);
+    if (ns) {
+      uint32_t cs = 0, cf = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < kCap / kWave; ++u) {
+        const uint32_t k = u * kWave + lane;
+        const bool in = k < nf, soon = in && (w0_of(fv[u]) & kEMask) < Q.H;
+        const uint64_t msn = __ballot(soon), mfr = __ballot(in && !soon);
+        if (soon) Q.slot(b + cs + (uint32_t)__popcll(msn & below)) = fv[u];
+        else if (in) Q.slot(b + ns + cf + (uint32_t)__popcll(mfr & below)) = fv[u];
+        cs += (uint32_t)__popcll(msn);
+        cf += (uint32_t)__popcll(mfr);
+      }
+      Q.pn += ns;
+      Q.fn -= ns;
+    }
   }
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const bool src_on = a.enabled[Q.src] != 0;
@@ -898,8 +925,11 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   // into the statistics every 2^14 batches (at most 2 counts per lane and batch), before a field
   // can overflow
   unsigned long long* const sc = a.stats + (size_t)(wg % kStatCopies) * kStSlots;
-  if (lane == 0 && (Q.qn | Q.pn | Q.fn | Q.rn))  // the queue state loaded (the stored part is added at the end)
-    atomicAdd(&sc[kStQueue], (unsigned long long)(16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn));
+  if (lane == 0 && (Q.qn | Q.pn | Q.fn | Q.rn)) {  // the queue state at the start (the end's is added there)
+    const unsigned long long b0 = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
+    atomicAdd(&sc[kStQueue], b0);  // the per-window model (bit-exact with the oracle)
+    if (load) atomicAdd(&sc[kStCarry], b0);  // what this call actually read from HBM
+  }
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
   auto flush_verdicts = [&]() {
@@ -1288,42 +1318,38 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   }
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   uint32_t next_ticket = 0;
-  if constexpr (kH) {
-    if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
-  }
-  // ---- write back the compacted ring, the sorted queue and the state
-  {
-    uint64_t* gr = a.ring + (size_t)s * kHeapCap;
-    uint4* gh = a.heap + (size_t)s * kHeapCap;
-    if constexpr (kH) {  // 16-B write-through stores (two ring entries per store)
-      const auto rr = region(gr, kHeapCap * 8u), rq = region(gh, kHeapCap * 16u);
-      for (uint32_t k = lane; 2 * k < Q.rn; k += kWave) {
-        const uint64_t d0 = Q.ring_d(2 * k), d1 = Q.ring_d(2 * k + 1);
-        st16_sc1(rr, 16u * k, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)));
-      }
-      for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) st16_sc1(rq, 16u * k, Q.slot(Q.rn + k));
-    } else {
-      for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
-      for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
+  if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
+  if (ph & kPhStore) {
+    // ---- write back the compacted ring (16-B stores, two entries each), the queue (near, then
+    // pool) and the state
+    const auto rr = region(a.ring + (size_t)s * kHeapCap, kHeapCap * 8u);
+    const auto rq = region(a.heap + (size_t)s * kHeapCap, kHeapCap * 16u);
+    for (uint32_t k = lane; 2 * k < Q.rn; k += kWave) {
+      const uint64_t d0 = Q.ring_d(2 * k), d1 = Q.ring_d(2 * k + 1);
+      st16(rr, 16u * k, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)));
     }
-  }
-  if (lane == 0) {
-    SrcState ns;
-    ns.tat = Q.tat;
-    ns.heap_n = Q.qn + Q.pn + Q.fn;
-    ns.near_n = Q.qn;
-    ns.ring_n = Q.rn;
-    ns.last_dup = last_dup;
-    ns.last_cor = last_cor;
-    ns.last_reo = last_reo;
-    if constexpr (kH) {
-      const auto rs = region(a.state + s, sizeof(SrcState));
-      const StatePair sp = __builtin_bit_cast(StatePair, ns);
-      st16_sc1(rs, 0, sp.lo);
-      st16_sc1(rs, 16, sp.hi);
-    } else {
+    for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) st16(rq, 16u * k, Q.slot(Q.rn + k));
+    if (lane == 0) {
+      SrcState ns;
+      ns.tat = Q.tat;
+      ns.heap_n = Q.qn + Q.pn + Q.fn;
+      ns.near_n = Q.qn;
+      ns.ring_n = Q.rn;
+      ns.last_dup = last_dup;
+      ns.last_cor = last_cor;
+      ns.last_reo = last_reo;
       a.state[s] = ns;
     }
+  } else {
+    carry->rh = Q.rh;
+    carry->rn = Q.rn;
+    carry->qn = Q.qn;
+    carry->pn = Q.pn;
+    carry->fn = Q.fn;
+    carry->tat = Q.tat;
+    carry->last_dup = last_dup;
+    carry->last_cor = last_cor;
+    carry->last_reo = last_reo;
   }
   stamp(a, wg, lane, 4, __builtin_amdgcn_s_memrealtime());
   stamp(a, wg, lane, 5, ((uint64_t)s << 32) | n_batches);
@@ -1348,6 +1374,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     if (lost) atomicAdd(&sc[kStLost], (unsigned long long)lost);
     if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
+    if (qbytes && (ph & kPhStore)) atomicAdd(&sc[kStCarry], (unsigned long long)qbytes);
     if (err) {
       atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
       if (a.err_host)  // the host's pinned copy (sticky; read at its sync points)
@@ -1369,67 +1396,48 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
 }
 
-// Several consecutive windows in one launch (tgsim_step_n): window k + 1 of a source starts as soon
-// as its window k is done, so the next window's heavy sources fill the CUs that the last dispatch
-// round of this window leaves idle (one launch tail and one launch gap per fused group instead of
-// one per window).  Persistent: the grid is what fits on the chip at once, and each workgroup takes
-// tickets in order until none is left (its next ticket claimed during the write-back of the
-// current one), so no slot waits for a workgroup dispatch between two sources.  Every claimed
-// ticket is held by a resident workgroup and waits only for a lower ticket (its source's previous
-// window), so the lowest unfinished ticket can always run: no deadlock.  The wait is bounded
-// anyway (kErrHandoff, then the window runs and the host reports -EIO).
+// Several consecutive windows in one launch (tgsim_step_n), SOURCE-MAJOR: a source's windows are
+// sequential anyway (window k + 1 starts from the queue window k leaves), so one wavefront runs all
+// of them back to back with the queue resident in LDS, loaded from HBM before the first window and
+// stored after the last (one HBM round trip of the queue per group, not per window; no hand-off
+// between CUs).  Sources are taken heaviest first (the dispatch order of the last window's HTB
+// records), so the longest chains start first.  Persistent: the grid is what fits on the chip at
+// once and each workgroup claims sources in order until none is left (its next claim issued during
+// the current source's write-back); otherwise one workgroup per source (the slots turn over, so an
+// exchange can be dispatched beside the launch).
 struct FusedSim {
   SimArgs w[kFuseMax];  // window k's arguments (tables and state shared, step fields its own)
 };
 __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f) {
   const SimArgs& a0 = fs.w[0];
   __shared__ SimLdsT<kHeapCap> lds;
-  const uint32_t total = f.n_win * a0.n_src;
+  const uint32_t total = a0.n_src;
   uint32_t t = 0;
   if (threadIdx.x == 0) t = atomicAdd(f.ticket, 1u) - f.ticket_base;
   t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   while (t < total) {
-    const uint32_t k = t / a0.n_src, pos = t - k * a0.n_src;
-    const uint32_t s = a0.order ? a0.order[pos] : pos;
-    // the heaviest sources (first in dispatch order) chain their windows through the launch: their
-    // waves issue first on their SIMDs, so the chain is not the launch's critical path
-    if (pos < f.prio_n) __builtin_amdgcn_s_setprio(3);
+    const uint32_t s = a0.order ? a0.order[t] : t;
+    // the heaviest sources (first in dispatch order) run at wave priority 3: their chains of
+    // windows are the launch's longest
+    if (t < f.prio_n) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(0);
-    const uint64_t t_wait = a0.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (k) {
-      const uint32_t need = f.step_base + k;
-      uint32_t late = 0;
-      if (threadIdx.x == 0) {
-        for (uint32_t spin = 0;
-             (int32_t)(__hip_atomic_load(f.done + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - need) < 0;) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spin > (1u << 22)) {
-            late = 1;
-            break;
-          }
-        }
-      }
-      if (__builtin_amdgcn_readfirstlane((int)late) && threadIdx.x == 0) {
-        atomicOr(&a0.stats[kStErr], (unsigned long long)kErrHandoff);
-        if (a0.err_host)
-          __hip_atomic_store(a0.err_host, (uint64_t)kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+    SrcCarry c;
+    uint32_t next = 0;
+    for (uint32_t k = 0; k < f.n_win; ++k) {
+      // window k's arguments read in place in the kernel-argument segment (scalar loads of
+      // invariant memory: re-read when needed instead of held in spilled SGPRs)
+      using KernargSimArgs = __attribute__((address_space(4))) const SimArgs;
+      const KernargSimArgs* ka =
+          (KernargSimArgs*)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                            k * sizeof(SimArgs));
+      const SimArgs& a = *(const SimArgs*)ka;
+      const bool last = k + 1 == f.n_win;
+      const uint32_t ph = (k == 0 ? kPhLoad : 0u) | (last ? kPhStore : 0u);
+      next = sim_source<false, kHeapCap>(a, s, k * total + t, lds, last && f.persistent ? f.ticket : nullptr,
+                                         f.ticket_base, &c, ph);
     }
-    if (a0.stamps && threadIdx.x == 0)  // diagnostics: 10-ns ticks spent waiting for the previous window
-      a0.stamps[(size_t)t * kStampSlots + kStampSlots - 1] = __builtin_amdgcn_s_memrealtime() - t_wait;
-    // window k's arguments read in place in the kernel-argument segment (scalar loads of invariant
-    // memory: re-read when needed instead of held in spilled SGPRs)
-    using KernargSimArgs = __attribute__((address_space(4))) const SimArgs;
-    const KernargSimArgs* ka =
-        (KernargSimArgs*)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                          k * sizeof(SimArgs));
-    const SimArgs& a = *(const SimArgs*)ka;
-    const uint32_t next = sim_source<false, kHeapCap, true>(a, s, t, lds, f.persistent ? f.ticket : nullptr,
-                                                            f.ticket_base);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
-    if (threadIdx.x == 0)
-      __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!f.persistent) break;  // one ticket per workgroup: the dispatcher interleaves other streams' work
+    if (!f.persistent) break;  // one source per workgroup: the dispatcher interleaves other streams' work
+    wave_lds_sync();  // the write-back's LDS reads are done before the next source's loads land
     t = next;
   }
 }
@@ -1703,6 +1711,7 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
     if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
     if (t_bytes) atomicAdd(&sc[kStBytes], (unsigned long long)t_bytes);
     if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
+    if (qb) atomicAdd(&sc[kStCarry], (unsigned long long)qb);
     if (err) {
       atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
       if (a.err_host)
@@ -2564,7 +2573,7 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
 }
 
 void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st) {
-  const uint32_t total = f.n_win * a.n_src;
+  const uint32_t total = a.n_src;  // source-major: one ticket per source
   FusedSim fs;
   for (uint32_t k = 0; k < kFuseMax; ++k) {
     fs.w[k] = a;

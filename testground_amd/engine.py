@@ -310,7 +310,38 @@ class CABIEngine:
                     "sync_counters")
         return int(ptr.value or 0), int(n.value)
 
+    # -- RCCL exchange owned by the engine (tgsim_comm_*) --------------------------------------------
+    def comm_init(self, comm_id: bytes, rank: int, nranks: int) -> None:
+        """Joins this engine to the run's exchange (collective; comm_id from comm_id() on one rank)."""
+        buf = C.create_string_buffer(bytes(comm_id), abi.COMM_ID_BYTES)
+        self._check(self._fn("comm_init")(self._h, buf, rank, nranks), "comm_init")
+
+    def comm_step(self, n_ticks: int) -> None:
+        self._check(self._fn("comm_step")(self._h, n_ticks), "comm_step")
+
+    def comm_launch(self, n_ticks: int) -> None:
+        self._check(self._fn("comm_launch")(self._h, n_ticks), "comm_launch")
+
+    def comm_finish(self) -> None:
+        self._check(self._fn("comm_finish")(self._h), "comm_finish")
+
+    def comm_run(self, n_ticks: int, n_steps: int, fuse: int = 1, slot_cap: int = 0) -> None:
+        self._check(self._fn("comm_run")(self._h, n_ticks, n_steps, fuse, slot_cap), "comm_run")
+
+    def comm_barrier(self, state: int, target: int) -> bool:
+        return bool(self._check(self._fn("comm_barrier")(self._h, state, target), "comm_barrier"))
+
+    def comm_info(self) -> dict:
+        i = abi.CommInfo()
+        self._check(self._fn("comm_info")(self._h, C.byref(i)), "comm_info")
+        return {"rank": i.rank, "nranks": i.nranks, "exchanged_records": i.exchanged_records,
+                "max_rank_count": i.max_rank_count, "slot_cap": i.slot_cap, "bounds": list(i.bounds[:i.nranks + 1])}
+
     # -- instrumentation -----------------------------------------------------------------------
+    def carry_bytes(self) -> int:
+        """HBM bytes the simulate kernels moved carrying queues between windows (tgsim_debug_carry_bytes)."""
+        return self._check(self._fn("debug_carry_bytes")(self._h), "debug_carry_bytes")
+
     def sim_kernel_ms(self, reset: bool = False) -> Tuple[float, int]:
         n = C.c_uint64()
         ms = self._fn("sim_kernel_ms")(self._h, C.byref(n), 1 if reset else 0)
@@ -322,6 +353,17 @@ class Engine(CABIEngine):
 
     def __init__(self, n_peers: int, **kw):
         super().__init__(load_library(), "tgsim_", n_peers, **kw)
+
+
+def comm_id() -> bytes:
+    """A fresh RCCL communicator id (tgsim_comm_id) for tgsim_comm_init; made on one rank and handed
+    to the others by the host."""
+    lib = load_library()
+    buf = C.create_string_buffer(abi.COMM_ID_BYTES)
+    rc = lib.tgsim_comm_id(buf)
+    if rc:
+        raise EngineError(rc, "tgsim_comm_id")
+    return buf.raw
 
 
 def packets(rows: Iterable[tuple]) -> np.ndarray:

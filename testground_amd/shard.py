@@ -4,12 +4,15 @@ Shaping is egress-only and per source (pkg/sidecar/link.go:22-40), so every rank
 contiguous range of sources and computes their verdicts and delivery times locally.  The only
 exchange is the hand-off of scheduled 24-B records to the destination's rank:
 
-    engine.step_sim  -> records grouped by destination shard (caller-owned buffer)
-    all_to_all       -> per-rank record counts, then the records (RCCL over xGMI on GPUs)
-    engine.deliver   -> per-destination delivery order on the receiving rank
+    simulate -> records grouped by destination shard
+    exchange -> per-rank record counts, then the records (RCCL over xGMI on GPUs)
+    deliver  -> per-destination delivery order on the receiving rank
 
-The same code drives the HIP engine with CUDA buffers (bench.py, backend "nccl" = RCCL) and, in
-tests, CPU-oracle shards with CPU buffers over `gloo`.
+On GPUs the engine does all of it itself (`CommStepper` over tgsim_comm_*: its own RCCL
+communicator, exchange stream and buffers), so the Go host of INTEGRATION.md and this module make
+the same calls.  `ShardedStepper` is the same exchange written with torch.distributed over the
+engine's split-phase calls (tgsim_step_sim_launch / _deliver_async): the tests run it with CPU
+oracle shards over `gloo`, as the restatement the engine's own exchange is checked against.
 """
 from __future__ import annotations
 
@@ -48,6 +51,52 @@ def device_table(ptr: int, n: int, device: torch.device) -> torch.Tensor:
 def shard_bounds(n_peers: int, world: int) -> List[int]:
     """Contiguous source ranges, as even as possible: rank r owns [b[r], b[r+1])."""
     return [(n_peers * r) // world for r in range(world)] + [n_peers]
+
+
+class CommStepper:
+    """The engine's own exchange (tgsim_comm_*), with ShardedStepper's interface: step() is one
+    closed-loop window (tgsim_comm_step), run() the pipelined slotted run (tgsim_comm_run),
+    barrier() the device all-reduce of a sync counter (tgsim_comm_barrier).  The RCCL id is made
+    on rank 0 and broadcast over the host's process group."""
+
+    def __init__(self, engine, bounds: Sequence[int], device: str = "cuda", group=None,
+                 slot_cap: Optional[int] = None):
+        from .engine import comm_id
+        self.engine = engine
+        self.bounds = list(bounds)
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        ids = [comm_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0, group=group, device=torch.device(device))
+        engine.comm_init(ids[0], rank, world)
+        got = engine.comm_info()["bounds"]
+        if got != self.bounds:
+            raise ValueError(f"engine shards {got} differ from the stepper's bounds {self.bounds}")
+        self.slot_cap = slot_cap
+
+    @property
+    def max_count(self) -> int:
+        return self.engine.comm_info()["max_rank_count"]
+
+    @property
+    def exchanged_records(self) -> int:
+        return self.engine.comm_info()["exchanged_records"]
+
+    def step(self, n_ticks: int, between: Optional[Callable[[], object]] = None) -> int:
+        """One window on every rank (collective).  `between` runs on the host while the window
+        simulates (its ConfigureNetwork calls take effect at the next launch)."""
+        self.engine.comm_launch(n_ticks)
+        if between is not None:
+            between()
+        self.engine.comm_finish()
+        return -1
+
+    def run(self, n_steps: int, n_ticks: int, fuse: int = 1) -> int:
+        self.engine.comm_run(n_ticks, n_steps, fuse, self.slot_cap or 0)
+        self.slot_cap = self.engine.comm_info()["slot_cap"]
+        return -1
+
+    def barrier(self, state: int, target: int) -> bool:
+        return self.engine.comm_barrier(state, target)
 
 
 class ShardedStepper:

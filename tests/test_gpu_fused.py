@@ -130,15 +130,17 @@ def test_three_shards_fused_slotted_exchange_equal_one():
     assert sum(t["scheduled"] for t in tot) == s_ref["scheduled"]
 
 
-def test_stepper_fused_slotted_run_equals_step():
-    """ShardedStepper.run(fuse=4) through RCCL at one rank: groups of four windows per launch and per
-    all-to-all, the same deliveries and statistics as the single-engine steps."""
+@pytest.mark.parametrize("exchange", ["engine", "torch"])
+def test_stepper_fused_slotted_run_equals_step(exchange):
+    """Sharded run(fuse=4) at one rank, through the engine's own exchange (tgsim_comm_run) and the
+    torch.distributed one: groups of four windows per launch and per exchange, the same deliveries
+    and statistics as the single-engine steps."""
     import os
 
     import torch
     import torch.distributed as dist
 
-    from testground_amd.shard import ShardedStepper, init_rccl
+    from testground_amd.shard import CommStepper, ShardedStepper, init_rccl
 
     torch.cuda.init()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -151,7 +153,8 @@ def test_stepper_fused_slotted_run_equals_step():
             wl.configure_storm(e, n)
         for _ in range(steps):
             sh.gen_storm(0.5, 1000)
-        st = ShardedStepper(sh, [0, n], device="cuda:0", slot_cap=400_000)
+        cls = CommStepper if exchange == "engine" else ShardedStepper
+        st = cls(sh, [0, n], device="cuda:0", slot_cap=400_000)
         assert st.run(steps, 1000, fuse=4) == -1
         assert _fused(sh) == steps  # 4 + 4 + 2
         want = []

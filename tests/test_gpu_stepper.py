@@ -1,7 +1,8 @@
-"""The production sharded stepper (testground_amd/shard.py: step_sim -> RCCL all-to-all ->
-asynchronous delivery overlapping the next k_sim) on one GPU with a world of one rank, against the
-single-engine step: identical verdicts and deliveries, open loop (storm) and closed loop (gossip,
-whose receipts feed the next window)."""
+"""The sharded step on one GPU with a world of one rank, against the single-engine step: identical
+verdicts and deliveries, open loop (storm) and closed loop (gossip, whose receipts feed the next
+window).  Every test runs both exchanges: the engine's own (CommStepper over tgsim_comm_*: its RCCL
+communicator, exchange stream and buffers, what bench.py and a Go host use) and the
+torch.distributed one over the split-phase ABI (ShardedStepper)."""
 import os
 
 import numpy as np
@@ -28,14 +29,20 @@ def rccl():
     dist.destroy_process_group()
 
 
-def test_stepper_storm_equals_step(rccl):
-    from testground_amd.shard import ShardedStepper
+@pytest.fixture(params=["engine", "torch"])
+def Stepper(request, rccl):
+    from testground_amd.shard import CommStepper, ShardedStepper
+
+    return CommStepper if request.param == "engine" else ShardedStepper
+
+
+def test_stepper_storm_equals_step(Stepper):
 
     n = 300
     ref, sh = Engine(n), Engine(n)
     for e in (ref, sh):
         wl.configure_storm(e, n)
-    st = ShardedStepper(sh, [0, n], device="cuda:0")
+    st = Stepper(sh, [0, n], device="cuda:0")
     for k in range(6):
         ref.gen_storm(0.5, 1500)
         sh.gen_storm(0.5, 1500)
@@ -46,8 +53,7 @@ def test_stepper_storm_equals_step(rccl):
         assert len(d_sh) == len(d_ref) and (d_sh == d_ref).all(), f"step {k}"
 
 
-def test_stepper_gossip_equals_step(rccl):
-    from testground_amd.shard import ShardedStepper
+def test_stepper_gossip_equals_step(Stepper):
 
     n = 1500
     ref = Engine(n, lookahead_ns=wl.GOSSIP_MIN_LAT)
@@ -55,7 +61,7 @@ def test_stepper_gossip_equals_step(rccl):
     for e in (ref, sh):
         wl.configure_gossip(e, n)
         e.gossip_init(n_floods=8, degree=8, msg_len=1024, start_gap_ticks=300, start_tick=0)
-    st = ShardedStepper(sh, [0, n], device="cuda:0")
+    st = Stepper(sh, [0, n], device="cuda:0")
     w = wl.gossip_window_ticks(ref)
     for k in range(25):
         ref.gen_gossip(w)
@@ -67,9 +73,8 @@ def test_stepper_gossip_equals_step(rccl):
     assert (sh.gossip_reached() == ref.gossip_reached()).all()
 
 
-def test_stepper_pipelined_run_equals_step(rccl):
+def test_stepper_pipelined_run_equals_step(Stepper):
     """run(): step k+1's k_sim launched before step k's exchange and delivery."""
-    from testground_amd.shard import ShardedStepper
 
     n, steps = 2000, 8
     ref, sh = Engine(n), Engine(n)
@@ -77,7 +82,7 @@ def test_stepper_pipelined_run_equals_step(rccl):
         wl.configure_storm(e, n)
     for _ in range(steps):
         sh.gen_storm(0.5, 1000)
-    ShardedStepper(sh, [0, n], device="cuda:0").run(steps, 1000)
+    Stepper(sh, [0, n], device="cuda:0").run(steps, 1000)
     want = []
     for _ in range(steps):
         ref.gen_storm(0.5, 1000)
@@ -90,17 +95,16 @@ def test_stepper_pipelined_run_equals_step(rccl):
     assert (s["offered"], s["scheduled"], s["by_verdict"]) == (r["offered"], r["scheduled"], r["by_verdict"])
 
 
-def test_stepper_epochs_staged_reshape_equals_step(rccl):
+def test_stepper_epochs_staged_reshape_equals_step(Stepper):
     """C5 through the stepper as bench.py runs it: epoch k+1's reshape staged on the host while
     epoch k simulates (between=), the barrier summed on the host group; the same verdicts,
     deliveries and barrier releases as reshaping before each single-engine step."""
-    from testground_amd.shard import ShardedStepper
 
     n, ticks = 3000, 800
     ref, sh = Engine(n), Engine(n)
     for e in (ref, sh):
         wl.configure_storm(e, n)
-    st = ShardedStepper(sh, [0, n], device="cuda:0")
+    st = Stepper(sh, [0, n], device="cuda:0")
     for k in range(5):
         if k:
             wl.epoch_reshape(ref, n, k)
@@ -118,10 +122,9 @@ def test_stepper_epochs_staged_reshape_equals_step(rccl):
         assert len(d_sh) == len(d_ref) > 0 and (d_sh == d_ref).all(), f"epoch {k}"
 
 
-def test_stepper_slotted_run_equals_step(rccl):
+def test_stepper_slotted_run_equals_step(Stepper):
     """run() with fixed-size exchange chunks (slot_cap): the host only enqueues, never reads a count;
     the same deliveries and statistics as the single-engine steps."""
-    from testground_amd.shard import ShardedStepper
 
     n, steps = 2000, 8
     ref, sh = Engine(n), Engine(n)
@@ -129,7 +132,7 @@ def test_stepper_slotted_run_equals_step(rccl):
         wl.configure_storm(e, n)
     for _ in range(steps):
         sh.gen_storm(0.5, 1000)
-    st = ShardedStepper(sh, [0, n], device="cuda:0", slot_cap=400_000)
+    st = Stepper(sh, [0, n], device="cuda:0", slot_cap=400_000)
     assert st.run(steps, 1000) == -1
     want = []
     for _ in range(steps):
@@ -143,10 +146,9 @@ def test_stepper_slotted_run_equals_step(rccl):
     assert (s["offered"], s["scheduled"], s["by_verdict"]) == (r["offered"], r["scheduled"], r["by_verdict"])
 
 
-def test_stepper_slotted_overflow_fails(rccl):
+def test_stepper_slotted_overflow_fails(Stepper):
     """A chunk too small for a step's records is an error (-ENOSPC), never a silent loss."""
     from testground_amd.engine import EngineError
-    from testground_amd.shard import ShardedStepper
 
     n = 500
     sh = Engine(n)
@@ -154,5 +156,5 @@ def test_stepper_slotted_overflow_fails(rccl):
     for _ in range(3):
         sh.gen_storm(0.5, 1000)
     with pytest.raises(EngineError, match="slot capacity"):
-        ShardedStepper(sh, [0, n], device="cuda:0", slot_cap=16).run(3, 1000)
+        Stepper(sh, [0, n], device="cuda:0", slot_cap=16).run(3, 1000)
         sh.sync()
