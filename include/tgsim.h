@@ -444,6 +444,13 @@ uint64_t tgsim_bridge_now_tick(void* bridge);              /* start of the next 
 int tgsim_udp_front_create(void* bridge, uint16_t port, void** out_front);
 int tgsim_udp_front_port(void* front);
 int tgsim_udp_front_register(void* front, uint32_t peer, uint32_t ipv4, uint16_t port);
+/* Header-less mode for unmodified UDP code: the front end binds a socket at (ipv4, port) (port 0:
+ * any) that stands for peer's data address.  A registered instance that sends a plain datagram to
+ * it sends to `peer` (no destination header); every delivery from `peer` leaves from that socket,
+ * so the receiver's recvfrom sees peer's data address as the source (no source header).  Any
+ * 127.0.0.0/8 address works without privileges.  Returns the bound port or -errno.  (TUN/TAP
+ * capture, which would carry TCP too, needs /dev/net/tun and CAP_NET_ADMIN: DESIGN.md §9.) */
+int tgsim_udp_front_bind_peer(void* front, uint32_t peer, uint32_t ipv4, uint16_t port);
 int64_t tgsim_udp_front_pump(void* front);
 void tgsim_udp_front_destroy(void* front);
 

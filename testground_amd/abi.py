@@ -142,7 +142,7 @@ EXPORTS = [
     "tgsim_bridge_create", "tgsim_bridge_destroy", "tgsim_bridge_send", "tgsim_bridge_step",
     "tgsim_bridge_recv", "tgsim_bridge_pending", "tgsim_bridge_in_flight", "tgsim_bridge_now_tick",
     "tgsim_bridge_link_removed",
-    "tgsim_udp_front_create", "tgsim_udp_front_port", "tgsim_udp_front_register",
+    "tgsim_udp_front_create", "tgsim_udp_front_port", "tgsim_udp_front_register", "tgsim_udp_front_bind_peer",
     "tgsim_udp_front_pump", "tgsim_udp_front_destroy",
 ]
 

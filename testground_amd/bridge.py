@@ -185,6 +185,7 @@ def _declare_bridge(lib: C.CDLL) -> None:
             ("tgsim_udp_front_create", C.c_int, [vp, C.c_uint16, C.POINTER(vp)]),
             ("tgsim_udp_front_port", C.c_int, [vp]),
             ("tgsim_udp_front_register", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint16]),
+            ("tgsim_udp_front_bind_peer", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint16]),
             ("tgsim_udp_front_pump", C.c_int64, [vp]),
             ("tgsim_udp_front_destroy", None, [vp])):
         fn = getattr(lib, name)
@@ -319,6 +320,14 @@ class NativeUdpFront:
         import ipaddress
         self.bridge._chk(self._lib.tgsim_udp_front_register(self._h, peer, int(ipaddress.IPv4Address(addr[0])), addr[1]),
                          "tgsim_udp_front_register")
+
+    def bind_peer(self, peer: int, addr: Tuple[str, int] = ("127.0.0.1", 0)) -> Tuple[str, int]:
+        """Header-less mode: a front-end socket at addr stands for peer's data address (plain
+        datagrams sent to it go to peer; peer's deliveries come from it).  Returns the bound address."""
+        import ipaddress
+        port = self.bridge._chk(self._lib.tgsim_udp_front_bind_peer(self._h, peer, int(ipaddress.IPv4Address(addr[0])),
+                                                                     addr[1]), "tgsim_udp_front_bind_peer")
+        return (addr[0], port)
 
     def pump(self) -> int:
         return self.bridge._chk(self._lib.tgsim_udp_front_pump(self._h), "tgsim_udp_front_pump")

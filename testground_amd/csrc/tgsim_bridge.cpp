@@ -16,6 +16,7 @@
 #include <poll.h>
 #include <stdint.h>
 #include <string.h>
+#include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -416,6 +417,12 @@ struct tgsim_udp_front_s {
   std::vector<uint32_t> hdr;
   std::vector<mmsghdr> txh;
   std::vector<iovec> txv;
+  // header-less mode: peer p's data address is a socket of the front end (vfd[p]); what arrives
+  // there is addressed to p, and what is delivered from p leaves from it
+  std::vector<int> vfd;                          // per peer, -1: none
+  std::unordered_map<int, uint32_t> vpeer;       // fd -> peer
+  int ep = -1;                                   // epoll set of the vfd sockets
+  std::vector<uint32_t> order;                   // deliveries grouped by source socket
 };
 using Uf = tgsim_udp_front_s;
 
@@ -445,6 +452,7 @@ int tgsim_udp_front_create(void* bridge, uint16_t port, void** out) {
   }
   F->port = ntohs(a.sin_port);
   F->addr.assign(F->br->n, sockaddr_in{});
+  F->vfd.assign(F->br->n, -1);
   F->rxbuf.resize(static_cast<size_t>(Uf::kBatch) * 65536);
   F->rxh.resize(Uf::kBatch);
   F->rxv.resize(Uf::kBatch);
@@ -467,10 +475,38 @@ int tgsim_udp_front_register(void* f, uint32_t peer, uint32_t ipv4, uint16_t por
   return 0;
 }
 
-int64_t tgsim_udp_front_pump(void* f) {
+int tgsim_udp_front_bind_peer(void* f, uint32_t peer, uint32_t ipv4, uint16_t port) {
   Uf* F = static_cast<Uf*>(f);
-  if (!F) return -EINVAL;
-  // ---- everything that arrived: recvmmsg batches into one bridge send per batch
+  if (!F || peer >= F->br->n || F->vfd[peer] >= 0) return -EINVAL;
+  if (F->ep < 0 && (F->ep = epoll_create1(0)) < 0) return -errno;
+  const int fd = socket(AF_INET, SOCK_DGRAM | SOCK_NONBLOCK, 0);
+  if (fd < 0) return -errno;
+  int sz = 4 << 20;
+  (void)setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof sz);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(ipv4);
+  a.sin_port = htons(port);
+  socklen_t al = sizeof a;
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.fd = fd;
+  if (bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) || getsockname(fd, reinterpret_cast<sockaddr*>(&a), &al) ||
+      epoll_ctl(F->ep, EPOLL_CTL_ADD, fd, &ev)) {
+    const int e = errno;
+    close(fd);
+    return -e;
+  }
+  F->vfd[peer] = fd;
+  F->vpeer[fd] = peer;
+  return ntohs(a.sin_port);
+}
+
+namespace {
+// The datagrams waiting on one socket, in recvmmsg batches, into bridge sends.  dst_fixed:
+// UINT32_MAX for the header socket (a 4-byte destination header leads each datagram), else the peer
+// whose data-address socket this is (the payload is the whole datagram).
+int64_t drain_socket(Uf* F, int fd, uint32_t dst_fixed) {
   for (;;) {
     for (unsigned i = 0; i < Uf::kBatch; ++i) {
       F->rxv[i].iov_base = F->rxbuf.data() + static_cast<size_t>(i) * 65536;
@@ -481,26 +517,29 @@ int64_t tgsim_udp_front_pump(void* f) {
       F->rxh[i].msg_hdr.msg_name = &F->rxa[i];
       F->rxh[i].msg_hdr.msg_namelen = sizeof(sockaddr_in);
     }
-    const int got = recvmmsg(F->fd, F->rxh.data(), Uf::kBatch, MSG_DONTWAIT, nullptr);
+    const int got = recvmmsg(fd, F->rxh.data(), Uf::kBatch, MSG_DONTWAIT, nullptr);
     if (got <= 0) break;
     F->s_src.clear();
     F->s_dst.clear();
     F->s_data.clear();
     F->s_off.assign(1, 0);
+    const size_t hdr = dst_fixed == UINT32_MAX ? 4 : 0;
     for (int i = 0; i < got; ++i) {
       const size_t len = F->rxh[i].msg_len;
       const sockaddr_in& sa = F->rxa[i];
       auto it = F->peer.find((static_cast<uint64_t>(ntohl(sa.sin_addr.s_addr)) << 16) | ntohs(sa.sin_port));
-      if (it == F->peer.end() || len < 4) continue;  // not an instance of this run
+      if (it == F->peer.end() || len < hdr) continue;  // not an instance of this run
       const uint8_t* m = F->rxbuf.data() + static_cast<size_t>(i) * 65536;
-      uint32_t dst;
-      memcpy(&dst, m, 4);
-      dst = ntohl(dst);
+      uint32_t dst = dst_fixed;
+      if (hdr) {
+        memcpy(&dst, m, 4);
+        dst = ntohl(dst);
+      }
       if (dst != TGSIM_EXTERNAL && dst >= F->br->n) continue;
-      if (len - 4 > kMaxPayload) continue;
+      if (len - hdr > kMaxPayload) continue;
       F->s_src.push_back(it->second);
       F->s_dst.push_back(dst);
-      F->s_data.insert(F->s_data.end(), m + 4, m + len);
+      F->s_data.insert(F->s_data.end(), m + hdr, m + len);
       F->s_off.push_back(F->s_data.size());
     }
     if (!F->s_src.empty()) {
@@ -509,6 +548,45 @@ int64_t tgsim_udp_front_pump(void* f) {
       if (rc < 0) return rc;
     }
     if (got < static_cast<int>(Uf::kBatch)) break;
+  }
+  return 0;
+}
+
+// sendmmsg of txh[i0, i1) from fd, waiting for room when the socket buffer is full.
+int send_all(int fd, mmsghdr* h, size_t m) {
+  for (size_t i = 0; i < m;) {
+    const int sent = sendmmsg(fd, h + i, static_cast<unsigned>(std::min<size_t>(m - i, 1024)), 0);
+    if (sent < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == ENOBUFS) {
+        pollfd pf{fd, POLLOUT, 0};
+        if (poll(&pf, 1, 1000) <= 0) return -EAGAIN;
+        continue;
+      }
+      return -errno;
+    }
+    i += static_cast<size_t>(sent);
+  }
+  return 0;
+}
+}  // namespace
+
+int64_t tgsim_udp_front_pump(void* f) {
+  Uf* F = static_cast<Uf*>(f);
+  if (!F) return -EINVAL;
+  // ---- everything that arrived: the header socket, then every ready data-address socket
+  int64_t rc = drain_socket(F, F->fd, UINT32_MAX);
+  if (rc < 0) return rc;
+  if (F->ep >= 0) {
+    epoll_event evs[256];
+    for (;;) {
+      const int k = epoll_wait(F->ep, evs, 256, 0);
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) break;
+      for (int i = 0; i < k; ++i)
+        if ((rc = drain_socket(F, evs[i].data.fd, F->vpeer[evs[i].data.fd])) < 0) return rc;
+      if (k < 256) break;
+    }
   }
   const int64_t n = tgsim_bridge_step(F->br);
   if (n < 0) return n;
@@ -525,33 +603,46 @@ int64_t tgsim_udp_front_pump(void* f) {
   F->hdr.resize(static_cast<size_t>(k));
   F->txh.resize(static_cast<size_t>(k));
   F->txv.resize(2 * static_cast<size_t>(k));
+  // deliveries from a source with a data-address socket leave from it, without a header (the
+  // receiver's recvfrom sees the source's address); the others leave from the header socket
+  F->order.resize(static_cast<size_t>(k));
+  for (int64_t i = 0; i < k; ++i) F->order[i] = static_cast<uint32_t>(i);
+  std::stable_sort(F->order.begin(), F->order.end(), [F](uint32_t x, uint32_t y) {
+    const int fx = F->vfd[F->msgs[x].src], fy = F->vfd[F->msgs[y].src];
+    return fx < fy;
+  });
   size_t m = 0;
-  for (int64_t i = 0; i < k; ++i) {
-    const tgsim_msg& g = F->msgs[i];
+  int cur = -2;
+  size_t run0 = 0;
+  for (int64_t r = 0; r <= k; ++r) {
+    const int fd = r < k ? F->vfd[F->msgs[F->order[r]].src] : -3;
+    if (fd != cur) {  // flush the run of the previous socket
+      if (m > run0) {
+        const int rc2 = send_all(cur < 0 ? F->fd : cur, F->txh.data() + run0, m - run0);
+        if (rc2) return rc2;
+      }
+      run0 = m;
+      cur = fd;
+    }
+    if (r == k) break;
+    const tgsim_msg& g = F->msgs[F->order[r]];
     sockaddr_in& to = F->addr[g.dst];
     if (!to.sin_port) continue;  // nobody listening for that instance
-    F->hdr[m] = htonl(g.src);
-    F->txv[2 * m] = iovec{&F->hdr[m], 4};
-    F->txv[2 * m + 1] = iovec{F->payload.data() + g.off, g.len};
     memset(&F->txh[m], 0, sizeof(mmsghdr));
-    F->txh[m].msg_hdr.msg_iov = &F->txv[2 * m];
-    F->txh[m].msg_hdr.msg_iovlen = 2;
+    if (fd < 0) {
+      F->hdr[m] = htonl(g.src);
+      F->txv[2 * m] = iovec{&F->hdr[m], 4};
+      F->txv[2 * m + 1] = iovec{F->payload.data() + g.off, g.len};
+      F->txh[m].msg_hdr.msg_iov = &F->txv[2 * m];
+      F->txh[m].msg_hdr.msg_iovlen = 2;
+    } else {
+      F->txv[2 * m] = iovec{F->payload.data() + g.off, g.len};
+      F->txh[m].msg_hdr.msg_iov = &F->txv[2 * m];
+      F->txh[m].msg_hdr.msg_iovlen = 1;
+    }
     F->txh[m].msg_hdr.msg_name = &to;
     F->txh[m].msg_hdr.msg_namelen = sizeof to;
     ++m;
-  }
-  for (size_t i = 0; i < m;) {
-    const int sent = sendmmsg(F->fd, F->txh.data() + i, static_cast<unsigned>(std::min<size_t>(m - i, 1024)), 0);
-    if (sent < 0) {
-      if (errno == EINTR) continue;
-      if (errno == EAGAIN || errno == ENOBUFS) {  // our send buffer is full: wait for room
-        pollfd pf{F->fd, POLLOUT, 0};
-        if (poll(&pf, 1, 1000) <= 0) return -EAGAIN;
-        continue;
-      }
-      return -errno;
-    }
-    i += static_cast<size_t>(sent);
   }
   return n;
 }
@@ -560,6 +651,9 @@ void tgsim_udp_front_destroy(void* f) {
   Uf* F = static_cast<Uf*>(f);
   if (!F) return;
   if (F->fd >= 0) close(F->fd);
+  for (int fd : F->vfd)
+    if (fd >= 0) close(fd);
+  if (F->ep >= 0) close(F->ep);
   delete F;
 }
 

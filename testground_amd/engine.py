@@ -340,6 +340,8 @@ class CABIEngine:
     # -- instrumentation -----------------------------------------------------------------------
     def carry_bytes(self) -> int:
         """HBM bytes the simulate kernels moved carrying queues between windows (tgsim_debug_carry_bytes)."""
+        if not hasattr(self._lib, self._p + "debug_carry_bytes"):  # an older library (A/B runs)
+            return 0
         return self._check(self._fn("debug_carry_bytes")(self._h), "debug_carry_bytes")
 
     def sim_kernel_ms(self, reset: bool = False) -> Tuple[float, int]:

@@ -319,3 +319,46 @@ def test_bridge_link_removal_resolves_queued_packets(make_oracle):
     for peer in range(n):
         assert bp.recv(peer) == bn.recv(peer)
     assert bp.in_flight() == bn.in_flight() == 0
+
+
+@native
+def test_native_udp_front_headerless(make_oracle):
+    """TUN/TAP is not available on the GPU box (no /dev/net/tun, no CAP_NET_ADMIN, user namespaces
+    disabled: DESIGN.md §9), so unmodified UDP code reaches the engine through per-peer data-address
+    sockets of the front end (tgsim_udp_front_bind_peer): an instance sends a plain datagram to the
+    peer's address and the peer's recvfrom returns the payload unchanged with the SENDER's data
+    address as the source, after the simulated link's delay.  No header either way."""
+    from testground_amd.bridge import NativeBridge, NativeUdpFront
+
+    n = 3
+    e = make_oracle(n, lookahead_ns=WINDOW * 1000)
+    for i in range(n):
+        e.configure(i, nw.Config(Network="default", Enable=True, Default=nw.LinkShape(Latency=3 * nw.Millisecond)))
+    b = NativeBridge(e, n, WINDOW)
+    front = NativeUdpFront(b)
+    socks, vaddr = [], []
+    try:
+        for i in range(n):
+            s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            s.bind(("127.0.0.1", 0))
+            s.settimeout(5)
+            front.register(i, s.getsockname())
+            socks.append(s)
+            vaddr.append(front.bind_peer(i))
+        for k in range(20):  # plain datagrams, addressed by the peer's data address only
+            socks[0].sendto(b"ping%02d" % k, vaddr[1 + k % 2])
+        socks[2].sendto(b"pong", vaddr[0])
+        time.sleep(0.05)
+        t0 = b.now_tick
+        delivered = sum(front.pump() for _ in range(6))
+        assert delivered == 21
+        got1 = sorted(socks[1].recvfrom(65536) for _ in range(10))
+        assert [m for m, _ in got1] == sorted(b"ping%02d" % k for k in range(0, 20, 2))
+        assert all(addr == vaddr[0] for _, addr in got1)  # the source's data address, no header
+        msg, addr = socks[0].recvfrom(65536)
+        assert msg == b"pong" and addr == vaddr[2]
+        assert b.now_tick - t0 == 6 * WINDOW and b.in_flight() == 0
+    finally:
+        front.close()
+        for s in socks:
+            s.close()
