@@ -317,6 +317,8 @@ struct tgsim_engine_s {
   bool order_valid = false;
   int order_by = 0;          // TGSIM_ORDER_BY: 0 HTB records of the last step, 1 its k_sim time per source
   DevBuf<uint32_t> d_dur;
+  DevBuf<uint32_t> d_chain;  // fused groups: each source's measured chain of windows (next group's order)
+  bool order_chain = true;   // TGSIM_FUSED_ORDER: chain (default) or records (the last window's HTB records)
   // fused windows (tgsim_step_n): per group parity p and window i the emit regions, their counts
   // and the per-destination histogram; ev_fgrp[p]: after the deliveries that last read set p
   struct LocalSet {
@@ -328,8 +330,9 @@ struct tgsim_engine_s {
   hipEvent_t ev_fgrp[2] = {};
   uint32_t fgrp = 0;                    // parity of the next fused group
   DevBuf<uint8_t> f_verdict[kFuseMax];  // verdicts of a group's windows but the last (discarded)
-  DevBuf<uint32_t> d_ticket;            // ticket counter of the fused launches
-  uint32_t ticket_no = 0;               // tickets issued by fused launches so far
+  DevBuf<uint32_t> d_done, d_ticket;    // per-source completion words (window-major), ticket counter
+  uint32_t step_no = 0, ticket_no = 0;  // windows and tickets issued by fused launches so far
+  bool source_major = false;            // TGSIM_FUSED_MAJOR=source: k_sim_fused_sm
   uint64_t fused_windows = 0;
   uint32_t fused_wgs = 0;
   bool persist_routed = false;  // TGSIM_FUSED_PERSIST: persistent grid for sharded (routed) groups too
@@ -736,6 +739,8 @@ int harvest_timing(Eng* E, bool wait) {
 int check_sim_error(Eng* E) {
   const uint64_t herr = E->h_err ? __atomic_load_n(E->h_err, __ATOMIC_RELAXED) : 0;
   if (herr & kErrTimeOverflow) return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
+  if (herr & kErrHandoff)
+    return E->fail(-EIO, "fused step: a source's previous window did not complete (hand-off timed out)");
   if (E->h_xerr && __atomic_load_n(E->h_xerr, __ATOMIC_RELAXED))
     return E->fail(-ENOSPC, "exchange: a step's records for one rank exceed the slot capacity");
   return 0;
@@ -1217,10 +1222,12 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   E->gen_q.erase(E->gen_q.begin(), E->gen_q.begin() + g);
   E->gen_q_ticks -= static_cast<uint64_t>(g) * n_ticks;
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_fgrp[p], 0));  // the deliveries that last read set p
-  if (!E->d_ticket.cap) {
+  if (E->d_done.cap < E->S) {
+    HIPCHK(E->d_done.ensure(E->S));
+    HIPCHK(hipMemsetAsync(E->d_done.p, 0, sizeof(uint32_t) * E->d_done.cap, E->st));
     HIPCHK(E->d_ticket.ensure(1));
     HIPCHK(hipMemsetAsync(E->d_ticket.p, 0, sizeof(uint32_t), E->st));
-    E->ticket_no = 0;
+    E->step_no = E->ticket_no = 0;
   }
   SimArgs a = base_sim_args(E);
   const bool ordered = E->S <= kOrderMaxSources;
@@ -1272,8 +1279,15 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   }
   f.n_win = g;
   f.prio_n = a.order ? E->prio_heavy : 0;
+  f.step_base = E->step_no;
   f.ticket_base = E->ticket_no;
   f.ticket = E->d_ticket.p;
+  f.done = E->d_done.p;
+  f.source_major = E->source_major ? 1u : 0u;
+  if (ordered && E->order_chain && E->source_major) {
+    HIPCHK(E->d_chain.ensure(E->S));
+    f.chain_dur = E->d_chain.p;
+  }
   hipEvent_t ev0, ev1;
   HIPCHK(take_event(E, &ev0));
   HIPCHK(take_event(E, &ev1));
@@ -1289,13 +1303,15 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.push_back({ev0, ev1, g});
-  // one ticket per source; every workgroup of the persistent grid claims until a claim fails, so the
-  // counter advances by the tickets plus one failed claim per workgroup (one claim per ticket otherwise)
-  E->ticket_no += E->S + (f.persistent ? std::min(E->fused_wgs, E->S) : 0u);
+  E->step_no += g;
+  // every workgroup of the persistent grid claims until a claim fails: the counter advances by the
+  // tickets (g per source window-major, one source-major) plus one failed claim per workgroup
+  const uint32_t tickets = E->source_major ? E->S : g * E->S;
+  E->ticket_no += tickets + (f.persistent ? std::min(E->fused_wgs, tickets) : 0u);
   E->fused_windows += g;
-  if (ordered) {  // the next launch's dispatch order, from the last window's HTB records
+  if (ordered) {  // the next launch's dispatch order: longest measured chains first (or the last window's HTB records)
     HIPCHK(E->d_order.ensure(E->S));
-    launch_order(E->fset[p][g - 1].emit_n.p, E->S, E->d_order.p, E->st);
+    launch_order(f.chain_dur ? f.chain_dur : E->fset[p][g - 1].emit_n.p, E->S, E->d_order.p, E->st);
     HIPCHK(hipGetLastError());
     E->order_valid = true;
   }
@@ -1524,6 +1540,8 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
+  if (const char* fo = getenv("TGSIM_FUSED_ORDER")) E->order_chain = strcmp(fo, "records") != 0;
+  if (const char* fm = getenv("TGSIM_FUSED_MAJOR")) E->source_major = strcmp(fm, "source") == 0;
   if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) {
     E->persist_routed = atoi(fp) != 0;
     E->persist_env = true;
@@ -1622,7 +1640,7 @@ void tgsim_destroy(void* e) {
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release();
+  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release(); E->d_chain.release();
   E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release();
   for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
   for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
@@ -1634,7 +1652,7 @@ void tgsim_destroy(void* e) {
     for (auto& ls : grp) { ls.emit.release(); ls.emit_n.release(); }
   for (auto& v : E->f_lcnt) v.release();
   for (auto& v : E->f_verdict) v.release();
-  E->d_ticket.release();
+  E->d_done.release(); E->d_ticket.release();
   for (hipEvent_t ev : E->ev_fgrp)
     if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : E->ev_pool) (void)hipEventDestroy(ev);
@@ -2214,9 +2232,12 @@ int64_t tgsim_debug_carry_bytes(void* e) {
   if (rc) return rc;
   std::vector<unsigned long long> all(static_cast<size_t>(kStSlots) * kStatCopies);
   HIPCHK(hipMemcpy(all.data(), E->d_stats.p, sizeof(unsigned long long) * all.size(), hipMemcpyDeviceToHost));
-  unsigned long long n = 0;
-  for (uint32_t c = 0; c < kStatCopies; ++c) n += all[static_cast<size_t>(c) * kStSlots + kStCarry];
-  return static_cast<int64_t>(n);
+  unsigned long long q = 0, skipped = 0;  // the per-window model minus what stayed in LDS
+  for (uint32_t c = 0; c < kStatCopies; ++c) {
+    q += all[static_cast<size_t>(c) * kStSlots + kStQueue];
+    skipped += all[static_cast<size_t>(c) * kStSlots + kStCarrySkip];
+  }
+  return static_cast<int64_t>(q - skipped);
 }
 
 int64_t tgsim_debug_fused_windows(void* e) {

@@ -74,7 +74,7 @@ struct CfgPatch {
 enum StatSlot {
   kStOffered = 0, kStScheduled, kStCloned, kStCorrupted, kStVerdict0,  // 4..11 verdicts
   kStBytes = 12, kStErr = 13, kStQueue = 14, kStLost = 15, kStFlushed = 16,
-  kStCarry = 17,  // queue state bytes the simulate kernels actually moved (a fused group: once per group)
+  kStCarrySkip = 17,  // modeled queue state bytes a source-major fused group kept in LDS (never moved)
   kStSlots = 20
 };
 // Counters are spread over kStatCopies copies (workgroup w adds into copy w % kStatCopies) so that
@@ -111,9 +111,11 @@ struct SimArgs {
 };
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 
-// Fused launch of up to kFuseMax consecutive windows (k_sim_fused), source-major: ticket t -> the
-// t-th source in dispatch order, whose windows one wavefront runs back to back;
-// the windows differ only in these per-window fields.
+// Fused launch of up to kFuseMax consecutive windows (k_sim_fused).  Window-major:
+// ticket t -> window t / S of the (t % S)-th source in dispatch order, started once the source's
+// window k - 1 has stored done[s] = step_base + k (the hand-off).  Source-major (k_sim_fused_sm):
+// ticket t -> the t-th source, whose windows one wavefront runs back to back.  The windows differ
+// only in these per-window fields.
 constexpr uint32_t kFuseMax = 8;
 struct FusedWindow {
   const uint64_t* off;
@@ -127,12 +129,18 @@ struct FusedWindow {
 struct FusedArgs {
   FusedWindow w[kFuseMax];
   uint32_t n_win;
+  uint32_t step_base;   // done[] value that window 0's predecessors have reached (window-major)
   uint32_t ticket_base; // *ticket before this launch (tickets are counted across launches)
   uint32_t* ticket;
+  uint32_t* done;       // [S] last completed window of each source (wrapping step counter; window-major)
+  uint32_t source_major;
   uint32_t prio_n;      // tickets at dispatch positions below prio_n run at wave priority 3
   uint32_t persistent;  // 1: a grid of resident workgroups claims tickets until none is left; 0: one
                         // workgroup per ticket (the slots turn over, so an exchange can be dispatched)
+  uint32_t* chain_dur;  // [S] each source's chain of windows in 10-ns ticks (the next group's dispatch
+                        // weight; source-major), or null
 };
+constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
 // Local delivery of a fused group: window w's emit regions, counts and CSR offsets; pos holds the
 // scatter cursors of the g * n_dst (window, destination) segments.
 struct GroupDeliver {

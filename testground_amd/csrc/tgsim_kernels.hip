@@ -768,19 +768,34 @@ __device__ __forceinline__ uint4 make_item(uint64_t e, uint32_t len, uint32_t fl
 // The carried netem queue and departure ring move between HBM and LDS with bounded buffer loads
 // and stores: the resource covers exactly the live entries, so a lane past the end reads 0 without
 // touching memory (one load instruction per 64 slots, no per-lane bounds branch).
+//
+// Hand-off of a source's carried state between the windows of one window-major fused launch
+// (k_sim_fused): window k+1 of a source may run on another CU or XCD than window k, inside the same
+// kernel, where neither the L1s nor the per-XCD L2s are coherent.  The producer writes every
+// handed-off byte with write-through (sc1) stores, drains them (vmcnt(0)), then one lane stores the
+// source's completion word; the consumer polls that word and reads every handed-off byte with
+// L1-bypassing sc1 buffer loads (MI355X_MICROARCH.md, "Valid forms", first row of the hand-off table).
 using v4u = unsigned int __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;  // buffer cache-policy bit SC1 (gfx940+)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t region(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
+template <int kPol>
 __device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kPol));
 }
+template <int kPol>
 __device__ __forceinline__ uint64_t ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+  return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, kPol));
 }
+template <int kPol>
 __device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)off, 0, kPol);
 }
+struct StatePair {
+  uint4 lo, hi;
+};
+static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
 
 // What a source carries from one window to the next when both run in the same wavefront
 // (k_sim_fused runs each source's windows back to back: the queue stays in LDS, only these
@@ -799,7 +814,10 @@ constexpr uint32_t kPhLoad = 1, kPhStore = 2;  // sim_source phases: queue from 
 // still in LDS from the source's previous window.  ph & kPhStore: they go back to HBM at the end;
 // otherwise into *carry.  *claim (when given) is the workgroup's next ticket, claimed before the
 // write-back so that the atomic's round trip overlaps the stores; returned minus claim_base.
-template <bool kOpen, uint32_t kCap>
+// kMode: 0 plain loads and stores (k_sim, k_sim_list); 1 the HBM state is handed off inside a
+// window-major fused launch (bounded sc1 loads and stores); 2 source-major fused (bounded loads).
+constexpr int kModePlain = 0, kModeHandoff = 1, kModeSourceMajor = 2;
+template <bool kOpen, uint32_t kCap, int kMode = kModePlain>
 __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
                                                uint32_t* claim = nullptr, uint32_t claim_base = 0,
                                                SrcCarry* carry = nullptr, uint32_t ph = kPhLoad | kPhStore) {
@@ -809,9 +827,16 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   const uint64_t t_begin = a.dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const SrcParams pp = a.params[s];
   const bool load = (ph & kPhLoad) != 0;
+  constexpr bool kH = kMode == kModeHandoff, kBounded = kMode != kModePlain;
+  constexpr int kPol = kH ? kSc1 : 0;
   SrcState st;  // dead after the set-up: the end writes a fresh state
   if (load) {
-    st = a.state[s];
+    if constexpr (kH) {
+      const auto rs = region(a.state + s, sizeof(SrcState));
+      st = __builtin_bit_cast(SrcState, (StatePair{ld16<kSc1>(rs, 0), ld16<kSc1>(rs, 16)}));
+    } else {
+      st = a.state[s];
+    }
   } else {
     st.tat = carry->tat;
     st.last_dup = carry->last_dup;
@@ -847,12 +872,22 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     // wait for each chunk inside its branch)
     uint64_t rv[kCap / kWave];
     uint4 qv[kCap / kWave];
-    const auto rr = region(gr, 8u * rn), rq = region(gh, 16u * qn);
+    if constexpr (kBounded) {
+      const auto rr = region(gr, 8u * rn), rq = region(gh, 16u * qn);
 #pragma unroll
-    for (uint32_t u = 0; u < kCap / kWave; ++u) {
-      const uint32_t k = u * kWave + lane;
-      rv[u] = ld8(rr, 8u * k);
-      qv[u] = ld16(rq, 16u * k);
+      for (uint32_t u = 0; u < kCap / kWave; ++u) {
+        const uint32_t k = u * kWave + lane;
+        rv[u] = ld8<kPol>(rr, 8u * k);
+        qv[u] = ld16<kPol>(rq, 16u * k);
+      }
+    } else {  // a lane past the end re-reads the last entry (the same line as its neighbours)
+      const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0;
+#pragma unroll
+      for (uint32_t u = 0; u < kCap / kWave; ++u) {
+        const uint32_t k = u * kWave + lane;
+        rv[u] = gr[k < rn ? k : rl];
+        qv[u] = gh[k < qn ? k : ql];
+      }
     }
     // every load issued before the partition's ballots, which the scheduler would otherwise
     // interleave with them (one HBM round trip per chunk)
@@ -928,7 +963,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   if (lane == 0 && (Q.qn | Q.pn | Q.fn | Q.rn)) {  // the queue state at the start (the end's is added there)
     const unsigned long long b0 = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
     atomicAdd(&sc[kStQueue], b0);  // the per-window model (bit-exact with the oracle)
-    if (load) atomicAdd(&sc[kStCarry], b0);  // what this call actually read from HBM
+    if (!load) atomicAdd(&sc[kStCarrySkip], b0);  // still in LDS: not read from HBM
   }
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
@@ -1322,13 +1357,19 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   if (ph & kPhStore) {
     // ---- write back the compacted ring (16-B stores, two entries each), the queue (near, then
     // pool) and the state
-    const auto rr = region(a.ring + (size_t)s * kHeapCap, kHeapCap * 8u);
-    const auto rq = region(a.heap + (size_t)s * kHeapCap, kHeapCap * 16u);
-    for (uint32_t k = lane; 2 * k < Q.rn; k += kWave) {
-      const uint64_t d0 = Q.ring_d(2 * k), d1 = Q.ring_d(2 * k + 1);
-      st16(rr, 16u * k, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)));
+    uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+    uint4* gh = a.heap + (size_t)s * kHeapCap;
+    if constexpr (kH) {  // 16-B write-through stores (two ring entries per store)
+      const auto rr = region(gr, kHeapCap * 8u), rq = region(gh, kHeapCap * 16u);
+      for (uint32_t k = lane; 2 * k < Q.rn; k += kWave) {
+        const uint64_t d0 = Q.ring_d(2 * k), d1 = Q.ring_d(2 * k + 1);
+        st16<kSc1>(rr, 16u * k, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)));
+      }
+      for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) st16<kSc1>(rq, 16u * k, Q.slot(Q.rn + k));
+    } else {
+      for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
+      for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
     }
-    for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) st16(rq, 16u * k, Q.slot(Q.rn + k));
     if (lane == 0) {
       SrcState ns;
       ns.tat = Q.tat;
@@ -1338,7 +1379,14 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
       ns.last_dup = last_dup;
       ns.last_cor = last_cor;
       ns.last_reo = last_reo;
-      a.state[s] = ns;
+      if constexpr (kH) {
+        const auto rs = region(a.state + s, sizeof(SrcState));
+        const StatePair sp = __builtin_bit_cast(StatePair, ns);
+        st16<kSc1>(rs, 0, sp.lo);
+        st16<kSc1>(rs, 16, sp.hi);
+      } else {
+        a.state[s] = ns;
+      }
     }
   } else {
     carry->rh = Q.rh;
@@ -1374,7 +1422,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     if (lost) atomicAdd(&sc[kStLost], (unsigned long long)lost);
     if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
-    if (qbytes && (ph & kPhStore)) atomicAdd(&sc[kStCarry], (unsigned long long)qbytes);
+    if (qbytes && !(ph & kPhStore)) atomicAdd(&sc[kStCarrySkip], (unsigned long long)qbytes);
     if (err) {
       atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
       if (a.err_host)  // the host's pinned copy (sticky; read at its sync points)
@@ -1396,19 +1444,81 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
 }
 
-// Several consecutive windows in one launch (tgsim_step_n), SOURCE-MAJOR: a source's windows are
-// sequential anyway (window k + 1 starts from the queue window k leaves), so one wavefront runs all
-// of them back to back with the queue resident in LDS, loaded from HBM before the first window and
-// stored after the last (one HBM round trip of the queue per group, not per window; no hand-off
-// between CUs).  Sources are taken heaviest first (the dispatch order of the last window's HTB
-// records), so the longest chains start first.  Persistent: the grid is what fits on the chip at
-// once and each workgroup claims sources in order until none is left (its next claim issued during
-// the current source's write-back); otherwise one workgroup per source (the slots turn over, so an
-// exchange can be dispatched beside the launch).
+// Several consecutive windows in one launch (tgsim_step_n).  Window k + 1 of a source depends only
+// on the source's own state after window k, so the next window's heavy sources fill the CUs that the
+// last dispatch round of this window leaves idle (one launch tail and one launch gap per fused group
+// instead of one per window).  Persistent: the grid is what fits on the chip at once, and each
+// workgroup takes tickets in order until none is left (its next ticket claimed during the write-back
+// of the current one), so no slot waits for a workgroup dispatch between two sources.
 struct FusedSim {
   SimArgs w[kFuseMax];  // window k's arguments (tables and state shared, step fields its own)
 };
+// Window k's arguments read in place in the kernel-argument segment (scalar loads of invariant
+// memory: re-read when needed instead of held in spilled SGPRs).
+__device__ __forceinline__ const SimArgs& kernarg_window(uint32_t k) {
+  using KernargSimArgs = __attribute__((address_space(4))) const SimArgs;
+  const KernargSimArgs* ka =
+      (KernargSimArgs*)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                        k * sizeof(SimArgs));
+  return *(const SimArgs*)ka;
+}
+
+// WINDOW-MAJOR (the default): ticket t is window t / S of the (t mod S)-th source in dispatch
+// order; a ticket of window k > 0 polls its source's completion word until window k - 1 has stored
+// it, and the queue crosses HBM between the windows (the sc1 hand-off above).  Every claimed ticket
+// is held by a resident workgroup and waits only for a lower ticket, so the lowest unfinished ticket
+// can always run: no deadlock; the wait is bounded anyway (kErrHandoff, then the host reports -EIO).
+// Tickets interleave the windows of all sources at a granularity of one source-window, which keeps
+// the launch's tail short (A/B against the source-major form below: DESIGN.md §5.2).
 __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f) {
+  const SimArgs& a0 = fs.w[0];
+  __shared__ SimLdsT<kHeapCap> lds;
+  const uint32_t total = f.n_win * a0.n_src;
+  uint32_t t = 0;
+  if (threadIdx.x == 0) t = atomicAdd(f.ticket, 1u) - f.ticket_base;
+  t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+  while (t < total) {
+    const uint32_t k = t / a0.n_src, pos = t - k * a0.n_src;
+    const uint32_t s = a0.order ? a0.order[pos] : pos;
+    // the heaviest sources (first in dispatch order) chain their windows through the launch: their
+    // waves issue first on their SIMDs, so the chain is not the launch's critical path
+    if (pos < f.prio_n) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);
+    if (k) {
+      const uint32_t need = f.step_base + k;
+      uint32_t late = 0;
+      if (threadIdx.x == 0) {
+        for (uint32_t spin = 0;
+             (int32_t)(__hip_atomic_load(f.done + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - need) < 0;) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spin > (1u << 22)) {
+            late = 1;
+            break;
+          }
+        }
+      }
+      if (__builtin_amdgcn_readfirstlane((int)late) && threadIdx.x == 0) {
+        atomicOr(&a0.stats[kStErr], (unsigned long long)kErrHandoff);
+        if (a0.err_host)
+          __hip_atomic_store(a0.err_host, (uint64_t)kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    const uint32_t next = sim_source<false, kHeapCap, kModeHandoff>(kernarg_window(k), s, t, lds,
+                                                            f.persistent ? f.ticket : nullptr, f.ticket_base);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
+    if (threadIdx.x == 0)
+      __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!f.persistent) break;  // one ticket per workgroup: the dispatcher interleaves other streams' work
+    t = next;
+  }
+}
+
+// SOURCE-MAJOR (TGSIM_FUSED_MAJOR=source): one wavefront runs all of a source's windows back to back
+// with the queue resident in LDS, loaded before the first window and stored after the last (one HBM
+// round trip of the queue per group, no hand-off), sources taken longest measured chain first.
+// Bit-exact with the window-major form, and 3 % less work, but its tail is coarse: a chain is a
+// whole group of windows, and chains mispredicted long start late.
+__global__ __launch_bounds__(kWave, 3) void k_sim_fused_sm(FusedSim fs, FusedArgs f) {
   const SimArgs& a0 = fs.w[0];
   __shared__ SimLdsT<kHeapCap> lds;
   const uint32_t total = a0.n_src;
@@ -1417,26 +1527,22 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f
   t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   while (t < total) {
     const uint32_t s = a0.order ? a0.order[t] : t;
-    // the heaviest sources (first in dispatch order) run at wave priority 3: their chains of
-    // windows are the launch's longest
     if (t < f.prio_n) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(0);
     SrcCarry c;
     uint32_t next = 0;
+    const uint64_t tc0 = f.chain_dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for (uint32_t k = 0; k < f.n_win; ++k) {
-      // window k's arguments read in place in the kernel-argument segment (scalar loads of
-      // invariant memory: re-read when needed instead of held in spilled SGPRs)
-      using KernargSimArgs = __attribute__((address_space(4))) const SimArgs;
-      const KernargSimArgs* ka =
-          (KernargSimArgs*)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                            k * sizeof(SimArgs));
-      const SimArgs& a = *(const SimArgs*)ka;
       const bool last = k + 1 == f.n_win;
       const uint32_t ph = (k == 0 ? kPhLoad : 0u) | (last ? kPhStore : 0u);
-      next = sim_source<false, kHeapCap>(a, s, k * total + t, lds, last && f.persistent ? f.ticket : nullptr,
-                                         f.ticket_base, &c, ph);
+      next = sim_source<false, kHeapCap, kModeSourceMajor>(kernarg_window(k), s, k * total + t, lds,
+                                         last && f.persistent ? f.ticket : nullptr, f.ticket_base, &c, ph);
     }
-    if (!f.persistent) break;  // one source per workgroup: the dispatcher interleaves other streams' work
+    if (f.chain_dur && threadIdx.x == 0) {  // longest chains first in the next group (LPT)
+      const uint64_t d = __builtin_amdgcn_s_memrealtime() - tc0;
+      f.chain_dur[s] = d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
+    }
+    if (!f.persistent) break;
     wave_lds_sync();  // the write-back's LDS reads are done before the next source's loads land
     t = next;
   }
@@ -1711,7 +1817,6 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
     if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
     if (t_bytes) atomicAdd(&sc[kStBytes], (unsigned long long)t_bytes);
     if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
-    if (qb) atomicAdd(&sc[kStCarry], (unsigned long long)qb);
     if (err) {
       atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
       if (a.err_host)
@@ -2573,7 +2678,7 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
 }
 
 void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st) {
-  const uint32_t total = a.n_src;  // source-major: one ticket per source
+  const uint32_t total = f.source_major ? a.n_src : f.n_win * a.n_src;  // tickets
   FusedSim fs;
   for (uint32_t k = 0; k < kFuseMax; ++k) {
     fs.w[k] = a;
@@ -2588,7 +2693,9 @@ void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipSt
     fs.w[k].t0_ns = w.t0_ns;
     fs.w[k].horizon_ns = w.horizon_ns;
   }
-  hipLaunchKernelGGL(k_sim_fused, dim3(f.persistent && n_wg < total ? n_wg : total), dim3(kWave), 0, st, fs, f);
+  const dim3 grid(f.persistent && n_wg < total ? n_wg : total);
+  if (f.source_major) hipLaunchKernelGGL(k_sim_fused_sm, grid, dim3(kWave), 0, st, fs, f);
+  else hipLaunchKernelGGL(k_sim_fused, grid, dim3(kWave), 0, st, fs, f);
 }
 
 uint32_t sim_fused_resident() {
