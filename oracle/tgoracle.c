@@ -1143,3 +1143,14 @@ int64_t tgo_gossip_reached(void* p, uint64_t* out, size_t cap) {
     }
     return o->g.n_floods;
 }
+
+/* Diagnostics (test infrastructure only): source s's departure ring (oldest first) and queued
+ * items' eligibility times (heap order).  Returns ring_n << 32 | heap_n. */
+int64_t tgo_debug_queue(void* p, uint32_t s, uint64_t* ring_d, uint64_t* item_e) {
+    oracle* o = (oracle*)p;
+    if (!o || s >= o->nsrc) return -EINVAL;
+    const source* S = &o->src[s];
+    for (uint32_t k = 0; k < S->ring_n; ++k) ring_d[k] = S->ring[(S->ring_head + k) % HCAP];
+    for (uint32_t k = 0; k < S->heap_n; ++k) item_e[k] = S->heap[k].e;
+    return ((int64_t)S->ring_n << 32) | S->heap_n;
+}

@@ -1470,9 +1470,12 @@ __device__ __forceinline__ const SimArgs& kernarg_window(uint32_t k) {
 // can always run: no deadlock; the wait is bounded anyway (kErrHandoff, then the host reports -EIO).
 // Tickets interleave the windows of all sources at a granularity of one source-window, which keeps
 // the launch's tail short (A/B against the source-major form below: DESIGN.md §5.2).
+#ifndef TGSIM_FUSED_CAP
+#define TGSIM_FUSED_CAP kHeapCap
+#endif
 __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f) {
   const SimArgs& a0 = fs.w[0];
-  __shared__ SimLdsT<kHeapCap> lds;
+  __shared__ SimLdsT<TGSIM_FUSED_CAP> lds;
   const uint32_t total = f.n_win * a0.n_src;
   uint32_t t = 0;
   if (threadIdx.x == 0) t = atomicAdd(f.ticket, 1u) - f.ticket_base;
@@ -1503,7 +1506,7 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f
           __hip_atomic_store(a0.err_host, (uint64_t)kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    const uint32_t next = sim_source<false, kHeapCap, kModeHandoff>(kernarg_window(k), s, t, lds,
+    const uint32_t next = sim_source<false, TGSIM_FUSED_CAP, kModeHandoff>(kernarg_window(k), s, t, lds,
                                                             f.persistent ? f.ticket : nullptr, f.ticket_base);
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
     if (threadIdx.x == 0)
