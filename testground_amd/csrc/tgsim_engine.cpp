@@ -312,6 +312,7 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_order;  // dispatch order of the next k_sim, computed behind this one
   DevBuf<uint32_t> d_work;   // sparse steps: k_sim_sparse's deferred sources, [0] = count, then ids
   int sparse_mode = -1;      // TGSIM_SPARSE: -1 auto, 0 never, 1 always
+  bool fold_recv = true;     // TGSIM_FOLD_RECV: single-shard gossip receipts folded into k_sim
   bool sparse_seen = false;  // h_work holds a measured worklist size
   uint32_t dense_streak = 0; // dense steps chosen because the last sparse step deferred too much
   bool order_valid = false;
@@ -837,6 +838,13 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     }
     a.dst_cnt = reinterpret_cast<unsigned long long*>(E->d_lcnt.p);
   }
+  if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard
+    a.g_first = E->d_gfirst.p;
+    a.g_pend = E->d_gpend.p;
+    a.g_fwd = E->d_gfwd.p;
+    a.g_floods = E->gossip.n_floods;
+    a.g_degree = E->gossip.degree;
+  }
   // Sparse steps (few packets per source, or more sources than the order kernel ranks): open
   // queues run in the register-only k_sim_sparse, the rest in k_sim_list; dense steps: k_sim in
   // heavy-first order.  The results are the same either way.
@@ -1077,6 +1085,17 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
     HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, sq));
   }
   HIPCHK(E->d_dpos.ensure(nseg));
+  if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins), straight
+                       // from the inbound records on the simulate stream, where the next window's
+                       // generation runs: it waits for the records' arrival, not for any sort; records
+                       // of this shard's own sources were folded in at emission
+    if (!(E->fold_recv && E->S == E->N)) {
+      if (wait) HIPCHK(hipStreamWaitEvent(E->st, wait, 0));
+      launch_gossip_recv_in(gossip_args(E, 0, 0), in, n, slot, E->fold_recv, E->st);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(E->ev_recv, E->st));
+  }
   launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq, slot, n_win);
   HIPCHK(hipGetLastError());
   int rc = 0;
@@ -1102,17 +1121,12 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
   launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq, slot, n_win);
   HIPCHK(hipGetLastError());
-  if (E->gossip_on) {  // receipts of the gossip workload (order-free: earliest tick wins)
-    if (slot) launch_gossip_recv_dev(gossip_args(E, 0, 0), E->d_scatter.p, E->d_dtot.p, sq);
-    else launch_gossip(gossip_args(E, 0, 0), in, n, nullptr, nullptr, nullptr, 0, sq);
-    HIPCHK(hipGetLastError());
-  }
   if (slot && !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES)) {  // the drain needs the record count
     HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
     HIPCHK(hipStreamSynchronize(sq));
     n = E->h_dtot;
   }
-  HIPCHK(hipEventRecord(E->ev_recv, sq));  // the next window's generation needs no more than this
+  if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
   tgsim_delivery* dst = nullptr;
   rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
@@ -1147,7 +1161,7 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, const uint32_t* emit_
     n = E->h_dtot;
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq);
+  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in);
   HIPCHK(hipGetLastError());
   if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
   tgsim_delivery* dst = nullptr;
@@ -1170,10 +1184,13 @@ int deliver_local(Eng* E) {
   hipStream_t sq = E->dst_st;
   HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
   HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
-  if (E->gossip_on) {  // receipts of the gossip workload, from the emit regions on the simulate
-                       // stream: the next window's generation waits for nothing on the delivery side
-    launch_gossip_recv_emit(gossip_args(E, 0, 0), E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, E->st);
-    HIPCHK(hipGetLastError());
+  if (E->gossip_on) {  // receipts of the gossip workload: folded into k_sim at emission, or read
+                       // from the emit regions on the simulate stream (TGSIM_FOLD_RECV=0); the next
+                       // window's generation waits for nothing on the delivery side
+    if (!E->fold_recv) {
+      launch_gossip_recv_emit(gossip_args(E, 0, 0), E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, E->st);
+      HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
   }
 
@@ -1539,6 +1556,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
+  if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
   if (const char* fo = getenv("TGSIM_FUSED_ORDER")) E->order_chain = strcmp(fo, "records") != 0;
   if (const char* fm = getenv("TGSIM_FUSED_MAJOR")) E->source_major = strcmp(fm, "source") == 0;

@@ -108,6 +108,12 @@ struct SimArgs {
   uint32_t* worklist;       // sparse steps: sources k_sim_sparse left for k_sim_list
   uint32_t* worklist_n;     // their count (zeroed before k_sim_sparse)
   uint32_t* dur;            // per source: this step's k_sim time in 10-ns ticks (dispatch weight), or null
+  // Gossip receipts folded into the simulate kernels (single shard, GossipArgs' tables), or null:
+  // every emitted record is a receipt at its destination the moment its delivery time is known
+  uint32_t* g_first;        // [s][64] earliest receipt tick
+  uint64_t* g_pend;         // [s] received, not yet forwarded
+  const uint64_t* g_fwd;    // [s] forwarded (stable during the step: written by k_gossip_write before it)
+  uint32_t g_floods, g_degree;
 };
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 

@@ -189,6 +189,39 @@ __device__ __forceinline__ uint64_t delayed(const SrcParams& p, uint64_t T, uint
   return delay > 0 ? T + (uint64_t)delay : T;
 }
 
+// Gossip receipt of one emitted record (single shard; what k_gossip_recv does at delivery): the
+// earliest receipt tick of flood seq / degree at the destination, which becomes pending unless it
+// has forwarded the flood already (fw: the destination's forwarded mask).  Receipts are order-free
+// (the earliest tick wins), so folding them in at emission changes no result; the atomics return
+// nothing, so the wave never waits for them.  Only destinations of this shard are folded in; the
+// others' receipts are taken where their records are delivered (k_gossip_recv_in).
+struct RecvFold {
+  uint32_t* first;
+  uint64_t* pend;
+  const uint64_t* fwd;
+  uint32_t floods, degree, shard_begin, n_local;
+  uint64_t tick_ns;
+  double inv_tick;
+};
+__device__ __forceinline__ RecvFold recv_fold(const SimArgs& a) {
+  return RecvFold{a.g_first, a.g_pend,  a.g_fwd,   a.g_floods,
+                  a.g_degree, a.shard_begin, a.n_src, a.tick_ns, 1.0 / (double)a.tick_ns};
+}
+__device__ __forceinline__ void fold_receipt(const RecvFold& g, uint32_t dst, uint32_t seq, uint32_t flags, uint64_t d,
+                                             uint64_t fw) {
+  const uint32_t f = seq / g.degree, s = dst - g.shard_begin;
+  if (s >= g.n_local || f >= g.floods || (flags & TGSIM_FLAG_CORRUPT) || (fw >> f & 1ull)) return;
+  // t = d / tick + 1 without a 64-bit division: d < 2^46 is exact in a double, and the estimate is
+  // off by at most one
+  uint64_t q = (uint64_t)((double)d * g.inv_tick);
+  const int64_t r = (int64_t)(d - q * g.tick_ns);
+  q = r < 0 ? q - 1 : (uint64_t)r >= g.tick_ns ? q + 1 : q;
+  uint64_t t = q + 1;
+  if (t > 0xFFFFFFFEull) t = 0xFFFFFFFEull;
+  __hip_atomic_fetch_min(&g.first[(uint64_t)s * 64 + f], (uint32_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_or(&g.pend[s], 1ull << f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ uint32_t fib_lookup(const Interval* iv, uint32_t n, uint32_t ip) {
   uint32_t lo = 0, hi = n;  // binary search over sorted disjoint intervals
   while (lo < hi) {
@@ -299,6 +332,7 @@ struct SimQueue {
   uint64_t tat;             // HTB theoretical arrival time
   tgsim_delivery* emit;
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
+  RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
   uint32_t sched, corrupted, lost;
@@ -375,6 +409,8 @@ struct SimQueue {
         rw[1] = ((uint64_t)qi.w << 32) | src;
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
         if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
+        if (rf.first && qi.w - rf.shard_begin < rf.n_local)
+          fold_receipt(rf, qi.w, qi.z, flags, d, rf.fwd[qi.w - rf.shard_begin]);
         sched++;
         bytes += len;
         corrupted += (flags >> 1) & 1u;
@@ -817,7 +853,7 @@ constexpr uint32_t kPhLoad = 1, kPhStore = 2;  // sim_source phases: queue from 
 // kMode: 0 plain loads and stores (k_sim, k_sim_list); 1 the HBM state is handed off inside a
 // window-major fused launch (bounded sc1 loads and stores); 2 source-major fused (bounded loads).
 constexpr int kModePlain = 0, kModeHandoff = 1, kModeSourceMajor = 2;
-template <bool kOpen, uint32_t kCap, int kMode = kModePlain>
+template <bool kOpen, uint32_t kCap, int kMode = kModePlain, bool kRecv = false>
 __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
                                                uint32_t* claim = nullptr, uint32_t claim_base = 0,
                                                SrcCarry* carry = nullptr, uint32_t ph = kPhLoad | kPhStore) {
@@ -855,6 +891,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
+  Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
 #ifdef TGSIM_PROFILE
@@ -1444,6 +1481,14 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
   sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
 }
 
+// k_sim with the gossip receipts folded in (a dense window of the single-shard gossip loop).
+__global__ __launch_bounds__(kWave) void k_sim_recv(SimArgs a) {
+  __shared__ SimLdsT<kHeapCap> lds;
+  const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
+  if (s >= a.n_src) return;
+  sim_source<false, kHeapCap, kModePlain, true>(a, s, blockIdx.x, lds);
+}
+
 // Several consecutive windows in one launch (tgsim_step_n).  Window k + 1 of a source depends only
 // on the source's own state after window k, so the next window's heavy sources fill the CUs that the
 // last dispatch round of this window leaves idle (one launch tail and one launch gap per fused group
@@ -1689,6 +1734,19 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
     defer();
     return;
   }
+  // ---- write back the items HTB does not serve this step as the pool (no order needed); the
+  // registers holding the queue are free for the rest
+  uint4* wq = a.heap + (size_t)s * kHeapCap;
+  uint32_t wpos = 0;
+  auto keep = [&](bool f, const uint4& v) {
+    const uint64_t m = __ballot(f);
+    if (f) wq[wpos + (uint32_t)__popcll(m & below)] = v;
+    wpos += (uint32_t)__popcll(m);
+  };
+#pragma unroll
+  for (uint32_t u = 0; u < kSparseQ; ++u) keep(u * kWave + lane < qn && !due_q[u], q[u]);
+  keep(cand && !due_o, io);
+  keep(cand && cst == 2 && !due_c, ic);
   // ---- rank the served items by (e, seq, clone first) and put each in its rank's lane
   const bool hs = lane < ns;
   uint32_t rank = 0;
@@ -1703,6 +1761,12 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.z),
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.w));
   }
+  // the destinations' forwarded masks, for the receipts folded in below (in flight during the scan)
+  // (the 32-bit half of the mask that holds the record's flood bit: one register across the scan)
+  const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
+  const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
+                          ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
+                          : 0u;
   // ---- HTB: d = max(e, TAT before), TAT' = max(TAT, e - burst) + cost, one max-plus scan
   const uint64_t e = w0_of(x) & kEMask;
   const uint32_t xlen = x.y >> 14 & 0xFFFFu;
@@ -1729,6 +1793,7 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
     rw[1] = ((uint64_t)x.w << 32) | src;
     rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
     if (a.dst_cnt) atomicAdd(&a.dst_cnt[x.w], 1ull);
+    if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
     sched = 1;
     bytes = xlen;
     corrupted = (flags >> 1) & 1u;
@@ -1770,17 +1835,6 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
   const uint32_t sk0 = k0 > rn ? k0 - rn : 0u;        // served entries released
   if (hs && lane >= sk0) wr[old_kept + lane - sk0] = d;
   const uint32_t rn_new = old_kept + ns - sk0;
-  uint4* wq = a.heap + (size_t)s * kHeapCap;
-  uint32_t wpos = 0;
-  auto keep = [&](bool f, const uint4& v) {
-    const uint64_t m = __ballot(f);
-    if (f) wq[wpos + (uint32_t)__popcll(m & below)] = v;
-    wpos += (uint32_t)__popcll(m);
-  };
-#pragma unroll
-  for (uint32_t u = 0; u < kSparseQ; ++u) keep(u * kWave + lane < qn && !due_q[u], q[u]);
-  keep(cand && !due_o, io);
-  keep(cand && cst == 2 && !due_c, ic);
   if (lane == 0) {
     SrcState ns_;
     ns_.tat = tat_end;
@@ -1835,7 +1889,8 @@ __global__ __launch_bounds__(kWave) void k_sim_list(SimArgs a) {
   const uint32_t n = *a.worklist_n;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t s = a.worklist[i];
-    sim_source<false, kHeapCap>(a, s, s, lds);
+    if (a.g_first) sim_source<false, kHeapCap, kModePlain, true>(a, s, s, lds);
+    else sim_source<false, kHeapCap>(a, s, s, lds);
     wave_lds_sync();  // the write-back's LDS reads are done before the next source's loads land
   }
 }
@@ -2029,6 +2084,22 @@ __global__ __launch_bounds__(256) void k_gossip_recv_dev(GossipArgs g, const tgs
     gossip_recv_one(g, in[i]);
 }
 
+// Receipts of the records a shard receives, straight from the inbound buffer (flat, or slotted
+// chunks whose empty slots are skipped) before they are ordered: the next window's generation waits
+// for this kernel only.  skip_own: records from this shard's own sources were folded in at emission.
+__global__ __launch_bounds__(256) void k_gossip_recv_in(GossipArgs g, const tgsim_delivery* in, uint64_t n,
+                                                        uint64_t slot, uint32_t skip_own) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (slot) {
+      const uint64_t r = i / (slot + 1), j = i - r * (slot + 1);
+      if (j == 0 || j > in[r * (slot + 1)].t_ns) continue;
+    }
+    const tgsim_delivery rec = in[i];
+    if (skip_own && rec.src - g.shard_begin < g.n_src) continue;
+    gossip_recv_one(g, rec);
+  }
+}
+
 // The out-neighbour table (the hash of (seed, peer, k) once per peer and k, not at every forward).
 __global__ __launch_bounds__(256) void k_gossip_nbr(GossipArgs g, uint32_t* nbr) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2087,6 +2158,60 @@ __global__ __launch_bounds__(256) void k_gossip_count(GossipArgs g, uint64_t* co
     if (lane == i) c = n;
   }
   if (lane < kGossipPeers && s0 + lane < g.n_src) counts[s0 + lane] = c;
+}
+
+// Degree <= 8: every load is issued up front, in two dependent levels (the masks, offsets and the
+// 8 peers' neighbour lists, one per lane; then the pending receipt ticks), and nothing is read
+// after the first store.  The general kernel below re-read fwd[s], off[s] and the neighbours
+// between the record stores of one peer and the next (its loads could not pass stores that might
+// alias them): a chain of dependent round trips per peer.
+__global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint64_t* __restrict__ off,
+                                                       InRec* __restrict__ out) {
+  const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
+  if (s0 >= g.n_src) return;
+  const uint32_t deg = g.degree;
+  const bool pl = lane < kGossipPeers && s0 + lane < g.n_src;  // lane i < 8: peer s0 + i's words
+  const uint64_t pend_l = pl ? g.pend[s0 + lane] : 0ull;
+  const uint64_t fwd_l = pl ? g.fwd[s0 + lane] : 0ull;
+  const uint64_t off_l = pl ? off[s0 + lane] : 0ull;
+  // lane i * deg + k: neighbour k of peer s0 + i
+  const uint32_t nbr_l = lane < kGossipPeers * deg && s0 + lane / deg < g.n_src ? g.nbr[(uint64_t)s0 * deg + lane] : 0u;
+  uint64_t pend[kGossipPeers];
+  uint32_t t[kGossipPeers];
+#pragma unroll
+  for (uint32_t i = 0; i < kGossipPeers; ++i) {
+    pend[i] = readlane64(pend_l, i);
+    t[i] = (pend[i] >> lane & 1ull) ? g.first[(uint64_t)(s0 + i) * 64 + lane] : 0xFFFFFFFFu;
+  }
+  uint64_t due_l = 0;  // lane i: the floods peer s0 + i forwards in this window
+#pragma unroll
+  for (uint32_t i = 0; i < kGossipPeers; ++i) {
+    const bool me = gossip_due(g, pend[i], t[i], lane);
+    const uint64_t due = __ballot(me);
+    if (lane == i) due_l = due;
+    if (!due) continue;
+    // earliest receipt first, ties by flood id (seq order within a tick)
+    uint32_t rank = 0;
+    for (uint64_t m = due; m; m &= m - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      const uint32_t tj = readlane32(t[i], j);
+      rank += (tj < t[i] || (tj == t[i] && j < lane)) ? 1u : 0u;
+    }
+    if (!me) continue;
+    const uint64_t o = readlane64(off_l, i) + (uint64_t)rank * deg;
+    for (uint32_t k = 0; k < deg; ++k) {
+      InRec rec;
+      rec.dst = readlane32(nbr_l, i * deg + k);
+      rec.seq = lane * deg + k;
+      rec.tick = (uint32_t)(t[i] - g.win0);
+      rec.len = g.msg_len;
+      out[o + k] = rec;
+    }
+  }
+  if (pl && due_l) {
+    g.fwd[s0 + lane] = fwd_l | due_l;
+    g.pend[s0 + lane] = pend_l & ~due_l;  // receipts for a later window stay pending
+  }
 }
 
 __global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64_t* off, InRec* out) {
@@ -2398,6 +2523,38 @@ __global__ __launch_bounds__(256) void k_local_scatter(const tgsim_delivery* emi
   }
 }
 
+// The same with one lane per source (a few records each: the gossip windows): 64 sources' counts
+// and offsets in one coalesced load, then their records four at a time in lockstep, every load,
+// cursor atomic and store of a round independent of the others.  The wave per source above walks
+// its sources one after another, each behind four dependent round trips with 57 of 64 lanes idle.
+__global__ __launch_bounds__(256) void k_local_scatter_ls(const tgsim_delivery* __restrict__ emit,
+                                                          const uint32_t* __restrict__ emit_n,
+                                                          const uint64_t* __restrict__ off, uint32_t n_src,
+                                                          uint32_t dst_begin, uint64_t* pos,
+                                                          tgsim_delivery* __restrict__ out) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+  uint32_t n = 0;
+  const tgsim_delivery* base = emit;
+  if (s < n_src) {
+    n = emit_n[s];
+    base = emit + 2 * off[s] + (uint64_t)kHeapCap * s;
+  }
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(pos);
+  for (uint32_t i = 0; __ballot(i < n); i += 4) {
+    tgsim_delivery r[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (i + u < n) r[u] = base[i + u];
+    uint64_t at[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (i + u < n) at[u] = atomicAdd(&p[r[u].dst - dst_begin], 1ull);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (i + u < n) out[at[u]] = r[u];
+  }
+}
+
 // K5 for a fused group (tgsim_step_n): the g windows' histograms are ONE array of g * N counts
 // (window-major), so one scan, one scatter and one per-destination sort cover the whole group, and
 // the sorted output is the windows' deliveries one after the other (the drain order of g
@@ -2610,6 +2767,55 @@ __global__ __launch_bounds__(256) void k_dst_sort_group(tgsim_delivery* in, cons
   if (j == 0 && n) cnt[d] = 0;
 }
 
+// Ranks inside lane groups of G records (one destination each) with the keys in LDS: each lane
+// reads its group's keys as one 16-B word each, (t, src << 32 | seq), instead of five cross-lane
+// shuffles per key (k_dst_sort_group); only a packet and its duplicate share that key, and the
+// duplicate goes first.  Destinations with more than G records take the whole wavefront in turn
+// (sort_segment).
+template <uint32_t G>
+__global__ __launch_bounds__(256) void k_dst_sort_lds(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
+                                                      uint32_t n_dst, tgsim_delivery* out) {
+  constexpr uint32_t kPer = kWave / G;
+  __shared__ ulonglong2 keys[256];
+  __shared__ uint32_t orig[256];
+  const uint32_t wv = threadIdx.x >> 6, w = blockIdx.x * 4 + wv;
+  const uint32_t lane = threadIdx.x & 63u, g = lane / G, j = lane % G, d = w * kPer + g;
+  if (w * kPer >= n_dst) return;
+  const uint32_t n = d < n_dst ? (uint32_t)cnt[d] : 0u;
+  const uint64_t b = d < n_dst ? off[d] : 0ull;
+  const bool have = n <= G && j < n;
+  tgsim_delivery r;
+  ulonglong2 k = make_ulonglong2(~0ull, ~0ull);
+  uint32_t c = 1u;  // 0 for the duplicate, 1 for the original
+  if (have) {
+    r = in[b + j];
+    k = make_ulonglong2(r.t_ns, ((uint64_t)r.src << 32) | r.seq);
+    c = (r.flags & TGSIM_FLAG_DUP) ? 0u : 1u;
+  }
+  ulonglong2* kg = keys + wv * kWave + g * G;
+  uint32_t* cg = orig + wv * kWave + g * G;
+  kg[j] = k;
+  cg[j] = c;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t nm = have ? n : 0u;
+  const uint32_t qmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)readlane32(scan_max_u32(nm), kWave - 1));
+  uint32_t rank = 0;
+  for (uint32_t q = 0; q < qmax; ++q) {
+    const ulonglong2 o = kg[q];
+    bool lt = o.x < k.x || (o.x == k.x && o.y < k.y);
+    if (o.x == k.x && o.y == k.y && q != j) lt = cg[q] < c;  // the other copy of the same packet
+    rank += (q < n && lt) ? 1u : 0u;
+  }
+  if (have) out[b + rank] = r;
+  for (uint64_t big = __ballot(j == 0 && n > G); big; big &= big - 1) {
+    const uint32_t gl = (uint32_t)__builtin_ctzll(big);
+    sort_segment(in, readlane64(b, gl), readlane32(n, gl), out, lane);
+  }
+  if (j == 0 && n) cnt[d] = 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K8 metrics (opt-in): per-instance counters and log2 histograms folded after each step, one
 // wavefront per instance, no atomics on the counters (an instance is one wavefront's).
@@ -2677,7 +2883,8 @@ __global__ __launch_bounds__(256) void k_metrics_dst(const tgsim_delivery* recs,
 // ---------------------------------------------------------------------------------------------
 // Host-side launchers.
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
-  hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
+  if (a.g_first) hipLaunchKernelGGL(k_sim_recv, dim3(n_wg), dim3(kWave), 0, st, a);
+  else hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
 }
 
 void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st) {
@@ -2781,6 +2988,13 @@ void launch_gossip_recv_emit(const GossipArgs& g, const tgsim_delivery* emit, co
   hipLaunchKernelGGL(k_gossip_recv_emit, dim3(wgs), dim3(256), 0, st, g, emit, emit_n, off, n_src);
 }
 
+void launch_gossip_recv_in(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t slot, bool skip_own,
+                           hipStream_t st) {
+  if (!n) return;
+  const uint64_t wgs = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_gossip_recv_in, dim3((uint32_t)wgs), dim3(256), 0, st, g, recs, n, slot, skip_own ? 1u : 0u);
+}
+
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st) {
   hipLaunchKernelGGL(k_gossip_recv_dev, dim3(2048), dim3(256), 0, st, g, recs, n_dev);
 }
@@ -2794,6 +3008,7 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
   const uint32_t waves = (g.n_src + kGossipPeers - 1) / kGossipPeers;  // kGossipPeers peers per wavefront
   const dim3 grid((waves + 3) / 4), blk(256);
   if (phase == 1) hipLaunchKernelGGL(k_gossip_count, grid, blk, 0, st, g, counts);
+  else if (g.nbr && g.degree <= kWave / kGossipPeers) hipLaunchKernelGGL(k_gossip_write8, grid, blk, 0, st, g, off, out);
   else hipLaunchKernelGGL(k_gossip_write, grid, blk, 0, st, g, off, out);
 }
 
@@ -2865,8 +3080,13 @@ void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin
 }
 
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
-                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st) {
+                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
   if (!n_src) return;
+  if (n_hint <= 16ull * n_src) {  // a few records per source: one lane each
+    hipLaunchKernelGGL(k_local_scatter_ls, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
+                       dst_begin, pos, out);
+    return;
+  }
   const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);
   hipLaunchKernelGGL(k_local_scatter, dim3(wgs), dim3(256), 0, st, emit, emit_n, off, n_src, dst_begin, pos, out);
 }
@@ -2881,7 +3101,18 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
     const char* v = getenv("TGSIM_SORT_GROUP_MAX");
     return v ? (uint64_t)atoll(v) : 8ull;
   }();
-  if (n_hint <= group_max * n_dst)
+  static const int lds_sort = [] {  // TGSIM_SORT_LDS=0: the shuffle-ranked groups of 8
+    const char* v = getenv("TGSIM_SORT_LDS");
+    return v ? atoi(v) : 1;
+  }();
+  if (lds_sort && n_dst < (1u << 31) && n_hint <= 24ull * n_dst) {
+    if (n_hint <= 3ull * n_dst)
+      hipLaunchKernelGGL(k_dst_sort_lds<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
+    else if (n_hint <= 8ull * n_dst)
+      hipLaunchKernelGGL(k_dst_sort_lds<16>, dim3((n_dst + 15) / 16), dim3(256), 0, st, in, off, cnt, n_dst, out);
+    else
+      hipLaunchKernelGGL(k_dst_sort_lds<32>, dim3((n_dst + 7) / 8), dim3(256), 0, st, in, off, cnt, n_dst, out);
+  } else if (n_hint <= group_max * n_dst)
     hipLaunchKernelGGL(k_dst_sort_group<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
   else
     hipLaunchKernelGGL(k_dst_sort_wide<4>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);

@@ -58,6 +58,8 @@ void launch_gossip_nbr(const GossipArgs& g, uint32_t* nbr, hipStream_t st);
 void launch_gossip_recv_emit(const GossipArgs& g, const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off,
                              uint32_t n_src, hipStream_t st);
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st);
+void launch_gossip_recv_in(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t slot, bool skip_own,
+                           hipStream_t st);
 // Exclusive scan of in[0..n) into out[0..n] (out[n] = total, also stored at *total when non-null);
 // pos (optional) receives a copy of out[0..n), the scatter cursors.
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
@@ -77,7 +79,8 @@ void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, u
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
                         tgsim_delivery* out, hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
-                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st);
+                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
+                          uint64_t n_hint);
 // Orders each destination's records; resets cnt[] to zero for the next histogram.
 // (in, the scatter buffer, is overwritten for segments longer than 64.)
 // n_hint: about how many records (picks one wavefront per destination or eight).
