@@ -1606,9 +1606,7 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused_sm(FusedSim fs, FusedArg
 // not fit (correlated draws, a queue that could reach the limit, more than 64 offered packets, 256
 // queued items, 256 ring entries or 64 items to serve) writes nothing and goes to the worklist.
 constexpr uint32_t kSparseQ = 4;  // chunks of 64 queued items / ring entries held in registers
-__global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
-  const uint32_t s = blockIdx.x;
-  if (s >= a.n_src) return;
+__device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s) {
   const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1;
   stamp(a, s, lane, 0, __builtin_amdgcn_s_memrealtime());
@@ -1699,10 +1697,10 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
   const uint64_t T_enq = mc ? readlane64(T, 63u - (uint32_t)__builtin_clzll(mc)) : 0ull;
   stamp(a, s, lane, 2, __builtin_amdgcn_s_memrealtime());
   const uint64_t h = a.horizon_ns;
-  // ---- gather every item HTB serves this step (e < horizon) into lanes [0, ns)
   uint4 x = make_uint4(0, 0, 0, 0);
   uint32_t ns = 0;
   bool over = false;
+  // moves the lanes with f set (k of them) to lanes [ns, ns + k), in lane order, into x
   auto gather = [&](bool f, const uint4& v) {
     const uint64_t m = __ballot(f);
     if (!m) return;
@@ -1719,48 +1717,131 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
     if (lane >= ns && lane < ns + k) x = pv;
     ns += k;
   };
-  bool due_q[kSparseQ];
-#pragma unroll
-  for (uint32_t u = 0; u < kSparseQ; ++u) {
-    due_q[u] = u * kWave + lane < qn && (w0_of(q[u]) & kEMask) < h;
-    gather(due_q[u], q[u]);
-  }
-  const bool due_o = cand && (w0_of(io) & kEMask) < h, due_c = cand && cst == 2 && (w0_of(ic) & kEMask) < h;
-  gather(due_o, io);
-  gather(due_c, ic);
-  // remaining items: everything not served, written back as the pool
-  uint32_t nrem = qn + (uint32_t)__popcll(mc) + (uint32_t)__popcll(__ballot(cand && cst == 2)) - ns;
-  if (over || nrem > kSparseQ * kWave) {
-    defer();
-    return;
-  }
-  // ---- write back the items HTB does not serve this step as the pool (no order needed); the
-  // registers holding the queue are free for the rest
   uint4* wq = a.heap + (size_t)s * kHeapCap;
   uint32_t wpos = 0;
-  auto keep = [&](bool f, const uint4& v) {
-    const uint64_t m = __ballot(f);
-    if (f) wq[wpos + (uint32_t)__popcll(m & below)] = v;
-    wpos += (uint32_t)__popcll(m);
-  };
+  // The departure ring: old ring ++ served.  The last enqueue (at T_enq, after serving the items
+  // eligible before it) released the prefix departing before T_enq; the old ring's part of it is
+  // known before HTB runs, so the kept old entries are written back (and their registers freed) as
+  // soon as the source is known not to defer.
+  uint64_t* wr = a.ring + (size_t)s * kHeapCap;
+  uint32_t old_kept = rn;     // old entries still in the ring
+  bool ring_stop = T_enq == 0;  // the release stopped inside the old ring (or nothing was released)
+  auto write_old_ring = [&]() {
+    uint32_t k0 = 0;
+    if (T_enq) {
 #pragma unroll
-  for (uint32_t u = 0; u < kSparseQ; ++u) keep(u * kWave + lane < qn && !due_q[u], q[u]);
-  keep(cand && !due_o, io);
-  keep(cand && cst == 2 && !due_c, ic);
-  // ---- rank the served items by (e, seq, clone first) and put each in its rank's lane
-  const bool hs = lane < ns;
-  uint32_t rank = 0;
-  for (uint32_t j = 0; j < ns; ++j) {
-    const uint4 o = make_uint4(readlane32(x.x, j), readlane32(x.y, j), readlane32(x.z, j), 0u);
-    rank += (hs && (item_lt(o, x) || (!item_lt(x, o) && j < lane))) ? 1u : 0u;
+      for (uint32_t u = 0; u < kSparseQ; ++u) {
+        if (!ring_stop && u * kWave < rn) {
+          const uint64_t m = __ballot(u * kWave + lane < rn && rg[u] >= T_enq);
+          const uint32_t cnt = rn - u * kWave < kWave ? rn - u * kWave : kWave;
+          if (m) {
+            k0 += (uint32_t)__builtin_ctzll(m);
+            ring_stop = true;
+          } else {
+            k0 += cnt;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kSparseQ; ++u) {
+      const uint32_t k = u * kWave + lane;
+      if (k < rn && k >= k0) wr[k - k0] = rg[u];
+    }
+    old_kept = rn - k0;
+  };
+  // ---- FIFO sources (no jitter, no reordering, no duplicates: gossip): the stored queue is sorted
+  // (a whole near region) and the new items, in offer order, are sorted and not before its last
+  // item, so (queue ++ new) is sorted: HTB serves its prefix below the horizon, in that order, and
+  // the rest goes back sorted, shifted down, with no gather of the queue, no rank and no compaction.
+  bool fifo = st.near_n == qn && __ballot(cand && cst == 2) == 0;
+  if (fifo && mc) {
+    const uint64_t bc = mc & below;  // the candidate before each candidate, or the queue's last item
+    const uint32_t pl = bc ? 63u - (uint32_t)__builtin_clzll(bc) : lane;
+    uint4 prev = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.x),
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.y),
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.z), 0u);
+    bool first = cand && !bc;
+    if (qn) {
+      const uint32_t tl = (qn - 1) & (kWave - 1), tu = (qn - 1) >> 6;
+      uint4 qt = q[0];
+#pragma unroll
+      for (uint32_t u = 1; u < kSparseQ; ++u)
+        if (tu == u) qt = q[u];
+      if (first) prev = make_uint4(readlane32(qt.x, tl), readlane32(qt.y, tl), readlane32(qt.z, tl), 0u);
+    } else {
+      first = false;  // nothing queued: the first candidate has no predecessor
+    }
+    fifo = __ballot(cand && (bc || first) && item_lt(io, prev)) == 0;
   }
-  {
+  if (fifo) {
+    uint32_t nq = 0;  // the queue's prefix below the horizon
+#pragma unroll
+    for (uint32_t u = 0; u < kSparseQ; ++u)
+      if (u * kWave < qn) nq += (uint32_t)__popcll(__ballot(u * kWave + lane < qn && (w0_of(q[u]) & kEMask) < h));
+    const bool due_o = cand && (w0_of(io) & kEMask) < h;  // a prefix of the candidates
+    const uint32_t n_due = (uint32_t)__popcll(__ballot(due_o));
+    const uint32_t nrem = qn - nq + (uint32_t)__popcll(mc) - n_due;
+    if (nq + n_due > kWave || nrem > kSparseQ * kWave) {
+      defer();
+      return;
+    }
+    write_old_ring();
+    x = lane < nq ? q[0] : make_uint4(0, 0, 0, 0);
+    ns = nq;
+    gather(due_o, io);
+    // write back: queue items [nq, qn) to [0, qn - nq), then the candidates not served
+#pragma unroll
+    for (uint32_t u = 0; u < kSparseQ; ++u) {
+      const uint32_t k = u * kWave + lane;
+      if (k >= nq && k < qn) wq[k - nq] = q[u];
+    }
+    const uint32_t cr = (uint32_t)__popcll(mc & below);
+    if (cand && !due_o) wq[qn - nq + cr - n_due] = io;
+    wpos = nrem;
+  } else {
+    // ---- gather every item HTB serves this step (e < horizon) into lanes [0, ns)
+    bool due_q[kSparseQ];
+#pragma unroll
+    for (uint32_t u = 0; u < kSparseQ; ++u) {
+      due_q[u] = u * kWave + lane < qn && (w0_of(q[u]) & kEMask) < h;
+      gather(due_q[u], q[u]);
+    }
+    const bool due_o = cand && (w0_of(io) & kEMask) < h, due_c = cand && cst == 2 && (w0_of(ic) & kEMask) < h;
+    gather(due_o, io);
+    gather(due_c, ic);
+    // remaining items: everything not served, written back as the pool
+    uint32_t nrem = qn + (uint32_t)__popcll(mc) + (uint32_t)__popcll(__ballot(cand && cst == 2)) - ns;
+    if (over || nrem > kSparseQ * kWave) {
+      defer();
+      return;
+    }
+    write_old_ring();
+    // ---- write back the items HTB does not serve this step as the pool (no order needed); the
+    // registers holding the queue are free for the rest
+    auto keep = [&](bool f, const uint4& v) {
+      const uint64_t m = __ballot(f);
+      if (f) wq[wpos + (uint32_t)__popcll(m & below)] = v;
+      wpos += (uint32_t)__popcll(m);
+    };
+#pragma unroll
+    for (uint32_t u = 0; u < kSparseQ; ++u) keep(u * kWave + lane < qn && !due_q[u], q[u]);
+    keep(cand && !due_o, io);
+    keep(cand && cst == 2 && !due_c, ic);
+    // ---- rank the served items by (e, seq, clone first) and put each in its rank's lane
+    const bool hs = lane < ns;
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < ns; ++j) {
+      const uint4 o = make_uint4(readlane32(x.x, j), readlane32(x.y, j), readlane32(x.z, j), 0u);
+      rank += (hs && (item_lt(o, x) || (!item_lt(x, o) && j < lane))) ? 1u : 0u;
+    }
     const uint32_t to = (hs ? rank : lane) & (kWave - 1);
     x = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.x),
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.y),
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.z),
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.w));
   }
+  const bool hs = lane < ns;
   // the destinations' forwarded masks, for the receipts folded in below (in flight during the scan)
   // (the 32-bit half of the mask that holds the record's flood bit: one register across the scan)
   const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
@@ -1800,46 +1881,21 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
   } else if (hs) {
     lost = 1;
   }
-  // ---- the departure ring: old ring ++ served; the last enqueue (at T_enq, after serving the
-  // items eligible before it) released the prefix departing before T_enq
-  const uint32_t n1 = T_enq ? (uint32_t)__popcll(__ballot(hs && e < T_enq)) : 0u;
-  uint32_t k0 = 0;  // released prefix of old ring ++ served[0, n1)
-  if (T_enq) {
-    bool stop = false;
-#pragma unroll
-    for (uint32_t u = 0; u < kSparseQ; ++u) {
-      if (!stop && u * kWave < rn) {
-        const uint64_t m = __ballot(u * kWave + lane < rn && rg[u] >= T_enq);
-        const uint32_t cnt = rn - u * kWave < kWave ? rn - u * kWave : kWave;
-        if (m) {
-          k0 += (uint32_t)__builtin_ctzll(m);
-          stop = true;
-        } else {
-          k0 += cnt;
-        }
-      }
-    }
-    if (!stop) {
-      const uint64_t m = __ballot(lane < n1 && d >= T_enq);
-      k0 += m ? (uint32_t)__builtin_ctzll(m) : n1;
-    }
+  // ---- the served entries join the ring; those departing before the last enqueue were released
+  // with the old ring's prefix (when it released the whole old ring: ring_stop false)
+  uint32_t sk0 = 0;  // served entries released
+  if (T_enq && !ring_stop) {
+    const uint32_t n1 = (uint32_t)__popcll(__ballot(hs && e < T_enq));
+    const uint64_t m = __ballot(lane < n1 && d >= T_enq);
+    sk0 = m ? (uint32_t)__builtin_ctzll(m) : n1;
   }
-  // ---- write back: the ring from k0 on, then the pool of unserved items; the state
-  uint64_t* wr = a.ring + (size_t)s * kHeapCap;
-#pragma unroll
-  for (uint32_t u = 0; u < kSparseQ; ++u) {
-    const uint32_t k = u * kWave + lane;
-    if (k < rn && k >= k0) wr[k - k0] = rg[u];
-  }
-  const uint32_t old_kept = rn > k0 ? rn - k0 : 0u;  // old entries still in the ring
-  const uint32_t sk0 = k0 > rn ? k0 - rn : 0u;        // served entries released
   if (hs && lane >= sk0) wr[old_kept + lane - sk0] = d;
   const uint32_t rn_new = old_kept + ns - sk0;
   if (lane == 0) {
     SrcState ns_;
     ns_.tat = tat_end;
     ns_.heap_n = wpos;
-    ns_.near_n = 0;  // all of it pool
+    ns_.near_n = fifo ? wpos : 0;  // sorted (FIFO), or all of it pool
     ns_.ring_n = rn_new;
     ns_.last_dup = st.last_dup;
     ns_.last_cor = st.last_cor;
@@ -1880,6 +1936,10 @@ __global__ __launch_bounds__(kWave, 8) void k_sim_sparse(SimArgs a) {
         __hip_atomic_store(a.err_host, (uint64_t)kErrTimeOverflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+}
+
+__global__ __launch_bounds__(kWave, 7) void k_sim_sparse(SimArgs a) {
+  if (blockIdx.x < a.n_src) sparse_source(a, blockIdx.x);
 }
 
 // The general path for the worklist k_sim_sparse left: a grid-stride loop over the list (its
@@ -3082,7 +3142,7 @@ void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
   if (!n_src) return;
-  if (n_hint <= 16ull * n_src) {  // a few records per source: one lane each
+  if (n_hint <= 64ull * n_src) {  // up to tens of records per source (gossip, even at the flood's peak): one lane each
     hipLaunchKernelGGL(k_local_scatter_ls, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
                        dst_begin, pos, out);
     return;
@@ -3105,13 +3165,15 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
     const char* v = getenv("TGSIM_SORT_LDS");
     return v ? atoi(v) : 1;
   }();
-  if (lds_sort && n_dst < (1u << 31) && n_hint <= 24ull * n_dst) {
+  if (lds_sort && n_hint <= 48ull * n_dst) {
     if (n_hint <= 3ull * n_dst)
       hipLaunchKernelGGL(k_dst_sort_lds<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
     else if (n_hint <= 8ull * n_dst)
       hipLaunchKernelGGL(k_dst_sort_lds<16>, dim3((n_dst + 15) / 16), dim3(256), 0, st, in, off, cnt, n_dst, out);
-    else
+    else if (n_hint <= 18ull * n_dst)
       hipLaunchKernelGGL(k_dst_sort_lds<32>, dim3((n_dst + 7) / 8), dim3(256), 0, st, in, off, cnt, n_dst, out);
+    else
+      hipLaunchKernelGGL(k_dst_sort_lds<64>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
   } else if (n_hint <= group_max * n_dst)
     hipLaunchKernelGGL(k_dst_sort_group<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
   else
