@@ -295,6 +295,11 @@ struct tgsim_engine_s {
   // on the delivery stream while the next k_sim writes the other pair (swapped by deliver_local;
   // ev_local: the delivery that last read the pair)
   DevBuf<tgsim_delivery> d_emit, d_emit_alt;
+  DevBuf<uint32_t> d_eslot, d_eslot_alt;  // records' slots in their destinations' segments (emit_slot)
+  bool eslot_on = false;                  // the last k_sim wrote d_eslot (heavy sparse windows)
+  uint64_t slot_min = 16;                 // TGSIM_SLOT_MIN: offered packets per source from which it is on
+  uint64_t deliver_slack = 128;           // TGSIM_DELIVER_SLACK: queued items per source a bounded local
+                                          // delivery allows for (besides 2 per offered packet)
   DevBuf<uint32_t> d_emit_n, d_emit_n_alt;
   DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (k_dst_sort resets it)
   hipEvent_t ev_local = nullptr, ev_local_alt = nullptr;
@@ -313,6 +318,7 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_work;   // sparse steps: k_sim_sparse's deferred sources, [0] = count, then ids
   int sparse_mode = -1;      // TGSIM_SPARSE: -1 auto, 0 never, 1 always
   bool fold_recv = true;     // TGSIM_FOLD_RECV: single-shard gossip receipts folded into k_sim
+  bool rotated = false;      // a sparse step may have left queues in place (head slot != 0)
   bool sparse_seen = false;  // h_work holds a measured worklist size
   uint32_t dense_streak = 0; // dense steps chosen because the last sparse step deferred too much
   bool order_valid = false;
@@ -742,6 +748,8 @@ int check_sim_error(Eng* E) {
   if (herr & kErrTimeOverflow) return E->fail(-EOVERFLOW, "simulated time exceeds 2^46 ns");
   if (herr & kErrHandoff)
     return E->fail(-EIO, "fused step: a source's previous window did not complete (hand-off timed out)");
+  if (herr & kErrDeliverCap)
+    return E->fail(-ENOSPC, "local delivery: a window's records exceed the delivery buffers (TGSIM_DELIVER_SLACK)");
   if (E->h_xerr && __atomic_load_n(E->h_xerr, __ATOMIC_RELAXED))
     return E->fail(-ENOSPC, "exchange: a step's records for one rank exceed the slot capacity");
   return 0;
@@ -866,6 +874,14 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     if (sparse) E->dense_streak = 0;
   }
   a.worklist = a.worklist_n = nullptr;
+  // heavy sparse windows with a local delivery (the gossip flood's peak): the count atomics return
+  // each record's slot, so the scatter needs no atomics of its own
+  E->eslot_on = sparse && local_hist && E->n_in >= E->slot_min * E->S;
+  a.emit_slot = nullptr;
+  if (E->eslot_on) {
+    HIPCHK(E->d_eslot.ensure(emit_cap));
+    a.emit_slot = E->d_eslot.p;
+  }
   if (sparse) {
     HIPCHK(E->d_work.ensure(static_cast<size_t>(E->S) + 1));
     HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t), E->st));
@@ -877,7 +893,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   HIPCHK(take_event(E, &ev0));
   HIPCHK(take_event(E, &ev1));
   HIPCHK(hipEventRecord(ev0, E->st));
-  if (sparse) launch_sim_sparse(a, E->st);
+  if (sparse) {
+    launch_sim_sparse(a, E->st);
+    E->rotated = true;
+  }
   else launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
@@ -965,6 +984,7 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
   HIPCHK(hipEventRecord(E->ev_local, rs));  // the last reader of this emit pair
   std::swap(E->d_emit, E->d_emit_alt);
   std::swap(E->d_emit_n, E->d_emit_n_alt);
+  std::swap(E->d_eslot, E->d_eslot_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
   std::swap(E->ev_local, E->ev_local_alt);
   E->route_ranks[k] = n_ranks;
@@ -1143,8 +1163,8 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
 
 // The local delivery of one window on the delivery stream (after its k_sim): scan of the
 // per-destination histogram -> scatter straight from the emit regions -> per-destination order.
-int deliver_local_from(Eng* E, const tgsim_delivery* emit, const uint32_t* emit_n, uint64_t* lcnt,
-                       const uint64_t* off, uint64_t n_in) {
+int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uint64_t* lcnt,
+                       const uint64_t* off, uint64_t n_in, const uint32_t* eslot = nullptr) {
   const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
   HIPCHK(E->d_doff.ensure(nd + 1));
@@ -1154,14 +1174,22 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, const uint32_t* emit_
   launch_scan(lcnt, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
   HIPCHK(hipGetLastError());
   const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
-  uint64_t n = 2 * n_in + static_cast<uint64_t>(kHeapCap) * E->S;  // upper bound
+  // without the exact count (no host round trip): what the window's sources can emit, 2 per offered
+  // packet plus deliver_slack queued items each (the full netem limit of 1,024 would ask 24 GB of
+  // scatter and output buffers at 1M peers); k_deliver_guard checks the device's exact total
+  const uint64_t slack = std::min<uint64_t>(kHeapCap, E->deliver_slack);
+  uint64_t n = 2 * n_in + slack * E->S;
   if (need_n) {
     HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
     HIPCHK(hipStreamSynchronize(sq));
     n = E->h_dtot;
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in);
+  if (!need_n && slack < kHeapCap) {
+    launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, nd, E->d_err_host, sq);
+    HIPCHK(hipGetLastError());
+  }
+  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in, eslot, E->d_doff.p);
   HIPCHK(hipGetLastError());
   if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
   tgsim_delivery* dst = nullptr;
@@ -1194,12 +1222,14 @@ int deliver_local(Eng* E) {
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
   }
 
-  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in);
+  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in,
+                              E->eslot_on ? E->d_eslot.p : nullptr);
   if (rc) return rc;
   HIPCHK(hipEventRecord(E->ev_local, sq));
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   std::swap(E->d_emit, E->d_emit_alt);
   std::swap(E->d_emit_n, E->d_emit_n_alt);
+  std::swap(E->d_eslot, E->d_eslot_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
   std::swap(E->ev_local, E->ev_local_alt);
   return 0;
@@ -1239,6 +1269,11 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   E->gen_q.erase(E->gen_q.begin(), E->gen_q.begin() + g);
   E->gen_q_ticks -= static_cast<uint64_t>(g) * n_ticks;
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_fgrp[p], 0));  // the deliveries that last read set p
+  if (E->rotated) {  // the fused kernels' bounded loads read every queue from slot 0
+    launch_unrotate(E->d_heap.p, E->d_state.p, E->S, E->st);
+    HIPCHK(hipGetLastError());
+    E->rotated = false;
+  }
   if (E->d_done.cap < E->S) {
     HIPCHK(E->d_done.ensure(E->S));
     HIPCHK(hipMemsetAsync(E->d_done.p, 0, sizeof(uint32_t) * E->d_done.cap, E->st));
@@ -1557,6 +1592,8 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
+  if (const char* sm = getenv("TGSIM_SLOT_MIN")) E->slot_min = strtoull(sm, nullptr, 10);
+  if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) E->deliver_slack = strtoull(ds, nullptr, 10);
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
   if (const char* fo = getenv("TGSIM_FUSED_ORDER")) E->order_chain = strcmp(fo, "records") != 0;
   if (const char* fm = getenv("TGSIM_FUSED_MAJOR")) E->source_major = strcmp(fm, "source") == 0;
@@ -1655,7 +1692,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_eslot.release(); E->d_eslot_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release(); E->d_chain.release();
@@ -1828,6 +1865,11 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   }
   HIPCHK(E->d_in.ensure(reserve));
   HIPCHK(E->d_verdict.ensure(reserve));
+  // the emit regions of both parities and the record slots of the flood's heavy windows, for the
+  // same reserve (a hipFree + hipMalloc of several GB inside the flood stalls the loop)
+  const uint64_t emit_cap = 2 * reserve + static_cast<uint64_t>(kHeapCap) * E->S;
+  for (auto* b : {&E->d_emit, &E->d_emit_alt}) HIPCHK(b->ensure(emit_cap));
+  for (auto* b : {&E->d_eslot, &E->d_eslot_alt}) HIPCHK(b->ensure(emit_cap));
   E->gossip_on = true;
   return 0;
 }

@@ -48,6 +48,13 @@ struct alignas(16) SrcState {
   uint32_t last_dup, last_cor, last_reo;  // get_crandom() correlation state
 };
 static_assert(sizeof(SrcState) == 32, "SrcState must stay 32 B");
+// near_n packs the near region's length (bits 0..15) and the slot of the queue's first item in the
+// source's kHeapCap-slot HBM array (bits 16..25; the items wrap around).  The slot is 0 in the
+// compacted layout every writer but k_sim_sparse's FIFO path leaves; that path serves a prefix and
+// appends behind the tail in place instead of moving the queue down (k_unrotate compacts it again
+// before a fused launch, whose bounded loads assume slot 0).
+__host__ __device__ inline uint32_t q_near(const SrcState& s) { return s.near_n & 0xFFFFu; }
+__host__ __device__ inline uint32_t q_head(const SrcState& s) { return (s.near_n >> 16) & (kHeapCap - 1); }
 
 // Offered packet as staged on the device (16 B, CSR by source, ordered by (tick, seq)).
 struct alignas(16) InRec {
@@ -80,7 +87,12 @@ enum StatSlot {
 // Counters are spread over kStatCopies copies (workgroup w adds into copy w % kStatCopies) so that
 // a million one-source workgroups do not serialize on 16 addresses; readers sum the copies.  The
 // error word lives in copy 0 only.
-constexpr uint32_t kStatCopies = 64;
+#ifndef TGSIM_STAT_COPIES
+#define TGSIM_STAT_COPIES 2048
+#endif
+constexpr uint32_t kStatCopies = TGSIM_STAT_COPIES;  // 64 had ~16k adds per address and window at 1M
+                                                     // sources: adds to one address serialize (~12 ns
+                                                     // each), ~0.2 ms per window
 constexpr uint32_t kErrTimeOverflow = 1u;
 
 struct SimArgs {
@@ -114,6 +126,11 @@ struct SimArgs {
   uint64_t* g_pend;         // [s] received, not yet forwarded
   const uint64_t* g_fwd;    // [s] forwarded (stable during the step: written by k_gossip_write before it)
   uint32_t g_floods, g_degree;
+  // with dst_cnt: each record's slot inside its destination's segment, the value its count atomic
+  // returned (parallel to emit), so the local scatter needs no atomics of its own; or null
+  uint32_t* emit_slot;
+  uint64_t pad_;  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the
+                  // scheduler spilled 9 more SGPRs in k_sim_fused (155 -> 164)
 };
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 
@@ -147,6 +164,7 @@ struct FusedArgs {
                         // weight; source-major), or null
 };
 constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
+constexpr uint32_t kErrDeliverCap = 4u;  // a local delivery's records exceed its buffers (TGSIM_DELIVER_SLACK)
 // Local delivery of a fused group: window w's emit regions, counts and CSR offsets; pos holds the
 // scatter cursors of the g * n_dst (window, destination) segments.
 struct GroupDeliver {

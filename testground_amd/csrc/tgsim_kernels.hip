@@ -192,9 +192,9 @@ __device__ __forceinline__ uint64_t delayed(const SrcParams& p, uint64_t T, uint
 // Gossip receipt of one emitted record (single shard; what k_gossip_recv does at delivery): the
 // earliest receipt tick of flood seq / degree at the destination, which becomes pending unless it
 // has forwarded the flood already (fw: the destination's forwarded mask).  Receipts are order-free
-// (the earliest tick wins), so folding them in at emission changes no result; the atomics return
-// nothing, so the wave never waits for them.  Only destinations of this shard are folded in; the
-// others' receipts are taken where their records are delivered (k_gossip_recv_in).
+// (the earliest tick wins), so folding them in at emission changes no result.  Only destinations
+// of this shard are folded in; the others' receipts are taken where their records are delivered
+// (k_gossip_recv_in).
 struct RecvFold {
   uint32_t* first;
   uint64_t* pend;
@@ -218,8 +218,11 @@ __device__ __forceinline__ void fold_receipt(const RecvFold& g, uint32_t dst, ui
   q = r < 0 ? q - 1 : (uint64_t)r >= g.tick_ns ? q + 1 : q;
   uint64_t t = q + 1;
   if (t > 0xFFFFFFFEull) t = 0xFFFFFFFEull;
-  __hip_atomic_fetch_min(&g.first[(uint64_t)s * 64 + f], (uint32_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_or(&g.pend[s], 1ull << f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the first receipt ever (exactly one sees "none") marks the flood pending: one atomic per receipt
+  // and one per (peer, flood), not two per receipt (every one a memory-side request)
+  if (__hip_atomic_fetch_min(&g.first[(uint64_t)s * 64 + f], (uint32_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+      0xFFFFFFFFu)
+    __hip_atomic_fetch_or(&g.pend[s], 1ull << f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ uint32_t fib_lookup(const Interval* iv, uint32_t n, uint32_t ip) {
@@ -332,6 +335,7 @@ struct SimQueue {
   uint64_t tat;             // HTB theoretical arrival time
   tgsim_delivery* emit;
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
+  uint32_t* eslot;           // with dcnt: the records' slots in their destinations' segments, or null
   RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
@@ -408,7 +412,12 @@ struct SimQueue {
         rw[0] = d;
         rw[1] = ((uint64_t)qi.w << 32) | src;
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
-        if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
+        if (dcnt) {
+          if (eslot)
+            eslot[n_emit + __popcll(lm & ((1ull << lane) - 1))] = (uint32_t)atomicAdd(&dcnt[qi.w], 1ull);
+          else
+            atomicAdd(&dcnt[qi.w], 1ull);
+        }
         if (rf.first && qi.w - rf.shard_begin < rf.n_local)
           fold_receipt(rf, qi.w, qi.z, flags, d, rf.fwd[qi.w - rf.shard_begin]);
         sched++;
@@ -882,8 +891,8 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   SimQueue<kCap> Q{lds, pp, lane};
   Q.rh = load ? 0 : carry->rh;
   Q.rn = load ? st.ring_n : carry->rn;
-  Q.qn = load ? st.near_n : carry->qn;
-  Q.pn = load ? st.heap_n - st.near_n : carry->pn;  // on a load: the whole pool until it is split
+  Q.qn = load ? q_near(st) : carry->qn;
+  Q.pn = load ? st.heap_n - q_near(st) : carry->pn;  // on a load: the whole pool until it is split
   Q.fn = load ? 0 : carry->fn;
   Q.H = a.horizon_ns;
   Q.tat = st.tat;
@@ -891,6 +900,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
+  Q.eslot = kMode == kModePlain && a.emit_slot ? a.emit_slot + 2 * a.off[s] + (uint64_t)kHeapCap * s : nullptr;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
@@ -918,12 +928,12 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
         qv[u] = ld16<kPol>(rq, 16u * k);
       }
     } else {  // a lane past the end re-reads the last entry (the same line as its neighbours)
-      const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0;
+      const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0, qh = q_head(st);
 #pragma unroll
       for (uint32_t u = 0; u < kCap / kWave; ++u) {
         const uint32_t k = u * kWave + lane;
         rv[u] = gr[k < rn ? k : rl];
-        qv[u] = gh[k < qn ? k : ql];
+        qv[u] = gh[(qh + (k < qn ? k : ql)) & (kHeapCap - 1)];
       }
     }
     // every load issued before the partition's ballots, which the scheduler would otherwise
@@ -1610,11 +1620,10 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1;
   stamp(a, s, lane, 0, __builtin_amdgcn_s_memrealtime());
-  // the first 64 queued items and ring entries are read before the state says how many there are
-  // (the arrays have room for 1024 per source): one dependent load level instead of two
+  // the first 64 ring entries are read before the state says how many there are (the array has room
+  // for 1024 per source): one dependent load level instead of two; the queue starts at its head slot
   const uint4* gh = a.heap + (size_t)s * kHeapCap;
   const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
-  const uint4 q0 = gh[lane];
   const uint64_t r0 = gr[lane];
   const SrcState st = a.state[s];
   const SrcParams pp = a.params[s];
@@ -1624,22 +1633,53 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   auto defer = [&]() {
     if (lane == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
   };
+  const bool sorted_st = q_near(st) == qn;  // the whole queue is one sorted region
   if ((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 || (uint64_t)rn + qn + 2ull * n >= a.queue_limit || n > kWave ||
-      qn > kSparseQ * kWave || rn > kSparseQ * kWave) {
+      (!sorted_st && qn > kSparseQ * kWave) || rn > kSparseQ * kWave) {
     defer();
+    return;
+  }
+  unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
+  const uint4 qh0 = sorted_st && qn && !n ? gh[q_head(st)] : make_uint4(0, 0, 0, 0);
+  if (!n && (!qn || (sorted_st && (w0_of(qh0) & kEMask) >= a.horizon_ns))) {
+    // nothing offered and nothing eligible before the horizon: the state stays as it is (the ring
+    // is released only by an enqueue); only the per-window queue model is counted
+    if (lane == 0) {
+      a.emit_n[s] = 0;
+      const uint64_t qb = 32ull * qn + 16ull * rn;
+      if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
+      if (qn) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(32ull * qn - 16ull));
+      if (rn) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(16ull * rn - 8ull * (rn < kWave ? rn : kWave)));
+    }
     return;
   }
   const uint32_t src = a.shard_begin + s;
   stamp(a, s, lane, 1, __builtin_amdgcn_s_memrealtime());
-  // ---- loads: the rest of the queue and the ring (whole chunks, masked), the offered packets
+  // ---- loads: the queue (a sorted one: its first chunk and its last item; else whole chunks,
+  // masked), the rest of the ring, the offered packets
+  const uint32_t qh = q_head(st);
   uint4 q[kSparseQ];
   uint64_t rg[kSparseQ];
-  q[0] = lane < qn ? q0 : make_uint4(0, 0, 0, 0);
+  q[0] = lane < qn ? gh[(qh + lane) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
   rg[0] = lane < rn ? r0 : ~0ull;
+  auto load_rest = [&]() {
+#pragma unroll
+    for (uint32_t u = 1; u < kSparseQ; ++u) {
+      const uint32_t k = u * kWave + lane;
+      q[u] = k < qn ? gh[(qh + k) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  uint4 qt = make_uint4(0, 0, 0, 0);  // a sorted queue's last item
+  if (sorted_st) {
+    if (qn > kWave) qt = gh[(qh + qn - 1) & (kHeapCap - 1)];
+#pragma unroll
+    for (uint32_t u = 1; u < kSparseQ; ++u) q[u] = make_uint4(0, 0, 0, 0);
+  } else {
+    load_rest();
+  }
 #pragma unroll
   for (uint32_t u = 1; u < kSparseQ; ++u) {
     const uint32_t k = u * kWave + lane;
-    q[u] = k < qn ? gh[k] : make_uint4(0, 0, 0, 0);
     rg[u] = k < rn ? gr[k] : ~0ull;
   }
   InRec r = {};
@@ -1754,7 +1794,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   // (a whole near region) and the new items, in offer order, are sorted and not before its last
   // item, so (queue ++ new) is sorted: HTB serves its prefix below the horizon, in that order, and
   // the rest goes back sorted, shifted down, with no gather of the queue, no rank and no compaction.
-  bool fifo = st.near_n == qn && __ballot(cand && cst == 2) == 0;
+  bool fifo = sorted_st && __ballot(cand && cst == 2) == 0;
   if (fifo && mc) {
     const uint64_t bc = mc & below;  // the candidate before each candidate, or the queue's last item
     const uint32_t pl = bc ? 63u - (uint32_t)__builtin_clzll(bc) : lane;
@@ -1763,26 +1803,24 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
                             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.z), 0u);
     bool first = cand && !bc;
     if (qn) {
-      const uint32_t tl = (qn - 1) & (kWave - 1), tu = (qn - 1) >> 6;
-      uint4 qt = q[0];
-#pragma unroll
-      for (uint32_t u = 1; u < kSparseQ; ++u)
-        if (tu == u) qt = q[u];
-      if (first) prev = make_uint4(readlane32(qt.x, tl), readlane32(qt.y, tl), readlane32(qt.z, tl), 0u);
+      if (qn <= kWave) {
+        const uint32_t tl = qn - 1;
+        qt = make_uint4(readlane32(q[0].x, tl), readlane32(q[0].y, tl), readlane32(q[0].z, tl), 0u);
+      }
+      if (first) prev = qt;
     } else {
       first = false;  // nothing queued: the first candidate has no predecessor
     }
     fifo = __ballot(cand && (bc || first) && item_lt(io, prev)) == 0;
   }
+  uint32_t new_head = 0;
+  uint32_t q_moved = 0;  // queue items read or written in HBM (FIFO path: not the whole queue)
   if (fifo) {
-    uint32_t nq = 0;  // the queue's prefix below the horizon
-#pragma unroll
-    for (uint32_t u = 0; u < kSparseQ; ++u)
-      if (u * kWave < qn) nq += (uint32_t)__popcll(__ballot(u * kWave + lane < qn && (w0_of(q[u]) & kEMask) < h));
+    // the queue's prefix below the horizon (in its first chunk: 64 due items defer anyway)
+    const uint32_t nq = (uint32_t)__popcll(__ballot(lane < qn && (w0_of(q[0]) & kEMask) < h));
     const bool due_o = cand && (w0_of(io) & kEMask) < h;  // a prefix of the candidates
     const uint32_t n_due = (uint32_t)__popcll(__ballot(due_o));
-    const uint32_t nrem = qn - nq + (uint32_t)__popcll(mc) - n_due;
-    if (nq + n_due > kWave || nrem > kSparseQ * kWave) {
+    if (nq + n_due > kWave || (nq == kWave && qn > kWave)) {
       defer();
       return;
     }
@@ -1790,16 +1828,21 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     x = lane < nq ? q[0] : make_uint4(0, 0, 0, 0);
     ns = nq;
     gather(due_o, io);
-    // write back: queue items [nq, qn) to [0, qn - nq), then the candidates not served
-#pragma unroll
-    for (uint32_t u = 0; u < kSparseQ; ++u) {
-      const uint32_t k = u * kWave + lane;
-      if (k >= nq && k < qn) wq[k - nq] = q[u];
-    }
+    // in place: the served prefix leaves by moving the head slot, the candidates not served are
+    // appended behind the tail; nothing else moves
     const uint32_t cr = (uint32_t)__popcll(mc & below);
-    if (cand && !due_o) wq[qn - nq + cr - n_due] = io;
-    wpos = nrem;
+    if (cand && !due_o) wq[(qh + qn + cr - n_due) & (kHeapCap - 1)] = io;
+    new_head = (qh + nq) & (kHeapCap - 1);
+    wpos = qn - nq + (uint32_t)__popcll(mc) - n_due;
+    q_moved = (qn < kWave ? qn : kWave) + (qn > kWave ? 1u : 0u) + (uint32_t)__popcll(mc) - n_due;
   } else {
+    if (sorted_st) {  // sorted, but the new items do not extend it in order: the general path
+      if (qn > kSparseQ * kWave) {
+        defer();
+        return;
+      }
+      load_rest();
+    }
     // ---- gather every item HTB serves this step (e < horizon) into lanes [0, ns)
     bool due_q[kSparseQ];
 #pragma unroll
@@ -1873,7 +1916,13 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     rw[0] = d;
     rw[1] = ((uint64_t)x.w << 32) | src;
     rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-    if (a.dst_cnt) atomicAdd(&a.dst_cnt[x.w], 1ull);
+    if (a.dst_cnt) {
+      const uint32_t i = (uint32_t)__popcll(lm & below);
+      if (a.emit_slot)
+        a.emit_slot[2 * sbeg + (uint64_t)kHeapCap * s + i] = (uint32_t)atomicAdd(&a.dst_cnt[x.w], 1ull);
+      else
+        atomicAdd(&a.dst_cnt[x.w], 1ull);
+    }
     if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
     sched = 1;
     bytes = xlen;
@@ -1895,7 +1944,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     SrcState ns_;
     ns_.tat = tat_end;
     ns_.heap_n = wpos;
-    ns_.near_n = fifo ? wpos : 0;  // sorted (FIFO), or all of it pool
+    ns_.near_n = fifo ? wpos | new_head << 16 : 0;  // sorted in place (FIFO), or all of it pool, compacted
     ns_.ring_n = rn_new;
     ns_.last_dup = st.last_dup;
     ns_.last_cor = st.last_cor;
@@ -1919,10 +1968,12 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const uint32_t t_clone = ballot_count(staged && vc != TGSIM_V_NONE);
   const uint64_t t_bytes = wave_sum(bytes);
   const bool err = __ballot(perr != 0) != 0;
-  unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
   if (lane < 8 && vcnt) atomicAdd(&sc[kStVerdict0 + lane], (unsigned long long)vcnt);
   if (lane == 0) {
     const uint64_t qb = 16ull * qn + 8ull * rn + 16ull * wpos + 8ull * rn_new;
+    // the per-window model counts the whole queue loaded and stored; the FIFO path left most of it
+    const uint64_t q_kept = fifo ? 16ull * (qn + wpos - q_moved) : 0ull;
+    if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (t_sched) atomicAdd(&sc[kStScheduled], (unsigned long long)t_sched);
     if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
@@ -2015,14 +2066,41 @@ __global__ void k_apply_cfg(const CfgPatch* __restrict__ patches, uint32_t n, Sr
 // step boundary: they will leave the sender and find no port (or an address no longer in use), so
 // they are marked dead in place; the queue order and occupancy are unchanged.  One wavefront per
 // source, gone[] is per global peer.
+// Compacts every queue the sparse kernel left in place (head slot != 0) back to slot 0, for the fused
+// kernels' bounded loads: one wavefront per source, the whole queue in registers, then stored.
+__global__ __launch_bounds__(256) void k_unrotate(uint4* heap, SrcState* state, uint32_t n_src) {
+  const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (s >= n_src) return;
+  SrcState st = state[s];
+  const uint32_t qh = q_head(st), qn = st.heap_n;
+  if (!qh) return;
+  uint4* q = heap + (size_t)s * kHeapCap;
+  uint4 v[kHeapCap / kWave];
+#pragma unroll
+  for (uint32_t u = 0; u < kHeapCap / kWave; ++u) {  // branch-free: a lane past the end re-reads the head
+    const uint32_t k = u * kWave + lane;
+    v[u] = q[(qh + (k < qn ? k : 0u)) & (kHeapCap - 1)];
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // every lane's reads land before any lane writes
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (uint32_t u = 0; u < kHeapCap / kWave; ++u) {
+    const uint32_t k = u * kWave + lane;
+    if (k < qn) q[k] = v[u];
+  }
+  if (lane == 0) state[s].near_n = q_near(st);
+}
+
 __global__ __launch_bounds__(256) void k_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone) {
   const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (s >= n_src) return;
-  const uint32_t qn = state[s].heap_n;
+  const SrcState st = state[s];
+  const uint32_t qn = st.heap_n, qh = q_head(st);
   uint4* q = heap + (size_t)s * kHeapCap;
   for (uint32_t k = lane; k < qn; k += kWave) {
-    const uint32_t d = q[k].w;
-    if (d != kDeadDst && gone[d]) q[k].w = kDeadDst;
+    const uint32_t j = (qh + k) & (kHeapCap - 1);
+    const uint32_t d = q[j].w;
+    if (d != kDeadDst && gone[d]) q[j].w = kDeadDst;
   }
 }
 
@@ -2827,6 +2905,55 @@ __global__ __launch_bounds__(256) void k_dst_sort_group(tgsim_delivery* in, cons
   if (j == 0 && n) cnt[d] = 0;
 }
 
+// A local delivery without a host round trip sizes its scatter and output buffers by a bound
+// (tgsim_engine deliver_local_from); when the window's exact total (the scan's, on the device)
+// exceeds it, this empties the window's record counts so that no later kernel writes past the
+// buffers, and raises the sticky error (-ENOSPC at the next call).
+__global__ __launch_bounds__(256) void k_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
+                                                       uint32_t n_src, uint64_t* cnt, uint32_t n_dst,
+                                                       uint64_t* err_host) {
+  if (*total <= cap) return;
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, st = gridDim.x * blockDim.x;
+  if (i0 == 0 && err_host) __hip_atomic_store(err_host, (uint64_t)kErrDeliverCap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (uint32_t i = i0; i < n_src; i += st) emit_n[i] = 0;
+  for (uint32_t i = i0; i < n_dst; i += st) cnt[i] = 0;
+}
+
+// The same with the slots k_sim took from its per-destination count atomics: every record's place is
+// its destination's segment start plus its slot, so no atomic is needed here (each would be a
+// memory-side request of its own: at the flood's peak, tens of millions per window).
+__global__ __launch_bounds__(256) void k_local_scatter_slot(const tgsim_delivery* __restrict__ emit,
+                                                            const uint32_t* __restrict__ emit_slot,
+                                                            const uint32_t* __restrict__ emit_n,
+                                                            const uint64_t* __restrict__ off, uint32_t n_src,
+                                                            uint32_t dst_begin, const uint64_t* __restrict__ seg,
+                                                            tgsim_delivery* __restrict__ out) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+  uint32_t n = 0;
+  uint64_t b = 0;
+  if (s < n_src) {
+    n = emit_n[s];
+    b = 2 * off[s] + (uint64_t)kHeapCap * s;
+  }
+  for (uint32_t i = 0; __ballot(i < n); i += 4) {
+    tgsim_delivery r[4];
+    uint32_t sl[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (i + u < n) {
+        r[u] = emit[b + i + u];
+        sl[u] = emit_slot[b + i + u];
+      }
+    uint64_t at[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (i + u < n) at[u] = seg[r[u].dst - dst_begin] + sl[u];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (i + u < n) out[at[u]] = r[u];
+  }
+}
+
 // Ranks inside lane groups of G records (one destination each) with the keys in LDS: each lane
 // reads its group's keys as one 16-B word each, (t, src << 32 | seq), instead of five cross-lane
 // shuffles per key (k_dst_sort_group); only a packet and its duplicate share that key, and the
@@ -2994,6 +3121,10 @@ void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState
   hipLaunchKernelGGL(k_apply_cfg, dim3((n + 255) / 256), dim3(256), 0, st, p, n, params, state, stats);
 }
 
+void launch_unrotate(uint4* heap, SrcState* state, uint32_t n_src, hipStream_t st) {
+  if (n_src) hipLaunchKernelGGL(k_unrotate, dim3((n_src + 3) / 4), dim3(256), 0, st, heap, state, n_src);
+}
+
 void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone, hipStream_t st) {
   if (n_src) hipLaunchKernelGGL(k_purge, dim3((n_src + 3) / 4), dim3(256), 0, st, heap, state, n_src, gone);
 }
@@ -3139,9 +3270,20 @@ void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin
                      pos, out, slot, n_win);
 }
 
+void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n, uint32_t n_src, uint64_t* cnt,
+                          uint32_t n_dst, uint64_t* err_host, hipStream_t st) {
+  hipLaunchKernelGGL(k_deliver_guard, dim3(1024), dim3(256), 0, st, total, cap, emit_n, n_src, cnt, n_dst, err_host);
+}
+
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
-                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
+                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint,
+                          const uint32_t* emit_slot, const uint64_t* seg) {
   if (!n_src) return;
+  if (emit_slot) {  // slots from k_sim's count atomics: segment start + slot
+    hipLaunchKernelGGL(k_local_scatter_slot, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_slot, emit_n, off,
+                       n_src, dst_begin, seg, out);
+    return;
+  }
   if (n_hint <= 64ull * n_src) {  // up to tens of records per source (gossip, even at the flood's peak): one lane each
     hipLaunchKernelGGL(k_local_scatter_ls, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
                        dst_begin, pos, out);

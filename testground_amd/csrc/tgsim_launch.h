@@ -39,6 +39,7 @@ void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState
                       unsigned long long* stats, hipStream_t st);
 // marks queued items towards gone[dst] != 0 dead (kDeadDst)
 void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone, hipStream_t st);
+void launch_unrotate(uint4* heap, SrcState* state, uint32_t n_src, hipStream_t st);
 // *v0 (and *v1) into pinned slot[0], slot[1], then seq into slot[2] (system-scope release)
 void launch_publish(const uint64_t* v0, const uint32_t* v1, uint64_t* slot, uint64_t seq, hipStream_t st);
 // K7: table[state] += n; new value -> mirror[state] and *result (pinned), then *marker = seq
@@ -78,9 +79,11 @@ void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, u
                      hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
                         tgsim_delivery* out, hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
+void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n, uint32_t n_src, uint64_t* cnt,
+                          uint32_t n_dst, uint64_t* err_host, hipStream_t st);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
-                          uint64_t n_hint);
+                          uint64_t n_hint, const uint32_t* emit_slot = nullptr, const uint64_t* seg = nullptr);
 // Orders each destination's records; resets cnt[] to zero for the next histogram.
 // (in, the scatter buffer, is overwritten for segments longer than 64.)
 // n_hint: about how many records (picks one wavefront per destination or eight).

@@ -81,6 +81,33 @@ def test_step_n_falls_back_when_not_fusable(make_oracle):
     assert_same(g, c, "sparse windows through step_n")
 
 
+def test_step_n_after_sparse_fifo_windows(make_oracle):
+    """FIFO sources (fixed latency; no jitter, reordering or duplication) in sparse windows: the
+    sparse kernel serves the sorted queue's prefix and appends behind its tail in place, moving the
+    queue's head slot instead of the items.  Dense windows after them run fused, whose bounded loads
+    read every queue from slot 0 (k_unrotate compacts them first).  Every window equals the oracle."""
+    from testground_amd.network import configs_array
+
+    n = 300
+    g, c = Engine(n), make_oracle(n)
+    for e in (g, c):
+        e.configure_batch(np.arange(n), configs_array(np.full(n, 3_000_000), routing_policy=2))
+    for k in range(6):  # ~20 packets per source and window, ~60 queued: sparse, FIFO
+        for e in (g, c):
+            e.gen_storm(0.02, 1000)
+            e.step(1000)
+        assert_same(g, c, f"sparse FIFO window {k}")
+    model = g.stats()["queue_state_bytes"]
+    # (with ~60 queued items the first chunk is all of a queue: what stays in place is the store)
+    assert g.carry_bytes() < 0.8 * model, "the FIFO path left the queues in place"
+    for e in (g, c):
+        for _ in range(4):
+            e.gen_storm(0.5, 400)  # 200 packets per source: dense, fused
+        e.step_n(400, 4)
+    assert _fused(g) == 4
+    assert_same(g, c, "fused windows after in-place queues")
+
+
 def test_three_shards_fused_slotted_exchange_equal_one():
     """The fused slotted layout (tgsim_step_sim_launch_slotted_n: rank-major chunks, window-minor;
     tgsim_deliver_slotted_n_async) over three shards on one GPU, the chunks swapped by hand as the
