@@ -25,3 +25,8 @@ for sh in "" --sharded; do
   timeout -k 10 300 python bench.py --workload gossip --peers 125000 --no-cpu $sh > $O/b125.json 2> $O/b125.err || { tail $O/b125.err; exit 1; }
   python -c "import json; d=json.load(open('$O/b125.json')); r=d['roofline']; print('125k $sh', round(d['value']/1e9,3), 'G pkt/s', round(d['ms_per_step'],4), 'ms/step sim', round(r['kernel_ms_avg'],4))"
 done
+# the C3 headline beside it (no regression of the dense path)
+if [ -n "$STORM" ]; then
+  timeout -k 10 300 python bench.py --no-cpu --no-1m > $O/storm.json 2> $O/storm.err || { tail $O/storm.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/storm.json')); r=d['roofline']; print('storm', round(d['value']/1e9,3), 'G pkt/s', round(d['ms_per_step'],4), 'ms/step k_sim', round(r['kernel_ms_avg'],4))"
+fi
