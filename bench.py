@@ -79,7 +79,8 @@ def parse(argv=None):
                    help="storm: C3 heterogeneous shapes; open: C3 shapes at 1 Gbit/s driven below capacity "
                         "(the sub-capacity variant); fixed: L=5 ms, no jitter/loss/reorder (probe)")
     p.add_argument("--sharded", action="store_true",
-                   help="use the peer-sharded step (RCCL exchange) even at one rank, to time the N>1 path")
+                   help="use the engine's exchange (tgsim_comm_*) even at one rank; there it is the single-shard "
+                        "step (nothing to route) unless TGSIM_COMM_ROUTE1=1 keeps the routed N>1 path")
     p.add_argument("--exact-exchange", action="store_true",
                    help="sharded storm: exchange exact record counts every step instead of fixed-size chunks")
     p.add_argument("--no-1m", action="store_true",

@@ -10,18 +10,24 @@
 //   simulate stream   k_sim (or k_sim_fused) of window k, dispatch order of k+1
 //   routing stream    records of window k grouped by destination rank (tgsim_step_sim_launch*)
 //   exchange stream   (high priority) count all-to-all, grouped ncclSend/ncclRecv of the records
-//                     to and from every other rank; the own rank's records are copied on the device
-//                     (or, at one rank, delivered in place); records an event
+//                     to and from every other rank; the own rank's records are copied on the device;
+//                     records an event
 //   delivery stream   waits for that event: per-destination sort of the inbound records
 //
+// At one rank the engine owns every destination: nothing is routed or moved, and tgsim_comm_step /
+// tgsim_comm_run are the single-shard tgsim_step / tgsim_step_n (local delivery, fused groups).
+// TGSIM_COMM_ROUTE1=1 keeps the routed path at one rank (routing, then the delivery reads the routed
+// records in place), to time the N > 1 step's own kernels on one GPU.
+//
 // Buffers: out[k % 3] holds window k's routed records (two launched windows + one being exchanged),
-// in[k % 2] the inbound ones; ev_out[j] is the last reader of out[j] (the exchange, or at one rank
-// the delivery), ev_in[i] the delivery that last read in[i].  Every wait is an event on a stream;
-// the host blocks only where RCCL needs sizes it cannot know (the count exchange of tgsim_comm_step).
+// in[k % 2] the inbound ones; ev_out[j] is the last reader of out[j] (the exchange), ev_in[i] the
+// delivery that last read in[i].  Every wait is an event on a stream; the host blocks only where RCCL
+// needs sizes it cannot know (the count exchange of tgsim_comm_step).
 #include <dlfcn.h>
 #include <errno.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -126,6 +132,7 @@ struct Comm {
   uint64_t* h_cnt = nullptr;  // pinned: [0..8) sent, [8..16) received, [16] reduction result
   uint64_t exchanged = 0, max_count = 0, slot_cap = 0;
   bool launched = false;  // tgsim_comm_launch without its tgsim_comm_finish yet
+  bool local = false;     // one rank, not TGSIM_COMM_ROUTE1: the single-shard step
 };
 
 int fail(Comm* C, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
@@ -224,6 +231,8 @@ int allreduce_u64(Comm* C, const void* dev_src, uint64_t* result, ncclRedOp_t op
 
 extern "C" {
 
+int tgsim_step(void*, uint32_t);
+int tgsim_step_n(void*, uint32_t, uint32_t);
 int tgsim_step_sim_launch(void*, uint32_t, uint32_t, const uint32_t*, void*, size_t);
 int tgsim_step_sim_counts(void*, uint64_t*);
 int tgsim_step_sim_launch_slotted_n(void*, uint32_t, uint32_t, uint32_t, const uint32_t*, void*, uint64_t, void*);
@@ -299,6 +308,8 @@ int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
   // at one rank no RCCL kernel competes with the simulation for CU slots, so fused groups keep
   // their persistent grid (with more ranks the grid turns over to let the exchange in)
   engine_persist_routed(e, nranks == 1);
+  const char* r1 = getenv("TGSIM_COMM_ROUTE1");
+  C->local = nranks == 1 && !(r1 && atoi(r1));
   return 0;
 }
 
@@ -308,6 +319,14 @@ int tgsim_comm_launch(void* e, uint32_t n_ticks) {
   if (n_ticks == 0) return -EINVAL;
   if (C->launched) return engine_fail(e, -EBUSY, "comm_launch: the launched window is not finished (tgsim_comm_finish)");
   CHIP(hipSetDevice(C->dev));
+  if (C->local) {  // one rank owns every destination: nothing to route or move, so the window
+                         // is the single-shard step with its asynchronous local delivery (the count
+                         // of routed records is never read back: no host round trip)
+    CRC(tgsim_step(e, n_ticks));
+    C->k++;
+    C->launched = true;
+    return 0;
+  }
   const uint32_t j = C->k % 3;
   const int64_t cap = tgsim_sim_capacity(e);
   if (cap < 0) return static_cast<int>(cap);
@@ -325,6 +344,7 @@ int tgsim_comm_finish(void* e) {
   CHIP(hipSetDevice(C->dev));
   C->launched = false;
   const int nr = C->nranks;
+  if (C->local) return 0;  // tgsim_comm_launch ran the whole window
   const uint32_t j = C->k % 3, i = C->k % 2;
   uint64_t send[8] = {}, recv[8] = {}, soff[9] = {}, roff[9] = {};
   CRC(tgsim_step_sim_counts(e, send));  // the host waits for the routing's published counts
@@ -334,7 +354,7 @@ int tgsim_comm_finish(void* e) {
     C->max_count = std::max(C->max_count, send[r]);
   }
   C->exchanged += soff[nr];
-  if (nr == 1) {  // nothing to exchange: the delivery reads the routed records in place
+  if (nr == 1) {  // TGSIM_COMM_ROUTE1: nothing to exchange, the delivery reads the routed records in place
     CRC(tgsim_deliver_async(e, C->out[j].p, send[0], nullptr));
     CRC(tgsim_delivery_event(e, C->ev_out[j]));
     C->out_busy[j] = true;
@@ -374,6 +394,11 @@ int tgsim_comm_run(void* e, uint32_t n_ticks, uint32_t n_steps, uint32_t fuse, u
   if (!n_steps) return 0;
   CHIP(hipSetDevice(C->dev));
   const int nr = C->nranks;
+  if (C->local) {  // one rank: nothing to route or move; the single-shard fused groups
+    CRC(tgsim_step_n(e, n_ticks, n_steps));
+    C->k += n_steps;
+    return 0;
+  }
   if (!slot_cap) {  // from the exact windows so far, max over ranks (a collective every rank makes)
     uint64_t mx = 0;
     C->h_cnt[0] = C->max_count;
@@ -418,7 +443,7 @@ int tgsim_comm_run(void* e, uint32_t n_ticks, uint32_t n_steps, uint32_t fuse, u
     if (s + 2 < groups.size()) CRC(launch(groups[s + 2]));
     const uint64_t chunk = static_cast<uint64_t>(L.w) * (slot_cap + 1);  // records per rank
     C->exchanged += nr * chunk;
-    if (nr == 1) {  // the routed chunk is this rank's own: delivered in place
+    if (nr == 1) {  // TGSIM_COMM_ROUTE1: the routed chunk is this rank's own, delivered in place
       CRC(tgsim_deliver_slotted_n_async(e, C->out[L.j].p, 1, L.w, slot_cap, C->ev_routed[L.j]));
       CRC(tgsim_delivery_event(e, C->ev_out[L.j]));
       C->out_busy[L.j] = true;

@@ -862,7 +862,7 @@ constexpr uint32_t kPhLoad = 1, kPhStore = 2;  // sim_source phases: queue from 
 // kMode: 0 plain loads and stores (k_sim, k_sim_list); 1 the HBM state is handed off inside a
 // window-major fused launch (bounded sc1 loads and stores); 2 source-major fused (bounded loads).
 constexpr int kModePlain = 0, kModeHandoff = 1, kModeSourceMajor = 2;
-template <bool kOpen, uint32_t kCap, int kMode = kModePlain, bool kRecv = false>
+template <bool kOpen, uint32_t kCap, int kMode = kModePlain, bool kRecv = false, bool kSlots = false>
 __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
                                                uint32_t* claim = nullptr, uint32_t claim_base = 0,
                                                SrcCarry* carry = nullptr, uint32_t ph = kPhLoad | kPhStore) {
@@ -900,7 +900,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
-  Q.eslot = kMode == kModePlain && a.emit_slot ? a.emit_slot + 2 * a.off[s] + (uint64_t)kHeapCap * s : nullptr;
+  Q.eslot = kSlots && a.emit_slot ? a.emit_slot + 2 * a.off[s] + (uint64_t)kHeapCap * s : nullptr;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
@@ -2000,8 +2000,8 @@ __global__ __launch_bounds__(kWave) void k_sim_list(SimArgs a) {
   const uint32_t n = *a.worklist_n;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t s = a.worklist[i];
-    if (a.g_first) sim_source<false, kHeapCap, kModePlain, true>(a, s, s, lds);
-    else sim_source<false, kHeapCap>(a, s, s, lds);
+    if (a.g_first) sim_source<false, kHeapCap, kModePlain, true, true>(a, s, s, lds);
+    else sim_source<false, kHeapCap, kModePlain, false, true>(a, s, s, lds);
     wave_lds_sync();  // the write-back's LDS reads are done before the next source's loads land
   }
 }

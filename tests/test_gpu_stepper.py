@@ -1,8 +1,9 @@
 """The sharded step on one GPU with a world of one rank, against the single-engine step: identical
 verdicts and deliveries, open loop (storm) and closed loop (gossip, whose receipts feed the next
-window).  Every test runs both exchanges: the engine's own (CommStepper over tgsim_comm_*: its RCCL
-communicator, exchange stream and buffers, what bench.py and a Go host use) and the
-torch.distributed one over the split-phase ABI (ShardedStepper)."""
+window).  Every test runs the exchanges: the engine's own (CommStepper over tgsim_comm_*: its RCCL
+communicator, exchange stream and buffers, what bench.py and a Go host use; at one rank the
+single-shard step, or with TGSIM_COMM_ROUTE1=1 the routed path) and the torch.distributed one over
+the split-phase ABI (ShardedStepper)."""
 import os
 
 import numpy as np
@@ -29,11 +30,25 @@ def rccl():
     dist.destroy_process_group()
 
 
-@pytest.fixture(params=["engine", "torch"])
+class RoutedCommStepper:
+    """CommStepper at one rank with TGSIM_COMM_ROUTE1=1: the routed N > 1 path (routing kernels, the
+    delivery reading the routed records in place) instead of the single-shard step."""
+
+    def __new__(cls, *args, **kw):
+        from testground_amd.shard import CommStepper
+
+        os.environ["TGSIM_COMM_ROUTE1"] = "1"  # read by tgsim_comm_init
+        try:
+            return CommStepper(*args, **kw)
+        finally:
+            del os.environ["TGSIM_COMM_ROUTE1"]
+
+
+@pytest.fixture(params=["engine", "engine-routed", "torch"])
 def Stepper(request, rccl):
     from testground_amd.shard import CommStepper, ShardedStepper
 
-    return CommStepper if request.param == "engine" else ShardedStepper
+    return {"engine": CommStepper, "engine-routed": RoutedCommStepper, "torch": ShardedStepper}[request.param]
 
 
 def test_stepper_storm_equals_step(Stepper):
@@ -147,14 +162,25 @@ def test_stepper_slotted_run_equals_step(Stepper):
 
 
 def test_stepper_slotted_overflow_fails(Stepper):
-    """A chunk too small for a step's records is an error (-ENOSPC), never a silent loss."""
+    """A chunk too small for a step's records is an error (-ENOSPC), never a silent loss.  At one
+    rank the engine's own exchange routes nothing (tgsim_comm_run is the single-shard tgsim_step_n),
+    so no chunk can overflow there: the run equals the single engine instead."""
     from testground_amd.engine import EngineError
+    from testground_amd.shard import CommStepper
 
     n = 500
-    sh = Engine(n)
-    wl.configure_storm(sh, n)
-    for _ in range(3):
-        sh.gen_storm(0.5, 1000)
+    sh, ref = Engine(n), Engine(n)
+    for e in (sh, ref):
+        wl.configure_storm(e, n)
+        for _ in range(3):
+            e.gen_storm(0.5, 1000)
+    if Stepper is CommStepper:  # (RoutedCommStepper routes, and overflows below)
+        Stepper(sh, [0, n], device="cuda:0", slot_cap=16).run(3, 1000)
+        ref.step_n(1000, 3)
+        got, want = sh.drain(), ref.drain()
+        assert len(got) == len(want) > 1000 and (got == want).all()
+        assert sh.comm_info()["exchanged_records"] == 0
+        return
     with pytest.raises(EngineError, match="slot capacity"):
         Stepper(sh, [0, n], device="cuda:0", slot_cap=16).run(3, 1000)
         sh.sync()
