@@ -19,4 +19,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
   timeout -k 10 600 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $O/pmc/p$i -o run -- python3 bench.py $B > $O/pmc/p$i.log 2>&1 || { tail $O/pmc/p$i.log; exit 1; }
   echo "pmc pass $i ok"
 done
-python scripts/pmc_summary.py $O/pmc 70 1000000 0.5 5000 storm > $O/pmc_k_sim_gossip.json  # (bench.py's --shapes default) && cat $O/pmc_k_sim_gossip.json
+python scripts/pmc_summary.py $O/pmc 70 1000000 0.5 5000 gossip > $O/pmc_k_sim_gossip.json && cat $O/pmc_k_sim_gossip.json
