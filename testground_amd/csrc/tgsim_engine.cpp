@@ -216,7 +216,9 @@ struct tgsim_engine_s {
   std::vector<PendingTiming> ev_pending;
   std::vector<hipEvent_t> ev_pool;
   uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
-  uint64_t* h_pub = nullptr;    // pinned words a scan publishes: [0] total, [1] flag, [2] sequence
+  uint64_t* h_pub = nullptr;    // pinned words a scan publishes: [0] total, [1] flag, [2] sequence;
+                                // [4..6] the same for a gossip window generated ahead of its size
+  hipEvent_t ev_gpub = nullptr;
   uint64_t* dm_pub = nullptr;
   uint64_t pub_seq = 0;
   hipEvent_t ev_pub = nullptr;
@@ -279,6 +281,11 @@ struct tgsim_engine_s {
     DevBuf<InRec> in;
     uint64_t n = 0;
     uint32_t ticks = 0;
+    // a gossip window whose forwards were written before the host knew their total (published to
+    // h_pub[4..6] with sequence pub_seq): resolved by the step that consumes it
+    bool pending = false;
+    uint64_t pub_seq = 0;
+    GossipArgs g{};
   };
   std::vector<GenWindow> gen_q;   // device-generated traffic, one window per future step
   std::vector<GenWindow> gen_free;
@@ -294,15 +301,21 @@ struct tgsim_engine_s {
   // emit regions and per-destination histogram written by k_sim; a single-shard step reads them
   // on the delivery stream while the next k_sim writes the other pair (swapped by deliver_local;
   // ev_local: the delivery that last read the pair)
-  DevBuf<tgsim_delivery> d_emit, d_emit_alt;
-  DevBuf<uint32_t> d_eslot, d_eslot_alt;  // records' slots in their destinations' segments (emit_slot)
+  // Emit sets: window k's k_sim writes set k % emit_sets (d_emit, ...) while the deliveries of the
+  // windows before it read the others (the *_alt / *_3 sets, rotated after every window); k_sim waits
+  // only for the delivery of window k - emit_sets, so a delivery may lag (the gossip flood's peak)
+  DevBuf<tgsim_delivery> d_emit, d_emit_alt, d_emit_3;
+  DevBuf<uint32_t> d_eslot, d_eslot_alt, d_eslot_3;  // records' slots in their destinations' segments (emit_slot)
+  uint32_t emit_sets = 2;                            // TGSIM_EMIT_SETS: 2 or 3 (each set of a 1M-peer
+                                                     // engine is ~38 GB: its regions reserve 1,024
+                                                     // records per source)
   bool eslot_on = false;                  // the last k_sim wrote d_eslot (heavy sparse windows)
   uint64_t slot_min = 16;                 // TGSIM_SLOT_MIN: offered packets per source from which it is on
   uint64_t deliver_slack = 128;           // TGSIM_DELIVER_SLACK: queued items per source a bounded local
                                           // delivery allows for (besides 2 per offered packet)
-  DevBuf<uint32_t> d_emit_n, d_emit_n_alt;
-  DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (k_dst_sort resets it)
-  hipEvent_t ev_local = nullptr, ev_local_alt = nullptr;
+  DevBuf<uint32_t> d_emit_n, d_emit_n_alt, d_emit_n_3;
+  DevBuf<uint64_t> d_lcnt, d_lcnt_alt, d_lcnt_3;  // stays zero between steps (k_dst_sort resets it)
+  hipEvent_t ev_local = nullptr, ev_local_alt = nullptr, ev_local_3 = nullptr;
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
@@ -786,6 +799,44 @@ SimArgs base_sim_args(Eng* E) {
   return a;
 }
 
+// The next window's emit set: the current one becomes the newest being delivered.
+void rotate_emit(Eng* E) {
+  std::swap(E->d_emit, E->d_emit_alt);
+  std::swap(E->d_emit_n, E->d_emit_n_alt);
+  std::swap(E->d_eslot, E->d_eslot_alt);
+  std::swap(E->d_lcnt, E->d_lcnt_alt);
+  std::swap(E->ev_local, E->ev_local_alt);
+  if (E->emit_sets < 3) return;
+  // (a, b, c) -> (b, c, a): the set written two windows ago comes up once its delivery is the oldest
+  std::swap(E->d_emit_alt, E->d_emit_3);
+  std::swap(E->d_emit_n_alt, E->d_emit_n_3);
+  std::swap(E->d_eslot_alt, E->d_eslot_3);
+  std::swap(E->d_lcnt_alt, E->d_lcnt_3);
+  std::swap(E->ev_local_alt, E->ev_local_3);
+}
+
+// The size of a gossip window generated ahead of it (tgsim_gen_gossip): waits for the published
+// scan total; a window larger than its reserved buffer is written again into a larger one.
+int resolve_gen(Eng* E, Eng::GenWindow& w) {
+  if (!w.pending) return 0;
+  int rc = wait_published(E, &E->h_pub[6], w.pub_seq, E->ev_gpub, "gossip generation (scan total)");
+  if (rc) return rc;
+  const uint64_t total = __atomic_load_n(&E->h_pub[4], __ATOMIC_ACQUIRE);
+  const uint64_t late = __atomic_load_n(&E->h_pub[5], __ATOMIC_ACQUIRE);
+  w.pending = false;
+  if (late)
+    return E->fail(-EINVAL, "gossip: a receipt precedes the window at tick %llu (lookahead shorter than the window)",
+                   static_cast<unsigned long long>(w.g.win0));
+  if (total > w.in.cap) {  // the capped write skipped this window: write it into a larger buffer
+    HIPCHK(hipStreamSynchronize(E->st));  // (the old buffer is freed)
+    HIPCHK(w.in.ensure(total));
+    launch_gossip(w.g, nullptr, 0, nullptr, w.off.p, w.in.p, 2, E->st);
+    HIPCHK(hipGetLastError());
+  }
+  w.n = total;
+  return 0;
+}
+
 int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   int erc = check_sim_error(E);
   if (erc) return erc;
@@ -794,6 +845,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   if (!E->gen_q.empty()) {
     if (!E->staged.empty()) return E->fail(-EBUSY, "host packets and generated traffic in one step");
     Eng::GenWindow& w = E->gen_q.front();
+    int grc = resolve_gen(E, w);
+    if (grc) return grc;
     if (n_ticks != w.ticks)
       return E->fail(-EINVAL, "generated window spans %u ticks, step is %u", w.ticks, n_ticks);
     std::swap(E->d_off, w.off);
@@ -982,11 +1035,7 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
   HIPCHK(hipEventRecord(E->ev_route[k], rs));
   HIPCHK(hipEventRecord(E->ev_rt, rs));
   HIPCHK(hipEventRecord(E->ev_local, rs));  // the last reader of this emit pair
-  std::swap(E->d_emit, E->d_emit_alt);
-  std::swap(E->d_emit_n, E->d_emit_n_alt);
-  std::swap(E->d_eslot, E->d_eslot_alt);
-  std::swap(E->d_lcnt, E->d_lcnt_alt);
-  std::swap(E->ev_local, E->ev_local_alt);
+  rotate_emit(E);
   E->route_ranks[k] = n_ranks;
   E->route_cap[k] = out_cap;
   E->route_n++;
@@ -1227,11 +1276,7 @@ int deliver_local(Eng* E) {
   if (rc) return rc;
   HIPCHK(hipEventRecord(E->ev_local, sq));
   HIPCHK(hipEventRecord(E->ev_dst, sq));
-  std::swap(E->d_emit, E->d_emit_alt);
-  std::swap(E->d_emit_n, E->d_emit_n_alt);
-  std::swap(E->d_eslot, E->d_eslot_alt);
-  std::swap(E->d_lcnt, E->d_lcnt_alt);
-  std::swap(E->ev_local, E->ev_local_alt);
+  rotate_emit(E);
   return 0;
 }
 
@@ -1551,7 +1596,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_recv, E->dst_st), "event"))) return bail(rc);
-  for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt}) {
+  for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt, &E->ev_local_3}) {
     if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
     if ((rc = E->hip(hipEventRecord(*ev, E->dst_st), "event"))) return bail(rc);
   }
@@ -1571,10 +1616,11 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
     return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_gerr), sizeof(uint32_t)), "pinned"))) return bail(rc);
   *E->h_gerr = 0;
-  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_pub), 4 * sizeof(uint64_t),
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_pub), 8 * sizeof(uint64_t),
                                  hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
     return bail(rc);
-  memset(E->h_pub, 0, 4 * sizeof(uint64_t));
+  memset(E->h_pub, 0, 8 * sizeof(uint64_t));
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_gpub, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->dm_pub), E->h_pub, 0), "pinned")))
     return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_pub, hipEventDisableTiming), "event"))) return bail(rc);
@@ -1594,6 +1640,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
   if (const char* sm = getenv("TGSIM_SLOT_MIN")) E->slot_min = strtoull(sm, nullptr, 10);
   if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) E->deliver_slack = strtoull(ds, nullptr, 10);
+  if (const char* es = getenv("TGSIM_EMIT_SETS")) E->emit_sets = atoi(es) == 3 ? 3u : 2u;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
   if (const char* fo = getenv("TGSIM_FUSED_ORDER")) E->order_chain = strcmp(fo, "records") != 0;
   if (const char* fm = getenv("TGSIM_FUSED_MAJOR")) E->source_major = strcmp(fm, "source") == 0;
@@ -1692,7 +1739,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_eslot.release(); E->d_eslot_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_eslot.release(); E->d_eslot_alt.release(); E->d_emit_3.release(); E->d_emit_n_3.release(); E->d_eslot_3.release(); E->d_lcnt_3.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release(); E->d_chain.release();
@@ -1716,6 +1763,7 @@ void tgsim_destroy(void* e) {
   if (E->h_work) (void)hipHostFree(E->h_work);
   if (E->h_gerr) (void)hipHostFree(E->h_gerr);
   if (E->h_pub) (void)hipHostFree(E->h_pub);
+  if (E->ev_gpub) (void)hipEventDestroy(E->ev_gpub);
   if (E->ev_pub) (void)hipEventDestroy(E->ev_pub);
   if (E->h_edges) (void)hipHostFree(E->h_edges);
   for (hipEvent_t ev : E->ev_route)
@@ -1726,6 +1774,7 @@ void tgsim_destroy(void* e) {
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->ev_local) (void)hipEventDestroy(E->ev_local);
   if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);
+  if (E->ev_local_3) (void)hipEventDestroy(E->ev_local_3);
   if (E->dst_st) (void)hipStreamDestroy(E->dst_st);
   if (E->rt_st) (void)hipStreamDestroy(E->rt_st);
   if (E->st) (void)hipStreamDestroy(E->st);
@@ -1854,10 +1903,10 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   }
   HIPCHK(hipStreamSynchronize(E->st));
   // a flood's windows grow geometrically while it spreads: reserve the window buffers (generated
-  // input of two windows, the step's input and verdicts) for two forwards per peer and
-  // out-neighbour, so the first windows do not reallocate one after another (each hipFree +
-  // hipMalloc stalls the closed loop for 0.3-0.5 ms)
-  const size_t reserve = static_cast<size_t>(E->S) * g->degree * 2;
+  // input of two windows, the step's input and verdicts) for four forwards per peer and
+  // out-neighbour (the 1M-peer flood's peak windows offer ~30 packets per peer), so no window of the
+  // flood reallocates (each hipFree + hipMalloc stalls the closed loop for 0.3-0.5 ms)
+  const size_t reserve = static_cast<size_t>(E->S) * g->degree * 4;  // the flood's peak: ~30 per peer
   while (E->gen_free.size() < 2) E->gen_free.emplace_back();
   for (auto& w : E->gen_free) {
     HIPCHK(w.off.ensure(E->S + 1));
@@ -1868,8 +1917,10 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   // the emit regions of both parities and the record slots of the flood's heavy windows, for the
   // same reserve (a hipFree + hipMalloc of several GB inside the flood stalls the loop)
   const uint64_t emit_cap = 2 * reserve + static_cast<uint64_t>(kHeapCap) * E->S;
-  for (auto* b : {&E->d_emit, &E->d_emit_alt}) HIPCHK(b->ensure(emit_cap));
-  for (auto* b : {&E->d_eslot, &E->d_eslot_alt}) HIPCHK(b->ensure(emit_cap));
+  for (auto* b : {&E->d_emit, &E->d_emit_alt, &E->d_emit_3})
+    if (b != &E->d_emit_3 || E->emit_sets == 3) HIPCHK(b->ensure(emit_cap));
+  for (auto* b : {&E->d_eslot, &E->d_eslot_alt, &E->d_eslot_3})
+    if (b != &E->d_eslot_3 || E->emit_sets == 3) HIPCHK(b->ensure(emit_cap));
   E->gossip_on = true;
   return 0;
 }
@@ -1879,6 +1930,10 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   if (!E || !E->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
   if (!E->staged.empty()) return E->fail(-EBUSY, "host packets already pending for the next step");
   HIPCHK(hipSetDevice(E->dev));
+  for (auto& q : E->gen_q) {  // a window still unsized is sized (and written) before this one runs
+    int rc = resolve_gen(E, q);
+    if (rc) return rc;
+  }
   // receipts are folded on the delivery stream (the sort of the same delivery may still run)
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_recv, 0));
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));  // a free window's offsets may still be read by a routing
@@ -1892,19 +1947,24 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   HIPCHK(E->d_cnt.ensure(E->S));
   launch_gossip(g, nullptr, 0, E->d_cnt.p, nullptr, nullptr, 1, E->st);
   HIPCHK(hipGetLastError());
-  uint64_t total = 0;
-  uint32_t late = 0;
-  int rc = scan_counts(E, E->d_cnt, w.off, E->d_blk, E->d_tot, E->S, &total, nullptr, nullptr, E->d_gerr.p, &late);
-  if (rc) return rc;
-  if (late) {
-    E->gen_free.push_back(std::move(w));
-    return E->fail(-EINVAL, "gossip: a receipt precedes the window at tick %llu (lookahead shorter than the window)",
-                   static_cast<unsigned long long>(win0));
-  }
-  HIPCHK(w.in.ensure(total ? total : 1));  // reserved by tgsim_gossip_init for typical windows
-  launch_gossip(g, nullptr, 0, nullptr, w.off.p, w.in.p, 2, E->st);  // the step runs behind it on E->st
+  // scan, then the forwards at once, without waiting for the total: the buffer is reserved for the
+  // flood's peak, and a window larger than it writes nothing here (the kernel compares the device's
+  // total with the capacity) and is written again once its size is known (resolve_gen, at the step)
+  HIPCHK(w.off.ensure(E->S + 1));
+  HIPCHK(E->d_blk.ensure((E->S + 1023) / 1024 + 1));
+  HIPCHK(E->d_tot.ensure(1));
+  launch_scan(E->d_cnt.p, w.off.p, E->S, E->d_blk.p, E->d_tot.p, E->st, nullptr);
   HIPCHK(hipGetLastError());
-  w.n = total;
+  launch_publish(E->d_tot.p, E->d_gerr.p, E->dm_pub + 4, ++E->pub_seq, E->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(E->ev_gpub, E->st));
+  HIPCHK(w.in.ensure(1));
+  launch_gossip(g, nullptr, 0, nullptr, w.off.p, w.in.p, 2, E->st, w.in.cap, E->d_tot.p);
+  HIPCHK(hipGetLastError());
+  w.pending = true;
+  w.pub_seq = E->pub_seq;
+  w.g = g;
+  w.n = 0;
   w.ticks = n_ticks;
   E->gen_q_ticks += n_ticks;
   E->gen_q.push_back(std::move(w));
@@ -1930,6 +1990,10 @@ int64_t tgsim_gossip_reached(void* e, uint64_t* out, size_t cap) {
 int64_t tgsim_sim_capacity(void* e) {
   Eng* E = as_eng(e);
   if (!E) return -EINVAL;
+  if (!E->gen_q.empty()) {
+    int rc = resolve_gen(E, E->gen_q.front());
+    if (rc) return rc;
+  }
   const uint64_t n = !E->gen_q.empty() ? E->gen_q.front().n : E->staged.size();
   return static_cast<int64_t>(2 * n + static_cast<uint64_t>(kHeapCap) * E->S);
 }

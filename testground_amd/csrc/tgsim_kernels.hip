@@ -1620,11 +1620,10 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1;
   stamp(a, s, lane, 0, __builtin_amdgcn_s_memrealtime());
-  // the first 64 ring entries are read before the state says how many there are (the array has room
-  // for 1024 per source): one dependent load level instead of two; the queue starts at its head slot
+  // the queue starts at its head slot; the ring (needed only after the netem decisions) is read with
+  // the queue, as far as the state says it is live
   const uint4* gh = a.heap + (size_t)s * kHeapCap;
   const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
-  const uint64_t r0 = gr[lane];
   const SrcState st = a.state[s];
   const SrcParams pp = a.params[s];
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
@@ -1649,7 +1648,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
       const uint64_t qb = 32ull * qn + 16ull * rn;
       if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
       if (qn) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(32ull * qn - 16ull));
-      if (rn) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(16ull * rn - 8ull * (rn < kWave ? rn : kWave)));
+      if (rn) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(16ull * rn));
     }
     return;
   }
@@ -1661,7 +1660,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   uint4 q[kSparseQ];
   uint64_t rg[kSparseQ];
   q[0] = lane < qn ? gh[(qh + lane) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
-  rg[0] = lane < rn ? r0 : ~0ull;
+  rg[0] = lane < rn ? gr[lane] : ~0ull;
   auto load_rest = [&]() {
 #pragma unroll
     for (uint32_t u = 1; u < kSparseQ; ++u) {
@@ -2304,9 +2303,11 @@ __global__ __launch_bounds__(256) void k_gossip_count(GossipArgs g, uint64_t* co
 // between the record stores of one peer and the next (its loads could not pass stores that might
 // alias them): a chain of dependent round trips per peer.
 __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint64_t* __restrict__ off,
-                                                       InRec* __restrict__ out) {
+                                                       InRec* __restrict__ out, uint64_t out_cap,
+                                                       const uint64_t* total) {
   const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
   if (s0 >= g.n_src) return;
+  if (total && *total > out_cap) return;  // written again into a larger buffer (resolve_gen)
   const uint32_t deg = g.degree;
   const bool pl = lane < kGossipPeers && s0 + lane < g.n_src;  // lane i < 8: peer s0 + i's words
   const uint64_t pend_l = pl ? g.pend[s0 + lane] : 0ull;
@@ -2352,9 +2353,11 @@ __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint6
   }
 }
 
-__global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64_t* off, InRec* out) {
+__global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64_t* off, InRec* out,
+                                                      uint64_t out_cap, const uint64_t* total) {
   const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
   if (s0 >= g.n_src) return;
+  if (total && *total > out_cap) return;  // written again into a larger buffer (resolve_gen)
   uint32_t t[kGossipPeers];
   uint64_t pend[kGossipPeers];
   gossip_rows(g, s0, lane, t, pend);
@@ -3191,7 +3194,8 @@ void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, con
 }
 
 void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
-                   const uint64_t* off, InRec* out, int phase, hipStream_t st) {
+                   const uint64_t* off, InRec* out, int phase, hipStream_t st, uint64_t out_cap,
+                   const uint64_t* total) {
   if (phase == 0) {
     if (n) hipLaunchKernelGGL(k_gossip_recv, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, g, recs, n);
     return;
@@ -3199,8 +3203,10 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
   const uint32_t waves = (g.n_src + kGossipPeers - 1) / kGossipPeers;  // kGossipPeers peers per wavefront
   const dim3 grid((waves + 3) / 4), blk(256);
   if (phase == 1) hipLaunchKernelGGL(k_gossip_count, grid, blk, 0, st, g, counts);
-  else if (g.nbr && g.degree <= kWave / kGossipPeers) hipLaunchKernelGGL(k_gossip_write8, grid, blk, 0, st, g, off, out);
-  else hipLaunchKernelGGL(k_gossip_write, grid, blk, 0, st, g, off, out);
+  else if (g.nbr && g.degree <= kWave / kGossipPeers)
+    hipLaunchKernelGGL(k_gossip_write8, grid, blk, 0, st, g, off, out, out_cap, total);
+  else
+    hipLaunchKernelGGL(k_gossip_write, grid, blk, 0, st, g, off, out, out_cap, total);
 }
 
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums,

@@ -49,7 +49,8 @@ void launch_gen(const GenArgsHost& h, uint64_t* counts, const uint64_t* off, uin
                 InRec* out, int phase, hipStream_t st);
 // phase 0: fold delivered records into receipts; 1: per-source counts; 2: write the window.
 void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t* counts,
-                   const uint64_t* off, InRec* out, int phase, hipStream_t st);
+                   const uint64_t* off, InRec* out, int phase, hipStream_t st, uint64_t out_cap = 0,
+                   const uint64_t* total = nullptr);
 // K8 metrics folds (opt-in): per source after k_sim, per destination after the delivery sort.
 void launch_metrics_src(const MetricsArgs& m, hipStream_t st);
 void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_t n_dst, unsigned long long* dst,
