@@ -70,6 +70,29 @@ def build_oracle(force: bool = False) -> Path:
     return ORACLE_LIB
 
 
+MOCK_DIR = ROOT / "tests" / "mockrccl"
+MOCK_COMM_LIB = MOCK_DIR / "libtgsim_mockcomm.so"
+
+
+def build_engine_mockcomm(force: bool = False) -> Path:
+    """TEST build of the engine for tests/test_gpu_multirank.py: the product's kernel, engine and
+    bridge objects, tgsim_comm.cpp recompiled with -DTGSIM_COMM_TEST_TRANSPORT and the ranks-as-threads
+    transport of tests/mockrccl linked in (RCCL refuses two ranks on one GPU).  Lives under tests/;
+    libtgsim.so never contains it."""
+    prod = build_engine()
+    srcs = [CSRC / "tgsim_comm.cpp", MOCK_DIR / "mock_rccl.cpp"]
+    if not force and not _stale(MOCK_COMM_LIB, srcs + HEADERS + [prod]):
+        return MOCK_COMM_LIB
+    objs = [str(PKG / "build" / (s.stem + ".o")) for s in SOURCES if s.stem != "tgsim_comm"]
+    for src in srcs:
+        obj = MOCK_DIR / (src.stem + ".o")
+        subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
+                        "-DTGSIM_COMM_TEST_TRANSPORT", "-c", str(src), "-o", str(obj)], check=True)
+        objs.append(str(obj))
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(MOCK_COMM_LIB), *objs], check=True)
+    return MOCK_COMM_LIB
+
+
 def build_engine_host_asan() -> Path:
     """libtgsim built with AddressSanitizer + UBSan on its HOST code only (-Xarch_host; GPU code is
     never sanitized on this pool): the CPU tests of the C ABI (tests/test_abi.py) load it."""

@@ -45,7 +45,9 @@ namespace {
 constexpr size_t kRec = sizeof(tgsim_delivery);
 
 // librccl.so.1, loaded once per process (when torch has loaded it already, dlopen returns that
-// same instance, so one process never holds two RCCL runtimes).
+// same instance, so one process never holds two RCCL runtimes).  The test build of this file
+// (-DTGSIM_COMM_TEST_TRANSPORT, tests/mockrccl: a separate library the product never contains)
+// binds the linked-in ranks-as-threads transport instead, since RCCL refuses two ranks on one GPU.
 struct Rccl {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*);
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
@@ -58,43 +60,78 @@ struct Rccl {
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
   ncclResult_t (*GroupStart)();
   ncclResult_t (*GroupEnd)();
+  bool ok = false;
+  std::string why;
 };
 
-const Rccl* rccl(std::string* err) {
-  static Rccl r;
-  static bool done = false, ok = false;
-  static std::string why;
-  if (!done) {
-    done = true;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) {
-      why = std::string("librccl.so.1 not loadable: ") + dlerror();
-    } else {
-      bool all = true;
-      auto get = [&](auto& fp, const char* name) {
-        fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
-        if (!fp) {
-          all = false;
-          why = std::string("librccl.so.1 lacks ") + name;
-        }
-      };
-      get(r.GetUniqueId, "ncclGetUniqueId");
-      get(r.CommInitRank, "ncclCommInitRank");
-      get(r.CommDestroy, "ncclCommDestroy");
-      get(r.GetErrorString, "ncclGetErrorString");
-      get(r.AllReduce, "ncclAllReduce");
-      get(r.AllGather, "ncclAllGather");
-      get(r.AllToAll, "ncclAllToAll");
-      get(r.Send, "ncclSend");
-      get(r.Recv, "ncclRecv");
-      get(r.GroupStart, "ncclGroupStart");
-      get(r.GroupEnd, "ncclGroupEnd");
-      ok = all;
-    }
+#ifdef TGSIM_COMM_TEST_TRANSPORT
+#define MOCK_DECL(ret, name, ...) extern "C" ret mockrccl_##name(__VA_ARGS__);
+MOCK_DECL(ncclResult_t, GetUniqueId, ncclUniqueId*)
+MOCK_DECL(ncclResult_t, CommInitRank, ncclComm_t*, int, ncclUniqueId, int)
+MOCK_DECL(ncclResult_t, CommDestroy, ncclComm_t)
+MOCK_DECL(const char*, GetErrorString, ncclResult_t)
+MOCK_DECL(ncclResult_t, AllReduce, const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t)
+MOCK_DECL(ncclResult_t, AllGather, const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t)
+MOCK_DECL(ncclResult_t, AllToAll, const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t)
+MOCK_DECL(ncclResult_t, Send, const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)
+MOCK_DECL(ncclResult_t, Recv, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)
+MOCK_DECL(ncclResult_t, GroupStart, void)
+MOCK_DECL(ncclResult_t, GroupEnd, void)
+#undef MOCK_DECL
+
+Rccl load_rccl() {
+  Rccl r;
+  r.GetUniqueId = mockrccl_GetUniqueId;
+  r.CommInitRank = mockrccl_CommInitRank;
+  r.CommDestroy = mockrccl_CommDestroy;
+  r.GetErrorString = mockrccl_GetErrorString;
+  r.AllReduce = mockrccl_AllReduce;
+  r.AllGather = mockrccl_AllGather;
+  r.AllToAll = mockrccl_AllToAll;
+  r.Send = mockrccl_Send;
+  r.Recv = mockrccl_Recv;
+  r.GroupStart = mockrccl_GroupStart;
+  r.GroupEnd = mockrccl_GroupEnd;
+  r.ok = true;
+  return r;
+}
+#else
+Rccl load_rccl() {
+  Rccl r;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    r.why = std::string("librccl.so.1 not loadable: ") + dlerror();
+    return r;
   }
-  if (!ok && err) *err = why;
-  return ok ? &r : nullptr;
+  bool all = true;
+  auto get = [&](auto& fp, const char* name) {
+    fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+    if (!fp) {
+      all = false;
+      r.why = std::string("librccl.so.1 lacks ") + name;
+    }
+  };
+  get(r.GetUniqueId, "ncclGetUniqueId");
+  get(r.CommInitRank, "ncclCommInitRank");
+  get(r.CommDestroy, "ncclCommDestroy");
+  get(r.GetErrorString, "ncclGetErrorString");
+  get(r.AllReduce, "ncclAllReduce");
+  get(r.AllGather, "ncclAllGather");
+  get(r.AllToAll, "ncclAllToAll");
+  get(r.Send, "ncclSend");
+  get(r.Recv, "ncclRecv");
+  get(r.GroupStart, "ncclGroupStart");
+  get(r.GroupEnd, "ncclGroupEnd");
+  r.ok = all;
+  return r;
+}
+#endif
+
+const Rccl* rccl(std::string* err) {
+  static const Rccl r = load_rccl();  // thread-safe one-time initialisation
+  if (!r.ok && err) *err = r.why;
+  return r.ok ? &r : nullptr;
 }
 
 struct DevMem {

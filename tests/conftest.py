@@ -17,6 +17,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X; drives libtgsim.so through its C ABI")
 
 
+def pytest_collection_finish(session):
+    """torch ships its own HIP runtime: when the run holds GPU tests, let it initialise the device
+    before any engine library does, whatever the order the selected tests run in."""
+    if not any(item.get_closest_marker("gpu") for item in session.items):
+        return
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 @pytest.fixture(scope="session")
 def oracle_lib():
     """The CPU golden model (oracle/), the checker for every parity test."""

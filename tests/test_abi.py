@@ -46,6 +46,18 @@ def test_no_cpu_fallback(lib):
     assert ei.value.code == -errno.ENODEV
 
 
+def test_product_has_no_test_transport(lib):
+    """The ranks-as-threads transport (tests/mockrccl) lives only in the test build of the engine:
+    the product binds librccl.so.1 and nothing else."""
+    from testground_amd.build import MOCK_COMM_LIB, build_engine_mockcomm
+
+    assert not hasattr(lib, "mockrccl_Send")
+    test_lib = C.CDLL(str(build_engine_mockcomm()))
+    assert hasattr(test_lib, "mockrccl_Send") and MOCK_COMM_LIB.parent.name == "mockrccl"
+    for name in header_functions():
+        assert hasattr(test_lib, name), name
+
+
 def _random_shape(rng):
     return nw.LinkShape(
         Latency=int(rng.choice([0, 1, 999, 1000, 10**6, 123_456_789, 5 * 10**9, -5000, 3 * 3600 * 10**9])),
