@@ -334,6 +334,8 @@ struct tgsim_engine_s {
   bool rotated = false;      // a sparse step may have left queues in place (head slot != 0)
   bool sparse_seen = false;  // h_work holds a measured worklist size
   uint32_t dense_streak = 0; // dense steps chosen because the last sparse step deferred too much
+  uint32_t dense_div = 4;    // TGSIM_DENSE_DIV: dense when the last sparse step deferred > S / dense_div
+  bool trace_list = false;   // TGSIM_TRACE_LIST: print each sparse decision's deferred count
   bool order_valid = false;
   int order_by = 0;          // TGSIM_ORDER_BY: 0 HTB records of the last step, 1 its k_sim time per source
   DevBuf<uint32_t> d_dur;
@@ -923,7 +925,16 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     // last sparse step (copied to pinned memory behind it, read without waiting) decides; every
     // 64th such step runs sparse again to re-measure
     const uint32_t deferred = __atomic_load_n(E->h_work, __ATOMIC_RELAXED);
-    sparse = !(E->sparse_seen && 4ull * deferred > E->S) || ++E->dense_streak >= 64;
+    if (E->trace_list) {
+      fprintf(stderr, "tgsim: sparse step deferred %u of %u sources", deferred, E->S);
+#ifdef TGSIM_DEFER_STATS  // by reason (corr, limit, n>64, queue, ring, fifo-due, sorted-queue, rest), cumulative
+      uint32_t why[8] = {};
+      if (E->d_work.p && hipMemcpy(why, E->d_work.p + 1 + E->S, sizeof why, hipMemcpyDeviceToHost) == hipSuccess)
+        for (uint32_t w : why) fprintf(stderr, " %u", w);
+#endif
+      fprintf(stderr, "\n");
+    }
+    sparse = !(E->sparse_seen && static_cast<uint64_t>(E->dense_div) * deferred > E->S) || ++E->dense_streak >= 64;
     if (sparse) E->dense_streak = 0;
   }
   a.worklist = a.worklist_n = nullptr;
@@ -936,7 +947,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     a.emit_slot = E->d_eslot.p;
   }
   if (sparse) {
-    HIPCHK(E->d_work.ensure(static_cast<size_t>(E->S) + 1));
+    HIPCHK(E->d_work.ensure(static_cast<size_t>(E->S) + 1 + 8));  // (+8: TGSIM_DEFER_STATS)
     HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t), E->st));
     a.worklist_n = E->d_work.p;
     a.worklist = E->d_work.p + 1;
@@ -1637,6 +1648,8 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
+  if (const char* dd = getenv("TGSIM_DENSE_DIV")) E->dense_div = static_cast<uint32_t>(std::max(1, atoi(dd)));
+  E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
   if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
   if (const char* sm = getenv("TGSIM_SLOT_MIN")) E->slot_min = strtoull(sm, nullptr, 10);
   if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) E->deliver_slack = strtoull(ds, nullptr, 10);

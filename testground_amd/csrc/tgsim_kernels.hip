@@ -1417,11 +1417,23 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
       for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
       for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
     }
+    uint32_t near_out = Q.qn;
+    if constexpr (kSlots) {
+      // k_sim_list: a queue whose pool happens to follow its near region in order (FIFO sources: no
+      // jitter, reordering or duplication) is stored as one sorted region, so that the next step's
+      // k_sim_sparse serves it in place instead of deferring it again
+      const uint32_t tot = Q.qn + Q.pn + Q.fn;
+      if (Q.pn + Q.fn) {
+        bool bad = false;
+        for (uint32_t k = lane + 1; k < tot; k += kWave) bad |= item_lt(Q.slot(Q.rn + k), Q.slot(Q.rn + k - 1));
+        if (__ballot(bad) == 0) near_out = tot;
+      }
+    }
     if (lane == 0) {
       SrcState ns;
       ns.tat = Q.tat;
       ns.heap_n = Q.qn + Q.pn + Q.fn;
-      ns.near_n = Q.qn;
+      ns.near_n = near_out;
       ns.ring_n = Q.rn;
       ns.last_dup = last_dup;
       ns.last_cor = last_cor;
@@ -1629,20 +1641,21 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const uint32_t n = (uint32_t)(send - sbeg);
   const uint32_t rn = st.ring_n, qn = st.heap_n;
-  auto defer = [&]() {
+  auto defer = [&](uint32_t why) {
     if (lane == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
+#ifdef TGSIM_DEFER_STATS  // diagnostic build: deferrals by reason, behind the list
+    if (lane == 0) atomicAdd(a.worklist + a.n_src + why, 1u);
+#else
+    (void)why;
+#endif
   };
   const bool sorted_st = q_near(st) == qn;  // the whole queue is one sorted region
-  if ((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 || (uint64_t)rn + qn + 2ull * n >= a.queue_limit || n > kWave ||
-      (!sorted_st && qn > kSparseQ * kWave) || rn > kSparseQ * kWave) {
-    defer();
-    return;
-  }
   unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
   const uint4 qh0 = sorted_st && qn && !n ? gh[q_head(st)] : make_uint4(0, 0, 0, 0);
   if (!n && (!qn || (sorted_st && (w0_of(qh0) & kEMask) >= a.horizon_ns))) {
     // nothing offered and nothing eligible before the horizon: the state stays as it is (the ring
-    // is released only by an enqueue); only the per-window queue model is counted
+    // is released only by an enqueue); only the per-window queue model is counted.  Checked before
+    // the capacity limits below: an idle source with a long ring (the end of a flood) is not deferred
     if (lane == 0) {
       a.emit_n[s] = 0;
       const uint64_t qb = 32ull * qn + 16ull * rn;
@@ -1650,6 +1663,12 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
       if (qn) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(32ull * qn - 16ull));
       if (rn) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(16ull * rn));
     }
+    return;
+  }
+  if ((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 || (uint64_t)rn + qn + 2ull * n >= a.queue_limit || n > kWave ||
+      (!sorted_st && qn > kSparseQ * kWave) || rn > kSparseQ * kWave) {
+    defer((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 ? 0u : (uint64_t)rn + qn + 2ull * n >= a.queue_limit ? 1u
+          : n > kWave ? 2u : rn > kSparseQ * kWave ? 4u : 3u);
     return;
   }
   const uint32_t src = a.shard_begin + s;
@@ -1820,7 +1839,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     const bool due_o = cand && (w0_of(io) & kEMask) < h;  // a prefix of the candidates
     const uint32_t n_due = (uint32_t)__popcll(__ballot(due_o));
     if (nq + n_due > kWave || (nq == kWave && qn > kWave)) {
-      defer();
+      defer(5u);
       return;
     }
     write_old_ring();
@@ -1837,7 +1856,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   } else {
     if (sorted_st) {  // sorted, but the new items do not extend it in order: the general path
       if (qn > kSparseQ * kWave) {
-        defer();
+        defer(6u);
         return;
       }
       load_rest();
@@ -1855,7 +1874,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     // remaining items: everything not served, written back as the pool
     uint32_t nrem = qn + (uint32_t)__popcll(mc) + (uint32_t)__popcll(__ballot(cand && cst == 2)) - ns;
     if (over || nrem > kSparseQ * kWave) {
-      defer();
+      defer(7u);
       return;
     }
     write_old_ring();
