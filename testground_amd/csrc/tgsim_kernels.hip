@@ -1628,6 +1628,7 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused_sm(FusedSim fs, FusedArg
 // not fit (correlated draws, a queue that could reach the limit, more than 64 offered packets, 256
 // queued items, 256 ring entries or 64 items to serve) writes nothing and goes to the worklist.
 constexpr uint32_t kSparseQ = 4;  // chunks of 64 queued items / ring entries held in registers
+constexpr uint32_t kFifoRounds = 4;  // FIFO sources: items served per step, in rounds of 64
 __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s) {
   const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1;
@@ -1833,26 +1834,40 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   }
   uint32_t new_head = 0;
   uint32_t q_moved = 0;  // queue items read or written in HBM (FIFO path: not the whole queue)
+  uint32_t fifo_nq = 0, ns_all = 0, cpos = 0;  // FIFO: due queue items, all served, a due candidate's place
+  bool due_f = false;                           // FIFO: a due candidate
   if (fifo) {
-    // the queue's prefix below the horizon (in its first chunk: 64 due items defer anyway)
-    const uint32_t nq = (uint32_t)__popcll(__ballot(lane < qn && (w0_of(q[0]) & kEMask) < h));
+    // the queue's prefix below the horizon: its first chunk, and while a chunk is due entirely the
+    // next one (the served items run in rounds of 64 below, at most kFifoRounds)
+    uint32_t nq = (uint32_t)__popcll(__ballot(lane < qn && (w0_of(q[0]) & kEMask) < h));
+    for (uint32_t c = 1; c < kFifoRounds && nq == c * kWave && qn > nq; ++c) {
+      const uint32_t k = c * kWave + lane;
+      const uint4 v = k < qn ? gh[(qh + k) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
+      nq += (uint32_t)__popcll(__ballot(k < qn && (w0_of(v) & kEMask) < h));
+    }
     const bool due_o = cand && (w0_of(io) & kEMask) < h;  // a prefix of the candidates
-    const uint32_t n_due = (uint32_t)__popcll(__ballot(due_o));
-    if (nq + n_due > kWave || (nq == kWave && qn > kWave)) {
+    const uint64_t dm = __ballot(due_o);
+    const uint32_t n_due = (uint32_t)__popcll(dm);
+    if (nq + n_due > kFifoRounds * kWave || (nq == kFifoRounds * kWave && qn > nq)) {
       defer(5u);
       return;
     }
     write_old_ring();
+    fifo_nq = nq;
+    ns_all = nq + n_due;
+    due_f = due_o;
+    cpos = nq + (uint32_t)__popcll(dm & below);
     x = lane < nq ? q[0] : make_uint4(0, 0, 0, 0);
-    ns = nq;
-    gather(due_o, io);
+    ns = nq < kWave ? nq : kWave;
+    gather(due_o && cpos < kWave, io);
     // in place: the served prefix leaves by moving the head slot, the candidates not served are
     // appended behind the tail; nothing else moves
     const uint32_t cr = (uint32_t)__popcll(mc & below);
     if (cand && !due_o) wq[(qh + qn + cr - n_due) & (kHeapCap - 1)] = io;
     new_head = (qh + nq) & (kHeapCap - 1);
     wpos = qn - nq + (uint32_t)__popcll(mc) - n_due;
-    q_moved = (qn < kWave ? qn : kWave) + (qn > kWave ? 1u : 0u) + (uint32_t)__popcll(mc) - n_due;
+    q_moved = (qn < kWave ? qn : kWave) + (qn > kWave ? 1u : 0u) + (uint32_t)__popcll(mc) - n_due +
+              (nq > kWave ? nq - kWave : 0u);
   } else {
     if (sorted_st) {  // sorted, but the new items do not extend it in order: the general path
       if (qn > kSparseQ * kWave) {
@@ -1902,65 +1917,82 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.z),
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.w));
   }
-  const bool hs = lane < ns;
-  // the destinations' forwarded masks, for the receipts folded in below (in flight during the scan)
-  // (the 32-bit half of the mask that holds the record's flood bit: one register across the scan)
-  const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
-  const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
-                          ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
-                          : 0u;
-  // ---- HTB: d = max(e, TAT before), TAT' = max(TAT, e - burst) + cost, one max-plus scan
-  const uint64_t e = w0_of(x) & kEMask;
-  const uint32_t xlen = x.y >> 14 & 0xFFFFu;
-  const uint64_t c = ((uint64_t)xlen * pp.mult) >> (pp.shift_ext & 0xFFu);
-  uint64_t A = hs ? c : 0, Bm = hs ? (e > pp.burst_ns ? e - pp.burst_ns : 0) + c : 0;
-  scan_maxplus(A, Bm);
-  const uint64_t ta = st.tat + A;
-  const uint64_t tat_after = ta > Bm ? ta : Bm;
-  const uint64_t before = shr1_u64(tat_after, st.tat);
-  const uint64_t d = e > before ? e : before;
-  const uint64_t tat_end = ns ? readlane64(tat_after, ns - 1) : st.tat;
-  stamp(a, s, lane, 3, __builtin_amdgcn_s_memrealtime());
-  // ---- records of the served items (dead destinations leave the sender and are lost)
-  const bool live = hs && x.w != kDeadDst;
-  const uint64_t lm = __ballot(live);
-  const uint32_t n_live = (uint32_t)__popcll(lm);
-  tgsim_delivery* emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
-  uint32_t sched = 0, corrupted = 0, lost = 0;
+  if (!fifo) ns_all = ns;
+  // ---- HTB, records, receipts and the ring, for the served items in rounds of 64 lanes (more than
+  // one only on the FIFO path: the queue's due prefix, then the due candidates, in order)
+  uint64_t tat_c = st.tat;
+  uint32_t emitted = 0, sk0 = 0, t_sched = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
-  if (live) {
-    const uint32_t flags = x.y >> 30;
-    uint64_t* rw = reinterpret_cast<uint64_t*>(emit + (uint32_t)__popcll(lm & below));
-    rw[0] = d;
-    rw[1] = ((uint64_t)x.w << 32) | src;
-    rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-    if (a.dst_cnt) {
-      const uint32_t i = (uint32_t)__popcll(lm & below);
-      if (a.emit_slot)
-        a.emit_slot[2 * sbeg + (uint64_t)kHeapCap * s + i] = (uint32_t)atomicAdd(&a.dst_cnt[x.w], 1ull);
-      else
-        atomicAdd(&a.dst_cnt[x.w], 1ull);
+  bool releasing = T_enq && !ring_stop;  // served entries departing before the last enqueue are released
+  tgsim_delivery* const emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
+  for (uint32_t base = 0;; base += kWave) {
+    const bool hs = lane < ns;
+    // the destinations' forwarded masks, for the receipts folded in below (in flight during the scan)
+    // (the 32-bit half of the mask that holds the record's flood bit: one register across the scan)
+    const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
+    const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
+                            ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
+                            : 0u;
+    // HTB: d = max(e, TAT before), TAT' = max(TAT, e - burst) + cost, one max-plus scan
+    const uint64_t e = w0_of(x) & kEMask;
+    const uint32_t xlen = x.y >> 14 & 0xFFFFu;
+    const uint64_t c = ((uint64_t)xlen * pp.mult) >> (pp.shift_ext & 0xFFu);
+    uint64_t A = hs ? c : 0, Bm = hs ? (e > pp.burst_ns ? e - pp.burst_ns : 0) + c : 0;
+    scan_maxplus(A, Bm);
+    const uint64_t ta = tat_c + A;
+    const uint64_t tat_after = ta > Bm ? ta : Bm;
+    const uint64_t before = shr1_u64(tat_after, tat_c);
+    const uint64_t d = e > before ? e : before;
+    if (ns) tat_c = readlane64(tat_after, ns - 1);
+    stamp(a, s, lane, 3, __builtin_amdgcn_s_memrealtime());
+    // records of the served items (dead destinations leave the sender and are lost)
+    const bool live = hs && x.w != kDeadDst;
+    const uint64_t lm = __ballot(live);
+    if (live) {
+      const uint32_t flags = x.y >> 30;
+      const uint32_t i = emitted + (uint32_t)__popcll(lm & below);
+      uint64_t* rw = reinterpret_cast<uint64_t*>(emit + i);
+      rw[0] = d;
+      rw[1] = ((uint64_t)x.w << 32) | src;
+      rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
+      if (a.dst_cnt) {
+        if (a.emit_slot)
+          a.emit_slot[2 * sbeg + (uint64_t)kHeapCap * s + i] = (uint32_t)atomicAdd(&a.dst_cnt[x.w], 1ull);
+        else
+          atomicAdd(&a.dst_cnt[x.w], 1ull);
+      }
+      if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
+      bytes += xlen;
     }
-    if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
-    sched = 1;
-    bytes = xlen;
-    corrupted = (flags >> 1) & 1u;
-  } else if (hs) {
-    lost = 1;
+    emitted += (uint32_t)__popcll(lm);
+    t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
+    t_lost += (uint32_t)__popcll(__ballot(hs && !live));
+    // the served entries join the ring, behind the old entries kept; a prefix of them departing
+    // before the last enqueue was released with the old ring (when that released all of it)
+    if (releasing) {
+      const uint32_t n1 = (uint32_t)__popcll(__ballot(hs && e < T_enq));
+      const uint64_t m = __ballot(lane < n1 && d >= T_enq);
+      if (m) {
+        sk0 = base + (uint32_t)__builtin_ctzll(m);
+        releasing = false;
+      } else {
+        sk0 = base + n1;
+        releasing = n1 == kWave;
+      }
+    }
+    if (hs && base + lane >= sk0) wr[old_kept + base + lane - sk0] = d;
+    if (base + kWave >= ns_all) break;
+    // the next round (FIFO): the queue's due items from HBM, then the due candidates
+    const uint32_t nb = base + kWave, k = nb + lane;
+    x = k < fifo_nq ? gh[(qh + k) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
+    ns = fifo_nq > nb ? (fifo_nq - nb < kWave ? fifo_nq - nb : kWave) : 0u;
+    gather(due_f && cpos >= nb && cpos < nb + kWave, io);
   }
-  // ---- the served entries join the ring; those departing before the last enqueue were released
-  // with the old ring's prefix (when it released the whole old ring: ring_stop false)
-  uint32_t sk0 = 0;  // served entries released
-  if (T_enq && !ring_stop) {
-    const uint32_t n1 = (uint32_t)__popcll(__ballot(hs && e < T_enq));
-    const uint64_t m = __ballot(lane < n1 && d >= T_enq);
-    sk0 = m ? (uint32_t)__builtin_ctzll(m) : n1;
-  }
-  if (hs && lane >= sk0) wr[old_kept + lane - sk0] = d;
-  const uint32_t rn_new = old_kept + ns - sk0;
+  t_sched = emitted;
+  const uint32_t rn_new = old_kept + ns_all - sk0;
   if (lane == 0) {
     SrcState ns_;
-    ns_.tat = tat_end;
+    ns_.tat = tat_c;
     ns_.heap_n = wpos;
     ns_.near_n = fifo ? wpos | new_head << 16 : 0;  // sorted in place (FIFO), or all of it pool, compacted
     ns_.ring_n = rn_new;
@@ -1968,7 +2000,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     ns_.last_cor = st.last_cor;
     ns_.last_reo = st.last_reo;
     a.state[s] = ns_;
-    a.emit_n[s] = n_live;
+    a.emit_n[s] = emitted;
   }
   if (staged) a.verdict[sbeg + lane] = (uint8_t)vout;
   stamp(a, s, lane, 4, __builtin_amdgcn_s_memrealtime());
@@ -1982,7 +2014,6 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     const uint32_t t = ballot_count(staged && vo == v) + ballot_count(staged && vc == v);
     if (lane == v) vcnt = t;
   }
-  const uint32_t t_sched = ballot_count(sched != 0), t_cor = ballot_count(corrupted != 0), t_lost = ballot_count(lost != 0);
   const uint32_t t_clone = ballot_count(staged && vc != TGSIM_V_NONE);
   const uint64_t t_bytes = wave_sum(bytes);
   const bool err = __ballot(perr != 0) != 0;
@@ -1990,7 +2021,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   if (lane == 0) {
     const uint64_t qb = 16ull * qn + 8ull * rn + 16ull * wpos + 8ull * rn_new;
     // the per-window model counts the whole queue loaded and stored; the FIFO path left most of it
-    const uint64_t q_kept = fifo ? 16ull * (qn + wpos - q_moved) : 0ull;
+    const uint64_t q_kept = fifo && qn + wpos > q_moved ? 16ull * (qn + wpos - q_moved) : 0ull;
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (t_sched) atomicAdd(&sc[kStScheduled], (unsigned long long)t_sched);
