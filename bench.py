@@ -302,9 +302,10 @@ def run_bridge(a, world, rank, local, dist, want_cpu):
 
     for _ in range(20 + a.warmup):  # past the largest latency + jitter: the FIFOs are in steady state
         one()
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     got[:] = [0, 0]
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -381,6 +382,12 @@ def shard_bounds(peers, world, split):
     return total, [r * total // world for r in range(world)] + [total]
 
 
+def runs_cpu_baseline(rank, want_cpu):
+    """North star: the oracle is timed 'on the box's own host cores in the same run' beside the GPU
+    line at every world size; rank 0 runs it (after the timed region, the other ranks wait)."""
+    return want_cpu and rank == 0
+
+
 def headline_plan(a, world):
     """What the default line measures at this world size (bench.py --launch-check prints it)."""
     total, bounds = shard_bounds(a.peers, world, a.workload == "storm")
@@ -390,6 +397,7 @@ def headline_plan(a, world):
         plan["weak_per_gpu_peers_total"] = shard_bounds(a.peers, world, False)[0]
     if a.workload == "storm" and not a.no_1m:
         plan["at_1M_peers_total"] = shard_bounds(a.gossip_1m_peers, world, True)[0]
+    plan["cpu_baseline_ranks"] = [r for r in range(world) if runs_cpu_baseline(r, not a.no_cpu)]
     return plan
 
 
@@ -490,9 +498,12 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     x0 = stepper.exchanged_records if stepper is not None else 0
     eng.sim_kernel_ms(reset=True)
     c0 = eng.carry_bytes()
+    # the device is idle before the barrier (the engine's own communicator and torch's never have
+    # collectives in flight at once), and again after it (the barrier's kernel)
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_steps(steps)
     torch.cuda.synchronize()
@@ -531,6 +542,13 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     slot_cap = stepper.slot_cap if stepper is not None else None
     eng.close()
     del eng, stepper
+    cpu = None
+    if runs_cpu_baseline(rank, want_cpu):  # the oracle on this host's cores, beside the line at every N
+        cpu = cpu_baseline(a, workload, peers_total, lam, window,
+                           a.cpu_seconds if workload != "gossip" else a.cpu_seconds / 2)
+    if dist:  # the other ranks wait here for rank 0's CPU legs before the next collective
+        torch.cuda.synchronize()
+        dist.barrier()
     if rank != 0:
         return None
     base = (B_OFFERED * offered + B_SCHEDULED * scheduled) / max(1, steps) + B_SOURCE * peers
@@ -580,10 +598,10 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
                      "per": "window (one step of --window ticks; a fused dispatch counts each of its windows)"},
         "cpu_baseline": None,
     }
-    if world == 1 and want_cpu:
-        res["cpu_baseline"] = cpu_baseline(a, workload, peers_total, lam, window,
-                                           a.cpu_seconds if workload != "gossip" else a.cpu_seconds / 2)
-        res["cpu_baseline"]["gpu_over_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    if cpu is not None:
+        res["cpu_baseline"] = cpu
+        cpu["gpu_over_cpu"] = res["value"] / cpu["value"]
+        cpu["timed_on"] = f"rank 0's host cores, in the same run (world size {world})"
         import shutil
         missing = [t for t in ("docker", "tc") if shutil.which(t) is None]
         # the reference's local:docker sidecar + netem path is timed only where it runs

@@ -351,8 +351,11 @@ int tgsim_comm_info(void* engine, tgsim_comm_info_t* out);
  * <= the minimum netem delay, so that a window's receipts are known before the next window. */
 int tgsim_gossip_init(void* engine, const tgsim_gossip* g);
 /* Generates the next n_ticks window of gossip traffic on the device (origins + forwards of the
- * receipts delivered so far), like tgsim_gen_storm.  -EINVAL when a receipt precedes the window
- * (lookahead shorter than the window). */
+ * receipts delivered so far), like tgsim_gen_storm.  The generation runs ahead of the host, so a
+ * receipt that precedes the window (lookahead shorter than the window) is reported with -EINVAL by
+ * the step that consumes it (or tgsim_sim_capacity, or the next tgsim_gen_gossip): that window and
+ * every window queued after it are dropped without changing any peer's forwarded floods, and the
+ * error stays until tgsim_gossip_init. */
 int tgsim_gen_gossip(void* engine, uint32_t n_ticks);
 /* Per flood, the number of this shard's peers that have the flood (received or originated);
  * out[0..n_floods).  Returns n_floods. */

@@ -222,6 +222,7 @@ typedef struct {
     uint32_t* gen_seq;
     /* gossip workload (C4): receipt tick per (local peer, flood), forwarded-flood bitmask */
     int gossip_on;
+    int gossip_late; /* sticky until tgo_gossip_init: a receipt preceded a generated window */
     tgsim_gossip g;
     uint32_t* g_first;
     uint64_t* g_fwd;
@@ -1077,6 +1078,7 @@ int tgo_gossip_init(void* p, const tgsim_gossip* g) {
         o->g_first[64ull * (origin - o->o.shard_begin) + f] = (uint32_t)(g->start_tick + (uint64_t)f * g->start_gap_ticks);
     }
     o->gossip_on = 1;
+    o->gossip_late = 0;
     return 0;
 }
 
@@ -1097,7 +1099,24 @@ int tgo_gen_gossip(void* p, uint32_t n_ticks) {
     oracle* o = (oracle*)p;
     if (!o || !o->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
     if (o->n_off) return fail(o, -EBUSY, "host packets already pending for the next step");
+    if (o->gossip_late)
+        return fail(o, -EINVAL, "gossip: a receipt preceded an earlier window (tgsim_gossip_init starts a new flood)");
     uint64_t A = o->now_tick + o->gq_ticks, B = A + n_ticks;
+    /* A receipt before the window (lookahead shorter than the window) fails the flood before any
+     * peer's forwarded set changes; the windows queued ahead are dropped and the error stays, as the
+     * HIP engine reports it (there at the next step, since its generation runs ahead of the host). */
+    for (uint32_t s = 0; s < o->nsrc; ++s)
+        for (uint32_t f = 0; f < o->g.n_floods; ++f) {
+            uint32_t t = o->g_first[64ull * s + f];
+            if (!(o->g_fwd[s] >> f & 1) && t < A) {
+                for (size_t i = 0; i < o->gq_n; ++i) free(o->gq[i].pk);
+                o->gq_n = 0;
+                o->gq_ticks = 0;
+                o->gossip_late = 1;
+                return fail(o, -EINVAL, "gossip: a receipt at tick %u precedes the window at %llu", t,
+                            (unsigned long long)A);
+            }
+        }
     struct genwin* w = gen_window(o, n_ticks);
     for (uint32_t s = 0; s < o->nsrc; ++s) {
         uint32_t src = o->o.shard_begin + s;
@@ -1107,12 +1126,6 @@ int tgo_gen_gossip(void* p, uint32_t n_ticks) {
                 if (o->g_fwd[s] >> f & 1) continue;
                 uint32_t t = o->g_first[64ull * s + f];
                 if (t >= B) continue;
-                if (t < A) { /* the window is not queued */
-                    free(w->pk);
-                    o->gq_n--;
-                    return fail(o, -EINVAL, "gossip: receipt at tick %u precedes the window at %llu", t,
-                                (unsigned long long)A);
-                }
                 if (best < 0 || t < o->g_first[64ull * s + (uint32_t)best]) best = (int)f;
             }
             if (best < 0) break;

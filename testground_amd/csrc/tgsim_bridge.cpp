@@ -422,7 +422,6 @@ struct tgsim_udp_front_s {
   std::vector<int> vfd;                          // per peer, -1: none
   std::unordered_map<int, uint32_t> vpeer;       // fd -> peer
   int ep = -1;                                   // epoll set of the vfd sockets
-  std::vector<uint32_t> order;                   // deliveries grouped by source socket
 };
 using Uf = tgsim_udp_front_s;
 
@@ -604,18 +603,14 @@ int64_t tgsim_udp_front_pump(void* f) {
   F->txh.resize(static_cast<size_t>(k));
   F->txv.resize(2 * static_cast<size_t>(k));
   // deliveries from a source with a data-address socket leave from it, without a header (the
-  // receiver's recvfrom sees the source's address); the others leave from the header socket
-  F->order.resize(static_cast<size_t>(k));
-  for (int64_t i = 0; i < k; ++i) F->order[i] = static_cast<uint32_t>(i);
-  std::stable_sort(F->order.begin(), F->order.end(), [F](uint32_t x, uint32_t y) {
-    const int fx = F->vfd[F->msgs[x].src], fy = F->vfd[F->msgs[y].src];
-    return fx < fy;
-  });
+  // receiver's recvfrom sees the source's address); the others leave from the header socket.  They
+  // go out in delivery order (each destination's datagrams in simulated-time order, across senders
+  // too): a sendmmsg batch is flushed whenever the sending socket changes.
   size_t m = 0;
   int cur = -2;
   size_t run0 = 0;
   for (int64_t r = 0; r <= k; ++r) {
-    const int fd = r < k ? F->vfd[F->msgs[F->order[r]].src] : -3;
+    const int fd = r < k ? F->vfd[F->msgs[r].src] : -3;
     if (fd != cur) {  // flush the run of the previous socket
       if (m > run0) {
         const int rc2 = send_all(cur < 0 ? F->fd : cur, F->txh.data() + run0, m - run0);
@@ -625,7 +620,7 @@ int64_t tgsim_udp_front_pump(void* f) {
       cur = fd;
     }
     if (r == k) break;
-    const tgsim_msg& g = F->msgs[F->order[r]];
+    const tgsim_msg& g = F->msgs[r];
     sockaddr_in& to = F->addr[g.dst];
     if (!to.sin_port) continue;  // nobody listening for that instance
     memset(&F->txh[m], 0, sizeof(mmsghdr));

@@ -267,7 +267,6 @@ int allreduce_u64(Comm* C, const void* dev_src, uint64_t* result, ncclRedOp_t op
 }  // namespace
 
 extern "C" {
-
 int tgsim_step(void*, uint32_t);
 int tgsim_step_n(void*, uint32_t, uint32_t);
 int tgsim_step_sim_launch(void*, uint32_t, uint32_t, const uint32_t*, void*, size_t);
@@ -292,21 +291,15 @@ int tgsim_comm_id(void* out_id) {
   return 0;
 }
 
-int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
-  CommSlot* slot = engine_comm_slot(e);
-  if (!slot || !id || nranks < 1 || nranks > 8 || rank < 0 || rank >= nranks) return -EINVAL;
-  if (slot->state) return engine_fail(e, -EBUSY, "comm_init: the engine already has a communicator");
-  std::string why;
-  const Rccl* R = rccl(&why);
-  if (!R) return engine_fail(e, -ENOSYS, why.c_str());
-  Comm* C = new Comm();
-  C->eng = e;
-  C->R = R;
-  C->rank = rank;
-  C->nranks = nranks;
-  C->dev = engine_device(e);
-  slot->state = C;
-  slot->free_fn = comm_free;
+}  // extern "C"
+
+namespace {
+
+// Builds the communicator; the engine owns it only once every step succeeded (a failed init leaves
+// nothing attached, so a retry is possible and no later call sees a half-built one).
+int comm_build(Comm* C, const void* id) {
+  void* e = C->eng;
+  const int nranks = C->nranks;
   CHIP(hipSetDevice(C->dev));
   int lo = 0, hi = 0;
   CHIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -319,14 +312,14 @@ int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
   CHIP(C->d_cnt.ensure(32 * sizeof(uint64_t)));
   ncclUniqueId uid;
   memcpy(&uid, id, TGSIM_COMM_ID_BYTES);
-  CNCCL(R->CommInitRank(&C->nc, nranks, uid, rank));
+  CNCCL(C->R->CommInitRank(&C->nc, nranks, uid, C->rank));
   // gather every rank's shard and check that they tile [0, n_peers) in rank order
   uint32_t b0 = 0, b1 = 0;
   engine_shard(e, &b0, &b1);
   C->h_cnt[0] = b0;
   C->h_cnt[1] = b1;
   CHIP(hipMemcpyAsync(C->d_cnt.p, C->h_cnt, 2 * sizeof(uint64_t), hipMemcpyHostToDevice, C->xs));
-  CNCCL(R->AllGather(C->d_cnt.p, C->d_cnt.p + 2 * sizeof(uint64_t), 2, ncclUint64, C->nc, C->xs));
+  CNCCL(C->R->AllGather(C->d_cnt.p, C->d_cnt.p + 2 * sizeof(uint64_t), 2, ncclUint64, C->nc, C->xs));
   CHIP(hipMemcpyAsync(C->h_cnt + 2, C->d_cnt.p + 2 * sizeof(uint64_t), 2 * nranks * sizeof(uint64_t),
                       hipMemcpyDeviceToHost, C->xs));
   CHIP(hipStreamSynchronize(C->xs));
@@ -342,11 +335,38 @@ int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
   }
   if (C->bounds[nranks] != engine_peers(e))
     return fail(C, -EINVAL, "comm_init: the shards end at %u, not at n_peers %u", C->bounds[nranks], engine_peers(e));
+  const char* r1 = getenv("TGSIM_COMM_ROUTE1");
+  C->local = nranks == 1 && !(r1 && atoi(r1));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
+  CommSlot* slot = engine_comm_slot(e);
+  if (!slot || !id || nranks < 1 || nranks > 8 || rank < 0 || rank >= nranks) return -EINVAL;
+  if (slot->state) return engine_fail(e, -EBUSY, "comm_init: the engine already has a communicator");
+  std::string why;
+  const Rccl* R = rccl(&why);
+  if (!R) return engine_fail(e, -ENOSYS, why.c_str());
+  Comm* C = new Comm();
+  C->eng = e;
+  C->R = R;
+  C->rank = rank;
+  C->nranks = nranks;
+  C->dev = engine_device(e);
+  const int rc = comm_build(C, id);
+  if (rc) {
+    comm_free(C);
+    return rc;
+  }
+  slot->state = C;
+  slot->free_fn = comm_free;
   // at one rank no RCCL kernel competes with the simulation for CU slots, so fused groups keep
   // their persistent grid (with more ranks the grid turns over to let the exchange in)
   engine_persist_routed(e, nranks == 1);
-  const char* r1 = getenv("TGSIM_COMM_ROUTE1");
-  C->local = nranks == 1 && !(r1 && atoi(r1));
   return 0;
 }
 
@@ -370,6 +390,7 @@ int tgsim_comm_launch(void* e, uint32_t n_ticks) {
   CRC(grow(C, C->out[j], C->ev_out[j], C->out_busy[j], static_cast<size_t>(cap) * kRec));
   if (C->out_busy[j]) CRC(tgsim_wait_event(e, C->ev_out[j]));  // an earlier reader of out[j]
   CRC(tgsim_step_sim_launch(e, n_ticks, C->nranks, C->bounds, C->out[j].p, static_cast<size_t>(cap)));
+  CRC(engine_record_routed(e, C->ev_routed[j]));  // the exchange of out[j] waits for it on the device
   C->launched = true;
   return 0;
 }
@@ -392,7 +413,7 @@ int tgsim_comm_finish(void* e) {
   }
   C->exchanged += soff[nr];
   if (nr == 1) {  // TGSIM_COMM_ROUTE1: nothing to exchange, the delivery reads the routed records in place
-    CRC(tgsim_deliver_async(e, C->out[j].p, send[0], nullptr));
+    CRC(tgsim_deliver_async(e, C->out[j].p, send[0], C->ev_routed[j]));
     CRC(tgsim_delivery_event(e, C->ev_out[j]));
     C->out_busy[j] = true;
     return 0;
@@ -409,6 +430,7 @@ int tgsim_comm_finish(void* e) {
   }
   CRC(grow(C, C->in[i], C->ev_in[i], C->in_busy[i], std::max<uint64_t>(roff[nr], 1) * kRec));
   if (C->in_busy[i]) CHIP(hipStreamWaitEvent(C->xs, C->ev_in[i], 0));  // the delivery of window k - 2
+  CHIP(hipStreamWaitEvent(C->xs, C->ev_routed[j], 0));  // the routing that wrote out[j]
   CRC(exchange(C, C->out[j].p, C->in[i].p, send, soff, recv, roff));
   CHIP(hipEventRecord(C->ev_out[j], C->xs));
   C->out_busy[j] = true;

@@ -311,8 +311,11 @@ struct tgsim_engine_s {
                                                      // records per source)
   bool eslot_on = false;                  // the last k_sim wrote d_eslot (heavy sparse windows)
   uint64_t slot_min = 16;                 // TGSIM_SLOT_MIN: offered packets per source from which it is on
+  uint32_t wide_windows = 0;              // windows after a mid-run reshape whose bounded local delivery
+                                          // reserves the full netem limit per source (deliver_local_from)
   uint64_t deliver_slack = 128;           // TGSIM_DELIVER_SLACK: queued items per source a bounded local
                                           // delivery allows for (besides 2 per offered packet)
+  bool slack_forced = false;              // TGSIM_DELIVER_SLACK set: the bounded form at any size
   DevBuf<uint32_t> d_emit_n, d_emit_n_alt, d_emit_n_3;
   DevBuf<uint64_t> d_lcnt, d_lcnt_alt, d_lcnt_3;  // stays zero between steps (k_dst_sort resets it)
   hipEvent_t ev_local = nullptr, ev_local_alt = nullptr, ev_local_3 = nullptr;
@@ -371,6 +374,7 @@ struct tgsim_engine_s {
 
   // gossip workload (C4)
   bool gossip_on = false;
+  bool gossip_late = false;  // sticky until tgsim_gossip_init: a receipt preceded a generated window
   tgsim_gossip gossip{};
   DevBuf<uint32_t> d_gfirst, d_gerr, d_gnbr;
   DevBuf<uint64_t> d_gfwd, d_gpend;
@@ -590,6 +594,9 @@ int configure_k8s(Eng* E, uint32_t peer, const tgsim_config* cfg) {
   return 0;
 }
 
+constexpr uint32_t kWideAfterReshape = 16;
+constexpr uint64_t kExactBoundBytes = 1ull << 31;  // local delivery buffers sized for the worst case up to 2 GiB
+
 int flush_config(Eng* E) {
   if (E->any_gone) {  // packets queued towards a removed link: marked dead in every sender's queue
     HIPCHK(E->d_gone.ensure(E->N));
@@ -629,6 +636,7 @@ int flush_config(Eng* E) {
     HIPCHK(hipMemcpyAsync(E->d_params.p, ps.data(), sizeof(SrcParams) * E->S, hipMemcpyHostToDevice, E->st));
     HIPCHK(hipStreamSynchronize(E->st));
     E->params_dirty = false;
+    if (E->now_tick) E->wide_windows = kWideAfterReshape;
   }
   if (E->any_patch) {
     std::vector<CfgPatch> patches;
@@ -656,6 +664,7 @@ int flush_config(Eng* E) {
                        E->d_stats.p, E->st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(E->st));
+      if (E->now_tick) E->wide_windows = kWideAfterReshape;
     }
     E->any_patch = false;
   }
@@ -826,9 +835,12 @@ int resolve_gen(Eng* E, Eng::GenWindow& w) {
   const uint64_t total = __atomic_load_n(&E->h_pub[4], __ATOMIC_ACQUIRE);
   const uint64_t late = __atomic_load_n(&E->h_pub[5], __ATOMIC_ACQUIRE);
   w.pending = false;
-  if (late)
+  if (late) {  // the write kernels of this window (and of any after it) wrote nothing: the flag is set
+               // before them on the stream, so no peer's fwd/pend changed for it (drop_gen)
+    E->gossip_late = true;
     return E->fail(-EINVAL, "gossip: a receipt precedes the window at tick %llu (lookahead shorter than the window)",
                    static_cast<unsigned long long>(w.g.win0));
+  }
   if (total > w.in.cap) {  // the capped write skipped this window: write it into a larger buffer
     HIPCHK(hipStreamSynchronize(E->st));  // (the old buffer is freed)
     HIPCHK(w.in.ensure(total));
@@ -837,6 +849,14 @@ int resolve_gen(Eng* E, Eng::GenWindow& w) {
   }
   w.n = total;
   return 0;
+}
+
+// After a late receipt every generated window still queued is dropped (its buffers go back to
+// gen_free), so a caller that retries finds no half-generated window; the error stays (gossip_late).
+void drop_gen(Eng* E) {
+  for (auto& w : E->gen_q) E->gen_free.push_back(std::move(w));
+  E->gen_q.clear();
+  E->gen_q_ticks = 0;
 }
 
 int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
@@ -848,7 +868,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     if (!E->staged.empty()) return E->fail(-EBUSY, "host packets and generated traffic in one step");
     Eng::GenWindow& w = E->gen_q.front();
     int grc = resolve_gen(E, w);
-    if (grc) return grc;
+    if (grc) {
+      if (E->gossip_late) drop_gen(E);
+      return grc;
+    }
     if (n_ticks != w.ticks)
       return E->fail(-EINVAL, "generated window spans %u ticks, step is %u", w.ticks, n_ticks);
     std::swap(E->d_off, w.off);
@@ -1235,9 +1258,15 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uin
   HIPCHK(hipGetLastError());
   const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
   // without the exact count (no host round trip): what the window's sources can emit, 2 per offered
-  // packet plus deliver_slack queued items each (the full netem limit of 1,024 would ask 24 GB of
-  // scatter and output buffers at 1M peers); k_deliver_guard checks the device's exact total
-  const uint64_t slack = std::min<uint64_t>(kHeapCap, E->deliver_slack);
+  // packet plus the full netem limit per source.  Where that bound exceeds kExactBoundBytes (24 GB
+  // of scatter and output buffers at 1M peers), deliver_slack queued items per source instead, and
+  // k_deliver_guard checks the device's exact total: a window beyond it fails with -ENOSPC.  A
+  // mid-run reshape (a faster link releasing a deep queue) reserves the full limit for the windows
+  // after it; TGSIM_DELIVER_SLACK forces the bounded form (tests).
+  const bool exact_fits = (2 * n_in + static_cast<uint64_t>(kHeapCap) * E->S) * sizeof(tgsim_delivery) <= kExactBoundBytes;
+  const uint64_t slack =
+      E->wide_windows || (exact_fits && !E->slack_forced) ? kHeapCap : std::min<uint64_t>(kHeapCap, E->deliver_slack);
+  if (E->wide_windows) E->wide_windows--;
   uint64_t n = 2 * n_in + slack * E->S;
   if (need_n) {
     HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
@@ -1538,6 +1567,11 @@ int engine_fail(void* e, int code, const char* msg) { return as_eng(e)->fail(cod
 void engine_persist_routed(void* e, bool on) {
   if (!as_eng(e)->persist_env) as_eng(e)->persist_routed = on;
 }
+int engine_record_routed(void* e, hipEvent_t ev) {
+  Eng* E = as_eng(e);
+  HIPCHK(hipEventRecord(ev, E->rt_st));
+  return 0;
+}
 }  // namespace tgsim
 
 namespace {
@@ -1652,7 +1686,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
   if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
   if (const char* sm = getenv("TGSIM_SLOT_MIN")) E->slot_min = strtoull(sm, nullptr, 10);
-  if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) E->deliver_slack = strtoull(ds, nullptr, 10);
+  if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) {
+    E->deliver_slack = strtoull(ds, nullptr, 10);
+    E->slack_forced = true;
+  }
   if (const char* es = getenv("TGSIM_EMIT_SETS")) E->emit_sets = atoi(es) == 3 ? 3u : 2u;
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
   if (const char* fo = getenv("TGSIM_FUSED_ORDER")) E->order_chain = strcmp(fo, "records") != 0;
@@ -1886,6 +1923,7 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   if (g->start_tick < E->now_tick + E->gen_q_ticks) return E->fail(-EINVAL, "gossip: start tick in the past");
   HIPCHK(hipSetDevice(E->dev));
   E->gossip = *g;
+  E->gossip_late = false;
   HIPCHK(E->d_gfirst.ensure(static_cast<size_t>(E->S) * 64));
   HIPCHK(E->d_gfwd.ensure(E->S));
   HIPCHK(E->d_gpend.ensure(E->S));
@@ -1942,10 +1980,15 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   Eng* E = as_eng(e);
   if (!E || !E->gossip_on || n_ticks == 0 || n_ticks > 65536) return -EINVAL;
   if (!E->staged.empty()) return E->fail(-EBUSY, "host packets already pending for the next step");
+  if (E->gossip_late)
+    return E->fail(-EINVAL, "gossip: a receipt preceded an earlier window (tgsim_gossip_init starts a new flood)");
   HIPCHK(hipSetDevice(E->dev));
   for (auto& q : E->gen_q) {  // a window still unsized is sized (and written) before this one runs
     int rc = resolve_gen(E, q);
-    if (rc) return rc;
+    if (rc) {
+      if (E->gossip_late) drop_gen(E);
+      return rc;
+    }
   }
   // receipts are folded on the delivery stream (the sort of the same delivery may still run)
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_recv, 0));
@@ -2005,7 +2048,10 @@ int64_t tgsim_sim_capacity(void* e) {
   if (!E) return -EINVAL;
   if (!E->gen_q.empty()) {
     int rc = resolve_gen(E, E->gen_q.front());
-    if (rc) return rc;
+    if (rc) {
+      if (E->gossip_late) drop_gen(E);
+      return rc;
+    }
   }
   const uint64_t n = !E->gen_q.empty() ? E->gen_q.front().n : E->staged.size();
   return static_cast<int64_t>(2 * n + static_cast<uint64_t>(kHeapCap) * E->S);

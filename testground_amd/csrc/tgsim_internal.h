@@ -216,5 +216,8 @@ uint32_t engine_peers(void* engine);
 void engine_shard(void* engine, uint32_t* begin, uint32_t* end);
 int engine_fail(void* engine, int code, const char* msg);
 void engine_persist_routed(void* engine, bool on);  // unless TGSIM_FUSED_PERSIST was set
+// Records `ev` on the routing stream after every routing enqueued so far (the exchange of a launched
+// window waits for it on the device, not only for the host's view of the published edges).
+int engine_record_routed(void* engine, hipEvent_t ev);
 
 }  // namespace tgsim

@@ -2358,6 +2358,7 @@ __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint6
   const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
   if (s0 >= g.n_src) return;
   if (total && *total > out_cap) return;  // written again into a larger buffer (resolve_gen)
+  if (*g.err) return;  // a late receipt (k_gossip_count): the window is dropped, fwd/pend stay as they are
   const uint32_t deg = g.degree;
   const bool pl = lane < kGossipPeers && s0 + lane < g.n_src;  // lane i < 8: peer s0 + i's words
   const uint64_t pend_l = pl ? g.pend[s0 + lane] : 0ull;
@@ -2408,6 +2409,7 @@ __global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64
   const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
   if (s0 >= g.n_src) return;
   if (total && *total > out_cap) return;  // written again into a larger buffer (resolve_gen)
+  if (*g.err) return;  // a late receipt (k_gossip_count): the window is dropped, fwd/pend stay as they are
   uint32_t t[kGossipPeers];
   uint64_t pend[kGossipPeers];
   gossip_rows(g, s0, lane, t, pend);

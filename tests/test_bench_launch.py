@@ -41,6 +41,8 @@ def test_two_ranks_spawned_on_cpu():
         h = x["headline"]
         assert h["peers_total"] == 10_000 and h["bounds"] == [0, 5000, 10_000] and h["scaling"] == "strong"
         assert h["weak_per_gpu_peers_total"] == 20_000 and h["at_1M_peers_total"] == 1_000_000
+        # the CPU oracle is timed beside the N > 1 line too (rank 0's host cores)
+        assert h["cpu_baseline_ranks"] == [0]
 
 
 def test_world_mismatch_fails():

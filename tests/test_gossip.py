@@ -112,6 +112,50 @@ def test_gossip_window_longer_than_lookahead_is_rejected(make_oracle):
             e.step(W)
 
 
+def _late_run(e):
+    """Windows twice the lookahead: a receipt lands before a later window.  Returns the index of the
+    window whose gen or step failed, the flood state then, and whether the error stayed."""
+    wl.configure_gossip(e, 200)
+    e.gossip_init(n_floods=2, degree=4, msg_len=512, start_tick=0)
+    W = 2 * wl.gossip_window_ticks(e)
+    for k in range(20):
+        try:
+            e.gen_gossip(W)  # the oracle fails here; the HIP engine, generating ahead, at the step
+            e.step(W)
+        except EngineError as err:
+            assert "precedes the window" in str(err)
+            break
+    else:
+        raise AssertionError("no late receipt in 20 windows")
+    reached = e.gossip_reached()
+    with pytest.raises(EngineError, match="preceded an earlier window"):
+        e.gen_gossip(W)  # sticky until gossip_init
+    assert (e.gossip_reached() == reached).all()
+    e.gossip_init(n_floods=2, degree=4, msg_len=512, start_tick=e.stats()["now_tick"] + 1)
+    e.gen_gossip(wl.gossip_window_ticks(e))  # a new flood runs again
+    e.step(wl.gossip_window_ticks(e))
+    return k, reached
+
+
+@pytest.mark.gpu
+def test_gossip_late_receipt_gpu_equals_oracle(make_oracle):
+    """the late window changes no peer's forwarded floods on either engine (the HIP
+    engine's write kernels see the flag its count kernel set), the error is sticky until
+    tgsim_gossip_init, and both engines fail at the same window with the same flood state."""
+    from testground_amd.engine import Engine
+
+    k_cpu, r_cpu = _late_run(make_oracle(200, lookahead_ns=wl.GOSSIP_MIN_LAT))
+    gpu = Engine(200, lookahead_ns=wl.GOSSIP_MIN_LAT)
+    k_gpu, r_gpu = _late_run(gpu)
+    gpu.close()
+    assert k_gpu == k_cpu
+    assert (r_gpu == r_cpu).all()
+
+
+def test_gossip_late_receipt_is_sticky_on_oracle(make_oracle):
+    _late_run(make_oracle(200, lookahead_ns=wl.GOSSIP_MIN_LAT))
+
+
 def test_gossip_init_contract(make_oracle):
     e = make_oracle(10)
     for bad in (dict(n_floods=0), dict(n_floods=65), dict(degree=0), dict(degree=65), dict(msg_len=0)):
