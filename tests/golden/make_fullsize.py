@@ -51,14 +51,31 @@ def stats_list(st):
     return [int(st[k]) for k in STAT_KEYS] + [int(st["by_verdict"][k]) for k in sorted(st["by_verdict"])]
 
 
-def digest(eng):
+# The multi-rank tests split the peers into RANKS contiguous shards (bench.py shard_bounds).
+RANKS = 8
+
+
+def rank_bounds(n, world=RANKS):
+    return [r * n // world for r in range(world)] + [n]
+
+
+def digest(eng, by_rank=False):
     """One digest entry for the engine's last step: verdicts, every pending delivery (drain order),
-    statistics."""
+    statistics.  by_rank (fused groups): also the digest of each rank's share of the drain (its
+    destinations' records, in drain order) for an 8-way split -- a rank drains a group as its
+    destinations' records of window 0, then window 1, ..., which is the single drain filtered by
+    destination, not a slice of it."""
     v = eng.verdicts()
     d = eng.drain()
-    return {"n_verdicts": int(len(v)), "verdicts": hashlib.sha256(v.tobytes()).hexdigest(),
-            "n_deliveries": int(len(d)), "deliveries": hashlib.sha256(d.tobytes()).hexdigest(),
-            "stats": stats_list(eng.stats())}
+    e = {"n_verdicts": int(len(v)), "verdicts": hashlib.sha256(v.tobytes()).hexdigest(),
+         "n_deliveries": int(len(d)), "deliveries": hashlib.sha256(d.tobytes()).hexdigest(),
+         "stats": stats_list(eng.stats())}
+    if by_rank:
+        b = rank_bounds(eng.n_peers)
+        parts = [d[(d["dst"] >= b[r]) & (d["dst"] < b[r + 1])] for r in range(RANKS)]
+        e["n_deliveries_by_rank"] = [int(len(x)) for x in parts]
+        e["deliveries_by_rank"] = [hashlib.sha256(x.tobytes()).hexdigest() for x in parts]
+    return e
 
 
 def run_c3(eng, sink):
@@ -72,7 +89,7 @@ def run_c3(eng, sink):
         for _ in range(c["group"]):
             eng.gen_storm(c["lam"], c["window"])
         eng.step_n(c["window"], c["group"])
-        sink(f"fused group {g}", digest(eng))
+        sink(f"fused group {g}", digest(eng, by_rank=True))
 
 
 def run_c4(eng, sink):

@@ -1,0 +1,197 @@
+"""BASELINE.json configs[2..4] as DEFINED at N > 1, at full size, against the CPU oracle's digests.
+
+configs[3] is "1M-peer gossip flood sharded across 8xMI355X with per-tick RCCL all-to-all" and
+configs[2] is the 10k-instance storm "at 1/2/4/8 GPUs".  Here the engine's own exchange
+(tgsim_comm_*: routing by destination rank, the count all-to-all, grouped send/receive, slotted
+chunks of the pipelined fused run, per-rank delivery, the barrier all-reduce) runs with 8 ranks on
+one GPU -- ranks as threads over the test transport tests/mockrccl (RCCL refuses two ranks on one
+device; everything but the transport is the product's code, see tests/test_gpu_multirank.py) -- and
+every window is compared with the committed oracle digests (tests/golden/fullsize_*.json):
+
+  c4  1,000,000 peers, 125,000 per rank: 2 empty windows, then the 70 flood windows through
+      tgsim_comm_step (closed loop: forwards generated on the receiving rank from the records the
+      exchange brought in);
+  c3  10,000 instances, 1,250 per rank: the 60 settle windows through tgsim_comm_step (exact
+      exchange), then two groups of 8 windows, each one tgsim_comm_run (one k_sim_fused launch and one
+      all-to-all of slotted chunks per group);
+  c5  100,000 instances, 12,500 per rank: 6 epochs, reshaping on every rank and the epoch barrier
+      summed over the ranks on the device (tgsim_comm_barrier).
+
+A window's verdicts concatenated in rank order are the single engine's (sources are contiguous per
+rank), and so are its deliveries (a window drains in destination order); a fused group drains each
+rank's destinations window after window, so its deliveries are compared per rank
+(`deliveries_by_rank`, the single drain filtered by destination).  Statistics are summed over the
+ranks (the simulated clock is every rank's)."""
+import ctypes
+import hashlib
+import sys
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
+import make_fullsize as mf  # noqa: E402
+
+from testground_amd import abi  # noqa: E402
+from testground_amd import workloads as wl  # noqa: E402
+from testground_amd.build import MOCK_COMM_LIB  # noqa: E402
+from testground_amd.engine import CABIEngine  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+WORLD = mf.RANKS
+NOW = mf.STAT_KEYS.index("now_tick")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not MOCK_COMM_LIB.exists():
+        pytest.fail(f"{MOCK_COMM_LIB} not built (__graft_entry__.build())")
+    lib = ctypes.CDLL(str(MOCK_COMM_LIB))
+    abi.declare(lib, "tgsim_")
+    return lib
+
+
+class Checker:
+    """Collects each rank's share of a digest point; when all ranks have arrived (a thread barrier,
+    so every rank is at the same window), combines them in rank order and compares with the next
+    fixture entry.  Mismatches are recorded, not raised, so the other ranks' collectives go on."""
+
+    def __init__(self, name):
+        self.name = name
+        fx = mf.load(name)
+        self.entries = iter(fx["entries"])
+        self.config = fx["config"]
+        self.slots = [None] * WORLD
+        self.errors = []
+        self.seen = 0
+        self.bar = threading.Barrier(WORLD, action=self._combine)
+
+    def put(self, r, label, **kw):
+        self.slots[r] = (label, kw)
+        self.bar.wait(timeout=600)
+
+    def _combine(self):
+        want = next(self.entries)
+        labels = {s[0] for s in self.slots}
+        parts = [s[1] for s in self.slots]
+        self.slots = [None] * WORLD
+        self.seen += 1
+        if labels != {want["label"]}:
+            self.errors.append(f"labels {labels} != {want['label']}")
+            return
+        label = want["label"]
+        if "reached" in want:
+            got = [int(x) for x in np.sum([p["reached"] for p in parts], axis=0)]
+            if got != want["reached"]:
+                self.errors.append(f"{label}: reached {got[:4]}... != oracle {want['reached'][:4]}...")
+            return
+        stats = np.sum([p["stats"] for p in parts], axis=0)
+        stats[NOW] = parts[0]["stats"][NOW]
+        if [int(x) for x in stats] != want["stats"]:
+            self.errors.append(f"{label}: stats {list(stats)} != oracle {want['stats']}")
+        h = hashlib.sha256()
+        for p in parts:
+            h.update(p["verdicts"].tobytes())
+        if sum(len(p["verdicts"]) for p in parts) != want["n_verdicts"] or h.hexdigest() != want["verdicts"]:
+            self.errors.append(f"{label}: verdicts differ from the oracle's")
+        if "deliveries_by_rank" in want:
+            for r, p in enumerate(parts):
+                if (len(p["drain"]) != want["n_deliveries_by_rank"][r]
+                        or hashlib.sha256(p["drain"].tobytes()).hexdigest() != want["deliveries_by_rank"][r]):
+                    self.errors.append(f"{label}: rank {r}'s deliveries differ from the oracle's "
+                                       f"({len(p['drain'])} vs {want['n_deliveries_by_rank'][r]})")
+        else:
+            h = hashlib.sha256()
+            for p in parts:
+                h.update(p["drain"].tobytes())
+            if sum(len(p["drain"]) for p in parts) != want["n_deliveries"] or h.hexdigest() != want["deliveries"]:
+                self.errors.append(f"{label}: deliveries differ from the oracle's")
+
+    def window(self, r, label, e):
+        self.put(r, label, verdicts=e.verdicts(), drain=e.drain(), stats=mf.stats_list(e.stats()))
+
+
+def _run(lib, name, rank_fn):
+    chk = Checker(name)
+    n = chk.config["peers"]
+    kw = mf.engine_kwargs(name)
+    b = mf.rank_bounds(n, WORLD)
+    engs = [CABIEngine(lib, "tgsim_", n, shard=(b[r], b[r + 1]), device=0, **kw) for r in range(WORLD)]
+    buf = ctypes.create_string_buffer(abi.COMM_ID_BYTES)
+    assert lib.tgsim_comm_id(buf) == 0
+
+    def one(r):
+        try:
+            engs[r].comm_init(buf.raw, r, WORLD)
+            rank_fn(r, engs[r], chk, n)
+        except BaseException:
+            chk.bar.abort()  # the other ranks stop at their next digest point instead of hanging
+            raise
+
+    try:
+        with ThreadPoolExecutor(WORLD) as ex:
+            futs = [ex.submit(one, r) for r in range(WORLD)]
+            for f in futs:
+                f.result(timeout=1200)
+    finally:
+        for e in engs:
+            e.close()
+    assert not chk.errors, "\n".join(chk.errors[:10])
+    assert chk.seen == len(mf.load(name)["entries"])
+    print(f"{name} at {WORLD} ranks: {chk.seen} digest points equal to the oracle's", flush=True)
+
+
+def _c4(r, e, chk, n):
+    c = mf.C4
+    wl.configure_gossip(e, n)
+    for _ in range(c["empty"]):
+        e.comm_step(c["window"])
+    e.drain()
+    e.gossip_init(n_floods=c["floods"], degree=c["degree"], msg_len=c["msg_len"], start_gap_ticks=c["gap"])
+    for k in range(c["windows"]):
+        e.gen_gossip(c["window"])
+        e.comm_step(c["window"])
+        chk.window(r, f"window {k}", e)
+    chk.put(r, "reached", reached=e.gossip_reached())
+
+
+def _c3(r, e, chk, n):
+    c = mf.C3
+    wl.configure_storm(e, n)
+    for k in range(c["settle"]):
+        e.gen_storm(c["lam"], c["window"])
+        e.comm_step(c["window"])
+        chk.window(r, f"window {k}", e)
+    for g in range(c["groups"]):
+        for _ in range(c["group"]):
+            e.gen_storm(c["lam"], c["window"])
+        e.comm_run(c["window"], c["group"], c["group"], 0)  # one fused launch, one all-to-all
+        e.sync()
+        chk.window(r, f"fused group {g}", e)
+
+
+def _c5(r, e, chk, n):
+    c = mf.C5
+    lo, hi = e.shard
+    wl.configure_storm(e, n)
+    for k in range(c["epochs"]):
+        wl.run_epoch(e, n, k, hi - lo, step=e.comm_step, barrier=e.comm_barrier)
+        chk.window(r, f"epoch {k}", e)
+
+
+@pytest.mark.timeout(1200)
+def test_c4_gossip_1m_at_8_ranks_equals_oracle(lib):
+    _run(lib, "c4", _c4)
+
+
+@pytest.mark.timeout(900)
+def test_c3_storm_10k_at_8_ranks_equals_oracle(lib):
+    _run(lib, "c3", _c3)
+
+
+@pytest.mark.timeout(900)
+def test_c5_epochs_100k_at_8_ranks_equals_oracle(lib):
+    _run(lib, "c5", _c5)
