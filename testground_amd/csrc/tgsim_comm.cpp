@@ -24,6 +24,7 @@
 // delivery that last read in[i].  Every wait is an event on a stream; the host blocks only where RCCL
 // needs sizes it cannot know (the count exchange of tgsim_comm_step).
 #include <dlfcn.h>
+#include <sched.h>
 #include <errno.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -36,13 +37,16 @@
 
 #include <rccl/rccl.h>  // types only: the functions are resolved from librccl.so.1 at run time
 
-#include "tgsim_internal.h"
+#include "tgsim_launch.h"
 
 using namespace tgsim;
 
 namespace {
 
 constexpr size_t kRec = sizeof(tgsim_delivery);
+// Grid of the sharded fused groups at N > 1: the exchange's kernels (RCCL) and the group delivery need
+// CU slots while the next group simulates; 0 lets the grid turn over (one workgroup per ticket).
+constexpr uint32_t kRoutedGridPct = 0;
 
 // librccl.so.1, loaded once per process (when torch has loaded it already, dlopen returns that
 // same instance, so one process never holds two RCCL runtimes).  The test build of this file
@@ -166,7 +170,11 @@ struct Comm {
   bool out_busy[3] = {}, in_busy[2] = {};
   uint64_t k = 0;  // launched windows (groups) so far
   DevMem d_cnt;    // count exchange and reductions: 2 x 8 u64
-  uint64_t* h_cnt = nullptr;  // pinned: [0..8) sent, [8..16) received, [16] reduction result
+  uint64_t* h_cnt = nullptr;  // pinned: [0..8) sent, [8..16) received (+ [16] its sequence word),
+                              // [17] reduction result
+  uint64_t cnt_seq = 0;       // sequence of the received counts published into h_cnt[16]
+  hipEvent_t ev_cnt = nullptr;  // after the last count all-to-all's publish (tells a fault from a slow step)
+  uint64_t route1_cap[3] = {};  // TGSIM_COMM_ROUTE1: the capacity-sized chunk of out[j]
   uint64_t exchanged = 0, max_count = 0, slot_cap = 0;
   bool launched = false;  // tgsim_comm_launch without its tgsim_comm_finish yet
   bool local = false;     // one rank, not TGSIM_COMM_ROUTE1: the single-shard step
@@ -214,6 +222,7 @@ void comm_free(void* p) {
   for (hipEvent_t e : C->ev_routed)
     if (e) (void)hipEventDestroy(e);
   if (C->ev_sig) (void)hipEventDestroy(C->ev_sig);
+  if (C->ev_cnt) (void)hipEventDestroy(C->ev_cnt);
   if (C->h_cnt) (void)hipHostFree(C->h_cnt);
   if (C->xs) (void)hipStreamDestroy(C->xs);
   delete C;
@@ -254,13 +263,31 @@ int exchange(Comm* C, const uint8_t* out, uint8_t* in, const uint64_t* send, con
   return 0;
 }
 
+// Spins until the count all-to-all's publish of the received counts (h_cnt[8..8+nranks), sequence
+// word h_cnt[8 + nranks]); the event after it tells a fault from a slow exchange.
+int wait_counts(Comm* C) {
+  uint64_t* w = C->h_cnt + 8 + C->nranks;
+  for (uint32_t it = 1;; ++it) {
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == C->cnt_seq) return 0;
+    if ((it & 255) == 0) {
+      const hipError_t q = hipEventQuery(C->ev_cnt);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == C->cnt_seq) return 0;
+        return fail(C, -EIO, "comm: the count all-to-all finished without publishing");
+      }
+      if (q != hipErrorNotReady) return fail(C, -EIO, "comm: count all-to-all: %s", hipGetErrorString(q));
+      sched_yield();
+    }
+  }
+}
+
 // Sum (or max) of one u64 over the ranks, on the exchange stream; the host waits for it.
 int allreduce_u64(Comm* C, const void* dev_src, uint64_t* result, ncclRedOp_t op) {
-  CNCCL(C->R->AllReduce(dev_src, C->d_cnt.p + 16 * sizeof(uint64_t), 1, ncclUint64, op, C->nc, C->xs));
-  CHIP(hipMemcpyAsync(&C->h_cnt[16], C->d_cnt.p + 16 * sizeof(uint64_t), sizeof(uint64_t), hipMemcpyDeviceToHost,
+  CNCCL(C->R->AllReduce(dev_src, C->d_cnt.p + 24 * sizeof(uint64_t), 1, ncclUint64, op, C->nc, C->xs));
+  CHIP(hipMemcpyAsync(&C->h_cnt[17], C->d_cnt.p + 24 * sizeof(uint64_t), sizeof(uint64_t), hipMemcpyDeviceToHost,
                       C->xs));
   CHIP(hipStreamSynchronize(C->xs));
-  *result = C->h_cnt[16];
+  *result = C->h_cnt[17];
   return 0;
 }
 
@@ -272,6 +299,8 @@ int tgsim_step_n(void*, uint32_t, uint32_t);
 int tgsim_step_sim_launch(void*, uint32_t, uint32_t, const uint32_t*, void*, size_t);
 int tgsim_step_sim_counts(void*, uint64_t*);
 int tgsim_step_sim_launch_slotted_n(void*, uint32_t, uint32_t, uint32_t, const uint32_t*, void*, uint64_t, void*);
+int tgsim_step_sim_launch_slotted(void*, uint32_t, uint32_t, const uint32_t*, void*, uint64_t, void*);
+int tgsim_deliver_slotted_async(void*, const void*, uint32_t, uint64_t, void*);
 int tgsim_step_sim_release(void*);
 int tgsim_deliver_async(void*, const void*, size_t, void*);
 int tgsim_deliver_slotted_n_async(void*, const void*, uint32_t, uint32_t, uint64_t, void*);
@@ -308,6 +337,7 @@ int comm_build(Comm* C, const void* id) {
   for (auto& ev : C->ev_in) CHIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (auto& ev : C->ev_routed) CHIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   CHIP(hipEventCreateWithFlags(&C->ev_sig, hipEventDisableTiming));
+  CHIP(hipEventCreateWithFlags(&C->ev_cnt, hipEventDisableTiming));
   CHIP(hipHostMalloc(reinterpret_cast<void**>(&C->h_cnt), 32 * sizeof(uint64_t), hipHostMallocDefault));
   CHIP(C->d_cnt.ensure(32 * sizeof(uint64_t)));
   ncclUniqueId uid;
@@ -335,6 +365,7 @@ int comm_build(Comm* C, const void* id) {
   }
   if (C->bounds[nranks] != engine_peers(e))
     return fail(C, -EINVAL, "comm_init: the shards end at %u, not at n_peers %u", C->bounds[nranks], engine_peers(e));
+  memset(C->h_cnt, 0, 32 * sizeof(uint64_t));  // no stale word may read as a published sequence
   const char* r1 = getenv("TGSIM_COMM_ROUTE1");
   C->local = nranks == 1 && !(r1 && atoi(r1));
   return 0;
@@ -366,7 +397,7 @@ int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
   slot->free_fn = comm_free;
   // at one rank no RCCL kernel competes with the simulation for CU slots, so fused groups keep
   // their persistent grid (with more ranks the grid turns over to let the exchange in)
-  engine_persist_routed(e, nranks == 1);
+  engine_persist_routed(e, nranks == 1 ? 100u : kRoutedGridPct);
   return 0;
 }
 
@@ -387,6 +418,16 @@ int tgsim_comm_launch(void* e, uint32_t n_ticks) {
   const uint32_t j = C->k % 3;
   const int64_t cap = tgsim_sim_capacity(e);
   if (cap < 0) return static_cast<int>(cap);
+  if (C->nranks == 1) {  // TGSIM_COMM_ROUTE1: one chunk of the step's whole capacity, delivered in place
+                         // from its count header, so the host never waits for the routing
+    CRC(grow(C, C->out[j], C->ev_out[j], C->out_busy[j], (static_cast<size_t>(cap) + 1) * kRec));
+    if (C->out_busy[j]) CRC(tgsim_wait_event(e, C->ev_out[j]));
+    CRC(tgsim_step_sim_launch_slotted(e, n_ticks, 1, C->bounds, C->out[j].p, static_cast<uint64_t>(cap),
+                                      C->ev_routed[j]));
+    C->route1_cap[j] = static_cast<uint64_t>(cap);
+    C->launched = true;
+    return 0;
+  }
   CRC(grow(C, C->out[j], C->ev_out[j], C->out_busy[j], static_cast<size_t>(cap) * kRec));
   if (C->out_busy[j]) CRC(tgsim_wait_event(e, C->ev_out[j]));  // an earlier reader of out[j]
   CRC(tgsim_step_sim_launch(e, n_ticks, C->nranks, C->bounds, C->out[j].p, static_cast<size_t>(cap)));
@@ -405,25 +446,33 @@ int tgsim_comm_finish(void* e) {
   if (C->local) return 0;  // tgsim_comm_launch ran the whole window
   const uint32_t j = C->k % 3, i = C->k % 2;
   uint64_t send[8] = {}, recv[8] = {}, soff[9] = {}, roff[9] = {};
-  CRC(tgsim_step_sim_counts(e, send));  // the host waits for the routing's published counts
+  if (nr == 1) {  // TGSIM_COMM_ROUTE1: nothing to exchange; retired without a wait, delivered in place
+    CRC(tgsim_step_sim_release(e));
+    C->k++;
+    C->exchanged += C->route1_cap[j] + 1;  // record slots, as in the slotted run
+    CRC(tgsim_deliver_slotted_async(e, C->out[j].p, 1, C->route1_cap[j], C->ev_routed[j]));
+    CRC(tgsim_delivery_event(e, C->ev_out[j]));
+    C->out_busy[j] = true;
+    return 0;
+  }
+  // the count all-to-all runs on the device right behind the routing (its per-rank counts never
+  // cross to the host first); the host waits once, for the received counts it publishes
+  const uint64_t* dsend = engine_route_counts_dev(e);
+  if (!dsend) return fail(C, -EIO, "comm_finish: no routed counts on the device");
+  CHIP(hipStreamWaitEvent(C->xs, C->ev_routed[j], 0));
+  CNCCL(C->R->AllToAll(dsend, C->d_cnt.p + 8 * sizeof(uint64_t), 1, ncclUint64, C->nc, C->xs));
+  launch_publish_words(reinterpret_cast<const uint64_t*>(C->d_cnt.p + 8 * sizeof(uint64_t)), static_cast<uint32_t>(nr),
+                       C->h_cnt + 8, ++C->cnt_seq, C->xs);
+  CHIP(hipGetLastError());
+  CHIP(hipEventRecord(C->ev_cnt, C->xs));
+  CRC(tgsim_step_sim_counts(e, send));  // the routing's own published edges (bookkeeping, overflow check)
   C->k++;
   for (int r = 0; r < nr; ++r) {
     soff[r + 1] = soff[r] + send[r];
     C->max_count = std::max(C->max_count, send[r]);
   }
   C->exchanged += soff[nr];
-  if (nr == 1) {  // TGSIM_COMM_ROUTE1: nothing to exchange, the delivery reads the routed records in place
-    CRC(tgsim_deliver_async(e, C->out[j].p, send[0], C->ev_routed[j]));
-    CRC(tgsim_delivery_event(e, C->ev_out[j]));
-    C->out_busy[j] = true;
-    return 0;
-  }
-  memcpy(C->h_cnt, send, nr * sizeof(uint64_t));
-  CHIP(hipMemcpyAsync(C->d_cnt.p, C->h_cnt, nr * sizeof(uint64_t), hipMemcpyHostToDevice, C->xs));
-  CNCCL(C->R->AllToAll(C->d_cnt.p, C->d_cnt.p + 8 * sizeof(uint64_t), 1, ncclUint64, C->nc, C->xs));
-  CHIP(hipMemcpyAsync(C->h_cnt + 8, C->d_cnt.p + 8 * sizeof(uint64_t), nr * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                      C->xs));
-  CHIP(hipStreamSynchronize(C->xs));
+  CRC(wait_counts(C));
   for (int r = 0; r < nr; ++r) {
     recv[r] = C->h_cnt[8 + r];
     roff[r + 1] = roff[r] + recv[r];
@@ -460,6 +509,7 @@ int tgsim_comm_run(void* e, uint32_t n_ticks, uint32_t n_steps, uint32_t fuse, u
   }
   if (!slot_cap) {  // from the exact windows so far, max over ranks (a collective every rank makes)
     uint64_t mx = 0;
+    if (nr == 1) CRC(engine_route_max(e, &C->max_count));  // TGSIM_COMM_ROUTE1: counts never came to the host
     C->h_cnt[0] = C->max_count;
     CHIP(hipMemcpyAsync(C->d_cnt.p, C->h_cnt, sizeof(uint64_t), hipMemcpyHostToDevice, C->xs));
     CRC(allreduce_u64(C, C->d_cnt.p, &mx, ncclMax));

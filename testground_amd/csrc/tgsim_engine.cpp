@@ -231,6 +231,8 @@ struct tgsim_engine_s {
   // per-rank record edges behind an event, per slot
   static constexpr uint32_t kRouteSlots = 2;
   uint64_t* h_edges = nullptr;  // kRouteSlots x 16 words
+  DevBuf<uint64_t> d_rsend;     // kRouteSlots x 16: the per-rank counts of each launched routing, on the
+                                // device (words 8..15 of slot 0: [8] the largest per-rank count so far)
   hipEvent_t ev_route[kRouteSlots] = {};
   uint32_t route_ranks[kRouteSlots] = {};
   size_t route_cap[kRouteSlots] = {};
@@ -286,6 +288,10 @@ struct tgsim_engine_s {
     bool pending = false;
     uint64_t pub_seq = 0;
     GossipArgs g{};
+    // the last readers of `off` once the window went back to the free list: the routing and the
+    // delivery enqueued before (a generation reusing the buffer waits for these, not for every
+    // routing and delivery since)
+    hipEvent_t rd_rt = nullptr, rd_dst = nullptr;
   };
   std::vector<GenWindow> gen_q;   // device-generated traffic, one window per future step
   std::vector<GenWindow> gen_free;
@@ -360,7 +366,8 @@ struct tgsim_engine_s {
   bool source_major = false;            // TGSIM_FUSED_MAJOR=source: k_sim_fused_sm
   uint64_t fused_windows = 0;
   uint32_t fused_wgs = 0;
-  bool persist_routed = false;  // TGSIM_FUSED_PERSIST: persistent grid for sharded (routed) groups too
+  uint32_t routed_pct = 0;      // sharded (routed) groups: 0 = one workgroup per ticket (the grid turns
+                                // over), else a persistent grid of this % of the resident workgroups
   bool persist_env = false;     // TGSIM_FUSED_PERSIST was set (the comm layer keeps its choice)
   CommSlot comm{};              // tgsim_comm_init's exchange state (tgsim_comm.cpp)
   uint32_t prio_heavy = 512;  // TGSIM_PRIO_HEAVY: heaviest sources of a fused launch at wave priority 3 (A/B: 128 +1 %, 512 +7.5 %, 2048 +7 %, 4096 +5 %)  // k_sim_fused's persistent grid (resident workgroups), at the first launch
@@ -851,10 +858,31 @@ int resolve_gen(Eng* E, Eng::GenWindow& w) {
   return 0;
 }
 
+// A window's buffers back to the free list: the readers of its offsets enqueued so far (a routing on
+// rt_st, a delivery on dst_st) are what its next generation waits for.
+int retire_gen(Eng* E, Eng::GenWindow&& w) {
+  if (!w.rd_rt) HIPCHK(hipEventCreateWithFlags(&w.rd_rt, hipEventDisableTiming));
+  if (!w.rd_dst) HIPCHK(hipEventCreateWithFlags(&w.rd_dst, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(w.rd_rt, E->rt_st));
+  HIPCHK(hipEventRecord(w.rd_dst, E->dst_st));
+  E->gen_free.push_back(std::move(w));
+  return 0;
+}
+
+// A free window for the next generation, its offsets' last readers awaited on the simulate stream.
+int take_gen(Eng* E, Eng::GenWindow* w) {
+  if (E->gen_free.empty()) return 0;
+  *w = std::move(E->gen_free.back());
+  E->gen_free.pop_back();
+  if (w->rd_rt) HIPCHK(hipStreamWaitEvent(E->st, w->rd_rt, 0));
+  if (w->rd_dst) HIPCHK(hipStreamWaitEvent(E->st, w->rd_dst, 0));
+  return 0;
+}
+
 // After a late receipt every generated window still queued is dropped (its buffers go back to
 // gen_free), so a caller that retries finds no half-generated window; the error stays (gossip_late).
 void drop_gen(Eng* E) {
-  for (auto& w : E->gen_q) E->gen_free.push_back(std::move(w));
+  for (auto& w : E->gen_q) (void)retire_gen(E, std::move(w));
   E->gen_q.clear();
   E->gen_q_ticks = 0;
 }
@@ -878,8 +906,9 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     std::swap(E->d_in, w.in);
     E->n_in = w.n;
     E->gen_q_ticks -= w.ticks;
-    E->gen_free.push_back(std::move(w));
+    int frc = retire_gen(E, std::move(w));  // the previous window's offsets: routing/delivery may read them
     E->gen_q.erase(E->gen_q.begin());
+    if (frc) return frc;
     E->perm.clear();
   } else {
     int rc = stage_host_input(E, n_ticks);
@@ -970,8 +999,11 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     a.emit_slot = E->d_eslot.p;
   }
   if (sparse) {
-    HIPCHK(E->d_work.ensure(static_cast<size_t>(E->S) + 1 + 8));  // (+8: TGSIM_DEFER_STATS)
+    // [0] the worklist's count, its sources, 8 words of TGSIM_DEFER_STATS, then k_sim_multi's list
+    // (count, sources)
+    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 1 + 8 + 1));
     HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t), E->st));
+    HIPCHK(hipMemsetAsync(E->d_work.p + 1 + E->S + 8, 0, sizeof(uint32_t), E->st));
     a.worklist_n = E->d_work.p;
     a.worklist = E->d_work.p + 1;
     a.order = nullptr;  // (stamps, when on, are indexed by source: n_wg = S)
@@ -1063,7 +1095,12 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
   // per-rank totals: pos[r * S] .. pos[(r + 1) * S], published to the slot's pinned words
   const uint32_t k = (E->route_head + E->route_n) % Eng::kRouteSlots;
   E->route_seq[k] = ++E->route_next_seq;
-  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->h_edges + 16 * k, E->route_seq[k], rs, out, slot_cap, E->d_xerr);
+  if (!E->d_rsend.p) {
+    HIPCHK(E->d_rsend.ensure(16 * Eng::kRouteSlots));
+    HIPCHK(hipMemsetAsync(E->d_rsend.p, 0, sizeof(uint64_t) * 16 * Eng::kRouteSlots, rs));
+  }
+  launch_route_edges(E->d_rpos.p, E->S, n_ranks, E->h_edges + 16 * k, E->route_seq[k], rs, out, slot_cap, E->d_xerr,
+                     0, E->d_rsend.p + 16 * k);
   HIPCHK(hipGetLastError());
   if (routed) HIPCHK(hipEventRecord(routed, rs));
   HIPCHK(hipEventRecord(E->ev_route[k], rs));
@@ -1199,7 +1236,11 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
     }
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
   }
-  launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq, slot, n_win);
+  // slotted input: chunk by chunk over the counts in the headers, the grid sized for what a chunk
+  // of this window can hold (2 records per offered packet), not for its capacity
+  const uint64_t n_chunks = slot ? n / (slot + 1) : 0, hint = std::max<uint64_t>(2 * E->n_in, 65536);
+  if (slot) launch_dst_slot(in, n_chunks, slot, hint, E->o.shard_begin, nd, E->d_dcnt.p, nullptr, sq, n_win);
+  else launch_dst_hist(in, n, E->o.shard_begin, nd, E->d_dcnt.p, sq, slot, n_win);
   HIPCHK(hipGetLastError());
   int rc = 0;
   if (n_win > 1) {
@@ -1222,7 +1263,8 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
                                    static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq, slot, n_win);
+  if (slot) launch_dst_slot(in, n_chunks, slot, hint, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq, n_win);
+  else launch_dst_scatter(in, n, E->o.shard_begin, nd, E->d_dpos.p, E->d_scatter.p, sq, slot, n_win);
   HIPCHK(hipGetLastError());
   if (slot && !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES)) {  // the drain needs the record count
     HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
@@ -1435,8 +1477,10 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   }
   // a sharded group's exchange (RCCL) and deliveries need CU slots while the next group simulates:
   // there the workgroups turn over (TGSIM_FUSED_PERSIST=1 forces the persistent grid)
-  f.persistent = gr ? (E->persist_routed ? 1u : 0u) : 1u;
-  launch_sim_fused(a, f, E->fused_wgs, E->st);
+  f.persistent = gr ? (E->routed_pct ? 1u : 0u) : 1u;
+  const uint32_t wgs = gr && E->routed_pct ? std::max(1u, E->fused_wgs * std::min(E->routed_pct, 100u) / 100u)
+                                           : E->fused_wgs;
+  launch_sim_fused(a, f, wgs, E->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.push_back({ev0, ev1, g});
@@ -1444,7 +1488,7 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   // every workgroup of the persistent grid claims until a claim fails: the counter advances by the
   // tickets (g per source window-major, one source-major) plus one failed claim per workgroup
   const uint32_t tickets = E->source_major ? E->S : g * E->S;
-  E->ticket_no += tickets + (f.persistent ? std::min(E->fused_wgs, tickets) : 0u);
+  E->ticket_no += tickets + (f.persistent ? std::min(wgs, tickets) : 0u);
   E->fused_windows += g;
   if (ordered) {  // the next launch's dispatch order: longest measured chains first (or the last window's HTB records)
     HIPCHK(E->d_order.ensure(E->S));
@@ -1544,7 +1588,10 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   std::swap(E->d_in, win[g - 1].in);
   E->n_in = win[g - 1].n;
   E->n_verdict = E->n_in;
-  for (uint32_t i = 0; i < g; ++i) E->gen_free.push_back(std::move(win[i]));
+  for (uint32_t i = 0; i < g; ++i) {
+    rc = retire_gen(E, std::move(win[i]));
+    if (rc) return rc;
+  }
   E->perm.clear();
   E->last_perm.clear();
   E->now_tick += static_cast<uint64_t>(g) * n_ticks;
@@ -1564,8 +1611,23 @@ void engine_shard(void* e, uint32_t* begin, uint32_t* end) {
   *end = as_eng(e)->o.shard_end;
 }
 int engine_fail(void* e, int code, const char* msg) { return as_eng(e)->fail(code, "%s", msg); }
-void engine_persist_routed(void* e, bool on) {
-  if (!as_eng(e)->persist_env) as_eng(e)->persist_routed = on;
+void engine_persist_routed(void* e, uint32_t pct) {
+  if (!as_eng(e)->persist_env) as_eng(e)->routed_pct = pct;
+}
+const uint64_t* engine_route_counts_dev(void* e) {
+  Eng* E = as_eng(e);
+  return E->route_n && E->d_rsend.p ? E->d_rsend.p + 16 * E->route_head : nullptr;
+}
+int engine_route_max(void* e, uint64_t* out) {
+  Eng* E = as_eng(e);
+  *out = 0;
+  if (!E->d_rsend.p) return 0;
+  HIPCHK(hipStreamSynchronize(E->rt_st));
+  uint64_t m[2 * Eng::kRouteSlots] = {};
+  for (uint32_t k = 0; k < Eng::kRouteSlots; ++k)
+    HIPCHK(hipMemcpy(&m[k], E->d_rsend.p + 16 * k + 8, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  for (uint32_t k = 0; k < Eng::kRouteSlots; ++k) *out = std::max(*out, m[k]);
+  return 0;
 }
 int engine_record_routed(void* e, hipEvent_t ev) {
   Eng* E = as_eng(e);
@@ -1694,8 +1756,9 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
   if (const char* fo = getenv("TGSIM_FUSED_ORDER")) E->order_chain = strcmp(fo, "records") != 0;
   if (const char* fm = getenv("TGSIM_FUSED_MAJOR")) E->source_major = strcmp(fm, "source") == 0;
-  if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) {
-    E->persist_routed = atoi(fp) != 0;
+  if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) {  // 0: turnover; 1: persistent, all resident
+    const int v = atoi(fp);                               // workgroups; 2..100: that % of them
+    E->routed_pct = v <= 0 ? 0u : v == 1 ? 100u : static_cast<uint32_t>(std::min(v, 100));
     E->persist_env = true;
   }
   if (const char* ph = getenv("TGSIM_PRIO_HEAVY")) E->prio_heavy = static_cast<uint32_t>(atoi(ph));
@@ -1793,9 +1856,14 @@ void tgsim_destroy(void* e) {
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release(); E->d_chain.release();
-  E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release();
-  for (auto& w : E->gen_q) { w.off.release(); w.in.release(); }
-  for (auto& w : E->gen_free) { w.off.release(); w.in.release(); }
+  E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release(); E->d_rsend.release();
+  for (auto* q : {&E->gen_q, &E->gen_free})
+    for (auto& w : *q) {
+      w.off.release();
+      w.in.release();
+      if (w.rd_rt) (void)hipEventDestroy(w.rd_rt);
+      if (w.rd_dst) (void)hipEventDestroy(w.rd_dst);
+    }
   for (auto& pr : E->ev_pending) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -1890,13 +1958,9 @@ int tgsim_gen_storm(void* e, double lambda, uint32_t n_ticks) {
   g.n_peers = E->N;
   g.n_ticks = n_ticks;
   g.now_tick = E->now_tick + E->gen_q_ticks;  // windows queue up back to back
-  HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));  // a free window's offsets may still be read by a delivery
-  HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));   // or a routing
-  Eng::GenWindow w;
-  if (!E->gen_free.empty()) {
-    w = std::move(E->gen_free.back());
-    E->gen_free.pop_back();
-  }
+  Eng::GenWindow w;  // a free window's offsets may still be read by a delivery or a routing
+  int trc = take_gen(E, &w);
+  if (trc) return trc;
   HIPCHK(E->d_cnt.ensure(E->S));
   launch_gen(g, E->d_cnt.p, nullptr, nullptr, nullptr, 0, E->st);
   HIPCHK(hipGetLastError());
@@ -1992,14 +2056,11 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   }
   // receipts are folded on the delivery stream (the sort of the same delivery may still run)
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_recv, 0));
-  HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));  // a free window's offsets may still be read by a routing
   const uint64_t win0 = E->now_tick + E->gen_q_ticks;
   const GossipArgs g = gossip_args(E, win0, n_ticks);
-  Eng::GenWindow w;
-  if (!E->gen_free.empty()) {
-    w = std::move(E->gen_free.back());
-    E->gen_free.pop_back();
-  }
+  Eng::GenWindow w;  // a free window's offsets may still be read by a routing or a delivery
+  int trc = take_gen(E, &w);
+  if (trc) return trc;
   HIPCHK(E->d_cnt.ensure(E->S));
   launch_gossip(g, nullptr, 0, E->d_cnt.p, nullptr, nullptr, 1, E->st);
   HIPCHK(hipGetLastError());

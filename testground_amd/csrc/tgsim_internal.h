@@ -215,9 +215,16 @@ int engine_device(void* engine);
 uint32_t engine_peers(void* engine);
 void engine_shard(void* engine, uint32_t* begin, uint32_t* end);
 int engine_fail(void* engine, int code, const char* msg);
-void engine_persist_routed(void* engine, bool on);  // unless TGSIM_FUSED_PERSIST was set
+// Grid of a sharded fused group (unless TGSIM_FUSED_PERSIST was set): 0 = one workgroup per ticket,
+// else a persistent grid of pct % of the resident workgroups.
+void engine_persist_routed(void* engine, uint32_t pct);
 // Records `ev` on the routing stream after every routing enqueued so far (the exchange of a launched
 // window waits for it on the device, not only for the host's view of the published edges).
 int engine_record_routed(void* engine, hipEvent_t ev);
+// Device address of the per-rank record counts of the oldest launched, unfinished routing (u64 per
+// rank, written by its last routing kernel), or null.
+const uint64_t* engine_route_counts_dev(void* engine);
+// The largest per-rank count any routing has written so far (waits for the routing stream).
+int engine_route_max(void* engine, uint64_t* out);
 
 }  // namespace tgsim

@@ -1618,6 +1618,289 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused_sm(FusedSim fs, FusedArg
   }
 }
 
+constexpr uint32_t kSparseQ = 4;  // chunks of 64 queued items / ring entries held in registers
+constexpr uint32_t kFifoRounds = 4;  // FIFO sources: items served per step, in rounds of 64
+
+// ---------------------------------------------------------------------------------------------
+// k_sim_multi: the FIFO sources k_sim_sparse cannot take in one round of lanes -- more than 64
+// offered packets, or more than kFifoRounds x 64 items to serve (the gossip flood's peak).  The same
+// FIFO path as sparse_source (the stored queue is one sorted region, the new items extend it in
+// order, so HTB serves the prefix below the horizon in that order and the rest stays in place), with
+// the candidates staged in LDS in offer order: any number of rounds of 64 offered packets and of
+// served items run in one wave, at a register-only cost per round.  A source that turns out not to
+// be FIFO (a clone that is queued, a new item before its predecessor) goes on to the general
+// worklist (k_sim_list).  One wave per source, a grid-stride loop over the list k_sim_sparse wrote.
+constexpr uint32_t kMultiCand = 1024;
+struct MultiLds {
+  uint4 c[kMultiCand];  // the candidates, in offer order (their due ones are a prefix)
+};
+
+__device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s, MultiLds& L) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t below = (1ull << lane) - 1;
+  const uint4* gh = a.heap + (size_t)s * kHeapCap;
+  const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
+  const SrcState st = a.state[s];
+  const SrcParams pp = a.params[s];
+  const uint64_t sbeg = a.off[s], send = a.off[s + 1];
+  const uint32_t n = (uint32_t)(send - sbeg);
+  const uint32_t rn = st.ring_n, qn = st.heap_n;
+  auto defer = [&]() {
+    if (lane == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
+  };
+  // (k_sim_sparse checked the rest: no correlated draws, below the netem limit even if every offered
+  // packet and a clone were queued, at most 256 ring entries, one sorted queue region)
+  if (n > kMultiCand) {
+    defer();
+    return;
+  }
+  unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
+  const uint32_t src = a.shard_begin + s;
+  const uint32_t qh = q_head(st);
+  uint64_t rg[kSparseQ];
+#pragma unroll
+  for (uint32_t u = 0; u < kSparseQ; ++u) {
+    const uint32_t k = u * kWave + lane;
+    rg[u] = k < rn ? gr[k] : ~0ull;
+  }
+  const uint4 qt = qn ? gh[(qh + qn - 1) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
+  const bool src_on = a.enabled[src] != 0;
+  const bool plain = src_on && !a.any_disabled && pp.rule_n == 0;
+  const uint32_t ext_v = (pp.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE;
+  const uint64_t h = a.horizon_ns;
+  // ---- netem decisions, 64 offered packets a round; candidates into LDS in offer order
+  uint32_t nc = 0, n_due = 0, perr = 0, vcnt = 0, t_clone = 0;
+  bool fifo = true, has_last = qn != 0;
+  uint4 last = qt;  // the item every next candidate must not precede
+  uint64_t T_enq = 0;
+  for (uint32_t base = 0; base < n; base += kWave) {
+    const bool staged = base + lane < n;
+    InRec r = {};
+    if (staged) r = a.in[sbeg + base + lane];
+    const uint64_t T = a.t0_ns + (uint64_t)r.tick * a.tick_ns;
+    const uint32_t len = r.len & 0xFFFFu;
+    uint32_t fv = 0u;
+    if (staged) fv = plain ? (r.dst == TGSIM_EXTERNAL ? ext_v : kFvPass) : filter(a, pp, src_on, r.dst);
+    uint32_t vout = 0xF0u | fv;
+    bool cand = false, queued_clone = false;
+    uint4 io = make_uint4(0, 0, 0, 0);
+    if (staged && fv == kFvPass) {
+      uint32_t r0[4];
+      philox(src, r.dst, r.seq, 0, a.key0, a.key1, r0);
+      const int count = 1 + (pp.thr_dup && pp.thr_dup >= r0[0]) - (pp.thr_loss && pp.thr_loss >= r0[1]);
+      if (count == 0) {
+        vout = 0xF0u | TGSIM_V_LOSS;
+      } else {
+        cand = true;
+        uint32_t cv = TGSIM_V_NONE;
+        if (count == 2) {  // the clone: lost before the queue keeps the source FIFO, queued does not
+          uint32_t r2[4];
+          philox(src, r.dst, r.seq, 2, a.key0, a.key1, r2);
+          if (pp.thr_loss && pp.thr_loss >= r2[0]) cv = TGSIM_V_LOSS;
+          else queued_clone = true;
+        }
+        const uint32_t flo = (pp.thr_cor && pp.thr_cor >= r0[2]) ? TGSIM_FLAG_CORRUPT : 0u;
+        const bool reo_o = pp.thr_reo && pp.thr_reo >= r0[3];
+        uint64_t eo = reo_o ? T : T + pp.lat_ns;
+        if (!reo_o && pp.sigma != 0) {
+          uint32_t r1[4];
+          philox(src, r.dst, r.seq, 1, a.key0, a.key1, r1);
+          eo = delayed(pp, T, r1[0]);
+        }
+        if (eo > kEMask) { perr = 1; eo = kEMask; }
+        io = make_item(eo, len, flo, r.seq, r.dst);
+        vout = (cv << 4) | TGSIM_V_SCHEDULED;
+      }
+    }
+    if (__ballot(queued_clone)) fifo = false;
+    const uint64_t mc = __ballot(cand);
+    // FIFO: no candidate before its predecessor (the candidate before it, or the last item so far)
+    const uint64_t bc = mc & below;
+    const uint32_t pl = bc ? 63u - (uint32_t)__builtin_clzll(bc) : lane;
+    uint4 prev = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.x),
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.y),
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.z), 0u);
+    if (!bc) prev = last;
+    if (__ballot(cand && (bc || has_last) && item_lt(io, prev))) fifo = false;
+    if (cand) L.c[nc + (uint32_t)__popcll(bc)] = io;
+    n_due += (uint32_t)__popcll(__ballot(cand && (w0_of(io) & kEMask) < h));
+    if (mc) {
+      const uint32_t ll = 63u - (uint32_t)__builtin_clzll(mc);
+      last = make_uint4(readlane32(io.x, ll), readlane32(io.y, ll), readlane32(io.z, ll), 0u);
+      has_last = true;
+      T_enq = readlane64(T, ll);
+    }
+    nc += (uint32_t)__popcll(mc);
+    if (staged) a.verdict[sbeg + base + lane] = (uint8_t)vout;  // rewritten by k_sim_list if deferred
+    const uint32_t vo = vout & 15u, vc = vout >> 4;
+#pragma unroll
+    for (uint32_t v = 0; v < 8; ++v) {
+      const uint32_t t = ballot_count(staged && vo == v) + ballot_count(staged && vc == v);
+      if (lane == v) vcnt += t;
+    }
+    t_clone += ballot_count(staged && vc != TGSIM_V_NONE);
+  }
+  if (!fifo) {
+    defer();
+    return;
+  }
+  wave_lds_sync();
+  // ---- the queue's prefix below the horizon: all of it when a candidate is due (every queued item
+  // precedes it), else its chunks from the head while they are due entirely
+  uint32_t nq = n_due ? qn : 0;
+  if (!n_due) {
+    for (uint32_t c = 0; c * kWave < qn; ++c) {
+      const uint32_t k = c * kWave + lane;
+      const uint4 v = k < qn ? gh[(qh + k) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
+      const uint32_t d = (uint32_t)__popcll(__ballot(k < qn && (w0_of(v) & kEMask) < h));
+      nq += d;
+      if (d < kWave) break;
+    }
+  }
+  // ---- the old ring: the prefix departing before the last enqueue is released (as in sparse_source)
+  uint64_t* wr = a.ring + (size_t)s * kHeapCap;
+  bool ring_stop = T_enq == 0;
+  uint32_t k0 = 0;
+  if (T_enq) {
+#pragma unroll
+    for (uint32_t u = 0; u < kSparseQ; ++u) {
+      if (!ring_stop && u * kWave < rn) {
+        const uint64_t m = __ballot(u * kWave + lane < rn && rg[u] >= T_enq);
+        const uint32_t cnt = rn - u * kWave < kWave ? rn - u * kWave : kWave;
+        if (m) {
+          k0 += (uint32_t)__builtin_ctzll(m);
+          ring_stop = true;
+        } else {
+          k0 += cnt;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < kSparseQ; ++u) {
+    const uint32_t k = u * kWave + lane;
+    if (k < rn && k >= k0) wr[k - k0] = rg[u];
+  }
+  const uint32_t old_kept = rn - k0;
+  // ---- in place: the candidates not served go behind the tail; the served prefix leaves by moving
+  // the head slot
+  uint4* wq = a.heap + (size_t)s * kHeapCap;
+  for (uint32_t c = n_due + lane; c < nc; c += kWave) wq[(qh + qn + c - n_due) & (kHeapCap - 1)] = L.c[c];
+  const uint32_t new_head = (qh + nq) & (kHeapCap - 1);
+  const uint32_t wpos = qn - nq + nc - n_due;
+  const uint32_t ns_all = nq + n_due;
+  // ---- HTB, records, receipts and the ring, for the served items in rounds of 64 lanes: the
+  // queue's due items from HBM, then the due candidates from LDS
+  uint64_t tat_c = st.tat;
+  uint32_t emitted = 0, sk0 = 0, t_cor = 0, t_lost = 0;
+  uint64_t bytes = 0;
+  bool releasing = T_enq && !ring_stop;
+  tgsim_delivery* const emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
+  for (uint32_t base = 0; base < ns_all; base += kWave) {
+    const uint32_t k = base + lane;
+    const uint32_t ns = ns_all - base < kWave ? ns_all - base : kWave;
+    const bool hs = lane < ns;
+    const uint4 x = k < nq ? gh[(qh + k) & (kHeapCap - 1)] : hs ? L.c[k - nq] : make_uint4(0, 0, 0, 0);
+    const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
+    const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
+                            ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
+                            : 0u;
+    const uint64_t e = w0_of(x) & kEMask;
+    const uint32_t xlen = x.y >> 14 & 0xFFFFu;
+    const uint64_t c = ((uint64_t)xlen * pp.mult) >> (pp.shift_ext & 0xFFu);
+    uint64_t A = hs ? c : 0, Bm = hs ? (e > pp.burst_ns ? e - pp.burst_ns : 0) + c : 0;
+    scan_maxplus(A, Bm);
+    const uint64_t ta = tat_c + A;
+    const uint64_t tat_after = ta > Bm ? ta : Bm;
+    const uint64_t before = shr1_u64(tat_after, tat_c);
+    const uint64_t d = e > before ? e : before;
+    tat_c = readlane64(tat_after, ns - 1);
+    const bool live = hs && x.w != kDeadDst;
+    const uint64_t lm = __ballot(live);
+    if (live) {
+      const uint32_t flags = x.y >> 30;
+      const uint32_t i = emitted + (uint32_t)__popcll(lm & below);
+      uint64_t* rw = reinterpret_cast<uint64_t*>(emit + i);
+      rw[0] = d;
+      rw[1] = ((uint64_t)x.w << 32) | src;
+      rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
+      if (a.dst_cnt) {
+        if (a.emit_slot)
+          a.emit_slot[2 * sbeg + (uint64_t)kHeapCap * s + i] = (uint32_t)atomicAdd(&a.dst_cnt[x.w], 1ull);
+        else
+          atomicAdd(&a.dst_cnt[x.w], 1ull);
+      }
+      if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
+      bytes += xlen;
+    }
+    emitted += (uint32_t)__popcll(lm);
+    t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
+    t_lost += (uint32_t)__popcll(__ballot(hs && !live));
+    if (releasing) {  // a prefix of the served entries departed before the last enqueue
+      const uint32_t n1 = (uint32_t)__popcll(__ballot(hs && e < T_enq));
+      const uint64_t m = __ballot(lane < n1 && d >= T_enq);
+      if (m) {
+        sk0 = base + (uint32_t)__builtin_ctzll(m);
+        releasing = false;
+      } else {
+        sk0 = base + n1;
+        releasing = n1 == kWave;
+      }
+    }
+    if (hs && k >= sk0) wr[old_kept + k - sk0] = d;
+  }
+  const uint32_t rn_new = old_kept + ns_all - sk0;
+  if (lane == 0) {
+    SrcState ns_;
+    ns_.tat = tat_c;
+    ns_.heap_n = wpos;
+    ns_.near_n = wpos | new_head << 16;  // sorted in place
+    ns_.ring_n = rn_new;
+    ns_.last_dup = st.last_dup;
+    ns_.last_cor = st.last_cor;
+    ns_.last_reo = st.last_reo;
+    a.state[s] = ns_;
+    a.emit_n[s] = emitted;
+  }
+  // ---- statistics
+  const uint64_t t_bytes = wave_sum(bytes);
+  const bool err = __ballot(perr != 0) != 0;
+  if (lane < 8 && vcnt) atomicAdd(&sc[kStVerdict0 + lane], (unsigned long long)vcnt);
+  if (lane == 0) {
+    const uint64_t qb = 16ull * qn + 8ull * rn + 16ull * wpos + 8ull * rn_new;
+    // HBM items of the queue this step touched: the due prefix read, the tail item, the appended ones
+    const uint32_t q_moved = nq + (qn ? 1u : 0u) + nc - n_due;
+    const uint64_t q_kept = qn + wpos > q_moved ? 16ull * (qn + wpos - q_moved) : 0ull;
+    if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
+    if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
+    if (emitted) atomicAdd(&sc[kStScheduled], (unsigned long long)emitted);
+    if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
+    if (t_cor) atomicAdd(&sc[kStCorrupted], (unsigned long long)t_cor);
+    if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
+    if (t_bytes) atomicAdd(&sc[kStBytes], (unsigned long long)t_bytes);
+    if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
+    if (err) {
+      atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
+      if (a.err_host)
+        __hip_atomic_store(a.err_host, (uint64_t)kErrTimeOverflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// The multi-round list k_sim_sparse wrote behind its worklist's statistics words: [n_src + 8] the
+// count, then the sources.
+__device__ __forceinline__ uint32_t* multi_list(const SimArgs& a) { return a.worklist + a.n_src + 8; }
+
+__global__ __launch_bounds__(kWave) void k_sim_multi(SimArgs a) {
+  __shared__ MultiLds L;
+  uint32_t* const list = multi_list(a);
+  const uint32_t n = list[0];
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    multi_source(a, list[1 + i], L);
+    wave_lds_sync();  // this source's LDS reads are done before the next one's writes
+  }
+}
+
 // Register-only form of an open-queue step (the sparse senders of a gossip flood): no LDS queue.
 // Every queued item (near and pool, up to 256) and every new item stay in registers; the items
 // HTB serves this step (e < horizon: at most 64, else the source is deferred) are gathered into
@@ -1627,8 +1910,7 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused_sm(FusedSim fs, FusedArg
 // released up to the last enqueue's offer time, every candidate is admitted.  A source that does
 // not fit (correlated draws, a queue that could reach the limit, more than 64 offered packets, 256
 // queued items, 256 ring entries or 64 items to serve) writes nothing and goes to the worklist.
-constexpr uint32_t kSparseQ = 4;  // chunks of 64 queued items / ring entries held in registers
-constexpr uint32_t kFifoRounds = 4;  // FIFO sources: items served per step, in rounds of 64
+// (FIFO sources with more than one round of lanes go to k_sim_multi above instead.)
 __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s) {
   const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1;
@@ -1651,6 +1933,13 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
 #endif
   };
   const bool sorted_st = q_near(st) == qn;  // the whole queue is one sorted region
+  // FIFO candidates beyond one round of lanes go to k_sim_multi (multi-round, candidates in LDS)
+  auto defer_multi = [&]() {
+    if (lane == 0) {
+      uint32_t* const l2 = multi_list(a);
+      l2[1 + atomicAdd(l2, 1u)] = s;
+    }
+  };
   unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
   const uint4 qh0 = sorted_st && qn && !n ? gh[q_head(st)] : make_uint4(0, 0, 0, 0);
   if (!n && (!qn || (sorted_st && (w0_of(qh0) & kEMask) >= a.horizon_ns))) {
@@ -1668,8 +1957,10 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   }
   if ((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 || (uint64_t)rn + qn + 2ull * n >= a.queue_limit || n > kWave ||
       (!sorted_st && qn > kSparseQ * kWave) || rn > kSparseQ * kWave) {
-    defer((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 ? 0u : (uint64_t)rn + qn + 2ull * n >= a.queue_limit ? 1u
-          : n > kWave ? 2u : rn > kSparseQ * kWave ? 4u : 3u);
+    const uint32_t why = (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 ? 0u : (uint64_t)rn + qn + 2ull * n >= a.queue_limit ? 1u
+                         : n > kWave ? 2u : rn > kSparseQ * kWave ? 4u : 3u;
+    if (why == 2u && sorted_st && rn <= kSparseQ * kWave) defer_multi();
+    else defer(why);
     return;
   }
   const uint32_t src = a.shard_begin + s;
@@ -1849,7 +2140,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     const uint64_t dm = __ballot(due_o);
     const uint32_t n_due = (uint32_t)__popcll(dm);
     if (nq + n_due > kFifoRounds * kWave || (nq == kFifoRounds * kWave && qn > nq)) {
-      defer(5u);
+      defer_multi();
       return;
     }
     write_old_ring();
@@ -2648,9 +2939,17 @@ __global__ __launch_bounds__(64 * W) void k_route_scatter(RouteArgs a) {
 // (system-scope release): the host polls that word instead of synchronizing on an event, which
 // would also wait for the next step's k_sim queued behind this kernel.
 __global__ void k_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
-                              tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow, uint64_t stride) {
+                              tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow, uint64_t stride,
+                              uint64_t* dev_counts) {
   const uint32_t r = threadIdx.x;
   if (r <= n_ranks) slot[r] = pos[(size_t)r * n_src];
+  // per-rank counts in device memory as well: the exchange's count all-to-all reads them on the
+  // device, so the host waits once, for the received counts, not first for these
+  if (dev_counts && r < n_ranks) {
+    const uint64_t c = pos[(size_t)(r + 1) * n_src] - pos[(size_t)r * n_src];
+    dev_counts[r] = c;
+    atomicMax(reinterpret_cast<unsigned long long*>(dev_counts + 8), (unsigned long long)c);  // the largest so far
+  }
   if (slot_cap && r < n_ranks) {  // slotted output: each rank's chunk starts with its record count
     const uint64_t c = pos[(size_t)(r + 1) * n_src] - pos[(size_t)r * n_src];
     tgsim_delivery h = {};
@@ -2687,6 +2986,28 @@ __global__ void k_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_be
   if (i >= n || slot_empty(in, i, slot)) return;
   const uint32_t d = in[i].dst - dst_begin;
   if (d < n_dst) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[seg_of(i, slot, n_win, n_dst, d)]), 1ull);
+}
+
+// Slotted input, chunk by chunk: blockIdx.y is the chunk (count header, then up to `slot` records),
+// the blocks of a chunk stride over the records its header announces.  The grid is sized for the
+// records a chunk usually holds, not for its capacity: a chunk sized by a bound (the one-rank routed
+// exchange reserves the whole step capacity) costs what it holds.
+template <bool kScatter>
+__global__ __launch_bounds__(256) void k_dst_slot(const tgsim_delivery* in, uint64_t slot, uint32_t dst_begin,
+                                                  uint32_t n_dst, uint64_t* cnt_or_pos, tgsim_delivery* out,
+                                                  uint32_t n_win) {
+  const uint64_t c = blockIdx.y;
+  const tgsim_delivery* ch = in + c * (slot + 1);
+  const uint64_t n = ch[0].t_ns < slot ? ch[0].t_ns : slot;
+  const uint64_t seg0 = n_win > 1 ? (c % n_win) * n_dst : 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const tgsim_delivery r = ch[1 + j];
+    const uint32_t d = r.dst - dst_begin;
+    if (d >= n_dst) continue;
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(&cnt_or_pos[seg0 + d]);
+    if constexpr (kScatter) out[atomicAdd(w, 1ull)] = r;
+    else atomicAdd(w, 1ull);
+  }
 }
 
 // Flat input (records received from every shard): pos[] starts as the exclusive scan of counts.
@@ -3162,6 +3483,7 @@ uint32_t sim_fused_resident() {
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
   if (!a.n_src) return;
   hipLaunchKernelGGL(k_sim_sparse, dim3(a.n_src), dim3(kWave), 0, st, a);
+  hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 8192 ? a.n_src : 8192), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
 }
 
@@ -3191,6 +3513,20 @@ __global__ void k_publish(const uint64_t* v0, const uint32_t* v1, uint64_t* slot
   __hip_atomic_store(&slot[1], (uint64_t)(v1 ? *v1 : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __threadfence_system();
   __hip_atomic_store(&slot[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// n device words to pinned host memory, then the sequence word host[n] (release, system scope): the
+// host spins on one word instead of synchronizing a stream.
+__global__ void k_publish_words(const uint64_t* src, uint32_t n, uint64_t* host, uint64_t seq) {
+  const uint32_t i = threadIdx.x;
+  if (i < n) __hip_atomic_store(&host[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __syncthreads();
+  if (i == 0) __hip_atomic_store(&host[n], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_publish_words(const uint64_t* src, uint32_t n, uint64_t* host, uint64_t seq, hipStream_t st) {
+  hipLaunchKernelGGL(k_publish_words, dim3(1), dim3(64), 0, st, src, n, host, seq);
 }
 
 void launch_publish(const uint64_t* v0, const uint32_t* v1, uint64_t* slot, uint64_t seq, hipStream_t st) {
@@ -3280,9 +3616,10 @@ void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_
 }
 
 void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
-                        hipStream_t st, tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow, uint64_t chunk_stride) {
+                        hipStream_t st, tgsim_delivery* out, uint64_t slot_cap, uint32_t* overflow, uint64_t chunk_stride,
+                        uint64_t* dev_counts) {
   hipLaunchKernelGGL(k_route_edges, dim3(1), dim3(64), 0, st, pos, n_src, n_ranks, slot, seq, out, slot_cap,
-                     overflow, chunk_stride ? chunk_stride : slot_cap + 1);
+                     overflow, chunk_stride ? chunk_stride : slot_cap + 1, dev_counts);
 }
 
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
@@ -3310,6 +3647,26 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st) {
   if (grid == 0) grid = 1;
   if (phase == 0) hipLaunchKernelGGL(k_route_count<4>, dim3(grid), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(k_route_scatter<4>, dim3(grid), dim3(256), 0, st, a);
+}
+
+// Blocks per chunk of a slotted input: enough for the chunk's expected records (slot_hint, e.g. the
+// last exchange's largest count) at 4 records per thread, at most 1,024.
+static uint32_t slot_blocks(uint64_t slot, uint64_t slot_hint) {
+  const uint64_t want = (slot_hint && slot_hint < slot ? slot_hint : slot) / 1024 + 1;
+  return (uint32_t)(want < 1024 ? want : 1024);
+}
+
+void launch_dst_slot(const tgsim_delivery* in, uint64_t n_chunks, uint64_t slot, uint64_t slot_hint, uint32_t dst_begin,
+                     uint32_t n_dst, uint64_t* cnt_or_pos, tgsim_delivery* out, hipStream_t st, uint32_t n_win) {
+  if (!n_chunks) return;
+  // a fused group's delivery runs beside k_sim_fused: single-wave workgroups fit where a CU has no
+  // room left for a 256-thread block
+  const uint32_t b = n_win > 1 ? 64u : 256u;
+  const dim3 grid(slot_blocks(slot, slot_hint) * (256u / b), (uint32_t)n_chunks);
+  if (out)
+    hipLaunchKernelGGL(k_dst_slot<true>, grid, dim3(b), 0, st, in, slot, dst_begin, n_dst, cnt_or_pos, out, n_win);
+  else
+    hipLaunchKernelGGL(k_dst_slot<false>, grid, dim3(b), 0, st, in, slot, dst_begin, n_dst, cnt_or_pos, out, n_win);
 }
 
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,

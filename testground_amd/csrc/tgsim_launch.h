@@ -72,10 +72,16 @@ void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
 // when a rank's count exceeds slot_cap.
 void launch_route_edges(const uint64_t* pos, uint32_t n_src, uint32_t n_ranks, uint64_t* slot, uint64_t seq,
                         hipStream_t st, tgsim_delivery* out = nullptr, uint64_t slot_cap = 0,
-                        uint32_t* overflow = nullptr, uint64_t chunk_stride = 0);
+                        uint32_t* overflow = nullptr, uint64_t chunk_stride = 0, uint64_t* dev_counts = nullptr);
+// n (<= 64) device words to pinned host memory, then `seq` into host[n] (the word a host spins on).
+void launch_publish_words(const uint64_t* src, uint32_t n, uint64_t* host, uint64_t seq, hipStream_t st);
 // slot != 0: slotted input of n = chunks * (slot + 1) records (see launch_route_edges); with
 // n_win > 1 chunk c holds window c % n_win, counted into cnt[(c % n_win) * n_dst + d] (a fused
 // group: rank-major chunks, window-minor), in single-wave workgroups
+// Slotted input (n_chunks chunks of a count header + up to `slot` records): histogram (out null) or
+// scatter through pos (out given), grid-stride over the counts the headers announce.
+void launch_dst_slot(const tgsim_delivery* in, uint64_t n_chunks, uint64_t slot, uint64_t slot_hint, uint32_t dst_begin,
+                     uint32_t n_dst, uint64_t* cnt_or_pos, tgsim_delivery* out, hipStream_t st, uint32_t n_win);
 void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* cnt,
                      hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,

@@ -362,3 +362,61 @@ def test_native_udp_front_headerless(make_oracle):
         front.close()
         for s in socks:
             s.close()
+
+
+@native
+def test_unmodified_udp_echo_program_through_front_end(make_oracle):
+    """an unmodified UDP program (tests/udp_echo_server.py, a separate process that
+    only binds a port and echoes what it receives to the sender's address) is instance 1; instance 0's
+    client sends plain datagrams to instance 1's data address.  Both directions cross the simulated
+    3 ms link through the C front end (recvmmsg -> engine window -> sendmmsg), with no framing: the
+    echo program sees instance 0's data address as the sender and replies to it, and the client gets
+    every payload back from instance 1's data address, no earlier than one simulated round trip.
+    (TCP plans stay out of reach: no TUN/TAP or capabilities on the GPU box)"""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from testground_amd.bridge import NativeBridge, NativeUdpFront
+
+    n, lat_ms = 2, 3
+    e = make_oracle(n, lookahead_ns=WINDOW * 1000)
+    for i in range(n):
+        e.configure(i, nw.Config(Network="default", Enable=True, Default=nw.LinkShape(Latency=lat_ms * nw.Millisecond)))
+    b = NativeBridge(e, n, WINDOW)
+    front = NativeUdpFront(b)
+    msgs = [b"echo-%03d" % k + bytes(range(k % 7)) for k in range(10)]
+    echo = subprocess.Popen([sys.executable, str(Path(__file__).with_name("udp_echo_server.py")), "0", str(len(msgs))],
+                            stdout=subprocess.PIPE, text=True)
+    cli = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        echo_port = int(echo.stdout.readline())
+        cli.bind(("127.0.0.1", 0))
+        cli.setblocking(False)
+        front.register(0, cli.getsockname())
+        front.register(1, ("127.0.0.1", echo_port))
+        vaddr = [front.bind_peer(i) for i in range(n)]
+        for m in msgs:
+            cli.sendto(m, vaddr[1])
+        time.sleep(0.05)
+        got, first_at = [], None
+        for w in range(400):
+            front.pump()
+            time.sleep(0.002)  # the echo program answers in wall-clock time
+            while True:
+                try:
+                    data, addr = cli.recvfrom(65536)
+                except BlockingIOError:
+                    break
+                assert addr == vaddr[1]  # from the echo instance's data address, no header
+                got.append(data)
+                first_at = first_at if first_at is not None else w + 1
+            if len(got) == len(msgs):
+                break
+        assert sorted(got) == sorted(msgs)
+        assert first_at >= 2 * lat_ms * 1000 // WINDOW  # a simulated round trip at least
+        assert echo.wait(timeout=10) == 0  # it saw all its datagrams
+    finally:
+        echo.kill()
+        cli.close()
+        front.close()
