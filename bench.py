@@ -587,7 +587,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         "verdict_mix": {k: float(v) / tot_v for k, v in zip(abi.VERDICT_NAMES, verd_all)},
         "setup_s": setup_s,
         "roofline": {"bound": "hbm", "kernel": "k_sim_fused (dense generated windows, a fused dispatch's time divided by its "
-                                               "windows) | k_sim (other dense steps) | k_sim_sparse + k_sim_list (sparse steps)",
+                                               "windows) | k_sim (other dense steps) | k_sim_sparse + k_sim_multi + k_sim_list (sparse steps)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic, "traffic_source": traffic_src,

@@ -22,7 +22,7 @@ for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
     per = defaultdict(lambda: defaultdict(float))
     name = {}
     for r in csv.DictReader(open(f)):
-        if any(k in r["Kernel_Name"] for k in FIRST + ("k_sim_list(",)):
+        if any(k in r["Kernel_Name"] for k in FIRST + ("k_sim_list(", "k_sim_multi(")):
             per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
             name[int(r["Dispatch_Id"])] = r["Kernel_Name"]
     step = []  # counters summed per dispatch group, in dispatch order, with its window count
@@ -39,7 +39,7 @@ for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
         for k, v in sv.items():
             vals[k].setdefault("v", []).extend([v / w] * w)
 avg = {k: sum(d["v"]) / len(d["v"]) for k, d in vals.items()}
-out = {"kernel": "tgsim::k_sim | k_sim_fused (dense windows) | k_sim_sparse + k_sim_list (sparse windows), per window", "counters_avg_per_launch": avg,
+out = {"kernel": "tgsim::k_sim | k_sim_fused (dense windows) | k_sim_sparse + k_sim_multi + k_sim_list (sparse windows), per window", "counters_avg_per_launch": avg,
        "hbm_bytes_per_launch": (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)) * 1024
        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg else None,
        "fetch_correction": "x2 (gfx950 FETCH_SIZE counts 64 B per 128 B request)",

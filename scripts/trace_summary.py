@@ -10,12 +10,12 @@ import sys
 trace, n = sys.argv[1], int(sys.argv[2])
 fuse = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 FIRST = ("k_sim(", "k_sim_sparse(", "k_sim_fused(")  # one of these opens every dispatch group
-rows = [r for r in csv.DictReader(open(trace)) if any(k in r["Kernel_Name"] for k in FIRST + ("k_sim_list(",))]
+rows = [r for r in csv.DictReader(open(trace)) if any(k in r["Kernel_Name"] for k in FIRST + ("k_sim_list(", "k_sim_multi("))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 disp = []
 for r in rows:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-    name = next(k for k in FIRST + ("k_sim_list(",) if k in r["Kernel_Name"])
+    name = next(k for k in FIRST + ("k_sim_list(", "k_sim_multi(") if k in r["Kernel_Name"])
     if name in FIRST or not disp:
         disp.append({"ms": 0.0, "kernels": []})
     disp[-1]["ms"] += d
@@ -33,7 +33,7 @@ mix = {}
 for d, w in timed:
     k = "+".join(d["kernels"]) + (f" x{w} windows" if w > 1 else "")
     mix[k] = mix.get(k, 0) + 1
-print(json.dumps({"kernels": "k_sim | k_sim_sparse + k_sim_list | k_sim_fused (per window)", "dispatch_groups": len(disp),
+print(json.dumps({"kernels": "k_sim | k_sim_sparse + k_sim_multi + k_sim_list | k_sim_fused (per window)", "dispatch_groups": len(disp),
                   "timed_windows": wins, "timed_dispatch_groups": len(timed),
                   "timed_avg_ms_per_window": ms / max(1, wins),
                   "timed_min_ms_per_window": min(d["ms"] / w for d, w in timed),

@@ -307,14 +307,12 @@ struct tgsim_engine_s {
   // emit regions and per-destination histogram written by k_sim; a single-shard step reads them
   // on the delivery stream while the next k_sim writes the other pair (swapped by deliver_local;
   // ev_local: the delivery that last read the pair)
-  // Emit sets: window k's k_sim writes set k % emit_sets (d_emit, ...) while the deliveries of the
-  // windows before it read the others (the *_alt / *_3 sets, rotated after every window); k_sim waits
-  // only for the delivery of window k - emit_sets, so a delivery may lag (the gossip flood's peak)
-  DevBuf<tgsim_delivery> d_emit, d_emit_alt, d_emit_3;
-  DevBuf<uint32_t> d_eslot, d_eslot_alt, d_eslot_3;  // records' slots in their destinations' segments (emit_slot)
-  uint32_t emit_sets = 2;                            // TGSIM_EMIT_SETS: 2 or 3 (each set of a 1M-peer
-                                                     // engine is ~38 GB: its regions reserve 1,024
-                                                     // records per source)
+  // Emit sets: window k's k_sim writes set k % 2 (d_emit, ...) while the delivery of the window
+  // before it reads the other (the *_alt set, swapped after every window); k_sim waits only for the
+  // delivery of window k - 2 (a third set, so that a delivery could lag two windows at the gossip
+  // flood's peak, was tried: at 1M peers a set is ~38 GB and the third one thrashed)
+  DevBuf<tgsim_delivery> d_emit, d_emit_alt;
+  DevBuf<uint32_t> d_eslot, d_eslot_alt;  // records' slots in their destinations' segments (emit_slot)
   bool eslot_on = false;                  // the last k_sim wrote d_eslot (heavy sparse windows)
   uint64_t slot_min = 16;                 // TGSIM_SLOT_MIN: offered packets per source from which it is on
   uint32_t wide_windows = 0;              // windows after a mid-run reshape whose bounded local delivery
@@ -322,9 +320,9 @@ struct tgsim_engine_s {
   uint64_t deliver_slack = 128;           // TGSIM_DELIVER_SLACK: queued items per source a bounded local
                                           // delivery allows for (besides 2 per offered packet)
   bool slack_forced = false;              // TGSIM_DELIVER_SLACK set: the bounded form at any size
-  DevBuf<uint32_t> d_emit_n, d_emit_n_alt, d_emit_n_3;
-  DevBuf<uint64_t> d_lcnt, d_lcnt_alt, d_lcnt_3;  // stays zero between steps (k_dst_sort resets it)
-  hipEvent_t ev_local = nullptr, ev_local_alt = nullptr, ev_local_3 = nullptr;
+  DevBuf<uint32_t> d_emit_n, d_emit_n_alt;
+  DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (k_dst_sort resets it)
+  hipEvent_t ev_local = nullptr, ev_local_alt = nullptr;
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
@@ -346,10 +344,6 @@ struct tgsim_engine_s {
   uint32_t dense_div = 4;    // TGSIM_DENSE_DIV: dense when the last sparse step deferred > S / dense_div
   bool trace_list = false;   // TGSIM_TRACE_LIST: print each sparse decision's deferred count
   bool order_valid = false;
-  int order_by = 0;          // TGSIM_ORDER_BY: 0 HTB records of the last step, 1 its k_sim time per source
-  DevBuf<uint32_t> d_dur;
-  DevBuf<uint32_t> d_chain;  // fused groups: each source's measured chain of windows (next group's order)
-  bool order_chain = true;   // TGSIM_FUSED_ORDER: chain (default) or records (the last window's HTB records)
   // fused windows (tgsim_step_n): per group parity p and window i the emit regions, their counts
   // and the per-destination histogram; ev_fgrp[p]: after the deliveries that last read set p
   struct LocalSet {
@@ -363,7 +357,6 @@ struct tgsim_engine_s {
   DevBuf<uint8_t> f_verdict[kFuseMax];  // verdicts of a group's windows but the last (discarded)
   DevBuf<uint32_t> d_done, d_ticket;    // per-source completion words (window-major), ticket counter
   uint32_t step_no = 0, ticket_no = 0;  // windows and tickets issued by fused launches so far
-  bool source_major = false;            // TGSIM_FUSED_MAJOR=source: k_sim_fused_sm
   uint64_t fused_windows = 0;
   uint32_t fused_wgs = 0;
   uint32_t routed_pct = 0;      // sharded (routed) groups: 0 = one workgroup per ticket (the grid turns
@@ -824,13 +817,6 @@ void rotate_emit(Eng* E) {
   std::swap(E->d_eslot, E->d_eslot_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
   std::swap(E->ev_local, E->ev_local_alt);
-  if (E->emit_sets < 3) return;
-  // (a, b, c) -> (b, c, a): the set written two windows ago comes up once its delivery is the oldest
-  std::swap(E->d_emit_alt, E->d_emit_3);
-  std::swap(E->d_emit_n_alt, E->d_emit_n_3);
-  std::swap(E->d_eslot_alt, E->d_eslot_3);
-  std::swap(E->d_lcnt_alt, E->d_lcnt_3);
-  std::swap(E->ev_local_alt, E->ev_local_3);
 }
 
 // The size of a gossip window generated ahead of it (tgsim_gen_gossip): waits for the published
@@ -933,11 +919,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   const uint32_t n_wg = (E->S + kSpw - 1) / kSpw;
   const bool ordered = kSpw == 1 && E->S <= kOrderMaxSources;
   a.order = ordered && E->order_valid ? E->d_order.p : nullptr;
-  a.dur = nullptr;
-  if (ordered && E->order_by == 1) {
-    HIPCHK(E->d_dur.ensure(E->S));
-    a.dur = E->d_dur.p;
-  }
+  a.dur = nullptr;  // (measured per-source time as the dispatch weight: tried, not kept)
   a.stamps = nullptr;
   if (E->stamps_on) {
     HIPCHK(E->d_stamps.ensure(static_cast<size_t>(n_wg) * kStampSlots));
@@ -1000,10 +982,11 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   }
   if (sparse) {
     // [0] the worklist's count, its sources, 8 words of TGSIM_DEFER_STATS, then k_sim_multi's list
-    // (count, sources)
-    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 1 + 8 + 1));
+    // (count, sources), then k_sparse_active's list of the non-idle sources (count, sources)
+    HIPCHK(E->d_work.ensure(3 * static_cast<size_t>(E->S) + 1 + 8 + 1 + 1));
     HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t), E->st));
     HIPCHK(hipMemsetAsync(E->d_work.p + 1 + E->S + 8, 0, sizeof(uint32_t), E->st));
+    HIPCHK(hipMemsetAsync(E->d_work.p + 1 + 2 * static_cast<size_t>(E->S) + 9, 0, sizeof(uint32_t), E->st));
     a.worklist_n = E->d_work.p;
     a.worklist = E->d_work.p + 1;
     a.order = nullptr;  // (stamps, when on, are indexed by source: n_wg = S)
@@ -1042,7 +1025,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   // workgroups fit; with many more sources than resident workgroups the dispatcher balances alone
   if (ordered && !sparse) {
     HIPCHK(E->d_order.ensure(E->S));
-    launch_order(a.dur ? a.dur : E->d_emit_n.p, E->S, E->d_order.p, E->st);
+    launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
     HIPCHK(hipGetLastError());
     E->order_valid = true;
   }
@@ -1366,7 +1349,7 @@ int deliver_local(Eng* E) {
 // dense windows on an engine that owns every peer, no host packets, no per-window diagnostics.
 bool fusable(Eng* E, uint32_t n_ticks, uint32_t g, bool routed = false) {
   if (g < 2 || (E->S != E->N && !routed) || !E->staged.empty() || E->gen_q.size() < g || E->metrics_on ||
-      E->gossip_on || E->sparse_mode == 1 || E->order_by != 0 || kSpw != 1)
+      E->gossip_on || E->sparse_mode == 1 || kSpw != 1)
     return false;
   for (uint32_t i = 0; i < g; ++i)
     if (E->gen_q[i].ticks != n_ticks || E->gen_q[i].n < 64ull * E->S) return false;  // sparse windows
@@ -1462,11 +1445,6 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   f.ticket_base = E->ticket_no;
   f.ticket = E->d_ticket.p;
   f.done = E->d_done.p;
-  f.source_major = E->source_major ? 1u : 0u;
-  if (ordered && E->order_chain && E->source_major) {
-    HIPCHK(E->d_chain.ensure(E->S));
-    f.chain_dur = E->d_chain.p;
-  }
   hipEvent_t ev0, ev1;
   HIPCHK(take_event(E, &ev0));
   HIPCHK(take_event(E, &ev1));
@@ -1487,12 +1465,12 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   E->step_no += g;
   // every workgroup of the persistent grid claims until a claim fails: the counter advances by the
   // tickets (g per source window-major, one source-major) plus one failed claim per workgroup
-  const uint32_t tickets = E->source_major ? E->S : g * E->S;
+  const uint32_t tickets = g * E->S;
   E->ticket_no += tickets + (f.persistent ? std::min(wgs, tickets) : 0u);
   E->fused_windows += g;
-  if (ordered) {  // the next launch's dispatch order: longest measured chains first (or the last window's HTB records)
+  if (ordered) {  // the next launch's dispatch order: the last window's HTB records, heaviest first
     HIPCHK(E->d_order.ensure(E->S));
-    launch_order(f.chain_dur ? f.chain_dur : E->fset[p][g - 1].emit_n.p, E->S, E->d_order.p, E->st);
+    launch_order(E->fset[p][g - 1].emit_n.p, E->S, E->d_order.p, E->st);
     HIPCHK(hipGetLastError());
     E->order_valid = true;
   }
@@ -1703,7 +1681,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_recv, E->dst_st), "event"))) return bail(rc);
-  for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt, &E->ev_local_3}) {
+  for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt}) {
     if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
     if ((rc = E->hip(hipEventRecord(*ev, E->dst_st), "event"))) return bail(rc);
   }
@@ -1752,10 +1730,6 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
     E->deliver_slack = strtoull(ds, nullptr, 10);
     E->slack_forced = true;
   }
-  if (const char* es = getenv("TGSIM_EMIT_SETS")) E->emit_sets = atoi(es) == 3 ? 3u : 2u;
-  if (const char* ob = getenv("TGSIM_ORDER_BY")) E->order_by = atoi(ob);
-  if (const char* fo = getenv("TGSIM_FUSED_ORDER")) E->order_chain = strcmp(fo, "records") != 0;
-  if (const char* fm = getenv("TGSIM_FUSED_MAJOR")) E->source_major = strcmp(fm, "source") == 0;
   if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) {  // 0: turnover; 1: persistent, all resident
     const int v = atoi(fp);                               // workgroups; 2..100: that % of them
     E->routed_pct = v <= 0 ? 0u : v == 1 ? 100u : static_cast<uint32_t>(std::min(v, 100));
@@ -1852,10 +1826,10 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_eslot.release(); E->d_eslot_alt.release(); E->d_emit_3.release(); E->d_emit_n_3.release(); E->d_eslot_3.release(); E->d_lcnt_3.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_eslot.release(); E->d_eslot_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
-  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release(); E->d_dur.release(); E->d_chain.release();
+  E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
   E->d_msrc.release(); E->d_mdst.release(); E->d_mhist.release(); E->d_work.release(); E->d_rsend.release();
   for (auto* q : {&E->gen_q, &E->gen_free})
     for (auto& w : *q) {
@@ -1892,7 +1866,6 @@ void tgsim_destroy(void* e) {
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->ev_local) (void)hipEventDestroy(E->ev_local);
   if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);
-  if (E->ev_local_3) (void)hipEventDestroy(E->ev_local_3);
   if (E->dst_st) (void)hipStreamDestroy(E->dst_st);
   if (E->rt_st) (void)hipStreamDestroy(E->rt_st);
   if (E->st) (void)hipStreamDestroy(E->st);
@@ -2032,10 +2005,8 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   // the emit regions of both parities and the record slots of the flood's heavy windows, for the
   // same reserve (a hipFree + hipMalloc of several GB inside the flood stalls the loop)
   const uint64_t emit_cap = 2 * reserve + static_cast<uint64_t>(kHeapCap) * E->S;
-  for (auto* b : {&E->d_emit, &E->d_emit_alt, &E->d_emit_3})
-    if (b != &E->d_emit_3 || E->emit_sets == 3) HIPCHK(b->ensure(emit_cap));
-  for (auto* b : {&E->d_eslot, &E->d_eslot_alt, &E->d_eslot_3})
-    if (b != &E->d_eslot_3 || E->emit_sets == 3) HIPCHK(b->ensure(emit_cap));
+  for (auto* b : {&E->d_emit, &E->d_emit_alt}) HIPCHK(b->ensure(emit_cap));
+  for (auto* b : {&E->d_eslot, &E->d_eslot_alt}) HIPCHK(b->ensure(emit_cap));
   E->gossip_on = true;
   return 0;
 }

@@ -136,9 +136,8 @@ constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (T
 
 // Fused launch of up to kFuseMax consecutive windows (k_sim_fused).  Window-major:
 // ticket t -> window t / S of the (t % S)-th source in dispatch order, started once the source's
-// window k - 1 has stored done[s] = step_base + k (the hand-off).  Source-major (k_sim_fused_sm):
-// ticket t -> the t-th source, whose windows one wavefront runs back to back.  The windows differ
-// only in these per-window fields.
+// window k - 1 has stored done[s] = step_base + k (the hand-off).  The windows differ only in these
+// per-window fields.
 constexpr uint32_t kFuseMax = 8;
 struct FusedWindow {
   const uint64_t* off;
@@ -156,12 +155,9 @@ struct FusedArgs {
   uint32_t ticket_base; // *ticket before this launch (tickets are counted across launches)
   uint32_t* ticket;
   uint32_t* done;       // [S] last completed window of each source (wrapping step counter; window-major)
-  uint32_t source_major;
   uint32_t prio_n;      // tickets at dispatch positions below prio_n run at wave priority 3
   uint32_t persistent;  // 1: a grid of resident workgroups claims tickets until none is left; 0: one
                         // workgroup per ticket (the slots turn over, so an exchange can be dispatched)
-  uint32_t* chain_dur;  // [S] each source's chain of windows in 10-ns ticks (the next group's dispatch
-                        // weight; source-major), or null
 };
 constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
 constexpr uint32_t kErrDeliverCap = 4u;  // a local delivery's records exceed its buffers (TGSIM_DELIVER_SLACK)

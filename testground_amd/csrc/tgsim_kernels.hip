@@ -842,58 +842,37 @@ struct StatePair {
 };
 static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
 
-// What a source carries from one window to the next when both run in the same wavefront
-// (k_sim_fused runs each source's windows back to back: the queue stays in LDS, only these
-// wave-uniform scalars pass from one sim_source call to the next).
-struct SrcCarry {
-  uint32_t rh, rn, qn, pn, fn;
-  uint64_t tat;
-  uint32_t last_dup, last_cor, last_reo;
-};
-constexpr uint32_t kPhLoad = 1, kPhStore = 2;  // sim_source phases: queue from HBM / back to HBM
-
 // One source's step (K1-K4), run by one wavefront.  kOpen: the caller has checked that the step
 // is an open queue without correlated draws, so only the open path is compiled in (fewer
 // registers, a kCap-slot LDS queue).  wg: the slot of the stamps and the statistics copy.
-// ph & kPhLoad: the queue, ring and SrcState come from HBM; otherwise from *carry, with the queue
-// still in LDS from the source's previous window.  ph & kPhStore: they go back to HBM at the end;
-// otherwise into *carry.  *claim (when given) is the workgroup's next ticket, claimed before the
-// write-back so that the atomic's round trip overlaps the stores; returned minus claim_base.
-// kMode: 0 plain loads and stores (k_sim, k_sim_list); 1 the HBM state is handed off inside a
-// window-major fused launch (bounded sc1 loads and stores); 2 source-major fused (bounded loads).
-constexpr int kModePlain = 0, kModeHandoff = 1, kModeSourceMajor = 2;
+// The queue, ring and SrcState come from HBM and go back there at the end.  *claim (when given) is
+// the workgroup's next ticket, claimed before the write-back so that the atomic's round trip overlaps
+// the stores; returned minus claim_base.  kMode: 0 plain loads and stores (k_sim, k_sim_list); 1 the
+// HBM state is handed off inside a fused launch (bounded sc1 loads and stores).
+constexpr int kModePlain = 0, kModeHandoff = 1;
 template <bool kOpen, uint32_t kCap, int kMode = kModePlain, bool kRecv = false, bool kSlots = false>
 __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
-                                               uint32_t* claim = nullptr, uint32_t claim_base = 0,
-                                               SrcCarry* carry = nullptr, uint32_t ph = kPhLoad | kPhStore) {
+                                               uint32_t* claim = nullptr, uint32_t claim_base = 0) {
   const uint32_t lane = threadIdx.x;
   constexpr uint32_t kSlotMask = kCap - 1;
   stamp(a, wg, lane, 0, __builtin_amdgcn_s_memrealtime());
   const uint64_t t_begin = a.dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const SrcParams pp = a.params[s];
-  const bool load = (ph & kPhLoad) != 0;
   constexpr bool kH = kMode == kModeHandoff, kBounded = kMode != kModePlain;
   constexpr int kPol = kH ? kSc1 : 0;
   SrcState st;  // dead after the set-up: the end writes a fresh state
-  if (load) {
-    if constexpr (kH) {
-      const auto rs = region(a.state + s, sizeof(SrcState));
-      st = __builtin_bit_cast(SrcState, (StatePair{ld16<kSc1>(rs, 0), ld16<kSc1>(rs, 16)}));
-    } else {
-      st = a.state[s];
-    }
+  if constexpr (kH) {
+    const auto rs = region(a.state + s, sizeof(SrcState));
+    st = __builtin_bit_cast(SrcState, (StatePair{ld16<kSc1>(rs, 0), ld16<kSc1>(rs, 16)}));
   } else {
-    st.tat = carry->tat;
-    st.last_dup = carry->last_dup;
-    st.last_cor = carry->last_cor;
-    st.last_reo = carry->last_reo;
+    st = a.state[s];
   }
   SimQueue<kCap> Q{lds, pp, lane};
-  Q.rh = load ? 0 : carry->rh;
-  Q.rn = load ? st.ring_n : carry->rn;
-  Q.qn = load ? q_near(st) : carry->qn;
-  Q.pn = load ? st.heap_n - q_near(st) : carry->pn;  // on a load: the whole pool until it is split
-  Q.fn = load ? 0 : carry->fn;
+  Q.rh = 0;
+  Q.rn = st.ring_n;
+  Q.qn = q_near(st);
+  Q.pn = st.heap_n - q_near(st);  // the whole pool until it is split
+  Q.fn = 0;
   Q.H = a.horizon_ns;
   Q.tat = st.tat;
   Q.src = a.shard_begin + s;
@@ -909,7 +888,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   uint64_t* pf = Q.pf;
 #endif
   // ---- load the departure ring (compacted) and the sorted eligibility queue into LDS
-  if (load) {
+  {
     const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     const uint4* gh = a.heap + (size_t)s * kHeapCap;
     const uint32_t rn = Q.rn, qn = Q.qn + Q.pn;
@@ -960,38 +939,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     }
     Q.pn = cs;
     Q.fn = cf;
-  } else if (Q.fn) {
-    // the previous window's far pool holds every item with e >= its horizon; the ones below this
-    // window's horizon join the soon pool (placed right behind it, the rest behind them; neither
-    // part has an order): read all, then write, in one pass of registers
-    const uint32_t b = Q.rn + Q.qn + Q.pn, nf = Q.fn;
-    uint4 fv[kCap / kWave];
-#pragma unroll
-    for (uint32_t u = 0; u < kCap / kWave; ++u) {
-      const uint32_t k = u * kWave + lane;
-      fv[u] = k < nf ? Q.slot(b + k) : make_uint4(0, 0, 0, 0);
-    }
-    wave_lds_sync();
-    const uint64_t below = (1ull << lane) - 1;
-    uint32_t ns = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < kCap / kWave; ++u)
-      ns += ballot_count(u * kWave + lane < nf && (w0_of(fv[u]) & kEMask) < Q.H);
-    if (ns) {
-      uint32_t cs = 0, cf = 0;
-#pragma unroll
-      for (uint32_t u = 0; u < kCap / kWave; ++u) {
-        const uint32_t k = u * kWave + lane;
-        const bool in = k < nf, soon = in && (w0_of(fv[u]) & kEMask) < Q.H;
-        const uint64_t msn = __ballot(soon), mfr = __ballot(in && !soon);
-        if (soon) Q.slot(b + cs + (uint32_t)__popcll(msn & below)) = fv[u];
-        else if (in) Q.slot(b + ns + cf + (uint32_t)__popcll(mfr & below)) = fv[u];
-        cs += (uint32_t)__popcll(msn);
-        cf += (uint32_t)__popcll(mfr);
-      }
-      Q.pn += ns;
-      Q.fn -= ns;
-    }
   }
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const bool src_on = a.enabled[Q.src] != 0;
@@ -1010,7 +957,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   if (lane == 0 && (Q.qn | Q.pn | Q.fn | Q.rn)) {  // the queue state at the start (the end's is added there)
     const unsigned long long b0 = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
     atomicAdd(&sc[kStQueue], b0);  // the per-window model (bit-exact with the oracle)
-    if (!load) atomicAdd(&sc[kStCarrySkip], b0);  // still in LDS: not read from HBM
   }
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
@@ -1188,6 +1134,27 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
             const uint32_t nd = stop ? (uint32_t)__builtin_ctzll(stop) : kWave;
             // a lane keeps counting into this chunk only if every earlier entry was before its T
             const bool carry = D == base;
+#ifndef TGSIM_DEP64
+            // 32-bit times relative to the window start (the offer times of a window span less
+            // than 2^32 - 16 ns, checked): a departure before the window maps to 0, a far one
+            // saturates, so every comparison with an offer time keeps its outcome, at half the
+            // cross-lane traffic of the 64-bit search
+            if (T_max - a.t0_ns < 0xFFFFFFF0ull) {
+              const uint64_t dr = dep - a.t0_ns + 1;
+              const uint32_t dep32 = dep < a.t0_ns ? 0u : dr < 0xFFFFFFFFull ? (uint32_t)dr : 0xFFFFFFFFu;
+              const uint32_t T32 = (uint32_t)(T - a.t0_ns + 1);  // >= 1
+              if (nd > 16) {
+                const uint32_t pm = scan_max_u32(lane < nd ? dep32 : 0xFFFFFFFFu);
+                if (carry) D += count_le_sorted_u32(pm, T32 - 1);
+              } else {
+                bool alive = carry;
+                for (uint32_t l = 0; l < nd; ++l) {
+                  alive = alive && readlane32(dep32, l) < T32;
+                  D += alive ? 1u : 0u;
+                }
+              }
+            } else
+#endif
             if (nd > 16) {
               // prefix maxima of the chunk's first nd entries ascend: the lane's departures are
               // the entries before the first prefix maximum >= T (binary search over the lanes)
@@ -1401,7 +1368,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   uint32_t next_ticket = 0;
   if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
-  if (ph & kPhStore) {
+  {
     // ---- write back the compacted ring (16-B stores, two entries each), the queue (near, then
     // pool) and the state
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
@@ -1447,16 +1414,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
         a.state[s] = ns;
       }
     }
-  } else {
-    carry->rh = Q.rh;
-    carry->rn = Q.rn;
-    carry->qn = Q.qn;
-    carry->pn = Q.pn;
-    carry->fn = Q.fn;
-    carry->tat = Q.tat;
-    carry->last_dup = last_dup;
-    carry->last_cor = last_cor;
-    carry->last_reo = last_reo;
   }
   stamp(a, wg, lane, 4, __builtin_amdgcn_s_memrealtime());
   stamp(a, wg, lane, 5, ((uint64_t)s << 32) | n_batches);
@@ -1481,7 +1438,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     if (lost) atomicAdd(&sc[kStLost], (unsigned long long)lost);
     if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
-    if (qbytes && !(ph & kPhStore)) atomicAdd(&sc[kStCarrySkip], (unsigned long long)qbytes);
     if (err) {
       atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
       if (a.err_host)  // the host's pinned copy (sticky; read at its sync points)
@@ -1536,7 +1492,8 @@ __device__ __forceinline__ const SimArgs& kernarg_window(uint32_t k) {
 // is held by a resident workgroup and waits only for a lower ticket, so the lowest unfinished ticket
 // can always run: no deadlock; the wait is bounded anyway (kErrHandoff, then the host reports -EIO).
 // Tickets interleave the windows of all sources at a granularity of one source-window, which keeps
-// the launch's tail short (A/B against the source-major form below: DESIGN.md §5.2).
+// the launch's tail short (a source-major form, each source's windows back to back with its queue
+// resident in LDS, was bit-exact but slower: DESIGN.md §5.2).
 #ifndef TGSIM_FUSED_CAP
 #define TGSIM_FUSED_CAP kHeapCap
 #endif
@@ -1579,41 +1536,6 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f
     if (threadIdx.x == 0)
       __hip_atomic_store(f.done + s, f.step_base + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!f.persistent) break;  // one ticket per workgroup: the dispatcher interleaves other streams' work
-    t = next;
-  }
-}
-
-// SOURCE-MAJOR (TGSIM_FUSED_MAJOR=source): one wavefront runs all of a source's windows back to back
-// with the queue resident in LDS, loaded before the first window and stored after the last (one HBM
-// round trip of the queue per group, no hand-off), sources taken longest measured chain first.
-// Bit-exact with the window-major form, and 3 % less work, but its tail is coarse: a chain is a
-// whole group of windows, and chains mispredicted long start late.
-__global__ __launch_bounds__(kWave, 3) void k_sim_fused_sm(FusedSim fs, FusedArgs f) {
-  const SimArgs& a0 = fs.w[0];
-  __shared__ SimLdsT<kHeapCap> lds;
-  const uint32_t total = a0.n_src;
-  uint32_t t = 0;
-  if (threadIdx.x == 0) t = atomicAdd(f.ticket, 1u) - f.ticket_base;
-  t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-  while (t < total) {
-    const uint32_t s = a0.order ? a0.order[t] : t;
-    if (t < f.prio_n) __builtin_amdgcn_s_setprio(3);
-    else __builtin_amdgcn_s_setprio(0);
-    SrcCarry c;
-    uint32_t next = 0;
-    const uint64_t tc0 = f.chain_dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    for (uint32_t k = 0; k < f.n_win; ++k) {
-      const bool last = k + 1 == f.n_win;
-      const uint32_t ph = (k == 0 ? kPhLoad : 0u) | (last ? kPhStore : 0u);
-      next = sim_source<false, kHeapCap, kModeSourceMajor>(kernarg_window(k), s, k * total + t, lds,
-                                         last && f.persistent ? f.ticket : nullptr, f.ticket_base, &c, ph);
-    }
-    if (f.chain_dur && threadIdx.x == 0) {  // longest chains first in the next group (LPT)
-      const uint64_t d = __builtin_amdgcn_s_memrealtime() - tc0;
-      f.chain_dur[s] = d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
-    }
-    if (!f.persistent) break;
-    wave_lds_sync();  // the write-back's LDS reads are done before the next source's loads land
     t = next;
   }
 }
@@ -2329,8 +2251,52 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   }
 }
 
+// The active sources of a sparse step, one LANE per source: a source with nothing offered and nothing
+// eligible before the horizon keeps its state (the idle exit of sparse_source, counted the same way
+// here), the others are listed for k_sim_sparse, which then spends a wave only on them (most of the
+// million gossip peers are idle in most windows; a wave per idle peer had set a floor of ~0.25 ms
+// per window).  The list's order does not matter: every result is independent of it.
+__device__ __forceinline__ uint32_t* active_list(const SimArgs& a) { return a.worklist + 2 * a.n_src + 9; }
+
+__global__ __launch_bounds__(256) void k_sparse_active(SimArgs a) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63u;
+  bool act = false;
+  uint64_t qb = 0, skip = 0;
+  if (s < a.n_src) {
+    const SrcState st = a.state[s];
+    const uint32_t n = (uint32_t)(a.off[s + 1] - a.off[s]), qn = st.heap_n, rn = st.ring_n;
+    bool idle = !n;
+    if (idle && qn) {
+      idle = q_near(st) == qn &&
+             (w0_of(a.heap[(size_t)s * kHeapCap + q_head(st)]) & kEMask) >= a.horizon_ns;
+    }
+    if (idle) {
+      a.emit_n[s] = 0;
+      qb = 32ull * qn + 16ull * rn;
+      skip = (qn ? 32ull * qn - 16ull : 0ull) + 16ull * rn;
+    }
+    act = !idle;
+  }
+  const uint64_t m = __ballot(act);
+  uint32_t base = 0;
+  if (m) {
+    uint32_t* const list = active_list(a);
+    if (lane == 0) base = atomicAdd(list, (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (act) list[1 + base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = s;
+  }
+  qb = wave_sum(qb);
+  skip = wave_sum(skip);
+  if (lane == 0 && (qb | skip)) {
+    unsigned long long* const sc = a.stats + (size_t)((s / 64) % kStatCopies) * kStSlots;
+    if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
+    if (skip) atomicAdd(&sc[kStCarrySkip], (unsigned long long)skip);
+  }
+}
+
 __global__ __launch_bounds__(kWave, 7) void k_sim_sparse(SimArgs a) {
-  if (blockIdx.x < a.n_src) sparse_source(a, blockIdx.x);
+  const uint32_t* const list = active_list(a);
+  if (blockIdx.x < list[0]) sparse_source(a, list[1 + blockIdx.x]);
 }
 
 // The general path for the worklist k_sim_sparse left: a grid-stride loop over the list (its
@@ -3451,7 +3417,7 @@ void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
 }
 
 void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipStream_t st) {
-  const uint32_t total = f.source_major ? a.n_src : f.n_win * a.n_src;  // tickets
+  const uint32_t total = f.n_win * a.n_src;  // tickets
   FusedSim fs;
   for (uint32_t k = 0; k < kFuseMax; ++k) {
     fs.w[k] = a;
@@ -3467,8 +3433,7 @@ void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipSt
     fs.w[k].horizon_ns = w.horizon_ns;
   }
   const dim3 grid(f.persistent && n_wg < total ? n_wg : total);
-  if (f.source_major) hipLaunchKernelGGL(k_sim_fused_sm, grid, dim3(kWave), 0, st, fs, f);
-  else hipLaunchKernelGGL(k_sim_fused, grid, dim3(kWave), 0, st, fs, f);
+  hipLaunchKernelGGL(k_sim_fused, grid, dim3(kWave), 0, st, fs, f);
 }
 
 uint32_t sim_fused_resident() {
@@ -3482,6 +3447,7 @@ uint32_t sim_fused_resident() {
 
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
   if (!a.n_src) return;
+  hipLaunchKernelGGL(k_sparse_active, dim3((a.n_src + 255) / 256), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_sim_sparse, dim3(a.n_src), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 8192 ? a.n_src : 8192), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
