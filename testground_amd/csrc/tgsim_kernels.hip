@@ -1145,7 +1145,10 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
               const uint32_t T32 = (uint32_t)(T - a.t0_ns + 1);  // >= 1
               if (nd > 16) {
                 const uint32_t pm = scan_max_u32(lane < nd ? dep32 : 0xFFFFFFFFu);
-                if (carry) D += count_le_sorted_u32(pm, T32 - 1);
+                // every lane takes part in the search's cross-lane reads (a lane outside `carry` still
+                // provides its pm to the others), then only the carrying lanes add
+                const uint32_t lo = count_le_sorted_u32(pm, T32 - 1);
+                if (carry) D += lo;
               } else {
                 bool alive = carry;
                 for (uint32_t l = 0; l < nd; ++l) {
