@@ -856,10 +856,13 @@ int retire_gen(Eng* E, Eng::GenWindow&& w) {
 }
 
 // A free window for the next generation, its offsets' last readers awaited on the simulate stream.
+// The OLDEST retired window is taken: with three or more in rotation, its readers (the delivery
+// and routing of window k - 2) finished before window k's simulation started (which waited for them
+// through its emit pair), so the wait costs nothing where the delivery lags (the gossip flood's peak).
 int take_gen(Eng* E, Eng::GenWindow* w) {
   if (E->gen_free.empty()) return 0;
-  *w = std::move(E->gen_free.back());
-  E->gen_free.pop_back();
+  *w = std::move(E->gen_free.front());
+  E->gen_free.erase(E->gen_free.begin());
   if (w->rd_rt) HIPCHK(hipStreamWaitEvent(E->st, w->rd_rt, 0));
   if (w->rd_dst) HIPCHK(hipStreamWaitEvent(E->st, w->rd_dst, 0));
   return 0;
@@ -982,11 +985,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   }
   if (sparse) {
     // [0] the worklist's count, its sources, 8 words of TGSIM_DEFER_STATS, then k_sim_multi's list
-    // (count, sources), then k_sparse_active's list of the non-idle sources (count, sources)
-    HIPCHK(E->d_work.ensure(3 * static_cast<size_t>(E->S) + 1 + 8 + 1 + 1));
+    // (count, sources)
+    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 1 + 8 + 1));
     HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t), E->st));
     HIPCHK(hipMemsetAsync(E->d_work.p + 1 + E->S + 8, 0, sizeof(uint32_t), E->st));
-    HIPCHK(hipMemsetAsync(E->d_work.p + 1 + 2 * static_cast<size_t>(E->S) + 9, 0, sizeof(uint32_t), E->st));
     a.worklist_n = E->d_work.p;
     a.worklist = E->d_work.p + 1;
     a.order = nullptr;  // (stamps, when on, are indexed by source: n_wg = S)
@@ -1995,7 +1997,7 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   // out-neighbour (the 1M-peer flood's peak windows offer ~30 packets per peer), so no window of the
   // flood reallocates (each hipFree + hipMalloc stalls the closed loop for 0.3-0.5 ms)
   const size_t reserve = static_cast<size_t>(E->S) * g->degree * 4;  // the flood's peak: ~30 per peer
-  while (E->gen_free.size() < 2) E->gen_free.emplace_back();
+  while (E->gen_free.size() < 3) E->gen_free.emplace_back();  // three in rotation (take_gen)
   for (auto& w : E->gen_free) {
     HIPCHK(w.off.ensure(E->S + 1));
     HIPCHK(w.in.ensure(reserve));

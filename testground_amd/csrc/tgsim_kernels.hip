@@ -1134,30 +1134,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
             const uint32_t nd = stop ? (uint32_t)__builtin_ctzll(stop) : kWave;
             // a lane keeps counting into this chunk only if every earlier entry was before its T
             const bool carry = D == base;
-#ifndef TGSIM_DEP64
-            // 32-bit times relative to the window start (the offer times of a window span less
-            // than 2^32 - 16 ns, checked): a departure before the window maps to 0, a far one
-            // saturates, so every comparison with an offer time keeps its outcome, at half the
-            // cross-lane traffic of the 64-bit search
-            if (T_max - a.t0_ns < 0xFFFFFFF0ull) {
-              const uint64_t dr = dep - a.t0_ns + 1;
-              const uint32_t dep32 = dep < a.t0_ns ? 0u : dr < 0xFFFFFFFFull ? (uint32_t)dr : 0xFFFFFFFFu;
-              const uint32_t T32 = (uint32_t)(T - a.t0_ns + 1);  // >= 1
-              if (nd > 16) {
-                const uint32_t pm = scan_max_u32(lane < nd ? dep32 : 0xFFFFFFFFu);
-                // every lane takes part in the search's cross-lane reads (a lane outside `carry` still
-                // provides its pm to the others), then only the carrying lanes add
-                const uint32_t lo = count_le_sorted_u32(pm, T32 - 1);
-                if (carry) D += lo;
-              } else {
-                bool alive = carry;
-                for (uint32_t l = 0; l < nd; ++l) {
-                  alive = alive && readlane32(dep32, l) < T32;
-                  D += alive ? 1u : 0u;
-                }
-              }
-            } else
-#endif
             if (nd > 16) {
               // prefix maxima of the chunk's first nd entries ascend: the lane's departures are
               // the entries before the first prefix maximum >= T (binary search over the lanes)
@@ -2254,52 +2230,11 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   }
 }
 
-// The active sources of a sparse step, one LANE per source: a source with nothing offered and nothing
-// eligible before the horizon keeps its state (the idle exit of sparse_source, counted the same way
-// here), the others are listed for k_sim_sparse, which then spends a wave only on them (most of the
-// million gossip peers are idle in most windows; a wave per idle peer had set a floor of ~0.25 ms
-// per window).  The list's order does not matter: every result is independent of it.
-__device__ __forceinline__ uint32_t* active_list(const SimArgs& a) { return a.worklist + 2 * a.n_src + 9; }
-
-__global__ __launch_bounds__(256) void k_sparse_active(SimArgs a) {
-  const uint32_t s = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63u;
-  bool act = false;
-  uint64_t qb = 0, skip = 0;
-  if (s < a.n_src) {
-    const SrcState st = a.state[s];
-    const uint32_t n = (uint32_t)(a.off[s + 1] - a.off[s]), qn = st.heap_n, rn = st.ring_n;
-    bool idle = !n;
-    if (idle && qn) {
-      idle = q_near(st) == qn &&
-             (w0_of(a.heap[(size_t)s * kHeapCap + q_head(st)]) & kEMask) >= a.horizon_ns;
-    }
-    if (idle) {
-      a.emit_n[s] = 0;
-      qb = 32ull * qn + 16ull * rn;
-      skip = (qn ? 32ull * qn - 16ull : 0ull) + 16ull * rn;
-    }
-    act = !idle;
-  }
-  const uint64_t m = __ballot(act);
-  uint32_t base = 0;
-  if (m) {
-    uint32_t* const list = active_list(a);
-    if (lane == 0) base = atomicAdd(list, (uint32_t)__popcll(m));
-    base = __shfl(base, 0, 64);
-    if (act) list[1 + base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = s;
-  }
-  qb = wave_sum(qb);
-  skip = wave_sum(skip);
-  if (lane == 0 && (qb | skip)) {
-    unsigned long long* const sc = a.stats + (size_t)((s / 64) % kStatCopies) * kStSlots;
-    if (qb) atomicAdd(&sc[kStQueue], (unsigned long long)qb);
-    if (skip) atomicAdd(&sc[kStCarrySkip], (unsigned long long)skip);
-  }
-}
-
+// (A one-lane-per-source pass listing the active sources, so that idle peers cost no wave, was
+// measured and dropped: 4.17-4.21 against 4.40-4.41 G pkt/s at 1M peers -- an idle wave exits after
+// its first loads, cheaper than the pass over a million sources.)
 __global__ __launch_bounds__(kWave, 7) void k_sim_sparse(SimArgs a) {
-  const uint32_t* const list = active_list(a);
-  if (blockIdx.x < list[0]) sparse_source(a, list[1 + blockIdx.x]);
+  if (blockIdx.x < a.n_src) sparse_source(a, blockIdx.x);
 }
 
 // The general path for the worklist k_sim_sparse left: a grid-stride loop over the list (its
@@ -3450,7 +3385,6 @@ uint32_t sim_fused_resident() {
 
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
   if (!a.n_src) return;
-  hipLaunchKernelGGL(k_sparse_active, dim3((a.n_src + 255) / 256), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_sim_sparse, dim3(a.n_src), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 8192 ? a.n_src : 8192), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
