@@ -966,7 +966,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
       fprintf(stderr, "tgsim: sparse step deferred %u of %u sources", deferred, E->S);
 #ifdef TGSIM_DEFER_STATS  // by reason (corr, limit, n>64, queue, ring, fifo-due, sorted-queue, rest), cumulative
       uint32_t why[8] = {};
-      if (E->d_work.p && hipMemcpy(why, E->d_work.p + 1 + E->S, sizeof why, hipMemcpyDeviceToHost) == hipSuccess)
+      if (E->d_work.p && hipMemcpy(why, E->d_work.p + 2 + E->S, sizeof why, hipMemcpyDeviceToHost) == hipSuccess)
         for (uint32_t w : why) fprintf(stderr, " %u", w);
 #endif
       fprintf(stderr, "\n");
@@ -984,13 +984,12 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     a.emit_slot = E->d_eslot.p;
   }
   if (sparse) {
-    // [0] the worklist's count, its sources, 8 words of TGSIM_DEFER_STATS, then k_sim_multi's list
-    // (count, sources)
-    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 1 + 8 + 1));
-    HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t), E->st));
-    HIPCHK(hipMemsetAsync(E->d_work.p + 1 + E->S + 8, 0, sizeof(uint32_t), E->st));
+    // [0] the worklist's count, [1] k_sim_multi's, the worklist's sources, 8 words of
+    // TGSIM_DEFER_STATS, then k_sim_multi's sources
+    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 2 + 8));
+    HIPCHK(hipMemsetAsync(E->d_work.p, 0, 2 * sizeof(uint32_t), E->st));
     a.worklist_n = E->d_work.p;
-    a.worklist = E->d_work.p + 1;
+    a.worklist = E->d_work.p + 2;
     a.order = nullptr;  // (stamps, when on, are indexed by source: n_wg = S)
   }
   hipEvent_t ev0, ev1;

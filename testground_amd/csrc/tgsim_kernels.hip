@@ -1788,16 +1788,17 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s,
   }
 }
 
-// The multi-round list k_sim_sparse wrote behind its worklist's statistics words: [n_src + 8] the
-// count, then the sources.
+// The multi-round list k_sim_sparse writes: its count is the word after the worklist's count (one
+// memset clears both), its sources follow the worklist's statistics words.
+__device__ __forceinline__ uint32_t* multi_count(const SimArgs& a) { return a.worklist_n + 1; }
 __device__ __forceinline__ uint32_t* multi_list(const SimArgs& a) { return a.worklist + a.n_src + 8; }
 
 __global__ __launch_bounds__(kWave) void k_sim_multi(SimArgs a) {
   __shared__ MultiLds L;
-  uint32_t* const list = multi_list(a);
-  const uint32_t n = list[0];
+  const uint32_t* const list = multi_list(a);
+  const uint32_t n = *multi_count(a);
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    multi_source(a, list[1 + i], L);
+    multi_source(a, list[i], L);
     wave_lds_sync();  // this source's LDS reads are done before the next one's writes
   }
 }
@@ -1837,8 +1838,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   // FIFO candidates beyond one round of lanes go to k_sim_multi (multi-round, candidates in LDS)
   auto defer_multi = [&]() {
     if (lane == 0) {
-      uint32_t* const l2 = multi_list(a);
-      l2[1 + atomicAdd(l2, 1u)] = s;
+      multi_list(a)[atomicAdd(multi_count(a), 1u)] = s;
     }
   };
   unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
@@ -3386,7 +3386,7 @@ uint32_t sim_fused_resident() {
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
   if (!a.n_src) return;
   hipLaunchKernelGGL(k_sim_sparse, dim3(a.n_src), dim3(kWave), 0, st, a);
-  hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 8192 ? a.n_src : 8192), dim3(kWave), 0, st, a);
+  hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 2048 ? a.n_src : 2048), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
 }
 
