@@ -288,12 +288,11 @@ struct tgsim_engine_s {
     bool pending = false;
     uint64_t pub_seq = 0;
     GossipArgs g{};
-    // the last readers of `off` once the window went back to the free list: the routing and the
-    // delivery enqueued before (a generation reusing the buffer waits for these, not for every
-    // routing and delivery since)
-    hipEvent_t rd_rt = nullptr, rd_dst = nullptr;
+    // the simulate call (run_sim / step_n) that sent the window back to the free list; 0: never used
+    uint64_t retired_call = 0;
   };
   std::vector<GenWindow> gen_q;   // device-generated traffic, one window per future step
+  uint64_t sim_calls = 0;         // run_sim and fused-group calls so far (GenWindow::retired_call)
   std::vector<GenWindow> gen_free;
   uint64_t gen_q_ticks = 0;
   uint64_t n_in = 0;
@@ -844,27 +843,30 @@ int resolve_gen(Eng* E, Eng::GenWindow& w) {
   return 0;
 }
 
-// A window's buffers back to the free list: the readers of its offsets enqueued so far (a routing on
-// rt_st, a delivery on dst_st) are what its next generation waits for.
-int retire_gen(Eng* E, Eng::GenWindow&& w) {
-  if (!w.rd_rt) HIPCHK(hipEventCreateWithFlags(&w.rd_rt, hipEventDisableTiming));
-  if (!w.rd_dst) HIPCHK(hipEventCreateWithFlags(&w.rd_dst, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(w.rd_rt, E->rt_st));
-  HIPCHK(hipEventRecord(w.rd_dst, E->dst_st));
+// A window's buffers back to the free list, stamped with the simulate call that retired them (a
+// fused group's: always-wait, since its group delivery is awaited only by the group two later).
+constexpr uint64_t kRetiredByGroup = ~0ull >> 2;
+int retire_gen(Eng* E, Eng::GenWindow&& w, bool by_group = false) {
+  w.retired_call = by_group ? kRetiredByGroup : E->sim_calls;
   E->gen_free.push_back(std::move(w));
   return 0;
 }
 
-// A free window for the next generation, its offsets' last readers awaited on the simulate stream.
-// The OLDEST retired window is taken: with three or more in rotation, its readers (the delivery
-// and routing of window k - 2) finished before window k's simulation started (which waited for them
-// through its emit pair), so the wait costs nothing where the delivery lags (the gossip flood's peak).
+// A free window for the next generation (the OLDEST retired one).  Its offsets were last read by the
+// delivery and routing of the window they belonged to; those are waited for by the simulation of
+// the window two later (through its emit pair or fused buffer set), which the simulate stream runs
+// before this generation once two more simulate calls were made.  Otherwise (a short rotation) the
+// generation waits for the latest delivery and routing.  With the gossip driver's three windows in
+// rotation that never happens, so the generation never waits for a lagging delivery (an event per
+// window instead cost ~20 us of host time per step).
 int take_gen(Eng* E, Eng::GenWindow* w) {
   if (E->gen_free.empty()) return 0;
   *w = std::move(E->gen_free.front());
   E->gen_free.erase(E->gen_free.begin());
-  if (w->rd_rt) HIPCHK(hipStreamWaitEvent(E->st, w->rd_rt, 0));
-  if (w->rd_dst) HIPCHK(hipStreamWaitEvent(E->st, w->rd_dst, 0));
+  if (w->retired_call && E->sim_calls < w->retired_call + 2) {
+    HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));
+    HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));
+  }
   return 0;
 }
 
@@ -879,6 +881,7 @@ void drop_gen(Eng* E) {
 int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   int erc = check_sim_error(E);
   if (erc) return erc;
+  E->sim_calls++;
   erc = harvest_timing(E, false);
   if (erc) return erc;
   if (!E->gen_q.empty()) {
@@ -1370,6 +1373,7 @@ struct GroupRoute {  // a sharded group: the windows' records routed into slotte
 int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = nullptr) {
   int rc = check_sim_error(E);
   if (rc) return rc;
+  E->sim_calls++;
   rc = harvest_timing(E, false);
   if (rc) return rc;
   rc = flush_config(E);  // effective from the first window, as for g tgsim_step calls
@@ -1568,7 +1572,7 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   E->n_in = win[g - 1].n;
   E->n_verdict = E->n_in;
   for (uint32_t i = 0; i < g; ++i) {
-    rc = retire_gen(E, std::move(win[i]));
+    rc = retire_gen(E, std::move(win[i]), true);
     if (rc) return rc;
   }
   E->perm.clear();
@@ -1836,8 +1840,6 @@ void tgsim_destroy(void* e) {
     for (auto& w : *q) {
       w.off.release();
       w.in.release();
-      if (w.rd_rt) (void)hipEventDestroy(w.rd_rt);
-      if (w.rd_dst) (void)hipEventDestroy(w.rd_dst);
     }
   for (auto& pr : E->ev_pending) {
     (void)hipEventDestroy(pr.first);
