@@ -311,9 +311,6 @@ struct tgsim_engine_s {
   // delivery of window k - 2 (a third set, so that a delivery could lag two windows at the gossip
   // flood's peak, was tried: at 1M peers a set is ~38 GB and the third one thrashed)
   DevBuf<tgsim_delivery> d_emit, d_emit_alt;
-  DevBuf<uint32_t> d_eslot, d_eslot_alt;  // records' slots in their destinations' segments (emit_slot)
-  bool eslot_on = false;                  // the last k_sim wrote d_eslot (heavy sparse windows)
-  uint64_t slot_min = 16;                 // TGSIM_SLOT_MIN: offered packets per source from which it is on
   uint32_t wide_windows = 0;              // windows after a mid-run reshape whose bounded local delivery
                                           // reserves the full netem limit per source (deliver_local_from)
   uint64_t deliver_slack = 128;           // TGSIM_DELIVER_SLACK: queued items per source a bounded local
@@ -813,7 +810,6 @@ SimArgs base_sim_args(Eng* E) {
 void rotate_emit(Eng* E) {
   std::swap(E->d_emit, E->d_emit_alt);
   std::swap(E->d_emit_n, E->d_emit_n_alt);
-  std::swap(E->d_eslot, E->d_eslot_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
   std::swap(E->ev_local, E->ev_local_alt);
 }
@@ -978,14 +974,6 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     if (sparse) E->dense_streak = 0;
   }
   a.worklist = a.worklist_n = nullptr;
-  // heavy sparse windows with a local delivery (the gossip flood's peak): the count atomics return
-  // each record's slot, so the scatter needs no atomics of its own
-  E->eslot_on = sparse && local_hist && E->n_in >= E->slot_min * E->S;
-  a.emit_slot = nullptr;
-  if (E->eslot_on) {
-    HIPCHK(E->d_eslot.ensure(emit_cap));
-    a.emit_slot = E->d_eslot.p;
-  }
   if (sparse) {
     // [0] the worklist's count, [1] k_sim_multi's, the worklist's sources, 8 words of
     // TGSIM_DEFER_STATS, then k_sim_multi's sources
@@ -1276,7 +1264,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
 // The local delivery of one window on the delivery stream (after its k_sim): scan of the
 // per-destination histogram -> scatter straight from the emit regions -> per-destination order.
 int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uint64_t* lcnt,
-                       const uint64_t* off, uint64_t n_in, const uint32_t* eslot = nullptr) {
+                       const uint64_t* off, uint64_t n_in) {
   const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
   HIPCHK(E->d_doff.ensure(nd + 1));
@@ -1307,7 +1295,7 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uin
     launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
-  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in, eslot, E->d_doff.p);
+  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in);
   HIPCHK(hipGetLastError());
   if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
   tgsim_delivery* dst = nullptr;
@@ -1340,8 +1328,7 @@ int deliver_local(Eng* E) {
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
   }
 
-  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in,
-                              E->eslot_on ? E->d_eslot.p : nullptr);
+  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in);
   if (rc) return rc;
   HIPCHK(hipEventRecord(E->ev_local, sq));
   HIPCHK(hipEventRecord(E->ev_dst, sq));
@@ -1730,7 +1717,6 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (const char* dd = getenv("TGSIM_DENSE_DIV")) E->dense_div = static_cast<uint32_t>(std::max(1, atoi(dd)));
   E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
   if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
-  if (const char* sm = getenv("TGSIM_SLOT_MIN")) E->slot_min = strtoull(sm, nullptr, 10);
   if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) {
     E->deliver_slack = strtoull(ds, nullptr, 10);
     E->slack_forced = true;
@@ -1831,7 +1817,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_eslot.release(); E->d_eslot_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
@@ -2005,11 +1991,9 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   }
   HIPCHK(E->d_in.ensure(reserve));
   HIPCHK(E->d_verdict.ensure(reserve));
-  // the emit regions of both parities and the record slots of the flood's heavy windows, for the
-  // same reserve (a hipFree + hipMalloc of several GB inside the flood stalls the loop)
+  // the emit regions of both parities, for the same reserve (a hipFree + hipMalloc of several GB inside the flood stalls the loop)
   const uint64_t emit_cap = 2 * reserve + static_cast<uint64_t>(kHeapCap) * E->S;
   for (auto* b : {&E->d_emit, &E->d_emit_alt}) HIPCHK(b->ensure(emit_cap));
-  for (auto* b : {&E->d_eslot, &E->d_eslot_alt}) HIPCHK(b->ensure(emit_cap));
   E->gossip_on = true;
   return 0;
 }

@@ -126,12 +126,10 @@ struct SimArgs {
   uint64_t* g_pend;         // [s] received, not yet forwarded
   const uint64_t* g_fwd;    // [s] forwarded (stable during the step: written by k_gossip_write before it)
   uint32_t g_floods, g_degree;
-  // with dst_cnt: each record's slot inside its destination's segment, the value its count atomic
-  // returned (parallel to emit), so the local scatter needs no atomics of its own; or null
-  uint32_t* emit_slot;
-  uint64_t pad_;  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the
-                  // scheduler spilled 9 more SGPRs in k_sim_fused (155 -> 164)
+  uint64_t pad_[2];  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the
+                     // scheduler spilled 9 more SGPRs in k_sim_fused (155 -> 164)
 };
+static_assert(sizeof(SimArgs) == 264, "SimArgs must stay 264 B");
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 
 // Fused launch of up to kFuseMax consecutive windows (k_sim_fused).  Window-major:

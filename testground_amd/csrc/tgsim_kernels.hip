@@ -335,7 +335,6 @@ struct SimQueue {
   uint64_t tat;             // HTB theoretical arrival time
   tgsim_delivery* emit;
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
-  uint32_t* eslot;           // with dcnt: the records' slots in their destinations' segments, or null
   RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
@@ -412,12 +411,7 @@ struct SimQueue {
         rw[0] = d;
         rw[1] = ((uint64_t)qi.w << 32) | src;
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
-        if (dcnt) {
-          if (eslot)
-            eslot[n_emit + __popcll(lm & ((1ull << lane) - 1))] = (uint32_t)atomicAdd(&dcnt[qi.w], 1ull);
-          else
-            atomicAdd(&dcnt[qi.w], 1ull);
-        }
+        if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
         if (rf.first && qi.w - rf.shard_begin < rf.n_local)
           fold_receipt(rf, qi.w, qi.z, flags, d, rf.fwd[qi.w - rf.shard_begin]);
         sched++;
@@ -850,7 +844,7 @@ static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
 // the stores; returned minus claim_base.  kMode: 0 plain loads and stores (k_sim, k_sim_list); 1 the
 // HBM state is handed off inside a fused launch (bounded sc1 loads and stores).
 constexpr int kModePlain = 0, kModeHandoff = 1;
-template <bool kOpen, uint32_t kCap, int kMode = kModePlain, bool kRecv = false, bool kSlots = false>
+template <bool kOpen, uint32_t kCap, int kMode = kModePlain, bool kRecv = false, bool kList = false>
 __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
                                                uint32_t* claim = nullptr, uint32_t claim_base = 0) {
   const uint32_t lane = threadIdx.x;
@@ -879,7 +873,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
-  Q.eslot = kSlots && a.emit_slot ? a.emit_slot + 2 * a.off[s] + (uint64_t)kHeapCap * s : nullptr;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
@@ -1364,7 +1357,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
       for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
     }
     uint32_t near_out = Q.qn;
-    if constexpr (kSlots) {
+    if constexpr (kList) {
       // k_sim_list: a queue whose pool happens to follow its near region in order (FIFO sources: no
       // jitter, reordering or duplication) is stored as one sorted region, so that the next step's
       // k_sim_sparse serves it in place instead of deferring it again
@@ -1725,12 +1718,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s,
       rw[0] = d;
       rw[1] = ((uint64_t)x.w << 32) | src;
       rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-      if (a.dst_cnt) {
-        if (a.emit_slot)
-          a.emit_slot[2 * sbeg + (uint64_t)kHeapCap * s + i] = (uint32_t)atomicAdd(&a.dst_cnt[x.w], 1ull);
-        else
-          atomicAdd(&a.dst_cnt[x.w], 1ull);
-      }
+      if (a.dst_cnt) atomicAdd(&a.dst_cnt[x.w], 1ull);
       if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
       bytes += xlen;
     }
@@ -2147,12 +2135,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
       rw[0] = d;
       rw[1] = ((uint64_t)x.w << 32) | src;
       rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-      if (a.dst_cnt) {
-        if (a.emit_slot)
-          a.emit_slot[2 * sbeg + (uint64_t)kHeapCap * s + i] = (uint32_t)atomicAdd(&a.dst_cnt[x.w], 1ull);
-        else
-          atomicAdd(&a.dst_cnt[x.w], 1ull);
-      }
+      if (a.dst_cnt) atomicAdd(&a.dst_cnt[x.w], 1ull);
       if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
       bytes += xlen;
     }
@@ -3199,41 +3182,6 @@ __global__ __launch_bounds__(256) void k_deliver_guard(const uint64_t* total, ui
   for (uint32_t i = i0; i < n_dst; i += st) cnt[i] = 0;
 }
 
-// The same with the slots k_sim took from its per-destination count atomics: every record's place is
-// its destination's segment start plus its slot, so no atomic is needed here (each would be a
-// memory-side request of its own: at the flood's peak, tens of millions per window).
-__global__ __launch_bounds__(256) void k_local_scatter_slot(const tgsim_delivery* __restrict__ emit,
-                                                            const uint32_t* __restrict__ emit_slot,
-                                                            const uint32_t* __restrict__ emit_n,
-                                                            const uint64_t* __restrict__ off, uint32_t n_src,
-                                                            uint32_t dst_begin, const uint64_t* __restrict__ seg,
-                                                            tgsim_delivery* __restrict__ out) {
-  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-  uint32_t n = 0;
-  uint64_t b = 0;
-  if (s < n_src) {
-    n = emit_n[s];
-    b = 2 * off[s] + (uint64_t)kHeapCap * s;
-  }
-  for (uint32_t i = 0; __ballot(i < n); i += 4) {
-    tgsim_delivery r[4];
-    uint32_t sl[4];
-#pragma unroll
-    for (uint32_t u = 0; u < 4; ++u)
-      if (i + u < n) {
-        r[u] = emit[b + i + u];
-        sl[u] = emit_slot[b + i + u];
-      }
-    uint64_t at[4];
-#pragma unroll
-    for (uint32_t u = 0; u < 4; ++u)
-      if (i + u < n) at[u] = seg[r[u].dst - dst_begin] + sl[u];
-#pragma unroll
-    for (uint32_t u = 0; u < 4; ++u)
-      if (i + u < n) out[at[u]] = r[u];
-  }
-}
-
 // Ranks inside lane groups of G records (one destination each) with the keys in LDS: each lane
 // reads its group's keys as one 16-B word each, (t, src << 32 | seq), instead of five cross-lane
 // shuffles per key (k_dst_sort_group); only a packet and its duplicate share that key, and the
@@ -3594,14 +3542,8 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
 }
 
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
-                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint,
-                          const uint32_t* emit_slot, const uint64_t* seg) {
+                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
   if (!n_src) return;
-  if (emit_slot) {  // slots from k_sim's count atomics: segment start + slot
-    hipLaunchKernelGGL(k_local_scatter_slot, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_slot, emit_n, off,
-                       n_src, dst_begin, seg, out);
-    return;
-  }
   if (n_hint <= 64ull * n_src) {  // up to tens of records per source (gossip, even at the flood's peak): one lane each
     hipLaunchKernelGGL(k_local_scatter_ls, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
                        dst_begin, pos, out);

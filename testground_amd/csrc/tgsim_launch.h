@@ -90,7 +90,7 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
                           uint32_t n_dst, uint64_t* err_host, hipStream_t st);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
-                          uint64_t n_hint, const uint32_t* emit_slot = nullptr, const uint64_t* seg = nullptr);
+                          uint64_t n_hint);
 // Orders each destination's records; resets cnt[] to zero for the next histogram.
 // (in, the scatter buffer, is overwritten for segments longer than 64.)
 // n_hint: about how many records (picks one wavefront per destination or eight).
