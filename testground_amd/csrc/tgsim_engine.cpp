@@ -225,7 +225,7 @@ struct tgsim_engine_s {
   uint64_t* h_err = nullptr;    // pinned host word k_sim stores the sticky error bits into
   uint64_t* d_err_host = nullptr;  // its device address
   uint32_t* h_xerr = nullptr;   // pinned sticky flag: a slotted exchange chunk overflowed (k_route_edges)
-  uint32_t* h_work = nullptr;   // pinned: sources the last sparse step deferred to k_sim_list
+  uint32_t* h_work = nullptr;   // pinned: sources the last sparse step deferred to k_sim_list, to k_sim_multi
   uint32_t* d_xerr = nullptr;   // its device address
   // launched, unfinished routed steps (tgsim_step_sim_launch), oldest at route_head: pinned
   // per-rank record edges behind an event, per slot
@@ -962,7 +962,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     // 64th such step runs sparse again to re-measure
     const uint32_t deferred = __atomic_load_n(E->h_work, __ATOMIC_RELAXED);
     if (E->trace_list) {
-      fprintf(stderr, "tgsim: sparse step deferred %u of %u sources", deferred, E->S);
+      fprintf(stderr, "tgsim: sparse step deferred %u of %u sources (multi-round %u)", deferred, E->S,
+              __atomic_load_n(E->h_work + 1, __ATOMIC_RELAXED));
 #ifdef TGSIM_DEFER_STATS  // by reason (corr, limit, n>64, queue, ring, fifo-due, sorted-queue, rest), cumulative
       uint32_t why[8] = {};
       if (E->d_work.p && hipMemcpy(why, E->d_work.p + 2 + E->S, sizeof why, hipMemcpyDeviceToHost) == hipSuccess)
@@ -995,7 +996,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev1, E->st));
   if (sparse) {
-    HIPCHK(hipMemcpyAsync(E->h_work, E->d_work.p, sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
+    HIPCHK(hipMemcpyAsync(E->h_work, E->d_work.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
     E->sparse_seen = true;
   }
   E->ev_pending.push_back({ev0, ev1, 1u});
@@ -1685,10 +1686,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
                                  hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
     return bail(rc);
   *E->h_xerr = 0;
-  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_work), sizeof(uint32_t),
+  if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_work), 2 * sizeof(uint32_t),
                                  hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
     return bail(rc);
-  *E->h_work = 0;
+  E->h_work[0] = E->h_work[1] = 0;
   if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_xerr), E->h_xerr, 0), "pinned")))
     return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_gerr), sizeof(uint32_t)), "pinned"))) return bail(rc);

@@ -1520,16 +1520,14 @@ constexpr uint32_t kFifoRounds = 4;  // FIFO sources: items served per step, in 
 // offered packets, or more than kFifoRounds x 64 items to serve (the gossip flood's peak).  The same
 // FIFO path as sparse_source (the stored queue is one sorted region, the new items extend it in
 // order, so HTB serves the prefix below the horizon in that order and the rest stays in place), with
-// the candidates staged in LDS in offer order: any number of rounds of 64 offered packets and of
-// served items run in one wave, at a register-only cost per round.  A source that turns out not to
-// be FIFO (a clone that is queued, a new item before its predecessor) goes on to the general
-// worklist (k_sim_list).  One wave per source, a grid-stride loop over the list k_sim_sparse wrote.
-constexpr uint32_t kMultiCand = 1024;
-struct MultiLds {
-  uint4 c[kMultiCand];  // the candidates, in offer order (their due ones are a prefix)
-};
-
-__device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s, MultiLds& L) {
+// the candidates written straight behind the queue's tail in offer order: any number of rounds of 64
+// offered packets and of served items run in one wave, at a register-only cost per round, and no
+// LDS (the wave count per SIMD is set by the registers).  The served prefix (the queue's due items,
+// then the due candidates) leaves by moving the head slot.  A source that turns out not to be FIFO
+// (a clone that is queued, a new item before its predecessor) goes on to the general worklist
+// (k_sim_list), which reads only the stored queue: the slots behind its tail are free space.  One wave
+// per source, a grid-stride loop over the list k_sim_sparse wrote.
+__device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s) {
   const uint32_t lane = threadIdx.x;
   const uint64_t below = (1ull << lane) - 1;
   const uint4* gh = a.heap + (size_t)s * kHeapCap;
@@ -1543,11 +1541,13 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s,
     if (lane == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
   };
   // (k_sim_sparse checked the rest: no correlated draws, below the netem limit even if every offered
-  // packet and a clone were queued, at most 256 ring entries, one sorted queue region)
-  if (n > kMultiCand) {
+  // packet and a clone were queued -- so the candidates fit behind the tail, qn + n < kHeapCap --, at
+  // most 256 ring entries, one sorted queue region)
+  if (qn + n >= kHeapCap) {
     defer();
     return;
   }
+  uint4* const wq = a.heap + (size_t)s * kHeapCap;
   unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
   const uint32_t src = a.shard_begin + s;
   const uint32_t qh = q_head(st);
@@ -1616,7 +1616,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s,
                             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.z), 0u);
     if (!bc) prev = last;
     if (__ballot(cand && (bc || has_last) && item_lt(io, prev))) fifo = false;
-    if (cand) L.c[nc + (uint32_t)__popcll(bc)] = io;
+    if (cand) wq[(qh + qn + nc + (uint32_t)__popcll(bc)) & (kHeapCap - 1)] = io;
     n_due += (uint32_t)__popcll(__ballot(cand && (w0_of(io) & kEMask) < h));
     if (mc) {
       const uint32_t ll = 63u - (uint32_t)__builtin_clzll(mc);
@@ -1638,7 +1638,9 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s,
     defer();
     return;
   }
-  wave_lds_sync();
+  // the candidates' stores complete before the serving rounds read the due ones back (other lanes'
+  // stores: the wave's own L1, so a workgroup-scope fence)
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   // ---- the queue's prefix below the horizon: all of it when a candidate is due (every queued item
   // precedes it), else its chunks from the head while they are due entirely
   uint32_t nq = n_due ? qn : 0;
@@ -1676,15 +1678,13 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s,
     if (k < rn && k >= k0) wr[k - k0] = rg[u];
   }
   const uint32_t old_kept = rn - k0;
-  // ---- in place: the candidates not served go behind the tail; the served prefix leaves by moving
-  // the head slot
-  uint4* wq = a.heap + (size_t)s * kHeapCap;
-  for (uint32_t c = n_due + lane; c < nc; c += kWave) wq[(qh + qn + c - n_due) & (kHeapCap - 1)] = L.c[c];
-  const uint32_t new_head = (qh + nq) & (kHeapCap - 1);
+  // ---- in place: the served prefix (a due candidate means the whole queue is due) leaves by moving
+  // the head slot; the candidates not served are already behind the tail
+  const uint32_t new_head = (qh + nq + n_due) & (kHeapCap - 1);
   const uint32_t wpos = qn - nq + nc - n_due;
   const uint32_t ns_all = nq + n_due;
   // ---- HTB, records, receipts and the ring, for the served items in rounds of 64 lanes: the
-  // queue's due items from HBM, then the due candidates from LDS
+  // queue's due items, then the due candidates, contiguous from the head slot
   uint64_t tat_c = st.tat;
   uint32_t emitted = 0, sk0 = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
@@ -1694,7 +1694,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s,
     const uint32_t k = base + lane;
     const uint32_t ns = ns_all - base < kWave ? ns_all - base : kWave;
     const bool hs = lane < ns;
-    const uint4 x = k < nq ? gh[(qh + k) & (kHeapCap - 1)] : hs ? L.c[k - nq] : make_uint4(0, 0, 0, 0);
+    const uint4 x = hs ? gh[(qh + k) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
     const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
     const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
                             ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
@@ -1782,13 +1782,9 @@ __device__ __forceinline__ uint32_t* multi_count(const SimArgs& a) { return a.wo
 __device__ __forceinline__ uint32_t* multi_list(const SimArgs& a) { return a.worklist + a.n_src + 8; }
 
 __global__ __launch_bounds__(kWave) void k_sim_multi(SimArgs a) {
-  __shared__ MultiLds L;
   const uint32_t* const list = multi_list(a);
   const uint32_t n = *multi_count(a);
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    multi_source(a, list[i], L);
-    wave_lds_sync();  // this source's LDS reads are done before the next one's writes
-  }
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) multi_source(a, list[i]);
 }
 
 // Register-only form of an open-queue step (the sparse senders of a gossip flood): no LDS queue.
@@ -3334,6 +3330,7 @@ uint32_t sim_fused_resident() {
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
   if (!a.n_src) return;
   hipLaunchKernelGGL(k_sim_sparse, dim3(a.n_src), dim3(kWave), 0, st, a);
+  // (grids of 5,120 and 10,240 waves: the same 1M-peer window, within noise)
   hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 2048 ? a.n_src : 2048), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
 }
