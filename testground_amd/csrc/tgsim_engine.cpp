@@ -317,7 +317,7 @@ struct tgsim_engine_s {
                                           // delivery allows for (besides 2 per offered packet)
   bool slack_forced = false;              // TGSIM_DELIVER_SLACK set: the bounded form at any size
   DevBuf<uint32_t> d_emit_n, d_emit_n_alt;
-  DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (k_dst_sort resets it)
+  DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (the delivery's scan clears it)
   hipEvent_t ev_local = nullptr, ev_local_alt = nullptr;
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
@@ -1265,14 +1265,14 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
 // The local delivery of one window on the delivery stream (after its k_sim): scan of the
 // per-destination histogram -> scatter straight from the emit regions -> per-destination order.
 int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uint64_t* lcnt,
-                       const uint64_t* off, uint64_t n_in) {
+                       const uint64_t* off, uint64_t n_in, hipEvent_t released) {
   const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
   HIPCHK(E->d_dtot.ensure(1));
-  launch_scan(lcnt, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
+  launch_scan(lcnt, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p, lcnt);  // (clears lcnt)
   HIPCHK(hipGetLastError());
   const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
   // without the exact count (no host round trip): what the window's sources can emit, 2 per offered
@@ -1293,16 +1293,19 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uin
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
   if (!need_n && slack < kHeapCap) {
-    launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, nd, E->d_err_host, sq);
+    launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, E->d_doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
   launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in);
   HIPCHK(hipGetLastError());
+  // the emit set and its histogram are free once scattered: the window two later may write them
+  // while this one's per-destination sort still runs (the sort reads only the scatter buffer)
+  HIPCHK(hipEventRecord(released, sq));
   if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
   tgsim_delivery* dst = nullptr;
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, lcnt, nd, dst, sq, need_n ? n : n_in);
+  launch_dst_sort(E->d_scatter.p, E->d_doff.p, nullptr, nd, dst, sq, need_n ? n : n_in);
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
@@ -1329,9 +1332,8 @@ int deliver_local(Eng* E) {
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
   }
 
-  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in);
+  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in, E->ev_local);
   if (rc) return rc;
-  HIPCHK(hipEventRecord(E->ev_local, sq));
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   rotate_emit(E);
   return 0;

@@ -2647,7 +2647,7 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, ui
 }
 
 __global__ __launch_bounds__(256) void k_scan_local(const uint64_t* in, uint64_t* out, uint64_t n,
-                                                    uint64_t* block_sums) {
+                                                    uint64_t* block_sums, uint64_t* clear) {
   __shared__ uint64_t sh[17];
   const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x * 4;
   uint64_t v[4], s = 0;
@@ -2655,6 +2655,11 @@ __global__ __launch_bounds__(256) void k_scan_local(const uint64_t* in, uint64_t
   for (int i = 0; i < 4; ++i) {
     v[i] = base + i < n ? in[base + i] : 0;
     s += v[i];
+  }
+  if (clear) {  // the counts, read, are zero again for the next histogram
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (base + i < n) clear[base + i] = 0;
   }
   uint64_t total;
   uint64_t pre = block_excl_scan(s, sh, total);
@@ -2697,7 +2702,7 @@ __global__ __launch_bounds__(256) void k_scan_add(uint64_t* out, uint64_t n, con
 // Exclusive scan of up to kSmallScan counts in one workgroup (out[n] = total; pos = a copy).
 constexpr uint32_t kSmallScan = 16384;
 __global__ __launch_bounds__(1024) void k_scan_small(const uint64_t* in, uint64_t* out, uint64_t n,
-                                                     uint64_t* pos, uint64_t* total_out) {
+                                                     uint64_t* pos, uint64_t* total_out, uint64_t* clear) {
   __shared__ uint64_t sh[17];
   const uint32_t per = (uint32_t)((n + 1023) / 1024);  // <= 16
   const uint64_t base = (uint64_t)threadIdx.x * per;
@@ -2706,6 +2711,11 @@ __global__ __launch_bounds__(1024) void k_scan_small(const uint64_t* in, uint64_
   for (uint32_t i = 0; i < 16; ++i) {
     v[i] = (i < per && base + i < n) ? in[base + i] : 0;
     s += v[i];
+  }
+  if (clear) {
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i)
+      if (i < per && base + i < n) clear[base + i] = 0;
   }
   uint64_t total;
   uint64_t pre = block_excl_scan(s, sh, total);
@@ -3121,10 +3131,10 @@ __global__ __launch_bounds__(64 * W) void k_dst_sort_wide(tgsim_delivery* in, co
   const uint32_t d = blockIdx.x * W + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u;
   if (d >= n_dst) return;
-  const uint32_t n = (uint32_t)cnt[d];
+  const uint32_t n = (uint32_t)(off[d + 1] - off[d]);
   if (n == 0) return;
   sort_segment(in, off[d], n, out, lane);
-  if (lane == 0) cnt[d] = 0;
+  if (lane == 0 && cnt) cnt[d] = 0;
 }
 
 // 64/G destinations per wavefront (a few records each: gossip): a destination with at most G records
@@ -3139,8 +3149,8 @@ __global__ __launch_bounds__(256) void k_dst_sort_group(tgsim_delivery* in, cons
   const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u, g = lane / G, j = lane % G, d = w * kPer + g;
   if (w * kPer >= n_dst) return;
-  const uint32_t n = d < n_dst ? (uint32_t)cnt[d] : 0u;
   const uint64_t b = d < n_dst ? off[d] : 0ull;
+  const uint32_t n = d < n_dst ? (uint32_t)(off[d + 1] - b) : 0u;
   const bool have = n <= G && j < n;
   tgsim_delivery r;
   RecKey k{~0ull, ~0ull, 1u};
@@ -3161,21 +3171,22 @@ __global__ __launch_bounds__(256) void k_dst_sort_group(tgsim_delivery* in, cons
     const uint32_t gl = (uint32_t)__builtin_ctzll(big);
     sort_segment(in, readlane64(b, gl), readlane32(n, gl), out, lane);
   }
-  if (j == 0 && n) cnt[d] = 0;
+  if (j == 0 && n && cnt) cnt[d] = 0;
 }
 
 // A local delivery without a host round trip sizes its scatter and output buffers by a bound
 // (tgsim_engine deliver_local_from); when the window's exact total (the scan's, on the device)
 // exceeds it, this empties the window's record counts so that no later kernel writes past the
 // buffers, and raises the sticky error (-ENOSPC at the next call).
-__global__ __launch_bounds__(256) void k_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
-                                                       uint32_t n_src, uint64_t* cnt, uint32_t n_dst,
+__global__ __launch_bounds__(1024) void k_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
+                                                       uint32_t n_src, uint64_t* cnt, uint64_t* off, uint32_t n_dst,
                                                        uint64_t* err_host) {
   if (*total <= cap) return;
   const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x, st = gridDim.x * blockDim.x;
   if (i0 == 0 && err_host) __hip_atomic_store(err_host, (uint64_t)kErrDeliverCap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (uint32_t i = i0; i < n_src; i += st) emit_n[i] = 0;
   for (uint32_t i = i0; i < n_dst; i += st) cnt[i] = 0;
+  for (uint32_t i = i0; i <= n_dst; i += st) off[i] = 0;  // every segment empty: the sort writes nothing
 }
 
 // Ranks inside lane groups of G records (one destination each) with the keys in LDS: each lane
@@ -3192,8 +3203,8 @@ __global__ __launch_bounds__(256) void k_dst_sort_lds(tgsim_delivery* in, const 
   const uint32_t wv = threadIdx.x >> 6, w = blockIdx.x * 4 + wv;
   const uint32_t lane = threadIdx.x & 63u, g = lane / G, j = lane % G, d = w * kPer + g;
   if (w * kPer >= n_dst) return;
-  const uint32_t n = d < n_dst ? (uint32_t)cnt[d] : 0u;
   const uint64_t b = d < n_dst ? off[d] : 0ull;
+  const uint32_t n = d < n_dst ? (uint32_t)(off[d + 1] - b) : 0u;
   const bool have = n <= G && j < n;
   tgsim_delivery r;
   ulonglong2 k = make_ulonglong2(~0ull, ~0ull);
@@ -3224,7 +3235,7 @@ __global__ __launch_bounds__(256) void k_dst_sort_lds(tgsim_delivery* in, const 
     const uint32_t gl = (uint32_t)__builtin_ctzll(big);
     sort_segment(in, readlane64(b, gl), readlane32(n, gl), out, lane);
   }
-  if (j == 0 && n) cnt[d] = 0;
+  if (j == 0 && n && cnt) cnt[d] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3446,18 +3457,18 @@ void launch_gossip(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, 
 }
 
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums,
-                 uint64_t* total, hipStream_t st, uint64_t* pos) {
+                 uint64_t* total, hipStream_t st, uint64_t* pos, uint64_t* clear) {
   if (n == 0) {
     (void)hipMemsetAsync(out, 0, sizeof(uint64_t), st);
     if (total) (void)hipMemsetAsync(total, 0, sizeof(uint64_t), st);
     return;
   }
   if (n <= kSmallScan) {
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, pos, total);
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, pos, total, clear);
     return;
   }
   const uint64_t nb = (n + 1023) / 1024;
-  hipLaunchKernelGGL(k_scan_local, dim3((uint32_t)nb), dim3(256), 0, st, in, out, n, block_sums);
+  hipLaunchKernelGGL(k_scan_local, dim3((uint32_t)nb), dim3(256), 0, st, in, out, n, block_sums, clear);
   hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, block_sums, nb, total);
   hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)nb), dim3(256), 0, st, out, n, block_sums, pos,
                      (const uint64_t*)total);
@@ -3534,8 +3545,10 @@ void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin
 }
 
 void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n, uint32_t n_src, uint64_t* cnt,
-                          uint32_t n_dst, uint64_t* err_host, hipStream_t st) {
-  hipLaunchKernelGGL(k_deliver_guard, dim3(1024), dim3(256), 0, st, total, cap, emit_n, n_src, cnt, n_dst, err_host);
+                          uint64_t* off, uint32_t n_dst, uint64_t* err_host, hipStream_t st) {
+  // one workgroup: the check needs one dispatch slot (on the low-priority delivery stream behind a
+  // million-wave k_sim_sparse, 1,024 of them waited up to 1.5 ms); the clearing is the error path
+  hipLaunchKernelGGL(k_deliver_guard, dim3(1), dim3(1024), 0, st, total, cap, emit_n, n_src, cnt, off, n_dst, err_host);
 }
 
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,

@@ -64,8 +64,9 @@ void launch_gossip_recv_in(const GossipArgs& g, const tgsim_delivery* recs, uint
                            hipStream_t st);
 // Exclusive scan of in[0..n) into out[0..n] (out[n] = total, also stored at *total when non-null);
 // pos (optional) receives a copy of out[0..n), the scatter cursors.
+// clear: the input counts, zeroed as they are read (the histogram free for its next window), or null
 void launch_scan(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
-                 hipStream_t st, uint64_t* pos = nullptr);
+                 hipStream_t st, uint64_t* pos = nullptr, uint64_t* clear = nullptr);
 void launch_route(const RouteArgsHost& h, int phase, hipStream_t st);
 // edges[0..n_ranks] into slot[0..n_ranks] (pinned host memory), then seq into slot[15].
 // slotted output (slot_cap != 0): also each rank chunk's count header in out, and *overflow = 1
@@ -87,11 +88,12 @@ void launch_dst_hist(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, u
 void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin, uint32_t n_dst, uint64_t* pos,
                         tgsim_delivery* out, hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n, uint32_t n_src, uint64_t* cnt,
-                          uint32_t n_dst, uint64_t* err_host, hipStream_t st);
+                          uint64_t* off, uint32_t n_dst, uint64_t* err_host, hipStream_t st);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
                           uint64_t n_hint);
-// Orders each destination's records; resets cnt[] to zero for the next histogram.
+// Orders each destination's records (segment d: off[d] .. off[d + 1]); resets cnt[] to zero for the
+// next histogram unless cnt is null (the scan cleared it).
 // (in, the scatter buffer, is overwritten for segments longer than 64.)
 // n_hint: about how many records (picks one wavefront per destination or eight).
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
