@@ -3238,6 +3238,72 @@ __global__ __launch_bounds__(256) void k_dst_sort_lds(tgsim_delivery* in, const 
   if (j == 0 && n && cnt) cnt[d] = 0;
 }
 
+// Per-destination order of the scattered records, flattened over the records instead of the
+// destinations: a wavefront takes 64 consecutive records of the scatter buffer (a few destinations'
+// segments, or part of one), so no lane idles on a short segment and a window at the flood's peak
+// (~28 M records in 1 M segments) runs 440 k wave-iterations, not a wavefront per destination.  The
+// keys of the 192 records around the chunk are staged in LDS: a segment of at most 64 records that
+// holds one of the chunk's records lies inside them, and each record's rank is the number of its
+// segment's keys before its own (ties, which the key order never has, by position).  A longer
+// segment is sorted whole (sort_segment) by the wavefront holding its first record.  A persistent
+// grid walks the chunks up to the device's total (off[n_dst]); the destination counts are not read.
+__global__ __launch_bounds__(256) void k_dst_sort_flat(tgsim_delivery* in, const uint64_t* off, uint32_t n_dst,
+                                                       uint32_t dst_begin, tgsim_delivery* out) {
+  __shared__ uint64_t kt[4][3 * kWave], kq[4][3 * kWave];
+  __shared__ uint32_t kc[4][3 * kWave];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint64_t total = off[n_dst];
+  const uint64_t n_chunks = (total + kWave - 1) / kWave;
+  for (uint64_t c = (uint64_t)blockIdx.x * 4 + wv; c < n_chunks; c += (uint64_t)gridDim.x * 4) {
+    const uint64_t w0 = c * kWave;  // the staged window is [w0 - 64, w0 + 128)
+    tgsim_delivery r;
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u) {
+      const uint64_t j = w0 + u * kWave + lane;  // + 64
+      uint64_t t = ~0ull, q = ~0ull;
+      uint32_t cl = 1u;
+      if (j >= kWave && j - kWave < total) {
+        const tgsim_delivery x = in[j - kWave];
+        t = x.t_ns;
+        q = ((uint64_t)x.src << 32) | x.seq;
+        cl = (x.flags & TGSIM_FLAG_DUP) ? 0u : 1u;
+        if (u == 1) r = x;
+      }
+      kt[wv][u * kWave + lane] = t;
+      kq[wv][u * kWave + lane] = q;
+      kc[wv][u * kWave + lane] = cl;
+    }
+    const uint64_t i = w0 + lane;
+    const bool have = i < total;
+    uint64_t sb = 0, se = 0;
+    if (have) {
+      const uint32_t d = r.dst - dst_begin;
+      sb = off[d];
+      se = off[d + 1];
+    }
+    wave_lds_sync();
+    const bool small = have && se - sb <= kWave;
+    if (small) {
+      const uint64_t t = r.t_ns, q = ((uint64_t)r.src << 32) | r.seq;
+      const uint32_t cl = (r.flags & TGSIM_FLAG_DUP) ? 0u : 1u;
+      uint32_t rank = 0;
+      for (uint64_t j = sb; j < se; ++j) {
+        const uint32_t x = (uint32_t)(j + kWave - w0);
+        const uint64_t ot = kt[wv][x], oq = kq[wv][x];
+        const uint32_t oc = kc[wv][x];
+        rank += (rec_lt(ot, oq, oc, t, q, cl) || (!rec_lt(t, q, cl, ot, oq, oc) && j < i)) ? 1u : 0u;
+      }
+      out[sb + rank] = r;
+    }
+    for (uint64_t big = __ballot(have && !small && i == sb); big; big &= big - 1) {
+      const uint32_t gl = (uint32_t)__builtin_ctzll(big);
+      const uint64_t b = readlane64(sb, gl);
+      sort_segment(in, b, (uint32_t)(readlane64(se, gl) - b), out, lane);
+    }
+    wave_lds_sync();  // this chunk's LDS reads are done before the next chunk's writes
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K8 metrics (opt-in): per-instance counters and log2 histograms folded after each step, one
 // wavefront per instance, no atomics on the counters (an instance is one wavefront's).
@@ -3564,8 +3630,20 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
 }
 
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
+                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin) {
   if (!n_dst) return;
+  static const int flat = [] {
+    const char* v = getenv("TGSIM_SORT_FLAT");
+    return v ? atoi(v) : 1;
+  }();
+  if (flat && !cnt && n_hint <= 48ull * n_dst) {
+    // one pass of 64 records per wave-iteration over at most n_hint records, on a grid of at most
+    // 8,192 workgroups of 4 waves
+    const uint64_t chunks = (n_hint + kWave - 1) / kWave, wgs = (chunks + 3) / 4;
+    hipLaunchKernelGGL(k_dst_sort_flat, dim3((uint32_t)(wgs < 8192 ? (wgs ? wgs : 1) : 8192)), dim3(256), 0, st, in, off,
+                       n_dst, dst_begin, out);
+    return;
+  }
   // n_hint bounds the step's records (offered packets or the exact count).  Measured at the 1M-peer
   // flood's peak (up to ~20 records per destination): groups of 16 lanes 0.77 ms, of 32 3.8 ms
   // (the in-group shuffles), the wavefront per destination 1.4 ms

@@ -97,7 +97,7 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
 // (in, the scatter buffer, is overwritten for segments longer than 64.)
 // n_hint: about how many records (picks one wavefront per destination or eight).
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint);
+                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin = 0);
 // The fused group's K5 (single-wave workgroups, see k_scan_w1): scan of n counts, scatter of the
 // n_win windows' emit regions, one wavefront per (window, destination) segment.
 void launch_scan_w(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
