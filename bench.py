@@ -638,13 +638,18 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dist = None
     if world > 1 or a.sharded:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(free_port()))
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
         import torch.distributed as dist
         from testground_amd.shard import init_rccl
-        init_rccl(torch.device("cuda", local))
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            # one rank started without a launcher (--sharded): an in-process store, no TCP port to
+            # race for (a probed free port was once taken before the store bound it: EADDRINUSE)
+            init_rccl(torch.device("cuda", local), store=dist.HashStore(), rank=0, world_size=1)
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            init_rccl(torch.device("cuda", local))
     if a.workload == "bridge":
         res = run_bridge(a, world, rank, local, dist, want_cpu=not a.no_cpu)
     else:

@@ -712,12 +712,13 @@ int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev, c
 // lag the device by hundreds of microseconds (the closed gossip loop pays it every window).
 int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uint64_t>& blk,
                 DevBuf<uint64_t>& tot, uint64_t n, uint64_t* total, uint64_t* pos = nullptr,
-                hipStream_t stream = nullptr, const uint32_t* flag = nullptr, uint32_t* flag_out = nullptr) {
+                hipStream_t stream = nullptr, const uint32_t* flag = nullptr, uint32_t* flag_out = nullptr,
+                bool clear = false) {
   hipStream_t sq = stream ? stream : E->st;
   HIPCHK(off.ensure(n + 1));
   HIPCHK(blk.ensure((n + 1023) / 1024 + 1));
   HIPCHK(tot.ensure(1));
-  launch_scan(cnt.p, off.p, n, blk.p, tot.p, sq, pos);
+  launch_scan(cnt.p, off.p, n, blk.p, tot.p, sq, pos, clear ? cnt.p : nullptr);
   HIPCHK(hipGetLastError());
   launch_publish(tot.p, flag, E->dm_pub, ++E->pub_seq, sq);
   HIPCHK(hipGetLastError());
@@ -1229,11 +1230,11 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
     HIPCHK(E->d_doff.ensure(nd + 1));
     HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
     HIPCHK(E->d_dtot.ensure(1));
-    launch_scan(E->d_dcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p);
+    launch_scan(E->d_dcnt.p, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p, E->d_dcnt.p);
     HIPCHK(hipGetLastError());
   } else {
     uint64_t total = 0;
-    rc = scan_counts(E, E->d_dcnt, E->d_doff, E->d_dblk, E->d_dtot, nd, &total, E->d_dpos.p, sq);
+    rc = scan_counts(E, E->d_dcnt, E->d_doff, E->d_dblk, E->d_dtot, nd, &total, E->d_dpos.p, sq, nullptr, nullptr, true);
     if (rc) return rc;
     if (total != n) return E->fail(-EINVAL, "deliver: %llu of %llu records address other shards",
                                    static_cast<unsigned long long>(n - total), static_cast<unsigned long long>(n));
@@ -1252,7 +1253,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
   if (n_win > 1) launch_dst_sort_w1(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, static_cast<uint32_t>(nseg), dst, sq);
-  else launch_dst_sort(E->d_scatter.p, E->d_doff.p, E->d_dcnt.p, nd, dst, sq, n);
+  else launch_dst_sort(E->d_scatter.p, E->d_doff.p, nullptr, nd, dst, sq, n, E->o.shard_begin);  // (the scan cleared d_dcnt)
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);

@@ -3137,43 +3137,6 @@ __global__ __launch_bounds__(64 * W) void k_dst_sort_wide(tgsim_delivery* in, co
   if (lane == 0 && cnt) cnt[d] = 0;
 }
 
-// 64/G destinations per wavefront (a few records each: gossip): a destination with at most G records
-// is ordered by its lane group of G (ranks from in-group shuffles); longer segments take the whole
-// wavefront in turn.  G follows the step's records per destination (8 below 4 on average, 16 up to
-// 10, 32 up to 24: the flood's peak windows): one wavefront per destination, as k_dst_sort_wide
-// runs, left 60 of its 64 lanes idle for most destinations.
-template <uint32_t G>
-__global__ __launch_bounds__(256) void k_dst_sort_group(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
-                                                        uint32_t n_dst, tgsim_delivery* out) {
-  constexpr uint32_t kPer = kWave / G;
-  const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63u, g = lane / G, j = lane % G, d = w * kPer + g;
-  if (w * kPer >= n_dst) return;
-  const uint64_t b = d < n_dst ? off[d] : 0ull;
-  const uint32_t n = d < n_dst ? (uint32_t)(off[d + 1] - b) : 0u;
-  const bool have = n <= G && j < n;
-  tgsim_delivery r;
-  RecKey k{~0ull, ~0ull, 1u};
-  if (have) {
-    r = in[b + j];
-    k = rec_key(r);
-  }
-  uint32_t rank = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < G; ++q) {  // ties: input order, as wave_rank
-    const uint32_t from = g * G + q;
-    const uint64_t t = shfl64(k.t, from), sq = shfl64(k.sq, from);
-    const uint32_t c = (uint32_t)__shfl((int)k.c, (int)from, 64);
-    rank += (q < n && (rec_lt(t, sq, c, k.t, k.sq, k.c) || (!rec_lt(k.t, k.sq, k.c, t, sq, c) && q < j))) ? 1u : 0u;
-  }
-  if (have) out[b + rank] = r;
-  for (uint64_t big = __ballot(j == 0 && n > G); big; big &= big - 1) {
-    const uint32_t gl = (uint32_t)__builtin_ctzll(big);
-    sort_segment(in, readlane64(b, gl), readlane32(n, gl), out, lane);
-  }
-  if (j == 0 && n && cnt) cnt[d] = 0;
-}
-
 // A local delivery without a host round trip sizes its scatter and output buffers by a bound
 // (tgsim_engine deliver_local_from); when the window's exact total (the scan's, on the device)
 // exceeds it, this empties the window's record counts so that no later kernel writes past the
@@ -3187,55 +3150,6 @@ __global__ __launch_bounds__(1024) void k_deliver_guard(const uint64_t* total, u
   for (uint32_t i = i0; i < n_src; i += st) emit_n[i] = 0;
   for (uint32_t i = i0; i < n_dst; i += st) cnt[i] = 0;
   for (uint32_t i = i0; i <= n_dst; i += st) off[i] = 0;  // every segment empty: the sort writes nothing
-}
-
-// Ranks inside lane groups of G records (one destination each) with the keys in LDS: each lane
-// reads its group's keys as one 16-B word each, (t, src << 32 | seq), instead of five cross-lane
-// shuffles per key (k_dst_sort_group); only a packet and its duplicate share that key, and the
-// duplicate goes first.  Destinations with more than G records take the whole wavefront in turn
-// (sort_segment).
-template <uint32_t G>
-__global__ __launch_bounds__(256) void k_dst_sort_lds(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt,
-                                                      uint32_t n_dst, tgsim_delivery* out) {
-  constexpr uint32_t kPer = kWave / G;
-  __shared__ ulonglong2 keys[256];
-  __shared__ uint32_t orig[256];
-  const uint32_t wv = threadIdx.x >> 6, w = blockIdx.x * 4 + wv;
-  const uint32_t lane = threadIdx.x & 63u, g = lane / G, j = lane % G, d = w * kPer + g;
-  if (w * kPer >= n_dst) return;
-  const uint64_t b = d < n_dst ? off[d] : 0ull;
-  const uint32_t n = d < n_dst ? (uint32_t)(off[d + 1] - b) : 0u;
-  const bool have = n <= G && j < n;
-  tgsim_delivery r;
-  ulonglong2 k = make_ulonglong2(~0ull, ~0ull);
-  uint32_t c = 1u;  // 0 for the duplicate, 1 for the original
-  if (have) {
-    r = in[b + j];
-    k = make_ulonglong2(r.t_ns, ((uint64_t)r.src << 32) | r.seq);
-    c = (r.flags & TGSIM_FLAG_DUP) ? 0u : 1u;
-  }
-  ulonglong2* kg = keys + wv * kWave + g * G;
-  uint32_t* cg = orig + wv * kWave + g * G;
-  kg[j] = k;
-  cg[j] = c;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t nm = have ? n : 0u;
-  const uint32_t qmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)readlane32(scan_max_u32(nm), kWave - 1));
-  uint32_t rank = 0;
-  for (uint32_t q = 0; q < qmax; ++q) {
-    const ulonglong2 o = kg[q];
-    bool lt = o.x < k.x || (o.x == k.x && o.y < k.y);
-    if (o.x == k.x && o.y == k.y && q != j) lt = cg[q] < c;  // the other copy of the same packet
-    rank += (q < n && lt) ? 1u : 0u;
-  }
-  if (have) out[b + rank] = r;
-  for (uint64_t big = __ballot(j == 0 && n > G); big; big &= big - 1) {
-    const uint32_t gl = (uint32_t)__builtin_ctzll(big);
-    sort_segment(in, readlane64(b, gl), readlane32(n, gl), out, lane);
-  }
-  if (j == 0 && n && cnt) cnt[d] = 0;
 }
 
 // Per-destination order of the scattered records, flattened over the records instead of the
@@ -3632,42 +3546,17 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                      tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin) {
   if (!n_dst) return;
-  static const int flat = [] {
-    const char* v = getenv("TGSIM_SORT_FLAT");
-    return v ? atoi(v) : 1;
-  }();
-  if (flat && !cnt && n_hint <= 48ull * n_dst) {
-    // one pass of 64 records per wave-iteration over at most n_hint records, on a grid of at most
-    // 8,192 workgroups of 4 waves
+  if (!cnt && n_hint <= 48ull * n_dst) {
+    // up to tens of records per destination (gossip, sparse windows): 64 records per wave-iteration
+    // over the records, on a grid of at most 8,192 workgroups of 4 waves.  At the 1M-peer flood's
+    // peak it replaced a wavefront per destination (or lane groups of 8-32 for short segments):
+    // 4.66-4.70 against 4.57-4.60 G pkt/s
     const uint64_t chunks = (n_hint + kWave - 1) / kWave, wgs = (chunks + 3) / 4;
     hipLaunchKernelGGL(k_dst_sort_flat, dim3((uint32_t)(wgs < 8192 ? (wgs ? wgs : 1) : 8192)), dim3(256), 0, st, in, off,
                        n_dst, dst_begin, out);
     return;
   }
-  // n_hint bounds the step's records (offered packets or the exact count).  Measured at the 1M-peer
-  // flood's peak (up to ~20 records per destination): groups of 16 lanes 0.77 ms, of 32 3.8 ms
-  // (the in-group shuffles), the wavefront per destination 1.4 ms
-  static const uint64_t group_max = [] {  // TGSIM_SORT_GROUP_MAX: average records per destination
-    const char* v = getenv("TGSIM_SORT_GROUP_MAX");
-    return v ? (uint64_t)atoll(v) : 8ull;
-  }();
-  static const int lds_sort = [] {  // TGSIM_SORT_LDS=0: the shuffle-ranked groups of 8
-    const char* v = getenv("TGSIM_SORT_LDS");
-    return v ? atoi(v) : 1;
-  }();
-  if (lds_sort && n_hint <= 48ull * n_dst) {
-    if (n_hint <= 3ull * n_dst)
-      hipLaunchKernelGGL(k_dst_sort_lds<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
-    else if (n_hint <= 8ull * n_dst)
-      hipLaunchKernelGGL(k_dst_sort_lds<16>, dim3((n_dst + 15) / 16), dim3(256), 0, st, in, off, cnt, n_dst, out);
-    else if (n_hint <= 18ull * n_dst)
-      hipLaunchKernelGGL(k_dst_sort_lds<32>, dim3((n_dst + 7) / 8), dim3(256), 0, st, in, off, cnt, n_dst, out);
-    else
-      hipLaunchKernelGGL(k_dst_sort_lds<64>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
-  } else if (n_hint <= group_max * n_dst)
-    hipLaunchKernelGGL(k_dst_sort_group<8>, dim3((n_dst + 31) / 32), dim3(256), 0, st, in, off, cnt, n_dst, out);
-  else
-    hipLaunchKernelGGL(k_dst_sort_wide<4>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
+  hipLaunchKernelGGL(k_dst_sort_wide<4>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
 }
 
 void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,

@@ -92,10 +92,10 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
                           uint64_t n_hint);
-// Orders each destination's records (segment d: off[d] .. off[d + 1]); resets cnt[] to zero for the
-// next histogram unless cnt is null (the scan cleared it).
-// (in, the scatter buffer, is overwritten for segments longer than 64.)
-// n_hint: about how many records (picks one wavefront per destination or eight).
+// Orders each destination's records (segment d: off[d] .. off[d + 1]; dst_begin: the first
+// destination's id) and resets cnt[] to zero for the next histogram, unless cnt is null (the scan
+// cleared it: then sparse windows take the flattened sort).  (in, the scatter buffer, is
+// overwritten for segments longer than 64.)  n_hint: about how many records.
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                      tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin = 0);
 // The fused group's K5 (single-wave workgroups, see k_scan_w1): scan of n counts, scatter of the
