@@ -594,3 +594,45 @@ def test_sparse_long_queues(make_oracle, monkeypatch):
         assert_same(g, c, f"step {step}")
     # the queues did grow past the 128 items held in registers (state bytes: ~16 B x 2 per item)
     assert g.stats()["queue_state_bytes"] > 40 * n * 32 * 128 // 2
+
+
+@pytest.mark.parametrize("latency_ms", [0, 3])
+def test_flat_sort_hot_destinations(make_oracle, latency_ms):
+    """The flattened per-destination sort (k_dst_sort_flat: sparse windows, up to 48 records per
+    destination on average) with segments longer than its 64-record staging (three hot
+    destinations take ~30 % of the traffic: sorted whole by the wave holding their first record),
+    segments that straddle chunk boundaries, and duplicates whose delivery time equals their
+    original's (no latency, no rate limit: the clone-first tie rule); bit-exact with the oracle in
+    drain order."""
+    n = 200
+    rng = np.random.default_rng(11)
+    g, c = both(make_oracle, n)
+    for i in range(n):
+        s = nw.LinkShape(Latency=latency_ms * nw.Millisecond, Duplicate=20.0, Loss=2.0, Corrupt=1.0)
+        for e in (g, c):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=s))
+    seq = np.zeros(n, dtype=np.uint32)
+    for step in range(5):
+        m = 20 * n
+        src = rng.integers(0, n, m)
+        hot = rng.random(m) < 0.3
+        dst = np.where(hot, rng.integers(0, 3, m), (src + 1 + rng.integers(0, n - 1, m)) % n)
+        dst = np.where(dst == src, (src + 1) % n, dst)
+        pk = np.zeros(m, dtype=abi.PKT_DTYPE)
+        pk["src"], pk["dst"] = src, dst
+        pk["len"] = rng.integers(40, 1500, m)
+        pk["tick"] = rng.integers(0, 2000, m)
+        order = np.lexsort((pk["tick"], src))
+        counts = np.bincount(src, minlength=n)
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        sq = np.empty(m, dtype=np.uint32)
+        sq[order] = np.arange(m) - starts[src[order]] + seq[src[order]]
+        seq += counts.astype(np.uint32)
+        pk["seq"] = sq
+        g.submit(pk)
+        c.submit(pk)
+        g.step(2000)
+        c.step(2000)
+        _, d = assert_same(g, c, f"latency {latency_ms} ms step {step}")
+        if latency_ms == 0 or step >= 2:  # the hot segments exceed 64 records
+            assert np.bincount(d["dst"], minlength=n)[:3].min() > 64
