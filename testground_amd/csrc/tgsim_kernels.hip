@@ -2212,10 +2212,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
 // (A one-lane-per-source pass listing the active sources, so that idle peers cost no wave, was
 // measured and dropped: 4.17-4.21 against 4.40-4.41 G pkt/s at 1M peers -- an idle wave exits after
 // its first loads, cheaper than the pass over a million sources.)
-// Compiled for at least 6 waves per SIMD: it still fits 69 VGPRs (7 waves resident), with 41 SGPRs
-// spilled instead of 59 under a bound of 7 (A/B: simulate kernels 0.99-1.01 against 1.06-1.11 ms
-// per 1M-peer window); a bound of 8 spills VGPRs.
-__global__ __launch_bounds__(kWave, 6) void k_sim_sparse(SimArgs a) {
+__global__ __launch_bounds__(kWave, 7) void k_sim_sparse(SimArgs a) {
   if (blockIdx.x < a.n_src) sparse_source(a, blockIdx.x);
 }
 
