@@ -1297,7 +1297,7 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uin
     launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, E->d_doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
-  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in);
+  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
   // while this one's per-destination sort still runs (the sort reads only the scatter buffer)

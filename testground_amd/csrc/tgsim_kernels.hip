@@ -2935,6 +2935,7 @@ __global__ __launch_bounds__(256) void k_local_scatter(const tgsim_delivery* emi
 // cursor atomic and store of a round independent of the others; a pass over the records'
 // destinations first, so that a destination's records share one cursor atomic.  The wave per source above walks
 // its sources one after another, each behind four dependent round trips with 57 of 64 lanes idle.
+template <bool kAgg>
 __global__ __launch_bounds__(256) void k_local_scatter_ls(const tgsim_delivery* __restrict__ emit,
                                                           const uint32_t* __restrict__ emit_n,
                                                           const uint64_t* __restrict__ off, uint32_t n_src,
@@ -2948,6 +2949,22 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(const tgsim_delivery* 
     base = emit + 2 * off[s] + (uint64_t)kHeapCap * s;
   }
   unsigned long long* p = reinterpret_cast<unsigned long long*>(pos);
+  if constexpr (!kAgg) {  // records to many destinations (storm shapes): one cursor atomic each
+    for (uint32_t i = 0; __ballot(i < n); i += 4) {
+      tgsim_delivery r[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (i + u < n) r[u] = base[i + u];
+      uint64_t at[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (i + u < n) at[u] = atomicAdd(&p[r[u].dst - dst_begin], 1ull);
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (i + u < n) out[at[u]] = r[u];
+    }
+    return;
+  }
   // A source's records of a window go to few destinations (a gossip peer's 8 neighbours): the first
   // kScatterDst distinct ones take one cursor atomic each for all their records (every cursor atomic
   // is a memory-side request; at the flood's peak one per record held this kernel at the memory
@@ -3580,11 +3597,19 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
 }
 
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
-                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint) {
+                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint,
+                          bool few_dst) {
   if (!n_src) return;
   if (n_hint <= 64ull * n_src) {  // up to tens of records per source (gossip, even at the flood's peak): one lane each
-    hipLaunchKernelGGL(k_local_scatter_ls, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
-                       dst_begin, pos, out);
+    // few_dst (gossip: a peer forwards to its neighbours): one cursor atomic per destination of a
+    // source (1M-peer gossip +1-2 %); with records to many destinations that pass over the records
+    // costs more than it saves (sub-capacity storm 1.09 against 1.15-1.17 G pkt/s)
+    if (few_dst)
+      hipLaunchKernelGGL(k_local_scatter_ls<true>, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
+                         dst_begin, pos, out);
+    else
+      hipLaunchKernelGGL(k_local_scatter_ls<false>, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
+                         dst_begin, pos, out);
     return;
   }
   const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);

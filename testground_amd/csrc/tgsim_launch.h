@@ -91,7 +91,7 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
                           uint64_t* off, uint32_t n_dst, uint64_t* err_host, hipStream_t st);
 void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
-                          uint64_t n_hint);
+                          uint64_t n_hint, bool few_dst = false);
 // Orders each destination's records (segment d: off[d] .. off[d + 1]; dst_begin: the first
 // destination's id) and resets cnt[] to zero for the next histogram, unless cnt is null (the scan
 // cleared it: then sparse windows take the flattened sort).  (in, the scatter buffer, is
