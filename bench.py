@@ -318,7 +318,7 @@ def run_bridge(a, world, rank, local, dist, want_cpu):
     b.close()
     eng.close()
     if dist:
-        t = torch.tensor([el, float(got[0]), float(got[1])], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([el, float(got[0]), float(got[1])], dtype=torch.float64)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -382,6 +382,30 @@ def shard_bounds(peers, world, split):
     return total, [r * total // world for r in range(world)] + [total]
 
 
+# The host process group only carries the bench's own bookkeeping (the RCCL id broadcast, barriers,
+# the max/sum of the timed results); every data-path collective is the engine's own RCCL communicator
+# (tgsim_comm_*).  A gloo group keeps each process at ONE RCCL communicator: a second one (torch's
+# NCCL group) would double RCCL's streams and buffers on a box with 4 hardware queues per process.
+HOST_GROUP_BACKEND = "gloo"
+
+
+def init_host_group(world):
+    """The bench's host process group (gloo, over 127.0.0.1)."""
+    import torch.distributed as dist
+
+    if world == 1 and "MASTER_PORT" not in os.environ:
+        # one rank started without a launcher (--sharded): an in-process store, no TCP port to
+        # race for (a probed free port was once taken before the store bound it: EADDRINUSE)
+        dist.init_process_group(HOST_GROUP_BACKEND, store=dist.HashStore(), rank=0, world_size=1)
+    else:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        dist.init_process_group(HOST_GROUP_BACKEND)
+    return dist
+
+
 def runs_cpu_baseline(rank, want_cpu):
     """North star: the oracle is timed 'on the box's own host cores in the same run' beside the GPU
     line at every world size; rank 0 runs it (after the timed region, the other ranks wait)."""
@@ -431,7 +455,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     stepper = None
     if sharded:  # the engine's own RCCL exchange (tgsim_comm_*), as a Go host would drive it
         from testground_amd.shard import CommStepper
-        stepper = CommStepper(eng, bounds, device=f"cuda:{local}")
+        stepper = CommStepper(eng, bounds, device="cpu")  # the id crosses the gloo host group
     step = eng.step if stepper is None else stepper.step
     epoch = [0]
 
@@ -517,23 +541,22 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     exch = (stepper.exchanged_records - x0) if stepper is not None else 0
     sim_ms, n_launch = eng.sim_kernel_ms()
     if dist:
-        t = torch.tensor([el, float(offered), float(scheduled), float(exch), *verd], dtype=torch.float64,
-                         device=f"cuda:{local}")
+        t = torch.tensor([el, float(offered), float(scheduled), float(exch), *verd], dtype=torch.float64)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         el = float(mx[0])
         offered_all, scheduled_all, exch_all = float(t[1]), float(t[2]), float(t[3])
-        verd_all = t[4:].cpu().numpy()
+        verd_all = t[4:].numpy()
     else:
         offered_all, scheduled_all, exch_all, verd_all = float(offered), float(scheduled), 0.0, verd
     extra = {}
     if workload == "gossip":
         reached = eng.gossip_reached()
         if dist:
-            r = torch.as_tensor(reached.astype(np.int64), device=f"cuda:{local}")
+            r = torch.as_tensor(reached.astype(np.int64))
             dist.all_reduce(r)
-            reached = r.cpu().numpy()
+            reached = r.numpy()
         extra = {"floods": a.floods, "flood_gap_ticks": a.flood_gap,
                  "reached_min_frac": float(reached.min()) / peers_total,
                  "sim_ms_covered": (warmup + steps) * window / 1000}
@@ -623,9 +646,14 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.launch_check:
+        # the host group is created exactly as a measured run creates it (gloo touches no GPU)
+        dist = init_host_group(world)
+        backend = dist.get_backend()
+        dist.barrier()
+        dist.destroy_process_group()
         line = json.dumps({"rank": rank, "world": world, "local_rank": local, "gpus": a.gpus,
                            "launched_by_bench": os.environ.get("TGSIM_BENCH_LAUNCHED") == "1",
-                           "headline": headline_plan(a, world)})
+                           "host_group": backend, "headline": headline_plan(a, world)})
         os.write(1, (line + "\n").encode())  # one write: the ranks share the pipe
         return
     # the one JSON line goes to the original stdout; everything else (RCCL's version banner, library
@@ -638,18 +666,7 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dist = None
     if world > 1 or a.sharded:
-        import torch.distributed as dist
-        from testground_amd.shard import init_rccl
-        if world == 1 and "MASTER_PORT" not in os.environ:
-            # one rank started without a launcher (--sharded): an in-process store, no TCP port to
-            # race for (a probed free port was once taken before the store bound it: EADDRINUSE)
-            init_rccl(torch.device("cuda", local), store=dist.HashStore(), rank=0, world_size=1)
-        else:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(free_port()))
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
-            init_rccl(torch.device("cuda", local))
+        dist = init_host_group(world)
     if a.workload == "bridge":
         res = run_bridge(a, world, rank, local, dist, want_cpu=not a.no_cpu)
     else:

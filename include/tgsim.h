@@ -473,6 +473,9 @@ int64_t tgsim_debug_stamps(void* engine, uint64_t* out, size_t cap);
 int64_t tgsim_debug_carry_bytes(void* engine);
 /* Diagnostics: windows simulated by fused launches (tgsim_step_n) since the engine was created. */
 int64_t tgsim_debug_fused_windows(void* engine);
+/* Diagnostics of a TGSIM_CHECK build of the engine (scripts/check_build.sh): cross-lane reads whose
+ * source lanes were inactive so far, process-wide.  -ENOSYS in the product build. */
+int64_t tgsim_debug_exec_faults(void);
 
 #ifdef __cplusplus
 }

@@ -208,7 +208,10 @@ typedef struct {
     offered* off;
     size_t n_off, cap_off;
     /* device-generated windows queued ahead of the steps that consume them (tgsim_gen_*) */
-    struct genwin { offered* pk; size_t n, cap; uint32_t ticks; } *gq;
+    /* late: a gossip window generated while a receipt already preceded it (no packets); reported
+     * as the HIP engine reports it, by the call that resolves it: the step that consumes it,
+     * tgsim_sim_capacity, or the next tgsim_gen_gossip (its generation runs ahead of the host) */
+    struct genwin { offered* pk; size_t n, cap; uint32_t ticks; int late; uint32_t late_tick; uint64_t win0; } *gq;
     size_t gq_n, gq_cap;
     uint64_t gq_ticks;
     uint8_t* verdicts;
@@ -263,6 +266,20 @@ static struct genwin* gen_window(oracle* o, uint32_t n_ticks) {
     memset(w, 0, sizeof *w);
     w->ticks = n_ticks;
     return w;
+}
+
+/* The late window gq[i] is reported: it and every window queued after it are dropped (the ones
+ * before it stay queued and can still be stepped), and the error stays until gossip_init. */
+static int gen_report_late(oracle* o, size_t i) {
+    const uint32_t t = o->gq[i].late_tick;
+    const unsigned long long a = (unsigned long long)o->gq[i].win0;
+    for (size_t k = i; k < o->gq_n; ++k) {
+        free(o->gq[k].pk);
+        o->gq_ticks -= o->gq[k].ticks;
+    }
+    o->gq_n = i;
+    o->gossip_late = 1;
+    return fail(o, -EINVAL, "gossip: a receipt at tick %u precedes the window at %llu", t, a);
 }
 
 static void gen_push(struct genwin* w, const tgsim_pkt* k) {
@@ -820,6 +837,7 @@ static int step_core(oracle* o, uint32_t n_ticks) {
     if (n_ticks == 0) return -EINVAL;
     if (o->gq_n) { /* the oldest generated window is this step's input */
         if (o->n_off) return fail(o, -EBUSY, "host packets and generated traffic in one step");
+        if (o->gq[0].late) return gen_report_late(o, 0);
         if (o->gq[0].ticks != n_ticks)
             return fail(o, -EINVAL, "generated window spans %u ticks, step is %u", o->gq[0].ticks, n_ticks);
         free(o->off);
@@ -985,6 +1003,7 @@ int tgo_sync(void* p) { return p ? 0 : -EINVAL; }
 
 int64_t tgo_sim_capacity(void* p) {
     oracle* o = (oracle*)p;
+    if (o->gq_n && o->gq[0].late) return gen_report_late(o, 0);
     const size_t n = o->gq_n ? o->gq[0].n : o->n_off;
     return (int64_t)(2 * n + 1024ull * o->nsrc);
 }
@@ -1101,20 +1120,23 @@ int tgo_gen_gossip(void* p, uint32_t n_ticks) {
     if (o->n_off) return fail(o, -EBUSY, "host packets already pending for the next step");
     if (o->gossip_late)
         return fail(o, -EINVAL, "gossip: a receipt preceded an earlier window (tgsim_gossip_init starts a new flood)");
+    for (size_t i = 0; i < o->gq_n; ++i) /* a queued late window is reported first */
+        if (o->gq[i].late) return gen_report_late(o, i);
     uint64_t A = o->now_tick + o->gq_ticks, B = A + n_ticks;
     /* A receipt before the window (lookahead shorter than the window) fails the flood before any
-     * peer's forwarded set changes; the windows queued ahead are dropped and the error stays, as the
-     * HIP engine reports it (there at the next step, since its generation runs ahead of the host). */
+     * peer's forwarded set changes: the window is queued empty and marked late, and the call that
+     * resolves it reports it (gen_report_late), as the HIP engine does (its generation runs ahead
+     * of the host, so it learns of the late receipt only when it resolves the window's size). */
     for (uint32_t s = 0; s < o->nsrc; ++s)
         for (uint32_t f = 0; f < o->g.n_floods; ++f) {
             uint32_t t = o->g_first[64ull * s + f];
             if (!(o->g_fwd[s] >> f & 1) && t < A) {
-                for (size_t i = 0; i < o->gq_n; ++i) free(o->gq[i].pk);
-                o->gq_n = 0;
-                o->gq_ticks = 0;
-                o->gossip_late = 1;
-                return fail(o, -EINVAL, "gossip: a receipt at tick %u precedes the window at %llu", t,
-                            (unsigned long long)A);
+                struct genwin* lw = gen_window(o, n_ticks);
+                lw->late = 1;
+                lw->late_tick = t;
+                lw->win0 = A;
+                o->gq_ticks += n_ticks;
+                return 0;
             }
         }
     struct genwin* w = gen_window(o, n_ticks);

@@ -30,16 +30,19 @@ def _stale(target: Path, deps) -> bool:
 
 
 PROF_LIB = PKG / "libtgsim_prof.so"
+CHECK_LIB = PKG / "libtgsim_check.so"
 
 
-def build_engine(force: bool = False, verbose: bool = False, profile: bool = False) -> Path:
+def build_engine(force: bool = False, verbose: bool = False, profile: bool = False, check: bool = False) -> Path:
     """Compiles the HIP engine (kernels + host runtime) into libtgsim.so.  profile=True builds the
-    diagnostic variant libtgsim_prof.so (k_sim cycle counters in the stamp slots; scripts only)."""
-    lib = PROF_LIB if profile else LIB
+    diagnostic variant libtgsim_prof.so (k_sim cycle counters in the stamp slots; scripts only);
+    check=True the invariant-checking variant libtgsim_check.so (-DTGSIM_CHECK: queue invariants and
+    the cross-lane exec-mask guards; loaded by TGSIM_LIB=... for scripts/check_build.sh only)."""
+    lib = PROF_LIB if profile else CHECK_LIB if check else LIB
     if not force and not _stale(lib, SOURCES + HEADERS):
         return lib
     objs = []
-    build_dir = PKG / ("build_prof" if profile else "build")
+    build_dir = PKG / ("build_prof" if profile else "build_check" if check else "build")
     build_dir.mkdir(exist_ok=True)
     for src in SOURCES:
         obj = build_dir / (src.stem + ".o")
@@ -47,7 +50,8 @@ def build_engine(force: bool = False, verbose: bool = False, profile: bool = Fal
         # and 1.2 % off its time (A/B on the GPU)
         dev = ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"] if src.suffix == ".hip" else []
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", *dev,
-               "-Wno-unused-result", *(["-DTGSIM_PROFILE"] if profile else []), "-c", str(src), "-o", str(obj)]
+               "-Wno-unused-result", *(["-DTGSIM_PROFILE"] if profile else []),
+               *(["-DTGSIM_CHECK"] if check else []), "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -59,6 +60,7 @@ struct Rccl {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*);
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
   ncclResult_t (*CommDestroy)(ncclComm_t);
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;  // optional: frees a communicator whose peer never came
   const char* (*GetErrorString)(ncclResult_t);
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
@@ -76,6 +78,7 @@ struct Rccl {
 MOCK_DECL(ncclResult_t, GetUniqueId, ncclUniqueId*)
 MOCK_DECL(ncclResult_t, CommInitRank, ncclComm_t*, int, ncclUniqueId, int)
 MOCK_DECL(ncclResult_t, CommDestroy, ncclComm_t)
+MOCK_DECL(ncclResult_t, CommAbort, ncclComm_t)
 MOCK_DECL(const char*, GetErrorString, ncclResult_t)
 MOCK_DECL(ncclResult_t, AllReduce, const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t)
 MOCK_DECL(ncclResult_t, AllGather, const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t)
@@ -91,6 +94,7 @@ Rccl load_rccl() {
   r.GetUniqueId = mockrccl_GetUniqueId;
   r.CommInitRank = mockrccl_CommInitRank;
   r.CommDestroy = mockrccl_CommDestroy;
+  r.CommAbort = mockrccl_CommAbort;
   r.GetErrorString = mockrccl_GetErrorString;
   r.AllReduce = mockrccl_AllReduce;
   r.AllGather = mockrccl_AllGather;
@@ -131,6 +135,7 @@ Rccl load_rccl() {
   get(r.GroupStart, "ncclGroupStart");
   get(r.GroupEnd, "ncclGroupEnd");
   r.ok = all;
+  r.CommAbort = reinterpret_cast<ncclResult_t (*)(ncclComm_t)>(dlsym(h, "ncclCommAbort"));
   return r;
 }
 #endif
@@ -173,9 +178,16 @@ struct Comm {
   bool out_busy[3] = {}, in_busy[2] = {};
   uint64_t k = 0;  // launched windows (groups) so far
   DevMem d_cnt;    // count exchange and reductions: 2 x 8 u64
-  uint64_t* h_cnt = nullptr;  // pinned: [0..8) sent, [8..16) received (+ [16] its sequence word),
-                              // [17] reduction result
-  uint64_t cnt_seq = 0;       // sequence of the received counts published into h_cnt[16]
+  uint64_t* h_cnt = nullptr;  // pinned, coherent and mapped (the device publishes into it from a running
+                              // kernel): [0..8) sent, [8..8 + nranks) received + their sequence word,
+                              // [17] reduction result, [18] its sequence word
+  uint64_t cnt_seq = 0;       // sequence of the received counts published into h_cnt[8 + nranks]
+  uint64_t red_seq = 0;       // sequence of the reduction results published into h_cnt[18]
+  hipEvent_t ev_red = nullptr;  // after the last reduction's publish
+  // TGSIM_COMM_TIMEOUT_MS: how long the host waits for a collective whose peers may have stopped
+  // (a rank that died before the count all-to-all leaves the others' RCCL kernels waiting forever)
+  uint64_t timeout_ms = 300000;
+  bool timed_out = false;  // a collective never completed: the communicator is aborted, not drained
   hipEvent_t ev_cnt = nullptr;  // after the last count all-to-all's publish (tells a fault from a slow step)
   uint64_t route1_cap[3] = {};  // TGSIM_COMM_ROUTE1: the capacity-sized chunk of out[j]
   uint64_t exchanged = 0, max_count = 0, slot_cap = 0;
@@ -213,6 +225,12 @@ void comm_free(void* p) {
   Comm* C = static_cast<Comm*>(p);
   if (!C) return;
   (void)hipSetDevice(C->dev);
+  if (C->timed_out && C->nc && C->R->CommAbort) {
+    // a collective on xs waits for a peer that will never come: abort the communicator (its kernels
+    // leave), and only then drain the stream
+    (void)C->R->CommAbort(C->nc);
+    C->nc = nullptr;
+  }
   if (C->xs) (void)hipStreamSynchronize(C->xs);
   if (C->nc) (void)C->R->CommDestroy(C->nc);
   for (auto& b : C->out) b.release();
@@ -226,6 +244,7 @@ void comm_free(void* p) {
     if (e) (void)hipEventDestroy(e);
   if (C->ev_sig) (void)hipEventDestroy(C->ev_sig);
   if (C->ev_cnt) (void)hipEventDestroy(C->ev_cnt);
+  if (C->ev_red) (void)hipEventDestroy(C->ev_red);
   if (C->h_cnt) (void)hipHostFree(C->h_cnt);
   if (C->xs) (void)hipStreamDestroy(C->xs);
   delete C;
@@ -266,31 +285,48 @@ int exchange(Comm* C, const uint8_t* out, uint8_t* in, const uint64_t* send, con
   return 0;
 }
 
-// Spins until the count all-to-all's publish of the received counts (h_cnt[8..8+nranks), sequence
-// word h_cnt[8 + nranks]); the event after it tells a fault from a slow exchange.
-int wait_counts(Comm* C) {
-  uint64_t* w = C->h_cnt + 8 + C->nranks;
+// Spins until the device publishes `want` into the pinned word (system-scope release), bounded by
+// TGSIM_COMM_TIMEOUT_MS: a peer rank that stopped before the collective leaves it waiting forever, so
+// the rank fails with -ETIMEDOUT (rank and window in tgsim_last_error) instead of hanging; the event
+// recorded after the publish tells a fault from a slow exchange.
+int wait_word(Comm* C, const uint64_t* w, uint64_t want, hipEvent_t ev, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 1;; ++it) {
-    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == C->cnt_seq) return 0;
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == want) return 0;
     if ((it & 255) == 0) {
-      const hipError_t q = hipEventQuery(C->ev_cnt);
+      const hipError_t q = hipEventQuery(ev);
       if (q == hipSuccess) {
-        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == C->cnt_seq) return 0;
-        return fail(C, -EIO, "comm: the count all-to-all finished without publishing");
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == want) return 0;
+        return fail(C, -EIO, "comm: the %s finished without publishing", what);
       }
-      if (q != hipErrorNotReady) return fail(C, -EIO, "comm: count all-to-all: %s", hipGetErrorString(q));
+      if (q != hipErrorNotReady) return fail(C, -EIO, "comm: %s: %s", what, hipGetErrorString(q));
+      const uint64_t ms = static_cast<uint64_t>(
+          std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count());
+      if (ms >= C->timeout_ms) {
+        C->timed_out = true;
+        return fail(C, -ETIMEDOUT, "comm: rank %d of %d waited %llu ms for the %s of window %llu (a peer rank "
+                    "stopped?); the communicator is aborted at tgsim_destroy", C->rank, C->nranks,
+                    static_cast<unsigned long long>(ms), what, static_cast<unsigned long long>(C->k));
+      }
       sched_yield();
     }
   }
 }
 
-// Sum (or max) of one u64 over the ranks, on the exchange stream; the host waits for it.
+// The count all-to-all's publish of the received counts (h_cnt[8..8+nranks), sequence word
+// h_cnt[8 + nranks]).
+int wait_counts(Comm* C) { return wait_word(C, C->h_cnt + 8 + C->nranks, C->cnt_seq, C->ev_cnt, "count all-to-all"); }
+
+// Sum (or max) of one u64 over the ranks, on the exchange stream; the result is published to pinned
+// memory behind it and the host spins on its sequence word (bounded, as above).
 int allreduce_u64(Comm* C, const void* dev_src, uint64_t* result, ncclRedOp_t op) {
-  CNCCL(C->R->AllReduce(dev_src, C->d_cnt.p + 24 * sizeof(uint64_t), 1, ncclUint64, op, C->nc, C->xs));
-  CHIP(hipMemcpyAsync(&C->h_cnt[17], C->d_cnt.p + 24 * sizeof(uint64_t), sizeof(uint64_t), hipMemcpyDeviceToHost,
-                      C->xs));
-  CHIP(hipStreamSynchronize(C->xs));
-  *result = C->h_cnt[17];
+  const uint64_t* red = reinterpret_cast<const uint64_t*>(C->d_cnt.p + 24 * sizeof(uint64_t));
+  CNCCL(C->R->AllReduce(dev_src, const_cast<uint64_t*>(red), 1, ncclUint64, op, C->nc, C->xs));
+  launch_publish_words(red, 1, C->h_cnt + 17, ++C->red_seq, C->xs);
+  CHIP(hipGetLastError());
+  CHIP(hipEventRecord(C->ev_red, C->xs));
+  CRC(wait_word(C, C->h_cnt + 18, C->red_seq, C->ev_red, "all-reduce"));
+  *result = __atomic_load_n(C->h_cnt + 17, __ATOMIC_ACQUIRE);
   return 0;
 }
 
@@ -341,7 +377,12 @@ int comm_build(Comm* C, const void* id) {
   for (auto& ev : C->ev_routed) CHIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   CHIP(hipEventCreateWithFlags(&C->ev_sig, hipEventDisableTiming));
   CHIP(hipEventCreateWithFlags(&C->ev_cnt, hipEventDisableTiming));
-  CHIP(hipHostMalloc(reinterpret_cast<void**>(&C->h_cnt), 32 * sizeof(uint64_t), hipHostMallocDefault));
+  CHIP(hipEventCreateWithFlags(&C->ev_red, hipEventDisableTiming));
+  // coherent and mapped, as every other word the device publishes to the host: a system-scope release
+  // on coarse-grained memory would not order the count stores before their sequence word
+  CHIP(hipHostMalloc(reinterpret_cast<void**>(&C->h_cnt), 32 * sizeof(uint64_t),
+                     hipHostMallocCoherent | hipHostMallocMapped));
+  if (const char* to = getenv("TGSIM_COMM_TIMEOUT_MS")) C->timeout_ms = std::max<uint64_t>(1, strtoull(to, nullptr, 10));
   CHIP(C->d_cnt.ensure(32 * sizeof(uint64_t)));
   ncclUniqueId uid;
   memcpy(&uid, id, TGSIM_COMM_ID_BYTES);
@@ -399,7 +440,8 @@ int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
   slot->state = C;
   slot->free_fn = comm_free;
   // at one rank no RCCL kernel competes with the simulation for CU slots, so fused groups keep
-  // their persistent grid (with more ranks the grid turns over to let the exchange in)
+  // their whole persistent grid; with more ranks it holds kRoutedGridPct of the resident workgroups,
+  // the rest left free for RCCL's kernels and the group delivery
   engine_persist_routed(e, nranks == 1 ? 100u : kRoutedGridPct);
   return 0;
 }
@@ -407,6 +449,7 @@ int tgsim_comm_init(void* e, const void* id, int rank, int nranks) {
 int tgsim_comm_launch(void* e, uint32_t n_ticks) {
   Comm* C = comm_of(e);
   if (!C) return e ? engine_fail(e, -EINVAL, "comm_launch: no communicator (tgsim_comm_init)") : -EINVAL;
+  if (C->timed_out) return -ETIMEDOUT;  // a collective never completed (tgsim_last_error says which)
   if (n_ticks == 0) return -EINVAL;
   if (C->launched) return engine_fail(e, -EBUSY, "comm_launch: the launched window is not finished (tgsim_comm_finish)");
   CHIP(hipSetDevice(C->dev));
@@ -442,6 +485,7 @@ int tgsim_comm_launch(void* e, uint32_t n_ticks) {
 int tgsim_comm_finish(void* e) {
   Comm* C = comm_of(e);
   if (!C) return e ? engine_fail(e, -EINVAL, "comm_finish: no communicator (tgsim_comm_init)") : -EINVAL;
+  if (C->timed_out) return -ETIMEDOUT;  // a collective never completed (tgsim_last_error says which)
   if (!C->launched) return engine_fail(e, -EINVAL, "comm_finish: no launched window (tgsim_comm_launch)");
   CHIP(hipSetDevice(C->dev));
   C->launched = false;
@@ -500,6 +544,7 @@ int tgsim_comm_step(void* e, uint32_t n_ticks) {
 int tgsim_comm_run(void* e, uint32_t n_ticks, uint32_t n_steps, uint32_t fuse, uint64_t slot_cap) {
   Comm* C = comm_of(e);
   if (!C) return e ? engine_fail(e, -EINVAL, "comm_run: no communicator (tgsim_comm_init)") : -EINVAL;
+  if (C->timed_out) return -ETIMEDOUT;  // a collective never completed (tgsim_last_error says which)
   if (n_ticks == 0 || fuse == 0 || fuse > kFuseMax) return -EINVAL;
   if (C->launched) return engine_fail(e, -EBUSY, "comm_run: a launched window is not finished (tgsim_comm_finish)");
   if (!n_steps) return 0;
@@ -581,6 +626,7 @@ int tgsim_comm_run(void* e, uint32_t n_ticks, uint32_t n_steps, uint32_t fuse, u
 int tgsim_comm_barrier(void* e, uint32_t state, uint64_t target) {
   Comm* C = comm_of(e);
   if (!C) return e ? engine_fail(e, -EINVAL, "comm_barrier: no communicator (tgsim_comm_init)") : -EINVAL;
+  if (C->timed_out) return -ETIMEDOUT;  // a collective never completed (tgsim_last_error says which)
   if (state >= TGSIM_SYNC_STATES) return -EINVAL;
   CHIP(hipSetDevice(C->dev));
   void* table = nullptr;

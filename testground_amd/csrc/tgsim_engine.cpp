@@ -292,7 +292,8 @@ struct tgsim_engine_s {
     uint64_t retired_call = 0;
   };
   std::vector<GenWindow> gen_q;   // device-generated traffic, one window per future step
-  uint64_t sim_calls = 0;         // run_sim and fused-group calls so far (GenWindow::retired_call)
+  uint64_t sim_calls = 0;         // run_sim and fused-group calls that enqueued their simulate kernel
+                                  // (behind its emit set's last reader) so far (GenWindow::retired_call)
   std::vector<GenWindow> gen_free;
   uint64_t gen_q_ticks = 0;
   uint64_t n_in = 0;
@@ -844,7 +845,9 @@ int resolve_gen(Eng* E, Eng::GenWindow& w) {
 // fused group's: always-wait, since its group delivery is awaited only by the group two later).
 constexpr uint64_t kRetiredByGroup = ~0ull >> 2;
 int retire_gen(Eng* E, Eng::GenWindow&& w, bool by_group = false) {
-  w.retired_call = by_group ? kRetiredByGroup : E->sim_calls;
+  // the call retiring it is numbered sim_calls + 1 once its simulate kernel is enqueued (a call that
+  // fails before that never counts, so the stamp can only run ahead: more waiting, never less)
+  w.retired_call = by_group ? kRetiredByGroup : E->sim_calls + 1;
   E->gen_free.push_back(std::move(w));
   return 0;
 }
@@ -867,18 +870,20 @@ int take_gen(Eng* E, Eng::GenWindow* w) {
   return 0;
 }
 
-// After a late receipt every generated window still queued is dropped (its buffers go back to
-// gen_free), so a caller that retries finds no half-generated window; the error stays (gossip_late).
-void drop_gen(Eng* E) {
-  for (auto& w : E->gen_q) (void)retire_gen(E, std::move(w));
-  E->gen_q.clear();
-  E->gen_q_ticks = 0;
+// After a late receipt the late window gen_q[from] and every window queued after it are dropped
+// (their buffers go back to gen_free); the valid windows before it stay queued and can still be
+// stepped (include/tgsim.h); the error stays (gossip_late).
+void drop_gen(Eng* E, size_t from = 0) {
+  for (size_t i = from; i < E->gen_q.size(); ++i) {
+    E->gen_q_ticks -= E->gen_q[i].ticks;
+    (void)retire_gen(E, std::move(E->gen_q[i]));
+  }
+  E->gen_q.erase(E->gen_q.begin() + static_cast<std::ptrdiff_t>(std::min(from, E->gen_q.size())), E->gen_q.end());
 }
 
 int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   int erc = check_sim_error(E);
   if (erc) return erc;
-  E->sim_calls++;
   erc = harvest_timing(E, false);
   if (erc) return erc;
   if (!E->gen_q.empty()) {
@@ -995,6 +1000,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   }
   else launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
+  E->sim_calls++;  // behind the wait for this emit pair's last reader (ev_local): take_gen's count
   HIPCHK(hipEventRecord(ev1, E->st));
   if (sparse) {
     HIPCHK(hipMemcpyAsync(E->h_work, E->d_work.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
@@ -1364,7 +1370,6 @@ struct GroupRoute {  // a sharded group: the windows' records routed into slotte
 int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = nullptr) {
   int rc = check_sim_error(E);
   if (rc) return rc;
-  E->sim_calls++;
   rc = harvest_timing(E, false);
   if (rc) return rc;
   rc = flush_config(E);  // effective from the first window, as for g tgsim_step calls
@@ -1456,6 +1461,7 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
                                            : E->fused_wgs;
   launch_sim_fused(a, f, wgs, E->st);
   HIPCHK(hipGetLastError());
+  E->sim_calls++;  // behind the wait for set p's last readers (ev_fgrp): take_gen's count
   HIPCHK(hipEventRecord(ev1, E->st));
   E->ev_pending.push_back({ev0, ev1, g});
   E->step_no += g;
@@ -2009,10 +2015,11 @@ int tgsim_gen_gossip(void* e, uint32_t n_ticks) {
   if (E->gossip_late)
     return E->fail(-EINVAL, "gossip: a receipt preceded an earlier window (tgsim_gossip_init starts a new flood)");
   HIPCHK(hipSetDevice(E->dev));
-  for (auto& q : E->gen_q) {  // a window still unsized is sized (and written) before this one runs
-    int rc = resolve_gen(E, q);
+  for (size_t i = 0; i < E->gen_q.size(); ++i) {  // a window still unsized is sized (and written) before
+                                                  // this one runs
+    int rc = resolve_gen(E, E->gen_q[i]);
     if (rc) {
-      if (E->gossip_late) drop_gen(E);
+      if (E->gossip_late) drop_gen(E, i);  // the late window and any after it; the earlier ones stay
       return rc;
     }
   }
@@ -2445,6 +2452,8 @@ int64_t tgsim_debug_carry_bytes(void* e) {
   }
   return static_cast<int64_t>(q - skipped);
 }
+
+int64_t tgsim_debug_exec_faults(void) { return exec_faults(); }
 
 int64_t tgsim_debug_fused_windows(void* e) {
   Eng* E = as_eng(e);

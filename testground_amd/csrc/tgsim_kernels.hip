@@ -12,6 +12,7 @@
 //                  all-to-all; plain compaction on one GPU).
 //   k_dst_*        K5: counting sort of deliveries by destination, then a per-destination sort
 //                  by (t, src, seq, clone-first).
+#include <errno.h>
 #include "tgsim_launch.h"
 
 namespace tgsim {
@@ -95,13 +96,45 @@ static_assert(sizeof(SimLdsT<kHeapCap>) <= 65536, "simulate workgroup LDS");
 
 constexpr uint32_t kFvPass = 0xFFu;
 
+// Cross-lane guards (TGSIM_CHECK builds only): a readlane must name an active
+// lane, and the DPP scans, wave shuffles and the sorted-count search read every lane, so they need
+// the whole wave active.  Round 4's fault was exactly such a read inside a lane-divergent branch.
+// A violation is counted in tg_exec_faults (read by tgsim_debug_exec_faults) and the first few are
+// printed by the first active lane of the offending wave.
+#ifdef TGSIM_CHECK
+__device__ unsigned int tg_exec_faults;
+__device__ __noinline__ void tg_exec_fault(const char* what, uint64_t exec, uint32_t l) {
+  const uint32_t me = __lane_id();
+  if (me == (uint32_t)__builtin_ctzll(exec)) {
+    const unsigned int k = atomicAdd(&tg_exec_faults, 1u);
+    if (k < 16)
+      printf("EXEC CHECK %s: exec %016llx lane %u (block %u)\n", what, (unsigned long long)exec, l, blockIdx.x);
+  }
+}
+__device__ __forceinline__ void tg_full_exec(const char* what) {
+  const uint64_t x = __builtin_amdgcn_read_exec();
+  if (x != ~0ull) tg_exec_fault(what, x, 64u);
+}
+__device__ __forceinline__ void tg_lane_live(const char* what, uint32_t l) {
+  const uint64_t x = __builtin_amdgcn_read_exec();
+  if (l >= 64u || !(x >> l & 1ull)) tg_exec_fault(what, x, l);
+}
+#define TG_FULL_EXEC(what) tg_full_exec(what)
+#define TG_LANE_LIVE(what, l) tg_lane_live(what, l)
+#else
+#define TG_FULL_EXEC(what) ((void)0)
+#define TG_LANE_LIVE(what, l) ((void)0)
+#endif
+
 __device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l) {
+  TG_LANE_LIVE("readlane", l);
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
   return ((uint64_t)readlane32((uint32_t)(v >> 32), l) << 32) | readlane32((uint32_t)v, l);
 }
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  TG_FULL_EXEC("shfl64");
   const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
   return ((uint64_t)hi << 32) | lo;
 }
@@ -112,6 +145,7 @@ __device__ __forceinline__ uint32_t ballot_count(bool p) { return (uint32_t)__po
 // Lanes without a source lane read the identity.
 template <int CTRL, int ROWS>
 __device__ __forceinline__ uint32_t dpp(uint32_t id, uint32_t v) {
+  TG_FULL_EXEC("dpp scan");
   return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, ROWS, 0xF, false);
 }
 template <int CTRL, int ROWS>
@@ -174,6 +208,7 @@ __device__ __forceinline__ uint64_t scan_min_u64(uint64_t v) {
 
 // Count of the 64 lane values v (sorted ascending over lanes) that are <= t, for every lane's t.
 __device__ __forceinline__ uint32_t count_le_sorted_u32(uint32_t v, uint32_t t) {
+  TG_FULL_EXEC("count_le_sorted");
   uint32_t lo = 0;
 #pragma unroll
   for (uint32_t s = 32; s; s >>= 1)
@@ -253,6 +288,7 @@ __device__ __forceinline__ uint32_t filter(const SimArgs& a, const SrcParams& p,
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+  TG_FULL_EXEC("wave_sum");
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t lo = __shfl_xor((uint32_t)v, o, 64);
@@ -292,6 +328,7 @@ __device__ __forceinline__ void stamp(const SimArgs& a, uint32_t wg, uint32_t la
 // ds_bpermute for J = 32.
 template <uint32_t J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  TG_FULL_EXEC("xor_lane");
   uint32_t r;
   if constexpr (J == 1) r = dpp<0xB1, 0xF>(0u, v);       // quad_perm [1, 0, 3, 2]
   else if constexpr (J == 2) r = dpp<0x4E, 0xF>(0u, v);  // quad_perm [2, 3, 0, 1]
@@ -557,6 +594,7 @@ struct SimQueue {
         const uint32_t cx = (uint32_t)__popcll(mex);
         {  // taken items to lanes [gx, gx + cx) (forward permute; the others fill the rest)
           const uint32_t to = (ex ? rx : gx + cx + (uint32_t)__popcll(~mex & below)) & (kWave - 1);
+          TG_FULL_EXEC("ds_permute");
           const uint4 pv = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.x),
                                       (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.y),
                                       (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.z),
@@ -568,6 +606,7 @@ struct SimQueue {
           const uint64_t ma = __ballot(st);
           const uint32_t to = (st ? (uint32_t)__popcll(ma & below)
                                   : (uint32_t)__popcll(ma) + (uint32_t)__popcll(~ma & below)) & (kWave - 1);
+          TG_FULL_EXEC("ds_permute");
           av = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.x),
                           (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.y),
                           (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.z),
@@ -577,6 +616,7 @@ struct SimQueue {
         const bool hole = ex && k >= nx;
         const uint64_t mh = __ballot(hole);
         const uint32_t src = (gh + (uint32_t)__popcll(mh & below)) & (kWave - 1);
+        TG_FULL_EXEC("ds_permute");
         const uint4 fill = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)av.x),
                                       (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)av.y),
                                       (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)av.z),
@@ -669,6 +709,7 @@ struct SimQueue {
       // key order across the lanes, checked against each item's predecessor in one pass
       const uint64_t below = m & ((1ull << lane) - 1);
       const uint32_t prev = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
+      TG_FULL_EXEC("ds_permute");
       const uint4 pk = make_uint4((uint32_t)__shfl(it.x, (int)prev, 64), (uint32_t)__shfl(it.y, (int)prev, 64),
                                   (uint32_t)__shfl(it.z, (int)prev, 64), 0u);
       if (!__ballot(has && below && !item_lt(pk, it))) {
@@ -687,6 +728,7 @@ struct SimQueue {
     // lane r receives the position of the rank-r item through a forward permute (the LDS
     // crossbar, no LDS allocation); lanes without an item take ranks nm.., so every lane gets one
     const uint32_t to = has ? rank : nm + (uint32_t)__popcll(~m & ((1ull << lane) - 1));
+    TG_FULL_EXEC("ds_permute");
     const uint32_t sp_all = (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)(has ? pos : 0xFFFFFFFFu));
     uint32_t kL = 0;  // new items placed by moving the ring and the queue prefix down
     if (nm <= 8) {
@@ -1611,6 +1653,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     // FIFO: no candidate before its predecessor (the candidate before it, or the last item so far)
     const uint64_t bc = mc & below;
     const uint32_t pl = bc ? 63u - (uint32_t)__builtin_clzll(bc) : lane;
+    TG_FULL_EXEC("ds_permute");
     uint4 prev = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.x),
                             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.y),
                             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.z), 0u);
@@ -1945,6 +1988,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
       return;
     }
     const uint32_t to = (f ? ns + (uint32_t)__popcll(m & below) : ns + k + (uint32_t)__popcll(~m & below)) & (kWave - 1);
+    TG_FULL_EXEC("ds_permute");
     const uint4 pv = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.x),
                                 (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.y),
                                 (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)v.z),
@@ -1993,6 +2037,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   if (fifo && mc) {
     const uint64_t bc = mc & below;  // the candidate before each candidate, or the queue's last item
     const uint32_t pl = bc ? 63u - (uint32_t)__builtin_clzll(bc) : lane;
+    TG_FULL_EXEC("ds_permute");
     uint4 prev = make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.x),
                             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.y),
                             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)io.z), 0u);
@@ -2088,6 +2133,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
       rank += (hs && (item_lt(o, x) || (!item_lt(x, o) && j < lane))) ? 1u : 0u;
     }
     const uint32_t to = (hs ? rank : lane) & (kWave - 1);
+    TG_FULL_EXEC("ds_permute");
     x = make_uint4((uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.x),
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.y),
                    (uint32_t)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x.z),
@@ -3650,6 +3696,17 @@ void launch_scan_w(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* bloc
 
 void launch_local_scatter_group(const GroupDeliver& g, uint32_t n_win, hipStream_t st) {
   if (g.n_src && n_win) hipLaunchKernelGGL(k_local_scatter_group, dim3(n_win * g.n_src), dim3(64), 0, st, g);
+}
+
+// Cross-lane guard violations so far (TGSIM_CHECK builds; -ENOSYS in the product build).
+int64_t exec_faults() {
+#ifdef TGSIM_CHECK
+  unsigned int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(tg_exec_faults), sizeof n) != hipSuccess) return -EIO;
+  return n;
+#else
+  return -ENOSYS;
+#endif
 }
 
 

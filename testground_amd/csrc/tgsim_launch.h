@@ -103,6 +103,8 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
 void launch_scan_w(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
                    hipStream_t st, uint64_t* pos);
 void launch_local_scatter_group(const GroupDeliver& g, uint32_t n_win, hipStream_t st);
+// TGSIM_CHECK builds: cross-lane helper calls whose source lanes were inactive (-ENOSYS otherwise)
+int64_t exec_faults();
 void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                         tgsim_delivery* out, hipStream_t st);
 

@@ -35,6 +35,9 @@ def test_two_ranks_spawned_on_cpu():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert sorted(x["rank"] for x in lines) == [0, 1]
     assert all(x["world"] == 2 and x["gpus"] == 2 and x["launched_by_bench"] for x in lines)
+    # the host group is gloo, so each rank holds one RCCL communicator (the
+    # engine's own); the group was really created (and barriered) by the launched ranks
+    assert all(x["host_group"] == "gloo" for x in lines)
     # the headline at N = 2 is BASELINE configs[2] itself: 10,000 instances in total, split over the
     # ranks; the weak-scaling run and the 1M-peer flood ride along
     for x in lines:

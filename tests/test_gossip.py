@@ -156,6 +156,71 @@ def test_gossip_late_receipt_is_sticky_on_oracle(make_oracle):
     _late_run(make_oracle(200, lookahead_ns=wl.GOSSIP_MIN_LAT))
 
 
+def _late_run_ahead(e, depth):
+    """windows generated `depth` ahead of the steps (the bench's rotation), twice the
+    lookahead long, so a receipt precedes a generated window.  The late window is reported by the
+    call that resolves it (its step, or the next gen_gossip); it and anything queued after it are
+    dropped, the valid windows before it stay queued and step normally.  Returns every call's
+    outcome, with each step's deliveries."""
+    import hashlib
+
+    wl.configure_gossip(e, 200)
+    e.gossip_init(n_floods=2, degree=4, msg_len=512, start_tick=0)
+    W = 2 * wl.gossip_window_ticks(e)
+    ev, failed_at = [], None
+
+    def call(kind, fn):
+        try:
+            fn()
+        except EngineError as err:
+            msg = str(err)
+            ev.append((kind, "late" if "precedes the window" in msg else "sticky" if "preceded an earlier" in msg else msg))
+            return False
+        if kind == "step":
+            d = e.drain()
+            ev.append((kind, len(d), hashlib.sha256(d.tobytes()).hexdigest()[:16], e.stats()["now_tick"]))
+        else:
+            ev.append((kind, "ok"))
+        return True
+
+    for _ in range(depth):
+        call("gen", lambda: e.gen_gossip(W))
+    for k in range(30):
+        ok = call("step", lambda: e.step(W))
+        ok = call("gen", lambda: e.gen_gossip(W)) and ok
+        if not ok and failed_at is None:
+            failed_at = k
+        if failed_at is not None and k >= failed_at + depth + 1:
+            break
+    assert failed_at is not None, "no late receipt in 30 windows"
+    return ev
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_gossip_late_receipt_ahead_on_oracle(make_oracle, depth):
+    ev = _late_run_ahead(make_oracle(200, lookahead_ns=wl.GOSSIP_MIN_LAT), depth)
+    first = next(i for i, x in enumerate(ev) if x[1] == "late")
+    # every window generated before the late one was stepped, with deliveries, before the report or after it
+    steps_ok = [x for x in ev if x[0] == "step" and x[1] not in ("late", "sticky")]
+    assert len(steps_ok) >= depth and all(isinstance(x[1], int) for x in steps_ok)
+    assert ev.count(("gen", "late")) + ev.count(("step", "late")) == 1, ev  # reported once
+    assert all(x[1] == "sticky" for x in ev[first + 1:] if x[0] == "gen"), ev  # then sticky
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [2, 3])
+def test_gossip_late_receipt_ahead_gpu_equals_oracle(make_oracle, depth):
+    """The same calls on the HIP engine and the oracle: the same outcome at every call (which call
+    reports the late window, which windows still step) and the same deliveries at every step."""
+    from testground_amd.engine import Engine
+
+    cpu = _late_run_ahead(make_oracle(200, lookahead_ns=wl.GOSSIP_MIN_LAT), depth)
+    gpu_e = Engine(200, lookahead_ns=wl.GOSSIP_MIN_LAT)
+    gpu = _late_run_ahead(gpu_e, depth)
+    gpu_e.close()
+    assert gpu == cpu
+
+
 def test_gossip_init_contract(make_oracle):
     e = make_oracle(10)
     for bad in (dict(n_floods=0), dict(n_floods=65), dict(degree=0), dict(degree=65), dict(msg_len=0)):

@@ -191,3 +191,53 @@ def test_ranks_epochs_barrier(lib):
         assert len(d) == len(dr) > 0 and (d == dr).all(), f"epoch {k}"
         assert all(per_rank[r][k][1] for r in range(2)), f"epoch {k}: the barrier released"
         assert not any(per_rank[r][k][2] for r in range(2)), f"epoch {k}: one more than signalled"
+
+
+@pytest.mark.parametrize("where", ["count all-to-all", "all-reduce"])
+def test_rank_that_stops_times_out_peers(lib, monkeypatch, where):
+    """A rank that stops before a collective (here: returns before its count all-to-all, or before
+    the barrier's all-reduce) must not hang the others: their exchange stream waits at the mock's
+    gate exactly where RCCL's kernel would, and the engine's bounded host wait
+    (TGSIM_COMM_TIMEOUT_MS) fails them with -ETIMEDOUT naming the rank and the window; every later
+    call fails fast, and destroying the engine aborts the communicator instead of draining it."""
+    import errno
+    import time
+
+    from testground_amd.engine import EngineError
+
+    monkeypatch.setenv("TGSIM_COMM_TIMEOUT_MS", "1500")
+    n, ticks = 300, 1000
+    bounds = [0, 150, 300]
+
+    def rank(r, e):
+        wl.configure_storm(e, n)
+        e.gen_storm(0.5, ticks)
+        if where == "all-reduce":  # one good window first, then the barrier the other rank skips
+            e.comm_step(ticks)
+            e.signal_async(1, bounds[r + 1] - bounds[r])
+        if r == 1:
+            return None  # stops here: never posts the collective
+        t0 = time.monotonic()
+        try:
+            if where == "count all-to-all":
+                e.comm_step(ticks)
+            else:
+                e.comm_barrier(1, n)
+        except EngineError as ex:
+            waited = time.monotonic() - t0
+            try:  # the communicator is unusable from now on
+                e.comm_step(ticks)
+                again = 0
+            except EngineError as ex2:
+                again = ex2.code
+            return ex.code, ex.msg, waited, again
+        return "no error", "", time.monotonic() - t0, 0
+
+    t0 = time.monotonic()
+    per_rank, _ = _ranks(lib, n, bounds, rank)
+    assert time.monotonic() - t0 < 60, "a rank hung instead of timing out"
+    code, msg, waited, again = per_rank[0]
+    assert code == -errno.ETIMEDOUT, (code, msg)
+    assert 1.4 <= waited < 30, waited
+    assert f"rank 0 of 2 waited" in msg and where in msg and "window" in msg, msg
+    assert again == -errno.ETIMEDOUT
