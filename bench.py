@@ -85,6 +85,8 @@ def parse(argv=None):
                    help="sharded storm: exchange exact record counts every step instead of fixed-size chunks")
     p.add_argument("--no-1m", action="store_true",
                    help="storm: skip the at_1M_peers gossip run that accompanies the headline line")
+    p.add_argument("--no-variants", action="store_true",
+                   help="storm: skip the at_subcapacity and at_epochs runs that accompany the headline line")
     p.add_argument("--gossip-1m-peers", type=int, default=1_000_000,
                    help="total peers of the at_1M_peers run (split over the ranks)")
     p.add_argument("--launch-check", action="store_true",
@@ -143,7 +145,7 @@ def kernel_sha16() -> str:
     return hashlib.sha256((ROOT / "testground_amd" / "csrc" / "tgsim_kernels.hip").read_bytes()).hexdigest()[:16]
 
 
-def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds):
+def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds, shapes=None):
     """The CPU oracle (a 'port' of the reference semantics) timed on this host, on a bounded sample
     of the same workload: single thread, plus (storm/epochs) one oracle shard per thread."""
     from testground_amd import abi, workloads
@@ -192,11 +194,12 @@ def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds):
                            f"time; {sum(p for p, _, _ in res)} packets, {wall:.1f} s wall"),
                 "single_thread": one}
     sample_src = min(1000, peers_total)
+    shapes = shapes or a.shapes
 
     def leg(lo, hi, seconds):
         """One oracle shard [lo, hi) of the same workload stepped for ~seconds of step time."""
         e = CABIEngine(lib, "tgo_", peers_total, shard=(lo, hi))
-        workloads.configure_storm(e, peers_total, open_links=a.shapes == "open")
+        workloads.configure_storm(e, peers_total, open_links=shapes == "open")
         busy, steps = 0.0, 0
         while busy < seconds:
             if workload == "epochs" and steps:
@@ -234,12 +237,13 @@ def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds):
     return {"value": pkts / busy, "unit": "packets/s", "cores": 1, "kind": "port", "sample": sample}
 
 
-def load_pmc(workload, window, peers, lam, shapes="storm"):
-    """HBM traffic of k_sim from the committed PMC passes (rocprofv3 cannot run inside the bench).
-    Reported only when the file was collected on the same k_sim source (sha of tgsim_kernels.hip)
-    and the same workload configuration; the line names the file and its provenance either way."""
+def load_pmc(workload, window, peers, lam, shapes="storm", kind="k_sim"):
+    """HBM traffic of k_sim (kind "delivery": of the delivery kernels) from the committed PMC passes
+    (rocprofv3 cannot run inside the bench).  Reported only when the file was collected on the same
+    kernel source (sha of tgsim_kernels.hip) and the same workload configuration; the line names the
+    file and its provenance either way."""
     tag = workload if workload != "storm" or shapes == "storm" else f"storm_{shapes}"
-    f = ROOT / "profiles" / ("pmc_k_sim.json" if tag == "storm" else f"pmc_k_sim_{tag}.json")
+    f = ROOT / "profiles" / (f"pmc_{kind}.json" if tag == "storm" else f"pmc_{kind}_{tag}.json")
     src = {"file": str(f.relative_to(ROOT)), "kernel_sha16_now": kernel_sha16()}
     if not f.exists():
         return None, dict(src, status="absent")
@@ -421,12 +425,15 @@ def headline_plan(a, world):
         plan["weak_per_gpu_peers_total"] = shard_bounds(a.peers, world, False)[0]
     if a.workload == "storm" and not a.no_1m:
         plan["at_1M_peers_total"] = shard_bounds(a.gossip_1m_peers, world, True)[0]
+    if a.workload == "storm" and not a.no_variants:
+        plan["at_subcapacity_total"] = shard_bounds(a.peers, world, True)[0]
+        plan["at_epochs_total"] = shard_bounds(100_000, world, True)[0]
     plan["cpu_baseline_ranks"] = [r for r in range(world) if runs_cpu_baseline(r, not a.no_cpu)]
     return plan
 
 
 def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, local, dist, want_cpu,
-                 split=False):
+                 split=False, shapes=None):
     """Builds one engine shard on this rank, brings the workload to its timed state, times `steps`
     steps (barrier + synchronize on both sides, max over ranks) and returns the rank-0 result object
     (None on the other ranks).  `peers` instances per rank (weak scaling), or with split=True
@@ -439,6 +446,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     from testground_amd.network import configs_array
 
     sharded = dist is not None
+    shapes = shapes or a.shapes
     peers_total, bounds = shard_bounds(peers, world, split)
     lo, hi = bounds[rank], bounds[rank + 1]
     peers = hi - lo  # this rank's sources
@@ -448,8 +456,8 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     t_setup = time.perf_counter()
     if workload == "gossip":
         workloads.configure_gossip(eng, peers_total)
-    elif a.shapes in ("storm", "open"):
-        workloads.configure_storm(eng, peers_total, open_links=a.shapes == "open")
+    elif shapes in ("storm", "open"):
+        workloads.configure_storm(eng, peers_total, open_links=shapes == "open")
     else:
         eng.configure_batch(np.arange(peers_total), configs_array(np.full(peers_total, 5_000_000), routing_policy=2))
     stepper = None
@@ -521,6 +529,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     s0 = eng.stats()
     x0 = stepper.exchanged_records if stepper is not None else 0
     eng.sim_kernel_ms(reset=True)
+    eng.delivery_kernel_ms(reset=True)
     c0 = eng.carry_bytes()
     # the device is idle before the barrier (the engine's own communicator and torch's never have
     # collectives in flight at once), and again after it (the barrier's kernel)
@@ -540,6 +549,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     verd = np.array([s1["by_verdict"][k] - s0["by_verdict"][k] for k in abi.VERDICT_NAMES], dtype=np.float64)
     exch = (stepper.exchanged_records - x0) if stepper is not None else 0
     sim_ms, n_launch = eng.sim_kernel_ms()
+    dv_ms, n_dv = eng.delivery_kernel_ms()
     if dist:
         t = torch.tensor([el, float(offered), float(scheduled), float(exch), *verd], dtype=torch.float64)
         mx = t.clone()
@@ -563,12 +573,13 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     qbytes = s1["queue_state_bytes"] - s0["queue_state_bytes"]
     carry = eng.carry_bytes() - c0
     slot_cap = stepper.slot_cap if stepper is not None else None
+    n_dst_rank = hi - lo
     eng.close()
     del eng, stepper
     cpu = None
     if runs_cpu_baseline(rank, want_cpu):  # the oracle on this host's cores, beside the line at every N
         cpu = cpu_baseline(a, workload, peers_total, lam, window,
-                           a.cpu_seconds if workload != "gossip" else a.cpu_seconds / 2)
+                           a.cpu_seconds if workload == "storm" else a.cpu_seconds / 2, shapes=shapes)
     if dist:  # the other ranks wait here for rank 0's CPU legs before the next collective
         torch.cuda.synchronize()
         dist.barrier()
@@ -580,7 +591,7 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     gbs = (lambda b: b / (sim_ms * 1e-3) / 1e9) if sim_ms > 0 else (lambda b: None)
     achieved = gbs(per_launch)
     frac_of = lambda b: (gbs(b) / HBM_PEAK_GBS) if sim_ms > 0 else None  # noqa: E731
-    traffic, traffic_src = load_pmc(workload, window, peers, lam, a.shapes)
+    traffic, traffic_src = load_pmc(workload, window, peers, lam, shapes)
     tot_v = max(1.0, float(verd_all.sum()))
     res = {
         "metric": METRIC,
@@ -595,11 +606,11 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
         "data": f"synthetic (device-generated {workload} traffic, Philox-keyed)",
-        "config": dict({"workload": WORKLOAD_NAMES["storm_open" if workload == "storm" and a.shapes == "open"
+        "config": dict({"workload": WORKLOAD_NAMES["storm_open" if workload == "storm" and shapes == "open"
                                                    else workload],
                         "peers_per_gpu": peers, "peers_total": peers_total,
                         **({} if workload == "gossip" else {"lambda_per_tick": lam}), "tick_ns": 1000, "window_ticks": window, "settle_sim_ms": settle * window / 1000,
-                        "shapes": a.shapes if workload == "storm" else workload,
+                        "shapes": shapes if workload == "storm" else workload,
                         "queue_limit": a.queue_limit or 1000, "packets_per_step": offered_all / steps,
                         "parallelism": f"peer-sharded x{world}" + (" (RCCL exchange path)" if sharded else ""),
                         **({"exchange": "slotted" if slot_cap else "exact", "slot_cap_records_per_rank": slot_cap,
@@ -621,6 +632,22 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
                      "per": "window (one step of --window ticks; a fused dispatch counts each of its windows)"},
         "cpu_baseline": None,
     }
+    if dv_ms > 0 and n_dv:
+        # the delivery (K5) on its own stream: histogram scan (8 B count read, 8 B offset and 8 B
+        # cursor written, 8 B cleared per destination, 8 B offsets re-read by the sort), then per
+        # record 24 B read from the emit region + 24 B scattered + 24 B read + 24 B written in
+        # destination order; per source its 4 B emit count and 8 B offset (local delivery)
+        recs_w = scheduled / max(1, steps)
+        dv_bytes = 96 * recs_w + 40 * n_dst_rank + 12 * peers
+        dv_traffic, dv_src = load_pmc(workload, window, peers, lam, shapes, kind="delivery")
+        dv_gbs = dv_bytes / (dv_ms * 1e-3) / 1e9
+        res["roofline"]["delivery"] = {
+            "kernel": "k_scan_* + k_local_scatter_ls (or k_dst_hist/k_dst_scatter) + k_dst_sort_flat (or k_dst_sort_wide)",
+            "achieved": dv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dv_gbs / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_window": dv_bytes, "records_per_window": recs_w, "span_ms_avg": dv_ms,
+            "windows": n_dv, "traffic": dv_traffic, "traffic_source": dv_src,
+            "note": "span from the first delivery kernel to the sort on the delivery stream (HIP events), "
+                    "including the time its kernels wait for CU slots beside the next simulate kernel"}
     if cpu is not None:
         res["cpu_baseline"] = cpu
         cpu["gpu_over_cpu"] = res["value"] / cpu["value"]
@@ -689,6 +716,22 @@ def main(argv=None):
                                                     "scheduled_per_s", "verdict_mix", "setup_s", "roofline",
                                                     "cpu_baseline")}
             res["at_1M_peers"]["scaling"] = "strong (1M peers in total, split over the GPUs)"
+    if a.workload == "storm" and not a.no_variants:
+        # the rest of BASELINE.json's configs on the same line, each with its own roofline and CPU
+        # baseline: the sub-capacity storm (C3's shapes at 1 Gbit/s below
+        # capacity: the variant that exercises delay, HTB and delivery at rate) and C5's epochs
+        from testground_amd.workloads import STORM_OPEN_LAMBDA
+        keys = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "scheduled_per_s", "verdict_mix",
+                "setup_s", "roofline", "cpu_baseline")
+        sub = run_workload(a, "storm", a.peers, 30, 3, 2000, STORM_OPEN_LAMBDA, world, rank, local, dist,
+                           want_cpu=not a.no_cpu, split=True, shapes="open")
+        ep = run_workload(a, "epochs", 100_000, 10, 3, 1000, 0.2, world, rank, local, dist,
+                          want_cpu=not a.no_cpu, split=True)
+        if res is not None:
+            res["at_subcapacity"] = dict({k: sub[k] for k in keys},
+                                         scaling="strong (10,000 instances in total, split over the GPUs)")
+            res["at_epochs"] = dict({k: ep[k] for k in keys},
+                                    scaling="strong (100,000 instances in total, split over the GPUs)")
     if res is not None:
         os.write(json_fd, (json.dumps(res) + "\n").encode())
     if dist:

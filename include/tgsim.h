@@ -461,6 +461,11 @@ void tgsim_udp_front_destroy(void* front);
 /* Average device time (ms) of the simulate kernel over the steps since the last reset, measured
  * with HIP events on the engine's stream. */
 double tgsim_sim_kernel_ms(void* engine, uint64_t* n_launches, int reset);
+/* The same for the delivery (K5: per-destination histogram scan, scatter, per-destination sort),
+ * from its first kernel to its sort on the delivery stream, per window delivered (a fused group's
+ * delivery counts each of its windows).  The span includes the time its kernels wait for CU slots
+ * beside the next window's simulate kernel. */
+double tgsim_delivery_kernel_ms(void* engine, uint64_t* n_windows, int reset);
 void* tgsim_stream(void* engine);
 /* Diagnostics: with TGSIM_STAMPS set at create time, the simulate kernel records 24 words per
  * workgroup (s_memrealtime at its phase boundaries, batch count, HW_ID, queue sizes); copies them

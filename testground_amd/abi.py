@@ -135,7 +135,7 @@ EXPORTS = [
     "tgsim_step_sim_counts", "tgsim_delivery_event", "tgsim_step_sim_launch_slotted", "tgsim_step_sim_release",
     "tgsim_deliver_slotted_async", "tgsim_step_sim_launch_slotted_n", "tgsim_deliver_slotted_n_async",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
-    "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
+    "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_delivery_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
     "tgsim_debug_fused_windows", "tgsim_debug_carry_bytes", "tgsim_debug_exec_faults", "tgsim_step_n",
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
     "tgsim_comm_id", "tgsim_comm_init", "tgsim_comm_step", "tgsim_comm_launch", "tgsim_comm_finish", "tgsim_comm_run", "tgsim_comm_barrier", "tgsim_comm_info",
@@ -194,6 +194,7 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("signal_async", C.c_int, vp, C.c_uint32, C.c_uint32)
     f("sync_counters", C.c_int, vp, C.POINTER(vp), C.POINTER(C.c_uint32), vp)
     f("sim_kernel_ms", C.c_double, vp, C.POINTER(C.c_uint64), C.c_int)
+    f("delivery_kernel_ms", C.c_double, vp, C.POINTER(C.c_uint64), C.c_int)
     f("stream", vp, vp)
     f("debug_stamps", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("debug_fused_windows", C.c_int64, vp)

@@ -214,6 +214,9 @@ struct tgsim_engine_s {
     uint32_t windows;
   };
   std::vector<PendingTiming> ev_pending;
+  std::vector<PendingTiming> dv_pending;  // delivery spans on dst_st (first kernel to the sort), per window
+  double dv_ms = 0;
+  uint64_t dv_windows = 0;
   std::vector<hipEvent_t> ev_pool;
   uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
   uint64_t* h_pub = nullptr;    // pinned words a scan publishes: [0] total, [1] flag, [2] sequence;
@@ -267,6 +270,7 @@ struct tgsim_engine_s {
 
   DevBuf<SrcParams> d_params;
   DevBuf<SrcState> d_state;
+  DevBuf<uint64_t> d_qhint;  // SimArgs::qhint
   DevBuf<uint8_t> d_enabled;
   DevBuf<uint32_t> d_ip;
   DevBuf<Interval> d_rules;
@@ -760,6 +764,21 @@ int harvest_timing(Eng* E, bool wait) {
     E->ev_pool.push_back(pr.second);
   }
   E->ev_pending.erase(E->ev_pending.begin(), E->ev_pending.begin() + k);
+  for (k = 0; k < E->dv_pending.size(); ++k) {
+    auto& pr = E->dv_pending[k];
+    if (wait) {
+      HIPCHK(hipEventSynchronize(pr.second));
+    } else if (hipEventQuery(pr.second) != hipSuccess) {
+      break;
+    }
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+    E->dv_ms += ms;
+    E->dv_windows += pr.windows;
+    E->ev_pool.push_back(pr.first);
+    E->ev_pool.push_back(pr.second);
+  }
+  E->dv_pending.erase(E->dv_pending.begin(), E->dv_pending.begin() + k);
   return 0;
 }
 
@@ -790,6 +809,7 @@ SimArgs base_sim_args(Eng* E) {
   SimArgs a{};
   a.params = E->d_params.p;
   a.state = E->d_state.p;
+  a.qhint = E->d_qhint.p;
   a.enabled = E->d_enabled.p;
   a.ip = E->d_ip.p;
   a.rules = E->d_rules.p;
@@ -1203,6 +1223,10 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   const uint64_t nseg = static_cast<uint64_t>(n_win) * nd;
   hipStream_t sq = E->dst_st;
   if (wait) HIPCHK(hipStreamWaitEvent(sq, wait, 0));
+  hipEvent_t dv0, dv1;  // the delivery's span on its stream (bench: roofline.delivery)
+  HIPCHK(take_event(E, &dv0));
+  HIPCHK(take_event(E, &dv1));
+  HIPCHK(hipEventRecord(dv0, sq));
   if (E->d_dcnt.cap < nseg) {
     HIPCHK(E->d_dcnt.ensure(nseg));
     HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, sq));
@@ -1265,6 +1289,8 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
     HIPCHK(hipGetLastError());
   }
+  HIPCHK(hipEventRecord(dv1, sq));
+  E->dv_pending.push_back({dv0, dv1, n_win});
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   return 0;
 }
@@ -1275,6 +1301,10 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uin
                        const uint64_t* off, uint64_t n_in, hipEvent_t released) {
   const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
+  hipEvent_t dv0, dv1;  // the delivery's span on its stream (bench: roofline.delivery)
+  HIPCHK(take_event(E, &dv0));
+  HIPCHK(take_event(E, &dv1));
+  HIPCHK(hipEventRecord(dv0, sq));
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
@@ -1318,6 +1348,8 @@ int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uin
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
     HIPCHK(hipGetLastError());
   }
+  HIPCHK(hipEventRecord(dv1, sq));
+  E->dv_pending.push_back({dv0, dv1, 1u});
   return 0;
 }
 
@@ -1759,6 +1791,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->any_patch = false;
   if ((rc = E->hip(E->d_params.ensure(E->S), "alloc params"))) return bail(rc);
   if ((rc = E->hip(E->d_state.ensure(E->S), "alloc state"))) return bail(rc);
+  if ((rc = E->hip(E->d_qhint.ensure(E->S), "alloc queue-head hints"))) return bail(rc);
   if ((rc = E->hip(E->d_enabled.ensure(E->N), "alloc enabled"))) return bail(rc);
   if ((rc = E->hip(E->d_ip.ensure(E->N), "alloc ip"))) return bail(rc);
   if ((rc = E->hip(E->d_heap.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc heap"))) return bail(rc);
@@ -1787,6 +1820,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(E->d_off.ensure(E->S + 1), "alloc off"))) return bail(rc);
   if ((rc = E->hip(E->d_in.ensure(1), "alloc in"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_state.p, 0, sizeof(SrcState) * E->S), "memset"))) return bail(rc);
+  if ((rc = E->hip(hipMemset(E->d_qhint.p, 0, sizeof(uint64_t) * E->S), "memset"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_gen_seq.p, 0, sizeof(uint32_t) * E->S), "memset"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_stats.p, 0, sizeof(unsigned long long) * kStSlots * kStatCopies), "memset")))
     return bail(rc);
@@ -1824,7 +1858,7 @@ void tgsim_destroy(void* e) {
   if (E->sy_st) (void)hipStreamDestroy(E->sy_st);
   DevBuf<int> dummy;
   (void)dummy;
-  E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
+  E->d_params.release(); E->d_state.release(); E->d_qhint.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
@@ -1837,10 +1871,11 @@ void tgsim_destroy(void* e) {
       w.off.release();
       w.in.release();
     }
-  for (auto& pr : E->ev_pending) {
-    (void)hipEventDestroy(pr.first);
-    (void)hipEventDestroy(pr.second);
-  }
+  for (auto* pend : {&E->ev_pending, &E->dv_pending})
+    for (auto& pr : *pend) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
   for (auto& grp : E->fset)
     for (auto& ls : grp) { ls.emit.release(); ls.emit_n.release(); }
   for (auto& v : E->f_lcnt) v.release();
@@ -2420,6 +2455,19 @@ double tgsim_sim_kernel_ms(void* e, uint64_t* n, int reset) {
   if (reset) {
     E->sim_ms = 0;
     E->sim_launches = 0;
+  }
+  return avg;
+}
+
+double tgsim_delivery_kernel_ms(void* e, uint64_t* n, int reset) {
+  Eng* E = as_eng(e);
+  if (!E) return -1;
+  if (hipSetDevice(E->dev) != hipSuccess || sync_stream(E)) return -1;
+  const double avg = E->dv_windows ? E->dv_ms / static_cast<double>(E->dv_windows) : 0.0;
+  if (n) *n = E->dv_windows;
+  if (reset) {
+    E->dv_ms = 0;
+    E->dv_windows = 0;
   }
   return avg;
 }

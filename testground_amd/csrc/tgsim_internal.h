@@ -126,7 +126,11 @@ struct SimArgs {
   uint64_t* g_pend;         // [s] received, not yet forwarded
   const uint64_t* g_fwd;    // [s] forwarded (stable during the step: written by k_gossip_write before it)
   uint32_t g_floods, g_degree;
-  uint64_t pad_[2];  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the
+  // [s] a lower bound of the eligibility time of source s's queue head (0: unknown), kept by the
+  // sparse kernels' FIFO path so that an idle source's check needs no read of its queue head; every
+  // other writer of SrcState stores 0 (TGSIM_HEAD_HINT builds read it)
+  uint64_t* qhint;
+  uint64_t pad_[1];  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the
                      // scheduler spilled 9 more SGPRs in k_sim_fused (155 -> 164)
 };
 static_assert(sizeof(SimArgs) == 264, "SimArgs must stay 264 B");

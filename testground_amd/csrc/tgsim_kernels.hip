@@ -242,10 +242,23 @@ __device__ __forceinline__ RecvFold recv_fold(const SimArgs& a) {
   return RecvFold{a.g_first, a.g_pend,  a.g_fwd,   a.g_floods,
                   a.g_degree, a.shard_begin, a.n_src, a.tick_ns, 1.0 / (double)a.tick_ns};
 }
+// kFwdSentinel: a peer's forwarded floods also read as receipt tick 0 in its own row (the forward
+// kernels store it), so a receipt of a forwarded flood is a no-op atomicMin and the fold needs no
+// read of the destination's forwarded mask (a scattered 4-B read, i.e. a 128-B line, per record).
+#ifndef TGSIM_GOSSIP_NOFWD
+#define TGSIM_GOSSIP_NOFWD 0
+#endif
+constexpr bool kFwdSentinel = TGSIM_GOSSIP_NOFWD != 0;
+// kHeadHint: k_sim_sparse's idle check reads SimArgs::qhint (the queue head's eligibility time the
+// FIFO path stored) beside the state, instead of the head item itself behind it.
+#ifndef TGSIM_HEAD_HINT
+#define TGSIM_HEAD_HINT 0
+#endif
+constexpr bool kHeadHint = TGSIM_HEAD_HINT != 0;
 __device__ __forceinline__ void fold_receipt(const RecvFold& g, uint32_t dst, uint32_t seq, uint32_t flags, uint64_t d,
                                              uint64_t fw) {
   const uint32_t f = seq / g.degree, s = dst - g.shard_begin;
-  if (s >= g.n_local || f >= g.floods || (flags & TGSIM_FLAG_CORRUPT) || (fw >> f & 1ull)) return;
+  if (s >= g.n_local || f >= g.floods || (flags & TGSIM_FLAG_CORRUPT) || (!kFwdSentinel && (fw >> f & 1ull))) return;
   // t = d / tick + 1 without a 64-bit division: d < 2^46 is exact in a double, and the estimate is
   // off by at most one
   uint64_t q = (uint64_t)((double)d * g.inv_tick);
@@ -450,7 +463,7 @@ struct SimQueue {
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
         if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
         if (rf.first && qi.w - rf.shard_begin < rf.n_local)
-          fold_receipt(rf, qi.w, qi.z, flags, d, rf.fwd[qi.w - rf.shard_begin]);
+          fold_receipt(rf, qi.w, qi.z, flags, d, kFwdSentinel ? 0ull : rf.fwd[qi.w - rf.shard_begin]);
         sched++;
         bytes += len;
         corrupted += (flags >> 1) & 1u;
@@ -1419,6 +1432,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
       ns.last_dup = last_dup;
       ns.last_cor = last_cor;
       ns.last_reo = last_reo;
+      if (kHeadHint) a.qhint[s] = 0ull;  // unknown: the next sparse step reads the queue head
       if constexpr (kH) {
         const auto rs = region(a.state + s, sizeof(SrcState));
         const StatePair sp = __builtin_bit_cast(StatePair, ns);
@@ -1739,7 +1753,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     const bool hs = lane < ns;
     const uint4 x = hs ? gh[(qh + k) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
     const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
-    const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
+    const uint32_t fw = !kFwdSentinel && a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
                             ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
                             : 0u;
     const uint64_t e = w0_of(x) & kEMask;
@@ -1792,6 +1806,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     ns_.last_cor = st.last_cor;
     ns_.last_reo = st.last_reo;
     a.state[s] = ns_;
+    if (kHeadHint) a.qhint[s] = 0ull;
     a.emit_n[s] = emitted;
   }
   // ---- statistics
@@ -1841,7 +1856,7 @@ __global__ __launch_bounds__(kWave) void k_sim_multi(SimArgs a) {
 // queued items, 256 ring entries or 64 items to serve) writes nothing and goes to the worklist.
 // (FIFO sources with more than one round of lanes go to k_sim_multi above instead.)
 __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t below = (1ull << lane) - 1;
   stamp(a, s, lane, 0, __builtin_amdgcn_s_memrealtime());
   // the queue starts at its head slot; the ring (needed only after the netem decisions) is read with
@@ -1869,8 +1884,10 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     }
   };
   unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
-  const uint4 qh0 = sorted_st && qn && !n ? gh[q_head(st)] : make_uint4(0, 0, 0, 0);
-  if (!n && (!qn || (sorted_st && (w0_of(qh0) & kEMask) >= a.horizon_ns))) {
+  const uint64_t hint = kHeadHint ? a.qhint[s] : 0ull;  // a lower bound of the head's e (0: unknown)
+  const bool hint_idle = kHeadHint && hint >= a.horizon_ns;
+  const uint4 qh0 = sorted_st && qn && !n && !hint_idle ? gh[q_head(st)] : make_uint4(0, 0, 0, 0);
+  if (!n && (!qn || (sorted_st && (hint_idle || (w0_of(qh0) & kEMask) >= a.horizon_ns)))) {
     // nothing offered and nothing eligible before the horizon: the state stays as it is (the ring
     // is released only by an enqueue); only the per-window queue model is counted.  Checked before
     // the capacity limits below: an idle source with a long ring (the end of a flood) is not deferred
@@ -2152,7 +2169,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     // the destinations' forwarded masks, for the receipts folded in below (in flight during the scan)
     // (the 32-bit half of the mask that holds the record's flood bit: one register across the scan)
     const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
-    const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
+    const uint32_t fw = !kFwdSentinel && a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
                             ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
                             : 0u;
     // HTB: d = max(e, TAT before), TAT' = max(TAT, e - burst) + cost, one max-plus scan
@@ -2207,7 +2224,20 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   }
   t_sched = emitted;
   const uint32_t rn_new = old_kept + ns_all - sk0;
+  uint64_t hint_new = 0;  // the new queue head's e on the FIFO path, where it is in registers
+  if (kHeadHint && fifo && wpos) {
+    if (fifo_nq < qn) {  // an old item stays at the head
+      if (fifo_nq < kWave) hint_new = w0_of(make_uint4(readlane32(q[0].x, fifo_nq), readlane32(q[0].y, fifo_nq), 0u, 0u)) & kEMask;
+    } else {  // the first candidate not served
+      const uint64_t mnd = __ballot(cand && !due_f);
+      if (mnd) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(mnd);
+        hint_new = w0_of(make_uint4(readlane32(io.x, l), readlane32(io.y, l), 0u, 0u)) & kEMask;
+      }
+    }
+  }
   if (lane == 0) {
+    if (kHeadHint) a.qhint[s] = hint_new;
     SrcState ns_;
     ns_.tat = tat_c;
     ns_.heap_n = wpos;
@@ -2258,8 +2288,29 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
 // (A one-lane-per-source pass listing the active sources, so that idle peers cost no wave, was
 // measured and dropped: 4.17-4.21 against 4.40-4.41 G pkt/s at 1M peers -- an idle wave exits after
 // its first loads, cheaper than the pass over a million sources.)
-__global__ __launch_bounds__(kWave, 7) void k_sim_sparse(SimArgs a) {
-  if (blockIdx.x < a.n_src) sparse_source(a, blockIdx.x);
+// Sources per workgroup (one wave each) and their placement.  Workgroups are dealt round-robin
+// over the 8 XCDs (MI355X_MICROARCH.md §Workgroup dispatch: blocks b and b + 8 share one), each with
+// its own L2, so source s = blockIdx.x put neighbouring sources -- whose 32-B states, 64-B
+// parameters, 8-B offsets, offered records and emit counts share 128-B lines -- on eight different
+// L2s, each fetching the whole line.  With kSparseXcd the blocks of one XCD take one contiguous
+// eighth of the sources, so a line is fetched by one L2.
+#ifndef TGSIM_SPARSE_WPG
+#define TGSIM_SPARSE_WPG 1
+#endif
+#ifndef TGSIM_SPARSE_XCD
+#define TGSIM_SPARSE_XCD 0
+#endif
+constexpr uint32_t kSparseWpg = TGSIM_SPARSE_WPG;
+constexpr bool kSparseXcd = TGSIM_SPARSE_XCD != 0;
+__host__ __device__ inline uint32_t sparse_blocks(uint32_t n_src) {
+  const uint32_t nb = (n_src + kSparseWpg - 1) / kSparseWpg;
+  return kSparseXcd ? (nb + 7) / 8 * 8 : nb;
+}
+__global__ __launch_bounds__(kWave * kSparseWpg, 7) void k_sim_sparse(SimArgs a) {
+  const uint32_t b = blockIdx.x, w = threadIdx.x >> 6;
+  const uint32_t blk = kSparseXcd ? (b & 7u) * (gridDim.x >> 3) + (b >> 3) : b;
+  const uint32_t s = blk * kSparseWpg + w;
+  if (s < a.n_src) sparse_source(a, s);
 }
 
 // The general path for the worklist k_sim_sparse left: a grid-stride loop over the list (its
@@ -2608,6 +2659,7 @@ __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint6
       rank += (tj < t[i] || (tj == t[i] && j < lane)) ? 1u : 0u;
     }
     if (!me) continue;
+    if (kFwdSentinel) g.first[(uint64_t)(s0 + i) * 64 + lane] = 0u;  // forwarded: later receipts fold to nothing
     const uint64_t o = readlane64(off_l, i) + (uint64_t)rank * deg;
     for (uint32_t k = 0; k < deg; ++k) {
       InRec rec;
@@ -2651,6 +2703,7 @@ __global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64
       rank += (tj < t[i] || (tj == t[i] && j < lane)) ? 1u : 0u;
     }
     if (!me) continue;
+    if (kFwdSentinel) g.first[(uint64_t)s * 64 + lane] = 0u;  // forwarded: later receipts fold to nothing
     const uint32_t src = g.shard_begin + s;
     const uint64_t o = off[s] + (uint64_t)rank * g.degree;
     for (uint32_t k = 0; k < g.degree; ++k) {
@@ -3431,7 +3484,7 @@ uint32_t sim_fused_resident() {
 
 void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
   if (!a.n_src) return;
-  hipLaunchKernelGGL(k_sim_sparse, dim3(a.n_src), dim3(kWave), 0, st, a);
+  hipLaunchKernelGGL(k_sim_sparse, dim3(sparse_blocks(a.n_src)), dim3(kWave * kSparseWpg), 0, st, a);
   // (grids of 5,120 and 10,240 waves: the same 1M-peer window, within noise)
   hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 2048 ? a.n_src : 2048), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);

@@ -349,6 +349,12 @@ class CABIEngine:
         ms = self._fn("sim_kernel_ms")(self._h, C.byref(n), 1 if reset else 0)
         return ms, n.value
 
+    def delivery_kernel_ms(self, reset: bool = False) -> Tuple[float, int]:
+        """Average delivery span (ms) per delivered window on the delivery stream (HIP events)."""
+        n = C.c_uint64()
+        ms = self._fn("delivery_kernel_ms")(self._h, C.byref(n), 1 if reset else 0)
+        return ms, n.value
+
 
 class Engine(CABIEngine):
     """The MI355X engine (libtgsim.so)."""
