@@ -1618,7 +1618,8 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
   const bool plain = src_on && !a.any_disabled && pp.rule_n == 0;
   const uint32_t ext_v = (pp.shift_ext >> 8 & 1u) ? TGSIM_V_EXTERNAL : TGSIM_V_NO_ROUTE;
   const uint64_t h = a.horizon_ns;
-  // ---- netem decisions, 64 offered packets a round; candidates into LDS in offer order
+  // ---- netem decisions, 64 offered packets a round; candidates written behind the queue tail in HBM,
+  // in offer order
   uint32_t nc = 0, n_due = 0, perr = 0, vcnt = 0, t_clone = 0;
   bool fifo = true, has_last = qn != 0;
   uint4 last = qt;  // the item every next candidate must not precede
@@ -1864,7 +1865,6 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const uint4* gh = a.heap + (size_t)s * kHeapCap;
   const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
   const SrcState st = a.state[s];
-  const SrcParams pp = a.params[s];
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const uint32_t n = (uint32_t)(send - sbeg);
   const uint32_t rn = st.ring_n, qn = st.heap_n;
@@ -1877,7 +1877,8 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
 #endif
   };
   const bool sorted_st = q_near(st) == qn;  // the whole queue is one sorted region
-  // FIFO candidates beyond one round of lanes go to k_sim_multi (multi-round, candidates in LDS)
+  // FIFO candidates beyond one round of lanes go to k_sim_multi (multi-round, candidates written behind
+  // the queue tail in HBM)
   auto defer_multi = [&]() {
     if (lane == 0) {
       multi_list(a)[atomicAdd(multi_count(a), 1u)] = s;
@@ -1900,6 +1901,9 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     }
     return;
   }
+  // the parameters only once the source is known not to be idle (most of the million sources of an
+  // off-peak gossip window are; their 64-B rows stay unread), beside the offered records' loads
+  const SrcParams pp = a.params[s];
   if ((pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 || (uint64_t)rn + qn + 2ull * n >= a.queue_limit || n > kWave ||
       (!sorted_st && qn > kSparseQ * kWave) || rn > kSparseQ * kWave) {
     const uint32_t why = (pp.rho_dup | pp.rho_cor | pp.rho_reo) != 0 ? 0u : (uint64_t)rn + qn + 2ull * n >= a.queue_limit ? 1u
@@ -2307,7 +2311,10 @@ __host__ __device__ inline uint32_t sparse_blocks(uint32_t n_src) {
   return kSparseXcd ? (nb + 7) / 8 * 8 : nb;
 }
 __global__ __launch_bounds__(kWave * kSparseWpg, 7) void k_sim_sparse(SimArgs a) {
-  const uint32_t b = blockIdx.x, w = threadIdx.x >> 6;
+  // the source index must stay wave-uniform for the compiler (a VGPR index turns every per-source
+  // load into a vector load: 126 VGPR spills at 7 waves per SIMD), hence readfirstlane
+  const uint32_t b = blockIdx.x;
+  const uint32_t w = kSparseWpg > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
   const uint32_t blk = kSparseXcd ? (b & 7u) * (gridDim.x >> 3) + (b >> 3) : b;
   const uint32_t s = blk * kSparseWpg + w;
   if (s < a.n_src) sparse_source(a, s);

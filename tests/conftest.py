@@ -45,3 +45,17 @@ def make_oracle(oracle_lib):
     def _make(n_peers, **kw):
         return CABIEngine(oracle_lib, "tgo_", n_peers, **kw)
     return _make
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """With TGSIM_LIB naming a TGSIM_CHECK build (scripts/r05_check_build.sh), report the cross-lane
+    exec-mask guard violations the run's kernels counted."""
+    import os
+
+    lib = os.environ.get("TGSIM_LIB", "")
+    if not lib.endswith("_check.so"):
+        return
+    from testground_amd.engine import load_library
+
+    n = load_library().tgsim_debug_exec_faults()
+    print(f"\nTGSIM_CHECK exec-mask guard violations: {n}")

@@ -14,18 +14,21 @@
 // buffer may be reused after the call exactly as with RCCL).  Host waits are bounded (60 s): a rank
 // whose partner never posts gets ncclSystemError instead of a hang.
 //
-// The all-to-all and the all-reduce are asynchronous, as RCCL's are: the call records an event and
-// enqueues a gate kernel on the caller's stream and returns at once; the rank that posts last moves
-// the data (on a service stream, after every rank's event) and opens every gate.  So a rank whose
-// peer never posts sees its stream stop at the gate, exactly where RCCL's kernel would wait, and the
-// engine's own bounded host waits (TGSIM_COMM_TIMEOUT_MS) are what end it.  ncclCommAbort (and the
-// destroy of any rank) opens the gates of every collective that can no longer complete.
+// A partner that stopped (MOCKRCCL_ABANDON_MS, tests only): RCCL's collectives are asynchronous, so
+// a rank whose peer never joins returns from the call and its stream stops where RCCL's kernel would
+// wait.  With MOCKRCCL_ABANDON_MS set, a wait for a partner that exceeds it does the same: the call
+// returns success without the data and leaves a gate kernel on the caller's stream, which spins until
+// the communicator is aborted or destroyed (ncclCommAbort / ncclCommDestroy of any rank), bounded at
+// 120 s.  The engine's own bounded host waits (TGSIM_COMM_TIMEOUT_MS) are then what ends the rank.
+// Only an abandoned collective spins on the device: a spinning kernel can hold up other streams
+// that share its hardware queue, so the tests that use it keep every other rank idle meanwhile.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -44,29 +47,10 @@ struct Msg {
   bool copied = false;
 };
 
-// One asynchronous collective (all-to-all or all-reduce), matched across ranks by issue order.
-struct Coll {
-  int kind = 0;  // 0 all-to-all (bytes per peer), 1 all-reduce (count u64 words)
-  size_t bytes = 0, count = 0;
-  ncclRedOp_t op = ncclSum;
-  ncclDataType_t type = ncclUint64;
-  int posted = 0;
-  struct Part {
-    const void* send = nullptr;
-    void* recv = nullptr;
-    hipEvent_t ready = nullptr;
-    uint32_t* gate = nullptr;  // pinned, coherent: 0 closed, 1 data in place, 2 aborted
-  };
-  std::vector<Part> parts;
-};
-
 struct World {
   int n = 0, joined = 0, destroyed = 0;
   bool aborted = false;
-  std::vector<uint64_t> next_coll;                  // per rank: collectives issued so far
-  std::map<uint64_t, std::shared_ptr<Coll>> colls;  // not yet complete, by issue index
-  std::vector<uint32_t*> gates;                     // freed with the world
-  hipStream_t svc = nullptr;                        // the completing rank's copies
+  std::vector<uint32_t*> gates;  // pinned words of abandoned collectives' gate kernels (1: open)
   std::mutex m;
   std::condition_variable cv;
   std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> box;  // (src, dst) -> messages
@@ -111,6 +95,44 @@ size_t type_size(ncclDataType_t t) {
   }
 }
 
+// MOCKRCCL_ABANDON_MS (0: never): how long a collective waits for a stopped partner before it is
+// abandoned to a gate kernel.
+std::chrono::milliseconds abandon_after() {
+  const char* v = getenv("MOCKRCCL_ABANDON_MS");
+  const long ms = v ? atol(v) : 0;
+  return ms > 0 ? std::chrono::milliseconds(ms) : std::chrono::milliseconds(0);
+}
+
+// Holds the caller's stream until the world is aborted or destroyed (bounded: 120 s of
+// s_memrealtime at 100 MHz, so no wave outlives a test that forgot to).
+__global__ void k_gate(const uint32_t* gate) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 12000000000ull) break;
+    __builtin_amdgcn_s_sleep(100);
+  }
+}
+
+// The collective the caller waits for will never complete: its stream stops at a gate (as RCCL's
+// kernel would); the call itself returns success.  Called with w->m held.
+ncclResult_t abandon(World* w, hipStream_t s) {
+  uint32_t* gate = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&gate), sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) !=
+      hipSuccess)
+    return ncclUnhandledCudaError;
+  *gate = w->aborted ? 1u : 0u;
+  w->gates.push_back(gate);
+  hipLaunchKernelGGL(k_gate, dim3(1), dim3(1), 0, s, gate);
+  return hipGetLastError() == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+}
+
+// A rank left (destroy or abort): no abandoned collective can complete any more.
+void open_gates(World* w) {
+  std::lock_guard<std::mutex> l(w->m);
+  w->aborted = true;
+  for (uint32_t* g : w->gates) __atomic_store_n(g, 1u, __ATOMIC_RELEASE);
+}
+
 hipEvent_t new_event(World* w) {
   hipEvent_t e = nullptr;
   if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
@@ -143,6 +165,8 @@ ncclResult_t run(std::vector<Op>& ops) {
     {
       std::unique_lock<std::mutex> l(w->m);
       auto& q = w->box[{o.peer, o.comm->rank}];
+      const auto ab = abandon_after();
+      if (ab.count() && !w->cv.wait_for(l, ab, [&] { return !q.empty(); })) return abandon(w, o.s);
       if (!w->cv.wait_for(l, kWait, [&] { return !q.empty(); })) return ncclSystemError;
       msg = q.front();
       q.pop_front();
@@ -198,109 +222,18 @@ ncclResult_t host_allgather(ncclComm* c, const void* dev, size_t bytes, hipStrea
     w->ag_arrived = 0;
     w->ag_gen++;
     w->cv.notify_all();
-  } else if (!w->cv.wait_for(l, kWait, [&] { return w->ag_gen != gen; })) {
-    return ncclSystemError;
+  } else {
+    const auto ab = abandon_after();
+    if (ab.count() && !w->cv.wait_for(l, ab, [&] { return w->ag_gen != gen; })) {
+      w->ag_arrived--;  // this rank's contribution is withdrawn: the gather never completes
+      all->clear();
+      return abandon(w, s) == ncclSuccess ? ncclInProgress : ncclUnhandledCudaError;
+    }
+    if (!w->cv.wait_for(l, kWait, [&] { return w->ag_gen != gen; })) return ncclSystemError;
   }
   all->clear();
   for (auto& v : w->ag_out) all->insert(all->end(), v.begin(), v.end());
   return ncclSuccess;
-}
-
-// Holds the caller's stream until the collective's data is in place (or it was aborted); bounded
-// (120 s of s_memrealtime at 100 MHz) so that no wave outlives a test that forgot to abort.
-__global__ void k_gate(const uint32_t* gate) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 12000000000ull) break;
-    __builtin_amdgcn_s_sleep(100);
-  }
-}
-
-void open_gates(Coll& c, uint32_t v) {
-  for (auto& p : c.parts)
-    if (p.gate) __atomic_store_n(p.gate, v, __ATOMIC_RELEASE);
-}
-
-// The last rank to post moves the data once every rank's stream has reached the collective.
-ncclResult_t complete(World* w, Coll& c) {
-  for (auto& p : c.parts)
-    if (hipEventSynchronize(p.ready) != hipSuccess) return ncclUnhandledCudaError;
-  const int n = w->n;
-  if (c.kind == 0) {
-    for (int q = 0; q < n; ++q)
-      for (int r = 0; r < n; ++r)
-        if (c.bytes && hipMemcpyAsync(static_cast<uint8_t*>(c.parts[q].recv) + r * c.bytes,
-                                      static_cast<const uint8_t*>(c.parts[r].send) + q * c.bytes, c.bytes,
-                                      hipMemcpyDeviceToDevice, w->svc) != hipSuccess)
-          return ncclUnhandledCudaError;
-  } else {
-    std::vector<uint64_t> v(n * c.count), out(c.count);
-    for (int r = 0; r < n; ++r)
-      if (hipMemcpyAsync(v.data() + r * c.count, c.parts[r].send, c.count * 8, hipMemcpyDeviceToHost, w->svc) != hipSuccess)
-        return ncclUnhandledCudaError;
-    if (hipStreamSynchronize(w->svc) != hipSuccess) return ncclUnhandledCudaError;
-    for (size_t i = 0; i < c.count; ++i) {
-      uint64_t acc = v[i];
-      for (int k = 1; k < n; ++k) {
-        const uint64_t x = v[k * c.count + i];
-        if (c.op == ncclSum) acc += x;
-        else if (c.type == ncclUint64) acc = c.op == ncclMax ? std::max(acc, x) : std::min(acc, x);
-        else acc = static_cast<uint64_t>(c.op == ncclMax ? std::max<int64_t>(acc, x) : std::min<int64_t>(acc, x));
-      }
-      out[i] = acc;
-    }
-    for (int r = 0; r < n; ++r)
-      if (hipMemcpyAsync(c.parts[r].recv, out.data(), c.count * 8, hipMemcpyHostToDevice, w->svc) != hipSuccess)
-        return ncclUnhandledCudaError;
-  }
-  if (hipStreamSynchronize(w->svc) != hipSuccess) return ncclUnhandledCudaError;
-  open_gates(c, 1u);
-  return ncclSuccess;
-}
-
-ncclResult_t post(ncclComm* comm, const Coll& shape, const void* send, void* recv, hipStream_t s) {
-  World* w = comm->w;
-  uint32_t* gate = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&gate), sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) !=
-      hipSuccess)
-    return ncclUnhandledCudaError;
-  *gate = 0;
-  hipEvent_t ready = new_event(w);
-  if (!ready || hipEventRecord(ready, s) != hipSuccess) return ncclUnhandledCudaError;
-  hipLaunchKernelGGL(k_gate, dim3(1), dim3(1), 0, s, gate);
-  if (hipGetLastError() != hipSuccess) return ncclUnhandledCudaError;
-  std::shared_ptr<Coll> done;
-  {
-    std::lock_guard<std::mutex> l(w->m);
-    w->gates.push_back(gate);
-    if (w->aborted) {
-      *gate = 2u;
-      return ncclSystemError;
-    }
-    const uint64_t k = w->next_coll[comm->rank]++;
-    std::shared_ptr<Coll>& c = w->colls[k];
-    if (!c) {
-      c = std::make_shared<Coll>(shape);
-      c->parts.assign(w->n, {});
-    } else if (c->kind != shape.kind || c->bytes != shape.bytes || c->count != shape.count) {
-      *gate = 2u;
-      return ncclInvalidUsage;
-    }
-    c->parts[comm->rank] = {send, recv, ready, gate};
-    if (++c->posted == w->n) {
-      done = c;
-      w->colls.erase(k);
-    }
-  }
-  return done ? complete(w, *done) : ncclSuccess;
-}
-
-// Every collective that has not completed can no longer complete: its gates open as aborted.
-void abort_world(World* w) {
-  std::lock_guard<std::mutex> l(w->m);
-  w->aborted = true;
-  for (auto& kv : w->colls) open_gates(*kv.second, 2u);
-  w->colls.clear();
 }
 
 }  // namespace
@@ -327,8 +260,6 @@ ncclResult_t mockrccl_CommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id
     if (!slot) {
       slot = new World();
       slot->n = nranks;
-      slot->next_coll.assign(nranks, 0);
-      if (hipStreamCreateWithFlags(&slot->svc, hipStreamNonBlocking) != hipSuccess) return ncclUnhandledCudaError;
     }
     w = slot;
   }
@@ -345,7 +276,7 @@ ncclResult_t mockrccl_CommDestroy(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
   World* w = comm->w;
   delete comm;
-  abort_world(w);  // a rank that leaves never posts again
+  open_gates(w);  // a rank that leaves never posts again
   bool last;
   {
     std::lock_guard<std::mutex> l(w->m);
@@ -355,7 +286,6 @@ ncclResult_t mockrccl_CommDestroy(ncclComm_t comm) {
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : w->events) (void)hipEventDestroy(e);
     for (uint32_t* g : w->gates) (void)hipHostFree(g);
-    if (w->svc) (void)hipStreamDestroy(w->svc);
     std::lock_guard<std::mutex> l(g_m);
     for (auto it = g_worlds.begin(); it != g_worlds.end(); ++it)
       if (it->second == w) {
@@ -369,7 +299,7 @@ ncclResult_t mockrccl_CommDestroy(ncclComm_t comm) {
 
 ncclResult_t mockrccl_CommAbort(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
-  abort_world(comm->w);
+  open_gates(comm->w);
   return mockrccl_CommDestroy(comm);
 }
 
@@ -414,10 +344,13 @@ ncclResult_t mockrccl_AllToAll(const void* send, void* recv, size_t count, ncclD
                           hipStream_t s) {
   const size_t es = type_size(t);
   if (!es || !comm) return ncclInvalidArgument;
-  Coll shape;
-  shape.kind = 0;
-  shape.bytes = count * es;
-  return post(comm, shape, send, recv, s);
+  const size_t b = count * es;
+  std::vector<Op> ops;
+  for (int r = 0; r < comm->w->n; ++r) {
+    ops.push_back({true, const_cast<uint8_t*>(static_cast<const uint8_t*>(send)) + r * b, b, r, comm, s});
+    ops.push_back({false, static_cast<uint8_t*>(recv) + r * b, b, r, comm, s});
+  }
+  return run(ops);
 }
 
 ncclResult_t mockrccl_AllGather(const void* send, void* recv, size_t count, ncclDataType_t t, ncclComm_t comm,
@@ -426,6 +359,7 @@ ncclResult_t mockrccl_AllGather(const void* send, void* recv, size_t count, nccl
   if (!es || !comm) return ncclInvalidArgument;
   std::vector<uint8_t> all;
   ncclResult_t r = host_allgather(comm, send, count * es, s, &all);
+  if (r == ncclInProgress) return ncclSuccess;  // abandoned: the stream waits at its gate
   if (r != ncclSuccess) return r;
   return hipMemcpy(recv, all.data(), all.size(), hipMemcpyHostToDevice) == hipSuccess ? ncclSuccess
                                                                                      : ncclUnhandledCudaError;
@@ -435,12 +369,24 @@ ncclResult_t mockrccl_AllReduce(const void* send, void* recv, size_t count, nccl
                            ncclComm_t comm, hipStream_t s) {
   if (!comm || (t != ncclUint64 && t != ncclInt64) || (op != ncclSum && op != ncclMax && op != ncclMin))
     return ncclInvalidArgument;
-  Coll shape;
-  shape.kind = 1;
-  shape.count = count;
-  shape.op = op;
-  shape.type = t;
-  return post(comm, shape, send, recv, s);
+  std::vector<uint8_t> all;
+  ncclResult_t r = host_allgather(comm, send, count * 8, s, &all);
+  if (r == ncclInProgress) return ncclSuccess;  // abandoned: the stream waits at its gate
+  if (r != ncclSuccess) return r;
+  std::vector<uint64_t> v(all.size() / 8), out(count);
+  memcpy(v.data(), all.data(), all.size());
+  for (size_t i = 0; i < count; ++i) {
+    uint64_t acc = v[i];
+    for (int k = 1; k < comm->w->n; ++k) {
+      const uint64_t x = v[k * count + i];
+      if (op == ncclSum) acc += x;
+      else if (t == ncclUint64) acc = op == ncclMax ? std::max(acc, x) : std::min(acc, x);
+      else acc = static_cast<uint64_t>(op == ncclMax ? std::max<int64_t>(acc, x) : std::min<int64_t>(acc, x));
+    }
+    out[i] = acc;
+  }
+  return hipMemcpy(recv, out.data(), count * 8, hipMemcpyHostToDevice) == hipSuccess ? ncclSuccess
+                                                                                   : ncclUnhandledCudaError;
 }
 
 }  // extern "C"

@@ -195,19 +195,26 @@ def test_ranks_epochs_barrier(lib):
 
 @pytest.mark.parametrize("where", ["count all-to-all", "all-reduce"])
 def test_rank_that_stops_times_out_peers(lib, monkeypatch, where):
-    """A rank that stops before a collective (here: returns before its count all-to-all, or before
-    the barrier's all-reduce) must not hang the others: their exchange stream waits at the mock's
-    gate exactly where RCCL's kernel would, and the engine's bounded host wait
-    (TGSIM_COMM_TIMEOUT_MS) fails them with -ETIMEDOUT naming the rank and the window; every later
-    call fails fast, and destroying the engine aborts the communicator instead of draining it."""
+    """a rank that stops before a collective (here: returns before its count
+    all-to-all, or before the barrier's all-reduce) must not hang the others.  RCCL's collectives
+    are asynchronous, so the others' exchange streams stop where RCCL's kernel would wait; the test
+    transport does the same for a partner that never posts (MOCKRCCL_ABANDON_MS: the call returns and
+    a gate kernel holds the stream), and the engine's bounded host wait (TGSIM_COMM_TIMEOUT_MS) fails
+    the rank with -ETIMEDOUT naming the rank and the window; every later call fails fast, and
+    destroying the engine aborts the communicator (which opens the gate) instead of draining it.
+    The stopped rank finishes its own device work first: a spinning gate holds up any stream that
+    shares its hardware queue."""
     import errno
+    import threading
     import time
 
     from testground_amd.engine import EngineError
 
     monkeypatch.setenv("TGSIM_COMM_TIMEOUT_MS", "1500")
+    monkeypatch.setenv("MOCKRCCL_ABANDON_MS", "300")
     n, ticks = 300, 1000
     bounds = [0, 150, 300]
+    idle = threading.Event()
 
     def rank(r, e):
         wl.configure_storm(e, n)
@@ -216,7 +223,10 @@ def test_rank_that_stops_times_out_peers(lib, monkeypatch, where):
             e.comm_step(ticks)
             e.signal_async(1, bounds[r + 1] - bounds[r])
         if r == 1:
-            return None  # stops here: never posts the collective
+            e.sync()  # stops here, its device work done: never posts the collective
+            idle.set()
+            return None
+        assert idle.wait(60)
         t0 = time.monotonic()
         try:
             if where == "count all-to-all":
@@ -239,5 +249,5 @@ def test_rank_that_stops_times_out_peers(lib, monkeypatch, where):
     code, msg, waited, again = per_rank[0]
     assert code == -errno.ETIMEDOUT, (code, msg)
     assert 1.4 <= waited < 30, waited
-    assert f"rank 0 of 2 waited" in msg and where in msg and "window" in msg, msg
+    assert "rank 0 of 2 waited" in msg and where in msg and "window" in msg, msg
     assert again == -errno.ETIMEDOUT

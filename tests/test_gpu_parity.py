@@ -636,3 +636,45 @@ def test_flat_sort_hot_destinations(make_oracle, latency_ms):
         _, d = assert_same(g, c, f"latency {latency_ms} ms step {step}")
         if latency_ms == 0 or step >= 2:  # the hot segments exceed 64 records
             assert np.bincount(d["dst"], minlength=n)[:3].min() > 64
+
+
+def test_multi_round_fifo_sources(make_oracle, monkeypatch):
+    """k_sim_multi's own parity case.  FIFO links (no jitter, duplicates or reordering)
+    offered 150-300 packets per window each, so k_sim_sparse hands every such source to k_sim_multi
+    (more than 64 offered packets), whose rounds of 64 candidates go behind the queue tail and whose
+    due prefix runs past 256 items.  Every 10th source reorders (5 %) and every 10th + 4 duplicates
+    (3 %): their queue stops being FIFO partway through the candidates, after k_sim_multi already
+    wrote some behind the tail, and they go on to k_sim_list.  Bit-exact with the oracle, window by
+    window, with a high netem limit."""
+    monkeypatch.setenv("TGSIM_SPARSE", "1")
+    n = 60
+    rng = np.random.default_rng(23)
+    g, c = both(make_oracle, n, queue_limit=1024)
+    for i in range(n):
+        s = nw.LinkShape(Latency=int(rng.integers(1, 6)) * nw.Millisecond, Bandwidth=1 << 30, Loss=1.0,
+                         Reorder=5.0 if i % 10 == 3 else 0.0, Duplicate=3.0 if i % 10 == 7 else 0.0)
+        for e in (g, c):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=s))
+    seq = np.zeros(n, dtype=np.uint32)
+    for step in range(12):
+        per = rng.integers(150, 301, n)
+        src = np.repeat(np.arange(n), per)
+        m = len(src)
+        pk = np.zeros(m, dtype=abi.PKT_DTYPE)
+        pk["src"] = src
+        pk["dst"] = (src + 1 + rng.integers(0, n - 1, m)) % n
+        pk["len"] = rng.integers(40, 1500, m)
+        pk["tick"] = rng.integers(0, 4000, m)
+        order = np.lexsort((pk["tick"], src))
+        counts = np.bincount(src, minlength=n)
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        sq = np.empty(m, dtype=np.uint32)
+        sq[order] = np.arange(m) - starts[src[order]] + seq[src[order]]
+        seq += counts.astype(np.uint32)
+        pk["seq"] = sq
+        g.submit(pk)
+        c.submit(pk)
+        g.step(4000)
+        c.step(4000)
+        _, d = assert_same(g, c, f"step {step}")
+        assert len(d) > 0
