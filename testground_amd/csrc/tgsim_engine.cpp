@@ -316,6 +316,18 @@ struct tgsim_engine_s {
   // delivery of window k - 2 (a third set, so that a delivery could lag two windows at the gossip
   // flood's peak, was tried: at 1M peers a set is ~38 GB and the third one thrashed)
   DevBuf<tgsim_delivery> d_emit, d_emit_alt;
+  // where each emit set's records are (classic regions, or compact regions and a pool: DESIGN §4),
+  // and the per-source pool indices of each set
+  EmitRead el{}, el_alt{};
+  DevBuf<uint32_t> d_pidx, d_pidx_alt;
+  int emit_compact = 1;           // TGSIM_EMIT_COMPACT: 0 every window in the classic layout, 1 auto,
+                                  // 2 every sparse window compact (tests)
+  uint32_t emit_r = 64;           // TGSIM_EMIT_R: a compact region's reserve beyond 2 records per offered packet
+  uint32_t emit_pool = 64;        // TGSIM_EMIT_POOL: the compact pool's records per source
+  // the choice tgsim_sim_capacity made for the next window (run_sim takes it, so the exchange's
+  // buffers and the window agree even if the deferral count read in between changed)
+  int next_sparse = -1;
+  uint64_t next_sparse_n = 0;  // the window size it was made for
   uint32_t wide_windows = 0;              // windows after a mid-run reshape whose bounded local delivery
                                           // reserves the full netem limit per source (deliver_local_from)
   uint64_t deliver_slack = 128;           // TGSIM_DELIVER_SLACK: queued items per source a bounded local
@@ -791,6 +803,9 @@ int check_sim_error(Eng* E) {
     return E->fail(-EIO, "fused step: a source's previous window did not complete (hand-off timed out)");
   if (herr & kErrDeliverCap)
     return E->fail(-ENOSPC, "local delivery: a window's records exceed the delivery buffers (TGSIM_DELIVER_SLACK)");
+  if (herr & kErrEmitPool)
+    return E->fail(-ENOSPC, "sparse window: the sources that served more than their compact emit regions hold "
+                            "overflowed the emit pool (TGSIM_EMIT_POOL, or TGSIM_EMIT_COMPACT=0)");
   if (E->h_xerr && __atomic_load_n(E->h_xerr, __ATOMIC_RELAXED))
     return E->fail(-ENOSPC, "exchange: a step's records for one rank exceed the slot capacity");
   return 0;
@@ -825,12 +840,15 @@ SimArgs base_sim_args(Eng* E) {
   a.any_disabled = E->n_disabled ? 1u : 0u;
   a.tick_ns = E->o.tick_ns;
   a.err_host = E->d_err_host;
+  a.emit_r = kHeapCap;  // the classic emit layout unless run_sim picks the compact one
   return a;
 }
 
 // The next window's emit set: the current one becomes the newest being delivered.
 void rotate_emit(Eng* E) {
   std::swap(E->d_emit, E->d_emit_alt);
+  std::swap(E->el, E->el_alt);
+  std::swap(E->d_pidx, E->d_pidx_alt);
   std::swap(E->d_emit_n, E->d_emit_n_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
   std::swap(E->ev_local, E->ev_local_alt);
@@ -901,6 +919,50 @@ void drop_gen(Eng* E, size_t from = 0) {
   E->gen_q.erase(E->gen_q.begin() + static_cast<std::ptrdiff_t>(std::min(from, E->gen_q.size())), E->gen_q.end());
 }
 
+// Sparse or dense kernels for a window of n_in packets (commit: this is the window being launched;
+// the streak counter advances).  Sparse steps (few packets per source, or more sources than the
+// order kernel ranks): open queues run in the register-only k_sim_sparse, the rest in k_sim_list;
+// dense steps: k_sim in heavy-first order.  The results are the same either way.
+bool sparse_choice(Eng* E, uint64_t n_in, bool commit) {
+  if (E->sparse_mode >= 0) return E->sparse_mode == 1;
+  // dense traffic (C3, C5 at 100k peers; k_sim_sparse would defer every source with more than
+  // 64 packets anyway): the LDS queue, in heavy-first order when ranked
+  if (n_in >= 64ull * E->S) return false;
+  // up to 64 packets per source (gossip, even at the flood's peak of ~20): the register-only
+  // kernel wins unless the queues are too long for registers and it defers most sources to
+  // k_sim_list (2 waves/SIMD).  The worklist size of the last sparse step (copied to pinned memory
+  // behind it, read without waiting) decides; every 64th such step runs sparse again to re-measure
+  if (E->next_sparse >= 0 && E->next_sparse_n == n_in) {
+    const bool sp = E->next_sparse == 1;
+    if (commit) E->next_sparse = -1;
+    return sp;
+  }
+  const uint32_t deferred = __atomic_load_n(E->h_work, __ATOMIC_RELAXED);
+  const bool many = E->sparse_seen && static_cast<uint64_t>(E->dense_div) * deferred > E->S;
+  const bool sp = !many || E->dense_streak + 1 >= 64;
+  if (commit) {
+    E->dense_streak = sp ? 0 : E->dense_streak + 1;
+    E->next_sparse = -1;
+  } else {
+    E->next_sparse = sp ? 1 : 0;
+    E->next_sparse_n = n_in;
+  }
+  return sp;
+}
+
+// The compact emit layout: a sparse window whose classic regions (the netem limit per source) would
+// exceed kExactBoundBytes (24 GB per emit set at 1M peers) keeps emit_r records per source beyond 2
+// per offered packet and a pool for the few sources that serve more.
+bool compact_layout(Eng* E, uint64_t n_in, bool sparse) {
+  return sparse && E->emit_compact &&
+         (E->emit_compact == 2 ||
+          (2 * n_in + static_cast<uint64_t>(kHeapCap) * E->S) * sizeof(tgsim_delivery) > kExactBoundBytes);
+}
+uint64_t emit_records(Eng* E, uint64_t n_in, bool compact) {  // the emit buffer of one window
+  return compact ? 2 * n_in + static_cast<uint64_t>(E->emit_r + E->emit_pool) * E->S
+                 : 2 * n_in + static_cast<uint64_t>(kHeapCap) * E->S;
+}
+
 int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   int erc = check_sim_error(E);
   if (erc) return erc;
@@ -930,7 +992,9 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   }
   int rc = flush_config(E);
   if (rc) return rc;
-  const uint64_t emit_cap = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;
+  const bool sparse = sparse_choice(E, E->n_in, true);
+  const bool compact = compact_layout(E, E->n_in, sparse);
+  const uint64_t emit_cap = emit_records(E, E->n_in, compact);
   HIPCHK(E->d_verdict.ensure(E->n_in ? E->n_in : 1));
   // the local delivery or routing two steps back read this emit pair
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
@@ -942,12 +1006,20 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   a.verdict = E->d_verdict.p;
   a.emit = E->d_emit.p;
   a.emit_n = E->d_emit_n.p;
+  E->el = EmitRead{E->d_emit.p, nullptr, nullptr, kHeapCap};
+  if (compact) {  // regions of 2 n_s + emit_r records, then the pool
+    HIPCHK(E->d_pidx.ensure(E->S));
+    a.emit_r = E->emit_r;
+    a.emit_pool = E->d_emit.p + 2 * E->n_in + static_cast<uint64_t>(E->emit_r) * E->S;
+    a.emit_pool_idx = E->d_pidx.p;
+    a.emit_pool_cap = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(E->emit_pool) * E->S, 0xFFFFFFFFull));
+    E->el = EmitRead{E->d_emit.p, a.emit_pool, E->d_pidx.p, E->emit_r};
+  }
   a.t0_ns = E->now_tick * E->o.tick_ns;
   a.horizon_ns = (E->now_tick + n_ticks) * E->o.tick_ns + E->o.lookahead_ns;
   const uint32_t n_wg = (E->S + kSpw - 1) / kSpw;
   const bool ordered = kSpw == 1 && E->S <= kOrderMaxSources;
   a.order = ordered && E->order_valid ? E->d_order.p : nullptr;
-  a.dur = nullptr;  // (measured per-source time as the dispatch weight: tried, not kept)
   a.stamps = nullptr;
   if (E->stamps_on) {
     HIPCHK(E->d_stamps.ensure(static_cast<size_t>(n_wg) * kStampSlots));
@@ -970,44 +1042,24 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     a.g_floods = E->gossip.n_floods;
     a.g_degree = E->gossip.degree;
   }
-  // Sparse steps (few packets per source, or more sources than the order kernel ranks): open
-  // queues run in the register-only k_sim_sparse, the rest in k_sim_list; dense steps: k_sim in
-  // heavy-first order.  The results are the same either way.
-  bool sparse;
-  if (E->sparse_mode >= 0) {
-    sparse = E->sparse_mode == 1;
-  } else if (E->n_in >= 64ull * E->S) {
-    // dense traffic (C3, C5 at 100k peers; k_sim_sparse would defer every source with more than
-    // 64 packets anyway): the LDS queue, in heavy-first order when ranked
-    sparse = false;
-  } else {
-    // up to 64 packets per source (gossip, even at the flood's peak of ~20): the register-only
-    // kernel wins unless the queues are too long for
-    // registers and it defers most sources to k_sim_list (2 waves/SIMD).  The worklist size of the
-    // last sparse step (copied to pinned memory behind it, read without waiting) decides; every
-    // 64th such step runs sparse again to re-measure
-    const uint32_t deferred = __atomic_load_n(E->h_work, __ATOMIC_RELAXED);
-    if (E->trace_list) {
-      fprintf(stderr, "tgsim: sparse step deferred %u of %u sources (multi-round %u)", deferred, E->S,
-              __atomic_load_n(E->h_work + 1, __ATOMIC_RELAXED));
+  if (E->trace_list && E->sparse_mode < 0 && E->n_in < 64ull * E->S) {
+    fprintf(stderr, "tgsim: last sparse step deferred %u of %u sources (multi-round %u)%s",
+            __atomic_load_n(E->h_work, __ATOMIC_RELAXED), E->S, __atomic_load_n(E->h_work + 1, __ATOMIC_RELAXED),
+            compact ? " compact emit" : "");
 #ifdef TGSIM_DEFER_STATS  // by reason (corr, limit, n>64, queue, ring, fifo-due, sorted-queue, rest), cumulative
-      uint32_t why[8] = {};
-      if (E->d_work.p && hipMemcpy(why, E->d_work.p + 2 + E->S, sizeof why, hipMemcpyDeviceToHost) == hipSuccess)
-        for (uint32_t w : why) fprintf(stderr, " %u", w);
+    uint32_t why[8] = {};
+    if (E->d_work.p && hipMemcpy(why, E->d_work.p + 4 + E->S, sizeof why, hipMemcpyDeviceToHost) == hipSuccess)
+      for (uint32_t w : why) fprintf(stderr, " %u", w);
 #endif
-      fprintf(stderr, "\n");
-    }
-    sparse = !(E->sparse_seen && static_cast<uint64_t>(E->dense_div) * deferred > E->S) || ++E->dense_streak >= 64;
-    if (sparse) E->dense_streak = 0;
+    fprintf(stderr, "\n");
   }
-  a.worklist = a.worklist_n = nullptr;
+  a.worklist = nullptr;
   if (sparse) {
-    // [0] the worklist's count, [1] k_sim_multi's, the worklist's sources, 8 words of
-    // TGSIM_DEFER_STATS, then k_sim_multi's sources
-    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 2 + 8));
-    HIPCHK(hipMemsetAsync(E->d_work.p, 0, 2 * sizeof(uint32_t), E->st));
-    a.worklist_n = E->d_work.p;
-    a.worklist = E->d_work.p + 2;
+    // [0] the worklist's count, [1] k_sim_multi's, [2] emit-pool records claimed, [3] unused, the
+    // worklist's sources, 8 words of TGSIM_DEFER_STATS, then k_sim_multi's sources
+    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 4 + 8));
+    HIPCHK(hipMemsetAsync(E->d_work.p, 0, 4 * sizeof(uint32_t), E->st));
+    a.worklist = E->d_work.p + 4;
     a.order = nullptr;  // (stamps, when on, are indexed by source: n_wg = S)
   }
   hipEvent_t ev0, ev1;
@@ -1032,7 +1084,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     m.off = E->d_off.p;
     m.in = E->d_in.p;
     m.verdict = E->d_verdict.p;
-    m.emit = E->d_emit.p;
+    m.emit = E->el;
     m.emit_n = E->d_emit_n.p;
     m.state = E->d_state.p;
     m.n_src = E->S;
@@ -1073,7 +1125,7 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
   HIPCHK(hipStreamWaitEvent(rs, E->ev_sim, 0));
   RouteArgsHost h;
   memset(&h, 0, sizeof h);
-  h.emit = E->d_emit.p;
+  h.emit = E->el;
   h.emit_n = E->d_emit_n.p;
   h.off = E->d_off.p;
   h.n_src = E->S;
@@ -1297,7 +1349,7 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
 
 // The local delivery of one window on the delivery stream (after its k_sim): scan of the
 // per-destination histogram -> scatter straight from the emit regions -> per-destination order.
-int deliver_local_from(Eng* E, const tgsim_delivery* emit, uint32_t* emit_n, uint64_t* lcnt,
+int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t* lcnt,
                        const uint64_t* off, uint64_t n_in, hipEvent_t released) {
   const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
@@ -1365,13 +1417,13 @@ int deliver_local(Eng* E) {
                        // from the emit regions on the simulate stream (TGSIM_FOLD_RECV=0); the next
                        // window's generation waits for nothing on the delivery side
     if (!E->fold_recv) {
-      launch_gossip_recv_emit(gossip_args(E, 0, 0), E->d_emit.p, E->d_emit_n.p, E->d_off.p, E->S, E->st);
+      launch_gossip_recv_emit(gossip_args(E, 0, 0), E->el, E->d_emit_n.p, E->d_off.p, E->S, E->st);
       HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
   }
 
-  int rc = deliver_local_from(E, E->d_emit.p, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in, E->ev_local);
+  int rc = deliver_local_from(E, E->el, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in, E->ev_local);
   if (rc) return rc;
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   rotate_emit(E);
@@ -1522,7 +1574,7 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
     for (uint32_t i = 0; i < g; ++i) {
       RouteArgsHost h;
       memset(&h, 0, sizeof h);
-      h.emit = E->fset[p][i].emit.p;
+      h.emit = EmitRead{E->fset[p][i].emit.p, nullptr, nullptr, kHeapCap};  // fused windows: classic layout
       h.emit_n = E->fset[p][i].emit_n.p;
       h.off = win[i].off.p;
       h.n_src = E->S;
@@ -1757,6 +1809,9 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* dd = getenv("TGSIM_DENSE_DIV")) E->dense_div = static_cast<uint32_t>(std::max(1, atoi(dd)));
+  if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
+  if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
+  if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));
   E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
   if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
   if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) {
@@ -2037,7 +2092,7 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   HIPCHK(E->d_in.ensure(reserve));
   HIPCHK(E->d_verdict.ensure(reserve));
   // the emit regions of both parities, for the same reserve (a hipFree + hipMalloc of several GB inside the flood stalls the loop)
-  const uint64_t emit_cap = 2 * reserve + static_cast<uint64_t>(kHeapCap) * E->S;
+  const uint64_t emit_cap = emit_records(E, reserve, compact_layout(E, reserve, true));
   for (auto* b : {&E->d_emit, &E->d_emit_alt}) HIPCHK(b->ensure(emit_cap));
   E->gossip_on = true;
   return 0;
@@ -2119,7 +2174,8 @@ int64_t tgsim_sim_capacity(void* e) {
     }
   }
   const uint64_t n = !E->gen_q.empty() ? E->gen_q.front().n : E->staged.size();
-  return static_cast<int64_t>(2 * n + static_cast<uint64_t>(kHeapCap) * E->S);
+  // the records the next window can emit in the layout it will use (the choice is kept for it)
+  return static_cast<int64_t>(emit_records(E, n, compact_layout(E, n, sparse_choice(E, n, false))));
 }
 
 int tgsim_step_sim_launch(void* e, uint32_t n_ticks, uint32_t n_ranks, const uint32_t* bounds, void* d_out,
@@ -2273,7 +2329,8 @@ int tgsim_step(void* e, uint32_t n_ticks) {
   }
   int rc = run_sim(E, n_ticks);
   if (rc) return rc;
-  const uint64_t cap = 2 * E->n_in + static_cast<uint64_t>(kHeapCap) * E->S;
+  // the window's emit layout (run_sim's choice, rotated by the routing below) bounds its records
+  const uint64_t cap = emit_records(E, E->n_in, E->el.r != kHeapCap);
   HIPCHK(E->d_bucket.ensure(cap));
   const uint32_t bounds[2] = {0, E->N};
   uint64_t count = 0;

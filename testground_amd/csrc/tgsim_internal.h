@@ -106,7 +106,7 @@ struct SimArgs {
   uint8_t* verdict;         // one byte per offered packet
   uint4* heap;              // [s][kHeapCap] eligibility heap, 16 B items
   uint64_t* ring;           // [s][kHeapCap] departure times, compacted (head at 0)
-  tgsim_delivery* emit;     // per-source regions, base 2*off[s] + kHeapCap*s
+  tgsim_delivery* emit;     // per-source regions, base 2*off[s] + emit_r*s (EmitRead below)
   uint32_t* emit_n;         // records emitted per source this step
   unsigned long long* stats;
   uint32_t key0, key1;
@@ -117,9 +117,16 @@ struct SimArgs {
   uint64_t* stamps;         // diagnostics: kStampSlots s_memrealtime stamps per workgroup, or null
   unsigned long long* dst_cnt;  // single shard: per-destination histogram of the emitted records, or null
   uint64_t* err_host;       // pinned host word: the sticky error bits, or null
-  uint32_t* worklist;       // sparse steps: sources k_sim_sparse left for k_sim_list
-  uint32_t* worklist_n;     // their count (zeroed before k_sim_sparse)
-  uint32_t* dur;            // per source: this step's k_sim time in 10-ns ticks (dispatch weight), or null
+  // sparse steps: the sources k_sim_sparse left for k_sim_list; worklist[-4] their count,
+  // worklist[-3] k_sim_multi's, worklist[-2] the emit-pool records claimed (zeroed before k_sim_sparse)
+  uint32_t* worklist;
+  // The rest of the emit layout (EmitRead): source s's first 2 n_s + emit_r records at its region; a
+  // source with more (it served more than emit_r old queue items in the window) claims the rest from
+  // emit_pool (worklist[-2] counts the records claimed, emit_pool_cap bounds them) and stores where
+  // they start in emit_pool_idx[s].  emit_r = kHeapCap: the classic layout, which the netem limit
+  // keeps every source inside (no pool; dense steps and fused windows always use it).
+  tgsim_delivery* emit_pool;
+  uint32_t* emit_pool_idx;
   // Gossip receipts folded into the simulate kernels (single shard, GossipArgs' tables), or null:
   // every emitted record is a receipt at its destination the moment its delivery time is known
   uint32_t* g_first;        // [s][64] earliest receipt tick
@@ -130,8 +137,9 @@ struct SimArgs {
   // sparse kernels' FIFO path so that an idle source's check needs no read of its queue head; every
   // other writer of SrcState stores 0 (TGSIM_HEAD_HINT builds read it)
   uint64_t* qhint;
-  uint64_t pad_[1];  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the
-                     // scheduler spilled 9 more SGPRs in k_sim_fused (155 -> 164)
+  uint32_t emit_r, emit_pool_cap;
+  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the scheduler spilled
+  // 9 more SGPRs in k_sim_fused (155 -> 164)
 };
 static_assert(sizeof(SimArgs) == 264, "SimArgs must stay 264 B");
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
@@ -163,6 +171,22 @@ struct FusedArgs {
 };
 constexpr uint32_t kErrHandoff = 2u;  // a window waited too long for its source's previous window
 constexpr uint32_t kErrDeliverCap = 4u;  // a local delivery's records exceed its buffers (TGSIM_DELIVER_SLACK)
+constexpr uint32_t kErrEmitPool = 8u;    // a sparse window's records overflowed the emit pool (TGSIM_EMIT_POOL)
+
+// Where a window's records are, for the kernels that read them (scatter, routing, metrics,
+// receipts): record i of source s is at base + 2*off[s] + r*s + i for i < cap_s = 2 n_s + r, else at
+// pool + pool_idx[s] + (i - cap_s).  r = kHeapCap: the classic layout (no pool).
+struct EmitRead {
+  const tgsim_delivery* base;
+  const tgsim_delivery* pool;
+  const uint32_t* pool_idx;
+  uint32_t r;
+};
+__host__ __device__ inline const tgsim_delivery* emit_rec(const EmitRead& e, uint32_t s, uint64_t o0, uint64_t o1,
+                                                         uint32_t i, uint32_t pidx) {
+  const uint64_t cap = 2 * (o1 - o0) + e.r;
+  return i < cap ? e.base + 2 * o0 + (uint64_t)e.r * s + i : e.pool + pidx + (i - cap);
+}
 // Local delivery of a fused group: window w's emit regions, counts and CSR offsets; pos holds the
 // scatter cursors of the g * n_dst (window, destination) segments.
 struct GroupDeliver {
@@ -181,7 +205,7 @@ struct MetricsArgs {
   const uint64_t* off;          // the step's CSR offsets (S+1)
   const InRec* in;
   const uint8_t* verdict;
-  const tgsim_delivery* emit;   // per-source emit regions, base 2*off[s] + kHeapCap*s
+  EmitRead emit;                // the step's records (per-source regions and pool)
   const uint32_t* emit_n;
   const SrcState* state;
   uint32_t n_src;

@@ -13,6 +13,7 @@
 //   k_dst_*        K5: counting sort of deliveries by destination, then a per-destination sort
 //                  by (t, src, seq, clone-first).
 #include <errno.h>
+#include <stdlib.h>
 #include "tgsim_launch.h"
 
 namespace tgsim {
@@ -273,6 +274,40 @@ __device__ __forceinline__ void fold_receipt(const RecvFold& g, uint32_t dst, ui
     __hip_atomic_fetch_or(&g.pend[s], 1ull << f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Emit slots of one source in one window (SimArgs::emit_r): the first cap in its region,
+// the rest claimed from the window's pool.  A claim the pool cannot hold raises kErrEmitPool (-ENOSPC
+// at the next call) and the records past cap are dropped (over stays null).
+struct EmitOut {
+  tgsim_delivery* region;
+  tgsim_delivery* over;
+  uint32_t cap;
+  __device__ __forceinline__ bool fits(uint32_t i) const { return i < cap || over != nullptr; }
+  __device__ __forceinline__ tgsim_delivery* at(uint32_t i) const { return i < cap ? region + i : over + (i - cap); }
+};
+__device__ __forceinline__ EmitOut emit_out(const SimArgs& a, uint32_t s, uint64_t sbeg, uint64_t send) {
+  EmitOut o;
+  o.region = a.emit + 2 * sbeg + (uint64_t)a.emit_r * s;
+  o.over = nullptr;
+  o.cap = (uint32_t)(2 * (send - sbeg)) + a.emit_r;
+  return o;
+}
+// For up to `total` records: what exceeds the region comes from the pool, one atomic (lane 0; the
+// caller is wave-uniform).  The classic layout (emit_r = kHeapCap) never needs it.
+__device__ __forceinline__ void emit_claim(const SimArgs& a, uint32_t s, EmitOut& o, uint32_t total, uint32_t lane) {
+  if (total <= o.cap) return;
+  const uint32_t need = total - o.cap;
+  uint32_t at = 0;
+  if (lane == 0) at = atomicAdd(a.worklist - 2, need);
+  at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
+  if ((uint64_t)at + need <= a.emit_pool_cap) {
+    o.over = a.emit_pool + at;
+    if (lane == 0) a.emit_pool_idx[s] = at;
+  } else if (lane == 0) {
+    atomicOr(&a.stats[kStErr], (unsigned long long)kErrEmitPool);
+    if (a.err_host) __hip_atomic_store(a.err_host, (uint64_t)kErrEmitPool, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __device__ __forceinline__ uint32_t fib_lookup(const Interval* iv, uint32_t n, uint32_t ip) {
   uint32_t lo = 0, hi = n;  // binary search over sorted disjoint intervals
   while (lo < hi) {
@@ -372,7 +407,9 @@ __device__ __forceinline__ void wave_sort_items(uint4& v, bool has, uint32_t lan
   sort_merge<2>(v, vf, lane);
 }
 
-template <uint32_t kCap>
+// kOver: the records may run past the source's region into the emit pool (k_sim_list of a sparse
+// window in the compact layout: over/cap set by the caller); otherwise emit + n_emit, classic layout.
+template <uint32_t kCap, bool kOver = false>
 struct SimQueue {
   static constexpr uint32_t kSlotMask = kCap - 1;
   SimLdsT<kCap>& lds;
@@ -384,6 +421,8 @@ struct SimQueue {
   uint64_t H;               // the step's horizon: every serve is before it; soon items e < H <= far
   uint64_t tat;             // HTB theoretical arrival time
   tgsim_delivery* emit;
+  tgsim_delivery* over;      // kOver: records from cap on (null: the pool could not take them, dropped)
+  uint32_t cap;              // kOver: records that fit in the source's region
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
   RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
@@ -451,6 +490,40 @@ struct SimQueue {
   // An item whose destination went away while it was queued (kDeadDst, k_purge) still takes its
   // HTB turn and its place in the ring (it leaves the sender) but emits no record.
   __device__ __forceinline__ void commit(bool c, uint32_t n, const uint4& qi, uint64_t d, uint64_t tat_after) {
+    if constexpr (kOver) commit_over(c, n, qi, d, tat_after);
+    else commit_plain(c, n, qi, d, tat_after);
+  }
+  // records past the region with no pool space are dropped (kErrEmitPool)
+  __device__ __forceinline__ void commit_over(bool c, uint32_t n, const uint4& qi, uint64_t d, uint64_t tat_after) {
+    bool live = c && qi.w != kDeadDst;
+    const uint32_t ri = n_emit + (uint32_t)__popcll(__ballot(live) & ((1ull << lane) - 1));
+    live = live && (ri < cap || over != nullptr);
+    const uint64_t lm = __ballot(live);
+    if (c) {
+      *reinterpret_cast<uint2*>(&slot(rn + lane)) = make_uint2((uint32_t)d, (uint32_t)(d >> 32));
+      if (live) {
+        const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
+        uint64_t* rw = reinterpret_cast<uint64_t*>(ri >= cap ? over + (ri - cap) : emit + ri);
+        rw[0] = d;
+        rw[1] = ((uint64_t)qi.w << 32) | src;
+        rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
+        if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
+        if (rf.first && qi.w - rf.shard_begin < rf.n_local)
+          fold_receipt(rf, qi.w, qi.z, flags, d, kFwdSentinel ? 0ull : rf.fwd[qi.w - rf.shard_begin]);
+        sched++;
+        bytes += len;
+        corrupted += (flags >> 1) & 1u;
+      } else {
+        lost++;
+      }
+    }
+    tat = readlane64(tat_after, n - 1);
+    rn += n;
+    qn -= n;
+    n_emit += (uint32_t)__popcll(lm);
+    wave_lds_sync();
+  }
+  __device__ __forceinline__ void commit_plain(bool c, uint32_t n, const uint4& qi, uint64_t d, uint64_t tat_after) {
     const bool live = c && qi.w != kDeadDst;
     const uint64_t lm = __ballot(live);
     if (c) {
@@ -905,7 +978,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   const uint32_t lane = threadIdx.x;
   constexpr uint32_t kSlotMask = kCap - 1;
   stamp(a, wg, lane, 0, __builtin_amdgcn_s_memrealtime());
-  const uint64_t t_begin = a.dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const SrcParams pp = a.params[s];
   constexpr bool kH = kMode == kModeHandoff, kBounded = kMode != kModePlain;
   constexpr int kPol = kH ? kSc1 : 0;
@@ -916,7 +988,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   } else {
     st = a.state[s];
   }
-  SimQueue<kCap> Q{lds, pp, lane};
+  SimQueue<kCap, kList> Q{lds, pp, lane};
   Q.rh = 0;
   Q.rn = st.ring_n;
   Q.qn = q_near(st);
@@ -925,7 +997,14 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.H = a.horizon_ns;
   Q.tat = st.tat;
   Q.src = a.shard_begin + s;
-  Q.emit = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
+  // dense steps and fused windows: the classic layout; k_sim_list: the window's (EmitRead, emit_claim below)
+  Q.emit = a.emit + 2 * a.off[s] + (uint64_t)(kList ? a.emit_r : kHeapCap) * s;
+  if constexpr (kList) {  // at most the queue at the start plus two items per offered packet are served
+    EmitOut eo = emit_out(a, s, a.off[s], a.off[s + 1]);
+    emit_claim(a, s, eo, st.heap_n + (uint32_t)(2 * (a.off[s + 1] - a.off[s])), lane);
+    Q.over = eo.over;
+    Q.cap = eo.cap;
+  }
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
@@ -1388,10 +1467,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   QCHECK(4);
   PROF_ADD(13, e);
   if (lane == 0) a.emit_n[s] = Q.n_emit;
-  if (a.dur) {
-    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) a.dur[s] = (uint32_t)(t_end - t_begin);
-  }
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   uint32_t next_ticket = 0;
   if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
@@ -1594,7 +1669,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
   const uint32_t n = (uint32_t)(send - sbeg);
   const uint32_t rn = st.ring_n, qn = st.heap_n;
   auto defer = [&]() {
-    if (lane == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
+    if (lane == 0) a.worklist[atomicAdd(a.worklist - 4, 1u)] = s;
   };
   // (k_sim_sparse checked the rest: no correlated draws, below the netem limit even if every offered
   // packet and a clone were queued -- so the candidates fit behind the tail, qn + n < kHeapCap --, at
@@ -1747,7 +1822,8 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
   uint32_t emitted = 0, sk0 = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
   bool releasing = T_enq && !ring_stop;
-  tgsim_delivery* const emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
+  EmitOut eo = emit_out(a, s, sbeg, send);
+  emit_claim(a, s, eo, ns_all, lane);
   for (uint32_t base = 0; base < ns_all; base += kWave) {
     const uint32_t k = base + lane;
     const uint32_t ns = ns_all - base < kWave ? ns_all - base : kWave;
@@ -1767,12 +1843,14 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     const uint64_t before = shr1_u64(tat_after, tat_c);
     const uint64_t d = e > before ? e : before;
     tat_c = readlane64(tat_after, ns - 1);
-    const bool live = hs && x.w != kDeadDst;
+    bool live = hs && x.w != kDeadDst;
+    const bool dead = hs && !live;
+    const uint32_t i = emitted + (uint32_t)__popcll(__ballot(live) & below);
+    live = live && eo.fits(i);  // past the region with no pool space: dropped (kErrEmitPool)
     const uint64_t lm = __ballot(live);
     if (live) {
       const uint32_t flags = x.y >> 30;
-      const uint32_t i = emitted + (uint32_t)__popcll(lm & below);
-      uint64_t* rw = reinterpret_cast<uint64_t*>(emit + i);
+      uint64_t* rw = reinterpret_cast<uint64_t*>(eo.at(i));
       rw[0] = d;
       rw[1] = ((uint64_t)x.w << 32) | src;
       rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
@@ -1782,7 +1860,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     }
     emitted += (uint32_t)__popcll(lm);
     t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
-    t_lost += (uint32_t)__popcll(__ballot(hs && !live));
+    t_lost += (uint32_t)__popcll(__ballot(dead));
     if (releasing) {  // a prefix of the served entries departed before the last enqueue
       const uint32_t n1 = (uint32_t)__popcll(__ballot(hs && e < T_enq));
       const uint64_t m = __ballot(lane < n1 && d >= T_enq);
@@ -1837,7 +1915,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
 
 // The multi-round list k_sim_sparse writes: its count is the word after the worklist's count (one
 // memset clears both), its sources follow the worklist's statistics words.
-__device__ __forceinline__ uint32_t* multi_count(const SimArgs& a) { return a.worklist_n + 1; }
+__device__ __forceinline__ uint32_t* multi_count(const SimArgs& a) { return a.worklist - 3; }
 __device__ __forceinline__ uint32_t* multi_list(const SimArgs& a) { return a.worklist + a.n_src + 8; }
 
 __global__ __launch_bounds__(kWave) void k_sim_multi(SimArgs a) {
@@ -1869,7 +1947,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const uint32_t n = (uint32_t)(send - sbeg);
   const uint32_t rn = st.ring_n, qn = st.heap_n;
   auto defer = [&](uint32_t why) {
-    if (lane == 0) a.worklist[atomicAdd(a.worklist_n, 1u)] = s;
+    if (lane == 0) a.worklist[atomicAdd(a.worklist - 4, 1u)] = s;
 #ifdef TGSIM_DEFER_STATS  // diagnostic build: deferrals by reason, behind the list
     if (lane == 0) atomicAdd(a.worklist + a.n_src + why, 1u);
 #else
@@ -2167,7 +2245,8 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   uint32_t emitted = 0, sk0 = 0, t_sched = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
   bool releasing = T_enq && !ring_stop;  // served entries departing before the last enqueue are released
-  tgsim_delivery* const emit = a.emit + 2 * sbeg + (uint64_t)kHeapCap * s;
+  EmitOut eo = emit_out(a, s, sbeg, send);
+  emit_claim(a, s, eo, ns_all, lane);
   for (uint32_t base = 0;; base += kWave) {
     const bool hs = lane < ns;
     // the destinations' forwarded masks, for the receipts folded in below (in flight during the scan)
@@ -2189,12 +2268,14 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     if (ns) tat_c = readlane64(tat_after, ns - 1);
     stamp(a, s, lane, 3, __builtin_amdgcn_s_memrealtime());
     // records of the served items (dead destinations leave the sender and are lost)
-    const bool live = hs && x.w != kDeadDst;
+    bool live = hs && x.w != kDeadDst;
+    const bool dead = hs && !live;
+    const uint32_t i = emitted + (uint32_t)__popcll(__ballot(live) & below);
+    live = live && eo.fits(i);  // past the region with no pool space: dropped (kErrEmitPool)
     const uint64_t lm = __ballot(live);
     if (live) {
       const uint32_t flags = x.y >> 30;
-      const uint32_t i = emitted + (uint32_t)__popcll(lm & below);
-      uint64_t* rw = reinterpret_cast<uint64_t*>(emit + i);
+      uint64_t* rw = reinterpret_cast<uint64_t*>(eo.at(i));
       rw[0] = d;
       rw[1] = ((uint64_t)x.w << 32) | src;
       rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
@@ -2204,7 +2285,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     }
     emitted += (uint32_t)__popcll(lm);
     t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
-    t_lost += (uint32_t)__popcll(__ballot(hs && !live));
+    t_lost += (uint32_t)__popcll(__ballot(dead));
     // the served entries join the ring, behind the old entries kept; a prefix of them departing
     // before the last enqueue was released with the old ring (when that released all of it)
     if (releasing) {
@@ -2324,7 +2405,7 @@ __global__ __launch_bounds__(kWave * kSparseWpg, 7) void k_sim_sparse(SimArgs a)
 // length is read on the device, so the launch needs no host round trip).
 __global__ __launch_bounds__(kWave) void k_sim_list(SimArgs a) {
   __shared__ SimLdsT<kHeapCap> lds;
-  const uint32_t n = *a.worklist_n;
+  const uint32_t n = a.worklist[-4];
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t s = a.worklist[i];
     if (a.g_first) sim_source<false, kHeapCap, kModePlain, true, true>(a, s, s, lds);
@@ -2577,14 +2658,15 @@ __global__ __launch_bounds__(256) void k_gossip_nbr(GossipArgs g, uint32_t* nbr)
 // the gossip loop's next window then waits for k_sim and this kernel only, while the scatter and
 // the per-destination sort run beside it at low priority.  Receipts are order-free (earliest tick
 // wins), and a delivery of an already forwarded flood costs one read of its peer's mask.
-__global__ __launch_bounds__(256) void k_gossip_recv_emit(GossipArgs g, const tgsim_delivery* emit, const uint32_t* emit_n,
+__global__ __launch_bounds__(256) void k_gossip_recv_emit(GossipArgs g, EmitRead emit, const uint32_t* emit_n,
                                                           const uint64_t* off, uint32_t n_src) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nw = gridDim.x * 4;
   for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
     const uint32_t n = emit_n[s];
-    const tgsim_delivery* base = emit + 2 * off[s] + (uint64_t)kHeapCap * s;
-    for (uint32_t i = lane; i < n; i += kWave) gossip_recv_one(g, base[i]);
+    const uint64_t o0 = off[s], o1 = off[s + 1];
+    const uint32_t pidx = n > 2 * (o1 - o0) + emit.r ? emit.pool_idx[s] : 0u;
+    for (uint32_t i = lane; i < n; i += kWave) gossip_recv_one(g, *emit_rec(emit, s, o0, o1, i, pidx));
   }
 }
 
@@ -2844,9 +2926,9 @@ __global__ __launch_bounds__(1024) void k_scan_small(const uint64_t* in, uint64_
 // contended atomics: per (rank, source) counts -> one exclusive scan over [rank][source] -> every
 // source writes its records of rank r at off[r * S + s] in emission order.
 struct RouteArgs {
-  const tgsim_delivery* emit;
+  EmitRead emit;
   const uint32_t* emit_n;
-  const uint64_t* off;           // CSR offsets of the step input: region base 2*off[s] + kHeapCap*s
+  const uint64_t* off;           // CSR offsets of the step input (the emit regions, EmitRead)
   uint32_t n_src;
   uint32_t n_ranks;
   uint32_t bounds[9];
@@ -2875,11 +2957,12 @@ __global__ __launch_bounds__(64 * W) void k_route_count(RouteArgs a) {
       if (lane == 0) a.cnt[s] = n;
       continue;
     }
-    const tgsim_delivery* base = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
+    const uint64_t o0 = a.off[s], o1 = a.off[s + 1];
+    const uint32_t pidx = n > 2 * (o1 - o0) + a.emit.r ? a.emit.pool_idx[s] : 0u;
     uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
       const uint32_t i = i0 + lane;
-      const uint32_t rk = i < n ? rank_of(a, base[i].dst) : 0xFFFFFFFFu;
+      const uint32_t rk = i < n ? rank_of(a, emit_rec(a.emit, s, o0, o1, i, pidx)->dst) : 0xFFFFFFFFu;
 #pragma unroll
       for (uint32_t q = 0; q < 8; ++q) c[q] += __popcll(__ballot(rk == q));
     }
@@ -2898,7 +2981,8 @@ __global__ __launch_bounds__(64 * W) void k_route_scatter(RouteArgs a) {
   const uint32_t nw = gridDim.x * W;
   for (uint32_t s = blockIdx.x * W + (threadIdx.x >> 6); s < a.n_src; s += nw) {
     const uint32_t n = a.emit_n[s];
-    const tgsim_delivery* base = a.emit + 2 * a.off[s] + (uint64_t)kHeapCap * s;
+    const uint64_t o0 = a.off[s], o1 = a.off[s + 1];
+    const uint32_t pidx = n > 2 * (o1 - o0) + a.emit.r ? a.emit.pool_idx[s] : 0u;
     uint64_t run[8], edge[8];
 #pragma unroll
     for (uint32_t q = 0; q < 8; ++q) {
@@ -2910,7 +2994,7 @@ __global__ __launch_bounds__(64 * W) void k_route_scatter(RouteArgs a) {
       tgsim_delivery r;
       uint32_t rk = 0xFFFFFFFFu;
       if (i < n) {
-        r = base[i];
+        r = *emit_rec(a.emit, s, o0, o1, i, pidx);
         rk = rank_of(a, r.dst);
       }
       const uint64_t below = (1ull << lane) - 1;
@@ -3021,16 +3105,17 @@ __global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst
 }
 
 // Single shard: straight from k_sim's per-source emit regions (counts were taken by k_sim).
-__global__ __launch_bounds__(256) void k_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n,
+__global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint32_t* emit_n,
                                                        const uint64_t* off, uint32_t n_src, uint32_t dst_begin,
                                                        uint64_t* pos, tgsim_delivery* out) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nw = gridDim.x * 4;
   for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
     const uint32_t n = emit_n[s];
-    const tgsim_delivery* base = emit + 2 * off[s] + (uint64_t)kHeapCap * s;
+    const uint64_t o0 = off[s], o1 = off[s + 1];
+    const uint32_t pidx = n > 2 * (o1 - o0) + emit.r ? emit.pool_idx[s] : 0u;
     for (uint32_t i = lane; i < n; i += kWave) {
-      const tgsim_delivery r = base[i];
+      const tgsim_delivery r = *emit_rec(emit, s, o0, o1, i, pidx);
       out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[r.dst - dst_begin]), 1ull)] = r;
     }
   }
@@ -3042,25 +3127,30 @@ __global__ __launch_bounds__(256) void k_local_scatter(const tgsim_delivery* emi
 // destinations first, so that a destination's records share one cursor atomic.  The wave per source above walks
 // its sources one after another, each behind four dependent round trips with 57 of 64 lanes idle.
 template <bool kAgg>
-__global__ __launch_bounds__(256) void k_local_scatter_ls(const tgsim_delivery* __restrict__ emit,
+__global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
                                                           const uint32_t* __restrict__ emit_n,
                                                           const uint64_t* __restrict__ off, uint32_t n_src,
                                                           uint32_t dst_begin, uint64_t* pos,
                                                           tgsim_delivery* __restrict__ out) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-  uint32_t n = 0;
-  const tgsim_delivery* base = emit;
+  uint32_t n = 0, cap = 0;
+  const tgsim_delivery* base = emit.base;  // the source's region: its first cap records
+  const tgsim_delivery* over = emit.pool;  // the rest, from the pool
   if (s < n_src) {
     n = emit_n[s];
-    base = emit + 2 * off[s] + (uint64_t)kHeapCap * s;
+    const uint64_t o0 = off[s], o1 = off[s + 1];
+    cap = (uint32_t)(2 * (o1 - o0)) + emit.r;
+    base = emit.base + 2 * o0 + (uint64_t)emit.r * s;
+    if (n > cap) over = emit.pool + emit.pool_idx[s];
   }
+  auto rec = [&](uint32_t i) -> const tgsim_delivery& { return i < cap ? base[i] : over[i - cap]; };
   unsigned long long* p = reinterpret_cast<unsigned long long*>(pos);
   if constexpr (!kAgg) {  // records to many destinations (storm shapes): one cursor atomic each
     for (uint32_t i = 0; __ballot(i < n); i += 4) {
       tgsim_delivery r[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
-        if (i + u < n) r[u] = base[i + u];
+        if (i + u < n) r[u] = rec(i + u);
       uint64_t at[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
@@ -3083,7 +3173,7 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(const tgsim_delivery* 
   for (uint32_t i = 0; __ballot(i < n); i += 4) {
     uint32_t d[4];
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) d[u] = i + u < n ? base[i + u].dst : ~0u;
+    for (uint32_t u = 0; u < 4; ++u) d[u] = i + u < n ? rec(i + u).dst : ~0u;
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
       if (i + u >= n) continue;
@@ -3113,7 +3203,7 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(const tgsim_delivery* 
     tgsim_delivery r[4];
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u)
-      if (i + u < n) r[u] = base[i + u];
+      if (i + u < n) r[u] = rec(i + u);
     uint64_t w[4];
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
@@ -3416,9 +3506,9 @@ __global__ __launch_bounds__(256) void k_metrics_src(MetricsArgs m) {
     bytes += m.in[i].len & 0xFFFFu;
   }
   const uint32_t n_emit = m.emit_n[s];
-  const tgsim_delivery* e = m.emit + 2 * b0 + (uint64_t)kHeapCap * s;
+  const uint32_t pidx = n_emit > 2 * (b1 - b0) + m.emit.r ? m.emit.pool_idx[s] : 0u;
   uint64_t sbytes = 0;
-  for (uint32_t i = lane; i < n_emit; i += kWave) sbytes += e[i].len;
+  for (uint32_t i = lane; i < n_emit; i += kWave) sbytes += emit_rec(m.emit, s, b0, b1, i, pidx)->len;
   unsigned long long* row = m.src + (size_t)s * kMetricSrcWords;
   uint32_t tv[8];
 #pragma unroll
@@ -3455,6 +3545,14 @@ __global__ __launch_bounds__(256) void k_metrics_dst(const tgsim_delivery* recs,
 
 // ---------------------------------------------------------------------------------------------
 // Host-side launchers.
+// Diagnostic knobs of the delivery kernels' choice (A/B of the sub-capacity storm):
+// TGSIM_SPARSE_SORT=1 sorts sparse windows one wavefront per destination instead of flattened;
+// TGSIM_LOCAL_SCATTER=1 lane per source always, 2 wavefront per source always.
+static int env_knob(const char* name) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : 0;
+}
+
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   if (a.g_first) hipLaunchKernelGGL(k_sim_recv, dim3(n_wg), dim3(kWave), 0, st, a);
   else hipLaunchKernelGGL(k_sim, dim3(n_wg), dim3(kWave), 0, st, a);  // n_wg = ceil(n_src / kSpw)
@@ -3573,7 +3671,7 @@ void launch_gossip_nbr(const GossipArgs& g, uint32_t* nbr, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_gossip_nbr, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, g, nbr);
 }
 
-void launch_gossip_recv_emit(const GossipArgs& g, const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off,
+void launch_gossip_recv_emit(const GossipArgs& g, const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off,
                              uint32_t n_src, hipStream_t st) {
   if (!n_src) return;
   const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);
@@ -3702,11 +3800,12 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
   hipLaunchKernelGGL(k_deliver_guard, dim3(1), dim3(1024), 0, st, total, cap, emit_n, n_src, cnt, off, n_dst, err_host);
 }
 
-void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
+void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint,
                           bool few_dst) {
   if (!n_src) return;
-  if (n_hint <= 64ull * n_src) {  // up to tens of records per source (gossip, even at the flood's peak): one lane each
+  static const int mode = env_knob("TGSIM_LOCAL_SCATTER");
+  if ((n_hint <= 64ull * n_src && mode != 2) || mode == 1) {  // up to tens of records per source (gossip, even at the flood's peak): one lane each
     // few_dst (gossip: a peer forwards to its neighbours): one cursor atomic per destination of a
     // source (1M-peer gossip +1-2 %); with records to many destinations that pass over the records
     // costs more than it saves (sub-capacity storm 1.09 against 1.15-1.17 G pkt/s)
@@ -3725,7 +3824,8 @@ void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, co
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                      tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin) {
   if (!n_dst) return;
-  if (!cnt && n_hint <= 48ull * n_dst) {
+  static const int sparse_sort = env_knob("TGSIM_SPARSE_SORT");
+  if (!cnt && n_hint <= 48ull * n_dst && sparse_sort != 1) {
     // up to tens of records per destination (gossip, sparse windows): 64 records per wave-iteration
     // over the records, on a grid of at most 8,192 workgroups of 4 waves.  At the 1M-peer flood's
     // peak it replaced a wavefront per destination (or lane groups of 8-32 for short segments):

@@ -11,7 +11,7 @@ struct GenArgsHost {
 };
 
 struct RouteArgsHost {
-  const tgsim_delivery* emit;
+  EmitRead emit;
   const uint32_t* emit_n;
   const uint64_t* off;
   uint32_t n_src;
@@ -57,7 +57,7 @@ void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_
                         unsigned long long* hist, hipStream_t st);
 // Receipts of n_dev[0] records (count read on the device).
 void launch_gossip_nbr(const GossipArgs& g, uint32_t* nbr, hipStream_t st);
-void launch_gossip_recv_emit(const GossipArgs& g, const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off,
+void launch_gossip_recv_emit(const GossipArgs& g, const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off,
                              uint32_t n_src, hipStream_t st);
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st);
 void launch_gossip_recv_in(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t slot, bool skip_own,
@@ -89,7 +89,7 @@ void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin
                         tgsim_delivery* out, hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n, uint32_t n_src, uint64_t* cnt,
                           uint64_t* off, uint32_t n_dst, uint64_t* err_host, hipStream_t st);
-void launch_local_scatter(const tgsim_delivery* emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
+void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
                           uint64_t n_hint, bool few_dst = false);
 // Orders each destination's records (segment d: off[d] .. off[d + 1]; dst_begin: the first

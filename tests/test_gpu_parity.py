@@ -678,3 +678,81 @@ def test_multi_round_fifo_sources(make_oracle, monkeypatch):
         c.step(4000)
         _, d = assert_same(g, c, f"step {step}")
         assert len(d) > 0
+
+
+@pytest.mark.parametrize("reserve", [1, 8])
+def test_compact_emit_layout(make_oracle, monkeypatch, reserve):
+    """the compact emit layout (sparse windows keep 2 records per offered packet
+    plus `reserve` per source in place; a source that serves more of its old queue claims the rest
+    from the window's pool), forced on small windows with a tiny reserve so that most sources use the
+    pool, through k_sim_sparse, k_sim_multi and k_sim_list; bit-exact with the oracle."""
+    monkeypatch.setenv("TGSIM_SPARSE", "1")
+    monkeypatch.setenv("TGSIM_EMIT_COMPACT", "2")
+    monkeypatch.setenv("TGSIM_EMIT_R", str(reserve))
+    n = 80
+    rng = np.random.default_rng(31)
+    g, c = both(make_oracle, n, queue_limit=1024)
+    for i in range(n):
+        # latency longer than a window: old queue items are served next to a few new ones; every 8th
+        # source offers > 64 packets (k_sim_multi), every 10th + 3 duplicates (k_sim_list)
+        s = nw.LinkShape(Latency=int(rng.integers(3, 9)) * nw.Millisecond, Bandwidth=1 << 30, Loss=1.0,
+                         Duplicate=3.0 if i % 10 == 3 else 0.0)
+        for e in (g, c):
+            e.configure(i, nw.Config(Network="default", Enable=True, Default=s))
+    seq = np.zeros(n, dtype=np.uint32)
+    for step in range(14):
+        burst = step % 4 == 0  # bursts, then quiet windows that serve the queued items
+        per = np.where(np.arange(n) % 8 == 0, rng.integers(100, 200, n), rng.integers(20, 60, n)) if burst \
+            else rng.integers(0, 4, n)
+        src = np.repeat(np.arange(n), per)
+        m = len(src)
+        pk = np.zeros(m, dtype=abi.PKT_DTYPE)
+        pk["src"] = src
+        pk["dst"] = (src + 1 + rng.integers(0, n - 1, m)) % n
+        pk["len"] = rng.integers(40, 1500, m)
+        pk["tick"] = rng.integers(0, 2000, m)
+        order = np.lexsort((pk["tick"], src))
+        counts = np.bincount(src, minlength=n)
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        sq = np.empty(m, dtype=np.uint32)
+        sq[order] = np.arange(m) - starts[src[order]] + seq[src[order]]
+        seq += counts.astype(np.uint32)
+        pk["seq"] = sq
+        g.submit(pk)
+        c.submit(pk)
+        g.step(2000)
+        c.step(2000)
+        assert_same(g, c, f"reserve {reserve} step {step}")
+
+
+def test_compact_emit_pool_overflow_fails(monkeypatch):
+    """A compact window whose sources need more pool than it holds fails loudly (-ENOSPC at the
+    next call), never silently: records past a region with no pool space are not delivered."""
+    import errno
+
+    from testground_amd.engine import EngineError
+
+    monkeypatch.setenv("TGSIM_SPARSE", "1")
+    monkeypatch.setenv("TGSIM_EMIT_COMPACT", "2")
+    monkeypatch.setenv("TGSIM_EMIT_R", "1")
+    monkeypatch.setenv("TGSIM_EMIT_POOL", "0")
+    n = 40
+    g = Engine(n)
+    for i in range(n):
+        g.configure(i, nw.Config(Network="default", Enable=True,
+                                 Default=nw.LinkShape(Latency=5 * nw.Millisecond, Bandwidth=1 << 30)))
+    seq = np.zeros(n, dtype=np.uint32)
+    with pytest.raises(EngineError) as ei:
+        for step in range(6):
+            per = np.full(n, 30) if step == 0 else np.zeros(n, dtype=np.int64)
+            src = np.repeat(np.arange(n), per)
+            pk = np.zeros(len(src), dtype=abi.PKT_DTYPE)
+            pk["src"], pk["dst"] = src, (src + 1) % n
+            pk["len"], pk["tick"] = 100, 0
+            pk["seq"] = np.arange(len(src)) - np.repeat(np.concatenate([[0], np.cumsum(per)[:-1]]), per) + seq[src]
+            seq += per.astype(np.uint32)
+            g.submit(pk)
+            g.step(2000)
+        g.sync()
+    assert ei.value.code == -errno.ENOSPC and "emit pool" in str(ei.value)
+    g.close()
