@@ -410,6 +410,15 @@ def init_host_group(world):
     return dist
 
 
+T_START = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (the JSON line alone goes to stdout): a long default run keeps
+    writing, so that a watchdog on the GPU box never takes it for a hung run."""
+    print(f"bench [{time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def runs_cpu_baseline(rank, want_cpu):
     """North star: the oracle is timed 'on the box's own host cores in the same run' beside the GPU
     line at every world size; rank 0 runs it (after the timed region, the other ranks wait)."""
@@ -577,9 +586,12 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     eng.close()
     del eng, stepper
     cpu = None
+    progress(f"{workload} ({shapes if workload == 'storm' else workload}, {peers_total} peers): "
+             f"{offered_all / el / 1e9:.3f} G pkt/s, {el * 1e3 / steps:.4f} ms/step")
     if runs_cpu_baseline(rank, want_cpu):  # the oracle on this host's cores, beside the line at every N
         cpu = cpu_baseline(a, workload, peers_total, lam, window,
                            a.cpu_seconds if workload == "storm" else a.cpu_seconds / 2, shapes=shapes)
+        progress(f"{workload} CPU baseline: {cpu['value'] / 1e6:.1f} M pkt/s")
     if dist:  # the other ranks wait here for rank 0's CPU legs before the next collective
         torch.cuda.synchronize()
         dist.barrier()

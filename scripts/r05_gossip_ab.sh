@@ -11,7 +11,8 @@ for rep in 1 2; do
     lib=$PWD/testground_amd/libtgsim.so; env=TGSIM_X=0; dir=.
     case $v in cur) ;; tree:*) dir=${v#tree:}; lib=$PWD/$dir/testground_amd/libtgsim.so;; *=*) env=$v;; *) lib=$PWD/testground_amd/libtgsim_$v.so;; esac
     tag=$(echo $v | tr '=:/' '___')
-    ( cd $dir && env $env TGSIM_LIB=$lib timeout -k 10 300 python bench.py $ARGS > $O/${tag}_$rep.json 2> $O/${tag}_$rep.err ) || { echo "$v failed"; tail $O/${tag}_$rep.err; exit 1; }
+    targs=$ARGS; case $v in tree:*) targs=${ARGS//--no-variants/};; esac  # older trees lack the flag
+    ( cd $dir && env $env TGSIM_LIB=$lib timeout -k 10 300 python bench.py $targs > $O/${tag}_$rep.json 2> $O/${tag}_$rep.err ) || { echo "$v failed"; tail $O/${tag}_$rep.err; exit 1; }
     python -c "import json;d=json.loads(open('$O/${tag}_$rep.json').read().strip().splitlines()[-1]);print('$v', round(d['value']/1e9,3), 'G pkt/s', round(d['ms_per_step'],4), 'ms/step sim', round(d['roofline']['kernel_ms_avg'],4))"
   done
 done
