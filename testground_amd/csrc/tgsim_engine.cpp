@@ -217,6 +217,8 @@ struct tgsim_engine_s {
   std::vector<PendingTiming> dv_pending;  // delivery spans on dst_st (first kernel to the sort), per window
   double dv_ms = 0;
   uint64_t dv_windows = 0;
+  uint32_t dv_every = 1;   // TGSIM_DV_TIMING: time every k-th delivery (0: none)
+  uint64_t dv_count = 0;   // deliveries so far (the sampling counter)
   std::vector<hipEvent_t> ev_pool;
   uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
   uint64_t* h_pub = nullptr;    // pinned words a scan publishes: [0] total, [1] flag, [2] sequence;
@@ -1275,10 +1277,13 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
   const uint64_t nseg = static_cast<uint64_t>(n_win) * nd;
   hipStream_t sq = E->dst_st;
   if (wait) HIPCHK(hipStreamWaitEvent(sq, wait, 0));
-  hipEvent_t dv0, dv1;  // the delivery's span on its stream (bench: roofline.delivery)
-  HIPCHK(take_event(E, &dv0));
-  HIPCHK(take_event(E, &dv1));
-  HIPCHK(hipEventRecord(dv0, sq));
+  hipEvent_t dv0 = nullptr, dv1 = nullptr;  // the delivery's span on its stream (bench: roofline.delivery)
+  const bool timed = E->dv_every && E->dv_count++ % E->dv_every == 0;
+  if (timed) {
+    HIPCHK(take_event(E, &dv0));
+    HIPCHK(take_event(E, &dv1));
+    HIPCHK(hipEventRecord(dv0, sq));
+  }
   if (E->d_dcnt.cap < nseg) {
     HIPCHK(E->d_dcnt.ensure(nseg));
     HIPCHK(hipMemsetAsync(E->d_dcnt.p, 0, sizeof(uint64_t) * E->d_dcnt.cap, sq));
@@ -1341,8 +1346,10 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipEventRecord(dv1, sq));
-  E->dv_pending.push_back({dv0, dv1, n_win});
+  if (timed) {
+    HIPCHK(hipEventRecord(dv1, sq));
+    E->dv_pending.push_back({dv0, dv1, n_win});
+  }
   HIPCHK(hipEventRecord(E->ev_dst, sq));
   return 0;
 }
@@ -1353,10 +1360,13 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
                        const uint64_t* off, uint64_t n_in, hipEvent_t released) {
   const uint32_t nd = E->N;
   hipStream_t sq = E->dst_st;
-  hipEvent_t dv0, dv1;  // the delivery's span on its stream (bench: roofline.delivery)
-  HIPCHK(take_event(E, &dv0));
-  HIPCHK(take_event(E, &dv1));
-  HIPCHK(hipEventRecord(dv0, sq));
+  hipEvent_t dv0 = nullptr, dv1 = nullptr;  // the delivery's span on its stream (bench: roofline.delivery)
+  const bool timed = E->dv_every && E->dv_count++ % E->dv_every == 0;
+  if (timed) {
+    HIPCHK(take_event(E, &dv0));
+    HIPCHK(take_event(E, &dv1));
+    HIPCHK(hipEventRecord(dv0, sq));
+  }
   HIPCHK(E->d_doff.ensure(nd + 1));
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
@@ -1400,8 +1410,10 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipEventRecord(dv1, sq));
-  E->dv_pending.push_back({dv0, dv1, 1u});
+  if (timed) {
+    HIPCHK(hipEventRecord(dv1, sq));
+    E->dv_pending.push_back({dv0, dv1, 1u});
+  }
   return 0;
 }
 
@@ -1809,6 +1821,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* dd = getenv("TGSIM_DENSE_DIV")) E->dense_div = static_cast<uint32_t>(std::max(1, atoi(dd)));
+  if (const char* dv = getenv("TGSIM_DV_TIMING")) E->dv_every = static_cast<uint32_t>(std::max(0, atoi(dv)));
   if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
   if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));

@@ -3800,12 +3800,17 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
   hipLaunchKernelGGL(k_deliver_guard, dim3(1), dim3(1024), 0, st, total, cap, emit_n, n_src, cnt, off, n_dst, err_host);
 }
 
+constexpr uint32_t kLaneScatterMin = 65536;  // sources: below, the wavefront-per-source scatter
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint,
                           bool few_dst) {
   if (!n_src) return;
   static const int mode = env_knob("TGSIM_LOCAL_SCATTER");
-  if ((n_hint <= 64ull * n_src && mode != 2) || mode == 1) {  // up to tens of records per source (gossip, even at the flood's peak): one lane each
+  // up to tens of records per source and enough sources to fill the chip with one lane each (gossip at
+  // 1M peers, even at the flood's peak): one lane per source.  With fewer sources (the sub-capacity
+  // storm's 10,000: 40 workgroups) a wavefront per source spreads the records over 10,000 waves
+  // (A/B: 1.17-1.19 against 1.09-1.12 G pkt/s)
+  if ((n_hint <= 64ull * n_src && n_src >= kLaneScatterMin && mode != 2) || mode == 1) {
     // few_dst (gossip: a peer forwards to its neighbours): one cursor atomic per destination of a
     // source (1M-peer gossip +1-2 %); with records to many destinations that pass over the records
     // costs more than it saves (sub-capacity storm 1.09 against 1.15-1.17 G pkt/s)
