@@ -178,6 +178,7 @@ struct Comm {
   bool out_busy[3] = {}, in_busy[2] = {};
   uint64_t k = 0;  // launched windows (groups) so far
   DevMem d_cnt;    // count exchange and reductions: 2 x 8 u64
+  uint64_t* dm_cnt = nullptr;  // h_cnt's device address (the publish kernels store through it)
   uint64_t* h_cnt = nullptr;  // pinned, coherent and mapped (the device publishes into it from a running
                               // kernel): [0..8) sent, [8..8 + nranks) received + their sequence word,
                               // [17] reduction result, [18] its sequence word
@@ -322,7 +323,7 @@ int wait_counts(Comm* C) { return wait_word(C, C->h_cnt + 8 + C->nranks, C->cnt_
 int allreduce_u64(Comm* C, const void* dev_src, uint64_t* result, ncclRedOp_t op) {
   const uint64_t* red = reinterpret_cast<const uint64_t*>(C->d_cnt.p + 24 * sizeof(uint64_t));
   CNCCL(C->R->AllReduce(dev_src, const_cast<uint64_t*>(red), 1, ncclUint64, op, C->nc, C->xs));
-  launch_publish_words(red, 1, C->h_cnt + 17, ++C->red_seq, C->xs);
+  launch_publish_words(red, 1, C->dm_cnt + 17, ++C->red_seq, C->xs);
   CHIP(hipGetLastError());
   CHIP(hipEventRecord(C->ev_red, C->xs));
   CRC(wait_word(C, C->h_cnt + 18, C->red_seq, C->ev_red, "all-reduce"));
@@ -382,6 +383,7 @@ int comm_build(Comm* C, const void* id) {
   // on coarse-grained memory would not order the count stores before their sequence word
   CHIP(hipHostMalloc(reinterpret_cast<void**>(&C->h_cnt), 32 * sizeof(uint64_t),
                      hipHostMallocCoherent | hipHostMallocMapped));
+  CHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&C->dm_cnt), C->h_cnt, 0));
   if (const char* to = getenv("TGSIM_COMM_TIMEOUT_MS")) C->timeout_ms = std::max<uint64_t>(1, strtoull(to, nullptr, 10));
   CHIP(C->d_cnt.ensure(32 * sizeof(uint64_t)));
   ncclUniqueId uid;
@@ -509,7 +511,7 @@ int tgsim_comm_finish(void* e) {
   CHIP(hipStreamWaitEvent(C->xs, C->ev_routed[j], 0));
   CNCCL(C->R->AllToAll(dsend, C->d_cnt.p + 8 * sizeof(uint64_t), 1, ncclUint64, C->nc, C->xs));
   launch_publish_words(reinterpret_cast<const uint64_t*>(C->d_cnt.p + 8 * sizeof(uint64_t)), static_cast<uint32_t>(nr),
-                       C->h_cnt + 8, ++C->cnt_seq, C->xs);
+                       C->dm_cnt + 8, ++C->cnt_seq, C->xs);
   CHIP(hipGetLastError());
   CHIP(hipEventRecord(C->ev_cnt, C->xs));
   CRC(tgsim_step_sim_counts(e, send));  // the routing's own published edges (bookkeeping, overflow check)

@@ -218,6 +218,8 @@ struct tgsim_engine_s {
   double dv_ms = 0;
   uint64_t dv_windows = 0;
   uint32_t dv_every = 1;   // TGSIM_DV_TIMING: time every k-th delivery (0: none)
+  uint32_t sim_every = 1;  // TGSIM_SIM_TIMING: time every k-th per-window simulate launch (0: none)
+  uint64_t sim_count = 0;
   uint64_t dv_count = 0;   // deliveries so far (the sampling counter)
   std::vector<hipEvent_t> ev_pool;
   uint32_t* h_gerr = nullptr;   // pinned copy of the gossip driver's late-receipt flag
@@ -231,6 +233,7 @@ struct tgsim_engine_s {
   uint64_t* d_err_host = nullptr;  // its device address
   uint32_t* h_xerr = nullptr;   // pinned sticky flag: a slotted exchange chunk overflowed (k_route_edges)
   uint32_t* h_work = nullptr;   // pinned: sources the last sparse step deferred to k_sim_list, to k_sim_multi
+  uint32_t* dm_work = nullptr;  // its device address (k_work_done stores there)
   uint32_t* d_xerr = nullptr;   // its device address
   // launched, unfinished routed steps (tgsim_step_sim_launch), oldest at route_head: pinned
   // per-rank record edges behind an event, per slot
@@ -1059,28 +1062,36 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   if (sparse) {
     // [0] the worklist's count, [1] k_sim_multi's, [2] emit-pool records claimed, [3] unused, the
     // worklist's sources, 8 words of TGSIM_DEFER_STATS, then k_sim_multi's sources
-    HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 4 + 8));
-    HIPCHK(hipMemsetAsync(E->d_work.p, 0, 4 * sizeof(uint32_t), E->st));
+    if (E->d_work.cap < 2 * static_cast<size_t>(E->S) + 4 + 8) {
+      HIPCHK(E->d_work.ensure(2 * static_cast<size_t>(E->S) + 4 + 8));
+      HIPCHK(hipMemsetAsync(E->d_work.p, 0, sizeof(uint32_t) * E->d_work.cap, E->st));
+    }
     a.worklist = E->d_work.p + 4;
     a.order = nullptr;  // (stamps, when on, are indexed by source: n_wg = S)
   }
-  hipEvent_t ev0, ev1;
-  HIPCHK(take_event(E, &ev0));
-  HIPCHK(take_event(E, &ev1));
-  HIPCHK(hipEventRecord(ev0, E->st));
+  // the simulate kernels' span (bench: roofline): timing events cost the windows they bracket (a
+  // timestamped marker per launch), so TGSIM_SIM_TIMING can sample every k-th window
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  const bool timed = E->sim_every && E->sim_count++ % E->sim_every == 0;
+  if (timed) {
+    HIPCHK(take_event(E, &ev0));
+    HIPCHK(take_event(E, &ev1));
+    HIPCHK(hipEventRecord(ev0, E->st));
+  }
   if (sparse) {
-    launch_sim_sparse(a, E->st);
+    // the worklist counters start zeroed (at allocation, then by the kernel behind the last sparse
+    // step, which also publishes them to pinned memory: no fill or copy on the stream per window)
+    launch_sim_sparse(a, E->st, E->dm_work);
     E->rotated = true;
   }
   else launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
   E->sim_calls++;  // behind the wait for this emit pair's last reader (ev_local): take_gen's count
-  HIPCHK(hipEventRecord(ev1, E->st));
-  if (sparse) {
-    HIPCHK(hipMemcpyAsync(E->h_work, E->d_work.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, E->st));
-    E->sparse_seen = true;
+  if (timed) {
+    HIPCHK(hipEventRecord(ev1, E->st));
+    E->ev_pending.push_back({ev0, ev1, 1u});
   }
-  E->ev_pending.push_back({ev0, ev1, 1u});
+  if (sparse) E->sparse_seen = true;
   if (E->metrics_on) {
     MetricsArgs m;
     m.off = E->d_off.p;
@@ -1795,6 +1806,8 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
                                  hipHostMallocCoherent | hipHostMallocMapped), "pinned")))
     return bail(rc);
   E->h_work[0] = E->h_work[1] = 0;
+  if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->dm_work), E->h_work, 0), "pinned")))
+    return bail(rc);
   if ((rc = E->hip(hipHostGetDevicePointer(reinterpret_cast<void**>(&E->d_xerr), E->h_xerr, 0), "pinned")))
     return bail(rc);
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_gerr), sizeof(uint32_t)), "pinned"))) return bail(rc);
@@ -1821,6 +1834,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
   if (const char* dd = getenv("TGSIM_DENSE_DIV")) E->dense_div = static_cast<uint32_t>(std::max(1, atoi(dd)));
+  if (const char* st = getenv("TGSIM_SIM_TIMING")) E->sim_every = static_cast<uint32_t>(std::max(0, atoi(st)));
   if (const char* dv = getenv("TGSIM_DV_TIMING")) E->dv_every = static_cast<uint32_t>(std::max(0, atoi(dv)));
   if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));

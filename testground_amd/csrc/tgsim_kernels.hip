@@ -3587,12 +3587,22 @@ uint32_t sim_fused_resident() {
   return (uint32_t)(per_cu * cus);
 }
 
-void launch_sim_sparse(const SimArgs& a, hipStream_t st) {
+// Behind the last sparse kernel: the deferral counts to pinned host memory (the next step's sparse/dense
+// choice reads them without waiting) and every counter zeroed for the next sparse step.
+__global__ void k_work_done(uint32_t* work, uint32_t* host) {
+  const uint32_t i = threadIdx.x;
+  if (i < 2) __hip_atomic_store(&host[i], work[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (i < 4) work[i] = 0u;
+}
+
+void launch_sim_sparse(const SimArgs& a, hipStream_t st, uint32_t* work_host) {
   if (!a.n_src) return;
   hipLaunchKernelGGL(k_sim_sparse, dim3(sparse_blocks(a.n_src)), dim3(kWave * kSparseWpg), 0, st, a);
   // (grids of 5,120 and 10,240 waves: the same 1M-peer window, within noise)
   hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 2048 ? a.n_src : 2048), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
+  hipLaunchKernelGGL(k_work_done, dim3(1), dim3(64), 0, st, a.worklist - 4, work_host);
 }
 
 void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream_t st) {
