@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 B=testground_amd/build_$name; mkdir -p $B
 for f in tgsim_kernels.hip tgsim_engine.cpp tgsim_bridge.cpp tgsim_comm.cpp; do
-  dev=""; [ "${f##*.}" = hip ] && dev="-mllvm -amdgpu-use-amdgpu-trackers=1"
+  dev=""; [ "${f##*.}" = hip ] && dev="-mllvm -amdgpu-use-amdgpu-trackers=1 -mllvm -disable-promote-alloca-to-lds"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall $dev -Wno-unused-result "$@" \
     -c testground_amd/csrc/$f -o $B/${f%.*}.o &
 done

@@ -48,7 +48,10 @@ def build_engine(force: bool = False, verbose: bool = False, profile: bool = Fal
         obj = build_dir / (src.stem + ".o")
         # the AMDGPU register-pressure trackers in the scheduler: 40 % fewer SGPR spills in k_sim
         # and 1.2 % off its time (A/B on the GPU)
-        dev = ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"] if src.suffix == ".hip" else []
+        # (no promotion of private arrays to LDS: it gave the scatter kernels 3-12 KiB of LDS per
+        # workgroup for a record copy, which held the LDS that k_sim_list's workgroups wait for)
+        dev = ["-mllvm", "-amdgpu-use-amdgpu-trackers=1", "-mllvm", "-disable-promote-alloca-to-lds"] \
+            if src.suffix == ".hip" else []
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", *dev,
                "-Wno-unused-result", *(["-DTGSIM_PROFILE"] if profile else []),
                *(["-DTGSIM_CHECK"] if check else []), "-c", str(src), "-o", str(obj)]

@@ -765,6 +765,9 @@ hipError_t take_event(Eng* E, hipEvent_t* ev) {
 
 // Folds finished k_sim event pairs into the running average (wait: block until all are done).
 int harvest_timing(Eng* E, bool wait) {
+  // without waiting, only once many are pending: every event query is host time in the step's launch
+  // path, which short windows (the sub-capacity storm's 0.12 ms) cannot afford per window
+  if (!wait && E->ev_pending.size() + E->dv_pending.size() < 256) return 0;
   size_t k = 0;
   for (; k < E->ev_pending.size(); ++k) {
     auto& pr = E->ev_pending[k];
@@ -1081,7 +1084,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   if (sparse) {
     // the worklist counters start zeroed (at allocation, then by the kernel behind the last sparse
     // step, which also publishes them to pinned memory: no fill or copy on the stream per window)
-    launch_sim_sparse(a, E->st, E->dm_work);
+    launch_sim_sparse(a, E->st, E->dm_work, __atomic_load_n(E->h_work, __ATOMIC_RELAXED));
     E->rotated = true;
   }
   else launch_sim(a, n_wg, E->st);

@@ -3596,12 +3596,17 @@ __global__ void k_work_done(uint32_t* work, uint32_t* host) {
   if (i < 4) work[i] = 0u;
 }
 
-void launch_sim_sparse(const SimArgs& a, hipStream_t st, uint32_t* work_host) {
+void launch_sim_sparse(const SimArgs& a, hipStream_t st, uint32_t* work_host, uint32_t list_hint) {
   if (!a.n_src) return;
   hipLaunchKernelGGL(k_sim_sparse, dim3(sparse_blocks(a.n_src)), dim3(kWave * kSparseWpg), 0, st, a);
   // (grids of 5,120 and 10,240 waves: the same 1M-peer window, within noise)
   hipLaunchKernelGGL(k_sim_multi, dim3(a.n_src < 2048 ? a.n_src : 2048), dim3(kWave), 0, st, a);
-  hipLaunchKernelGGL(k_sim_list, dim3(a.n_src < 16384 ? a.n_src : 16384), dim3(kWave), 0, st, a);
+  // k_sim_list's grid from the last sparse step's deferrals (its length is read on the device; a
+  // grid-stride loop covers any count): each of its workgroups needs 16 KiB of LDS, and at the
+  // 1M-peer flood's peak, with the delivery kernels holding the LDS, 16,384 workgroups that found an
+  // empty list still waited 1.1 ms for it (the simulate stream's critical path)
+  const uint32_t lg = std::min<uint32_t>(std::min<uint32_t>(a.n_src, 16384u), std::max<uint32_t>(64u, 2u * list_hint));
+  hipLaunchKernelGGL(k_sim_list, dim3(lg), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_work_done, dim3(1), dim3(64), 0, st, a.worklist - 4, work_host);
 }
 

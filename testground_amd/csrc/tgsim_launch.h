@@ -33,7 +33,7 @@ void launch_sim_fused(const SimArgs& a, const FusedArgs& f, uint32_t n_wg, hipSt
 uint32_t sim_fused_resident();
 // sparse step: k_sim_sparse over every source, then k_sim_list over the ones it deferred
 // work_host: pinned words that receive the deferral counts (the counters are zeroed behind them)
-void launch_sim_sparse(const SimArgs& a, hipStream_t st, uint32_t* work_host);
+void launch_sim_sparse(const SimArgs& a, hipStream_t st, uint32_t* work_host, uint32_t list_hint);
 // no-op above kOrderMax (32768) sources
 void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream_t st);
 void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state,
