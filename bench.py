@@ -483,9 +483,11 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         elif workload == "epochs":  # traffic pre-generated; reshape + epoch + barrier
             k = epoch[0]
             if stepper is None:
-                if k:
-                    workloads.epoch_reshape(eng, peers_total, k)
-                step(window)  # asynchronous: the next reshape's host work overlaps this k_sim
+                # as the sharded step below: epoch k+1's ConfigureNetwork calls are staged on the
+                # host while epoch k simulates (the step is asynchronous) and take effect at the
+                # next step; epoch 0 runs on the initial configs
+                step(window)
+                workloads.epoch_reshape(eng, peers_total, k + 1)
             else:
                 # the sharded step waits for its records, so epoch k+1's ConfigureNetwork calls
                 # are staged on the host while epoch k simulates (epoch k's were staged during

@@ -335,6 +335,10 @@ int tgsim_comm_run(void* engine, uint32_t n_ticks, uint32_t n_steps, uint32_t fu
  * `state` are summed over the ranks by an all-reduce of the device counter tables; returns 1 when
  * the sum >= target, else 0.  Collective. */
 int tgsim_comm_barrier(void* engine, uint32_t state, uint64_t target);
+/* Every host wait of tgsim_comm_{step,finish,run,barrier} on a peer rank is bounded by
+ * TGSIM_COMM_TIMEOUT_MS (read at tgsim_comm_init; default 300000): a rank whose peer stopped gets
+ * -ETIMEDOUT naming the window, and every later tgsim_comm_* call on that engine fails the same way;
+ * tgsim_destroy then aborts the communicator (ncclCommAbort) instead of waiting on it. */
 typedef struct {
     int32_t rank, nranks;
     uint64_t exchanged_records; /* records (slotted: record slots) this rank has sent, self included */
@@ -478,7 +482,7 @@ int64_t tgsim_debug_stamps(void* engine, uint64_t* out, size_t cap);
 int64_t tgsim_debug_carry_bytes(void* engine);
 /* Diagnostics: windows simulated by fused launches (tgsim_step_n) since the engine was created. */
 int64_t tgsim_debug_fused_windows(void* engine);
-/* Diagnostics of a TGSIM_CHECK build of the engine (scripts/check_build.sh): cross-lane reads whose
+/* Diagnostics of a TGSIM_CHECK build of the engine (scripts/r05_check_build.sh): cross-lane reads whose
  * source lanes were inactive so far, process-wide.  -ENOSYS in the product build. */
 int64_t tgsim_debug_exec_faults(void);
 

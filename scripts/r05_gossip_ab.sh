@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=$PWD/gpurun_out/r05/${AB:-gossip_ab}; mkdir -p $O
 ARGS=${ARGS:-"--no-cpu --no-1m --workload gossip --peers ${PEERS:-1000000}"}
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in ${VARIANTS:-cur}; do
     lib=$PWD/testground_amd/libtgsim.so; env=TGSIM_X=0; dir=.
     case $v in cur) ;; tree:*) dir=${v#tree:}; lib=$PWD/$dir/testground_amd/libtgsim.so;; *=*) env=$v;; *) lib=$PWD/testground_amd/libtgsim_$v.so;; esac

@@ -754,6 +754,8 @@ int scan_counts(Eng* E, DevBuf<uint64_t>& cnt, DevBuf<uint64_t>& off, DevBuf<uin
 
 constexpr uint32_t kOrderMaxSources = 32768;  // = kOrderMax of the order kernel
 
+constexpr size_t kEventPool = 160;  // two pairs a window: 40 windows before the first harvest
+
 hipError_t take_event(Eng* E, hipEvent_t* ev) {
   if (!E->ev_pool.empty()) {
     *ev = E->ev_pool.back();
@@ -765,9 +767,10 @@ hipError_t take_event(Eng* E, hipEvent_t* ev) {
 
 // Folds finished k_sim event pairs into the running average (wait: block until all are done).
 int harvest_timing(Eng* E, bool wait) {
-  // without waiting, only once many are pending: every event query is host time in the step's launch
-  // path, which short windows (the sub-capacity storm's 0.12 ms) cannot afford per window
-  if (!wait && E->ev_pending.size() + E->dv_pending.size() < 256) return 0;
+  // without waiting, only once many are pending or the pool runs dry: every event query is host time in
+  // the step's launch path, which short windows (the sub-capacity storm's 0.12 ms) cannot afford per
+  // window, and so is every hipEventCreate (a drained pool in a 70-window flood created ~280 of them)
+  if (!wait && E->ev_pending.size() + E->dv_pending.size() < 256 && E->ev_pool.size() >= 4) return 0;
   size_t k = 0;
   for (; k < E->ev_pending.size(); ++k) {
     auto& pr = E->ev_pending[k];
@@ -1839,6 +1842,14 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (const char* dd = getenv("TGSIM_DENSE_DIV")) E->dense_div = static_cast<uint32_t>(std::max(1, atoi(dd)));
   if (const char* st = getenv("TGSIM_SIM_TIMING")) E->sim_every = static_cast<uint32_t>(std::max(0, atoi(st)));
   if (const char* dv = getenv("TGSIM_DV_TIMING")) E->dv_every = static_cast<uint32_t>(std::max(0, atoi(dv)));
+  if (E->sim_every || E->dv_every) {  // the timing events, created here rather than in the step path
+    E->ev_pool.resize(kEventPool);
+    for (hipEvent_t& ev : E->ev_pool)
+      if ((rc = E->hip(hipEventCreate(&ev), "event"))) {
+        ev = nullptr;
+        return bail(rc);
+      }
+  }
   if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
   if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));

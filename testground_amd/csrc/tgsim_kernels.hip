@@ -3605,7 +3605,9 @@ void launch_sim_sparse(const SimArgs& a, hipStream_t st, uint32_t* work_host, ui
   // grid-stride loop covers any count): each of its workgroups needs 16 KiB of LDS, and at the
   // 1M-peer flood's peak, with the delivery kernels holding the LDS, 16,384 workgroups that found an
   // empty list still waited 1.1 ms for it (the simulate stream's critical path)
-  const uint32_t lg = std::min<uint32_t>(std::min<uint32_t>(a.n_src, 16384u), std::max<uint32_t>(64u, 2u * list_hint));
+  static const int fixed = env_knob("TGSIM_LIST_GRID");  // A/B: a fixed grid instead of the hint
+  const uint32_t want = fixed > 0 ? static_cast<uint32_t>(fixed) : std::max<uint32_t>(64u, 2u * list_hint);
+  const uint32_t lg = std::min<uint32_t>(std::min<uint32_t>(a.n_src, 16384u), want);
   hipLaunchKernelGGL(k_sim_list, dim3(lg), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_work_done, dim3(1), dim3(64), 0, st, a.worklist - 4, work_host);
 }
