@@ -48,9 +48,9 @@ def build_engine(force: bool = False, verbose: bool = False, profile: bool = Fal
         obj = build_dir / (src.stem + ".o")
         # the AMDGPU register-pressure trackers in the scheduler: 40 % fewer SGPR spills in k_sim
         # and 1.2 % off its time (A/B on the GPU)
-        # (no promotion of private arrays to LDS: it gave the scatter kernels 3-12 KiB of LDS per
-        # workgroup for a record copy, which held the LDS that k_sim_list's workgroups wait for)
-        dev = ["-mllvm", "-amdgpu-use-amdgpu-trackers=1", "-mllvm", "-disable-promote-alloca-to-lds"] \
+        # (LLVM's promotion of private arrays to LDS stays on: without it the 1M-peer gossip window
+        # was 3 % slower, profiles/r05/ab/seventh_gossip)
+        dev = ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"] \
             if src.suffix == ".hip" else []
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", *dev,
                "-Wno-unused-result", *(["-DTGSIM_PROFILE"] if profile else []),

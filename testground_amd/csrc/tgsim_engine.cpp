@@ -327,6 +327,7 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_pidx, d_pidx_alt;
   int emit_compact = 1;           // TGSIM_EMIT_COMPACT: 0 every window in the classic layout, 1 auto,
                                   // 2 every sparse window compact (tests)
+  bool dst_slot = true;           // TGSIM_DST_SLOT: sparse windows place records by destination slot
   uint32_t emit_r = 64;           // TGSIM_EMIT_R: a compact region's reserve beyond 2 records per offered packet
   uint32_t emit_pool = 64;        // TGSIM_EMIT_POOL: the compact pool's records per source
   // the choice tgsim_sim_capacity made for the next window (run_sim takes it, so the exchange's
@@ -1045,6 +1046,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
       HIPCHK(hipMemsetAsync(E->d_lcnt.p, 0, sizeof(uint64_t) * E->d_lcnt.cap, E->st));
     }
     a.dst_cnt = reinterpret_cast<unsigned long long*>(E->d_lcnt.p);
+    // sparse windows: each record's destination slot from its histogram increment, so the scatter
+    // takes no cursor atomic (TGSIM_DST_SLOT=0: the cursors, for A/B)
+    a.dst_slot = sparse && E->dst_slot ? 1u : 0u;
+    E->el.slot = a.dst_slot;
   }
   if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard
     a.g_first = E->d_gfirst.p;
@@ -1412,7 +1417,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, E->d_doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
-  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
+  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
   // while this one's per-destination sort still runs (the sort reads only the scatter buffer)
@@ -1851,6 +1856,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
       }
   }
   if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
+  if (const char* ds = getenv("TGSIM_DST_SLOT")) E->dst_slot = atoi(ds) != 0;
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
   if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));
   E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;

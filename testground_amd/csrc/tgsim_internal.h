@@ -137,7 +137,11 @@ struct SimArgs {
   // sparse kernels' FIFO path so that an idle source's check needs no read of its queue head; every
   // other writer of SrcState stores 0 (TGSIM_HEAD_HINT builds read it)
   uint64_t* qhint;
-  uint32_t emit_r, emit_pool_cap;
+  // dst_slot (sparse windows of a single shard): each record's arrival rank at its destination (the
+  // value its dst_cnt increment returned) rides in its t_ns bits 46-63, so the local scatter places it
+  // with no atomic (kSlotShift, EmitRead::slot)
+  uint32_t emit_r : 31, dst_slot : 1;
+  uint32_t emit_pool_cap;
   // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the scheduler spilled
   // 9 more SGPRs in k_sim_fused (155 -> 164)
 };
@@ -181,7 +185,20 @@ struct EmitRead {
   const tgsim_delivery* pool;
   const uint32_t* pool_idx;
   uint32_t r;
+  uint32_t slot;  // the records carry their destination slot above kEMask in t_ns (SimArgs::dst_slot)
 };
+// A record's destination slot (its arrival rank among the window's records to that destination) in
+// t_ns above the delivery time (< 2^46); kSlotNone: the rank did not fit, the scatter claims a place
+// behind the first kSlotNone with a cursor atomic.
+constexpr uint32_t kSlotShift = 46;
+#ifdef TGSIM_CHECK  // the check build sends every rank from 3 on through the cursor fallback
+constexpr uint64_t kSlotNone = 3;
+#else
+constexpr uint64_t kSlotNone = (1ull << (64 - kSlotShift)) - 1;
+#endif
+__host__ __device__ inline uint64_t slot_bits(unsigned long long rank) {
+  return (uint64_t)(rank < kSlotNone ? rank : kSlotNone) << kSlotShift;
+}
 __host__ __device__ inline const tgsim_delivery* emit_rec(const EmitRead& e, uint32_t s, uint64_t o0, uint64_t o1,
                                                          uint32_t i, uint32_t pidx) {
   const uint64_t cap = 2 * (o1 - o0) + e.r;

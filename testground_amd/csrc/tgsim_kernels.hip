@@ -424,6 +424,7 @@ struct SimQueue {
   tgsim_delivery* over;      // kOver: records from cap on (null: the pool could not take them, dropped)
   uint32_t cap;              // kOver: records that fit in the source's region
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
+  bool dslot;                // kOver: the records carry their destination slot (SimArgs::dst_slot)
   RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
@@ -504,10 +505,14 @@ struct SimQueue {
       if (live) {
         const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
         uint64_t* rw = reinterpret_cast<uint64_t*>(ri >= cap ? over + (ri - cap) : emit + ri);
-        rw[0] = d;
+        uint64_t sl = 0;  // the record's destination slot (dst_slot), from the histogram increment
+        if (dcnt) {
+          if (dslot) sl = slot_bits(atomicAdd(&dcnt[qi.w], 1ull));
+          else atomicAdd(&dcnt[qi.w], 1ull);
+        }
         rw[1] = ((uint64_t)qi.w << 32) | src;
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
-        if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
+        rw[0] = d | sl;
         if (rf.first && qi.w - rf.shard_begin < rf.n_local)
           fold_receipt(rf, qi.w, qi.z, flags, d, kFwdSentinel ? 0ull : rf.fwd[qi.w - rf.shard_begin]);
         sched++;
@@ -1007,6 +1012,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   }
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
+  Q.dslot = kList && a.dst_slot;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
@@ -1851,10 +1857,14 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     if (live) {
       const uint32_t flags = x.y >> 30;
       uint64_t* rw = reinterpret_cast<uint64_t*>(eo.at(i));
-      rw[0] = d;
+      uint64_t sl = 0;  // the record's destination slot (dst_slot), from the histogram increment
+      if (a.dst_cnt) {
+        if (a.dst_slot) sl = slot_bits(atomicAdd(&a.dst_cnt[x.w], 1ull));
+        else atomicAdd(&a.dst_cnt[x.w], 1ull);
+      }
       rw[1] = ((uint64_t)x.w << 32) | src;
       rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-      if (a.dst_cnt) atomicAdd(&a.dst_cnt[x.w], 1ull);
+      rw[0] = d | sl;
       if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
       bytes += xlen;
     }
@@ -2276,10 +2286,14 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     if (live) {
       const uint32_t flags = x.y >> 30;
       uint64_t* rw = reinterpret_cast<uint64_t*>(eo.at(i));
-      rw[0] = d;
+      uint64_t sl = 0;  // the record's destination slot (dst_slot), from the histogram increment
+      if (a.dst_cnt) {
+        if (a.dst_slot) sl = slot_bits(atomicAdd(&a.dst_cnt[x.w], 1ull));
+        else atomicAdd(&a.dst_cnt[x.w], 1ull);
+      }
       rw[1] = ((uint64_t)x.w << 32) | src;
       rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-      if (a.dst_cnt) atomicAdd(&a.dst_cnt[x.w], 1ull);
+      rw[0] = d | sl;
       if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
       bytes += xlen;
     }
@@ -2391,7 +2405,10 @@ __host__ __device__ inline uint32_t sparse_blocks(uint32_t n_src) {
   const uint32_t nb = (n_src + kSparseWpg - 1) / kSparseWpg;
   return kSparseXcd ? (nb + 7) / 8 * 8 : nb;
 }
-__global__ __launch_bounds__(kWave * kSparseWpg, 7) void k_sim_sparse(SimArgs a) {
+#ifndef TGSIM_SPARSE_OCC
+#define TGSIM_SPARSE_OCC 7
+#endif
+__global__ __launch_bounds__(kWave * kSparseWpg, TGSIM_SPARSE_OCC) void k_sim_sparse(SimArgs a) {
   // the source index must stay wave-uniform for the compiler (a VGPR index turns every per-source
   // load into a vector load: 126 VGPR spills at 7 waves per SIMD), hence readfirstlane
   const uint32_t b = blockIdx.x;
@@ -2666,7 +2683,11 @@ __global__ __launch_bounds__(256) void k_gossip_recv_emit(GossipArgs g, EmitRead
     const uint32_t n = emit_n[s];
     const uint64_t o0 = off[s], o1 = off[s + 1];
     const uint32_t pidx = n > 2 * (o1 - o0) + emit.r ? emit.pool_idx[s] : 0u;
-    for (uint32_t i = lane; i < n; i += kWave) gossip_recv_one(g, *emit_rec(emit, s, o0, o1, i, pidx));
+    for (uint32_t i = lane; i < n; i += kWave) {
+      tgsim_delivery r = *emit_rec(emit, s, o0, o1, i, pidx);
+      r.t_ns &= kEMask;  // (a destination slot above it, EmitRead::slot)
+      gossip_recv_one(g, r);
+    }
   }
 }
 
@@ -3105,9 +3126,25 @@ __global__ void k_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst
 }
 
 // Single shard: straight from k_sim's per-source emit regions (counts were taken by k_sim).
+// A record's place in the scatter buffer: from its destination slot (records of a slotted window:
+// doff[d] + slot, no atomic; a slot that did not fit claims one behind the first kSlotNone places
+// with the cursor, which starts at doff[d]), else from the destination's cursor.
+template <bool kSlot>
+__device__ __forceinline__ uint64_t scatter_at(tgsim_delivery& r, uint32_t dst_begin, const uint64_t* doff,
+                                               unsigned long long* pos) {
+  const uint32_t d = r.dst - dst_begin;
+  if constexpr (kSlot) {
+    const uint64_t k = r.t_ns >> kSlotShift;
+    r.t_ns &= kEMask;
+    return k < kSlotNone ? doff[d] + k : kSlotNone + atomicAdd(&pos[d], 1ull);
+  }
+  return atomicAdd(&pos[d], 1ull);
+}
+
+template <bool kSlot>
 __global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint32_t* emit_n,
                                                        const uint64_t* off, uint32_t n_src, uint32_t dst_begin,
-                                                       uint64_t* pos, tgsim_delivery* out) {
+                                                       const uint64_t* doff, uint64_t* pos, tgsim_delivery* out) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nw = gridDim.x * 4;
   for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
@@ -3115,8 +3152,8 @@ __global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint
     const uint64_t o0 = off[s], o1 = off[s + 1];
     const uint32_t pidx = n > 2 * (o1 - o0) + emit.r ? emit.pool_idx[s] : 0u;
     for (uint32_t i = lane; i < n; i += kWave) {
-      const tgsim_delivery r = *emit_rec(emit, s, o0, o1, i, pidx);
-      out[atomicAdd(reinterpret_cast<unsigned long long*>(&pos[r.dst - dst_begin]), 1ull)] = r;
+      tgsim_delivery r = *emit_rec(emit, s, o0, o1, i, pidx);
+      out[scatter_at<kSlot>(r, dst_begin, doff, reinterpret_cast<unsigned long long*>(pos))] = r;
     }
   }
 }
@@ -3126,12 +3163,15 @@ __global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint
 // cursor atomic and store of a round independent of the others; a pass over the records'
 // destinations first, so that a destination's records share one cursor atomic.  The wave per source above walks
 // its sources one after another, each behind four dependent round trips with 57 of 64 lanes idle.
-template <bool kAgg>
+// kMode: kScatterEach one cursor atomic per record; kScatterAgg one per destination of a source (below);
+// kScatterSlot records that carry their destination slot, no atomic.
+constexpr int kScatterEach = 0, kScatterAgg = 1, kScatterSlot = 2;
+template <int kMode>
 __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
                                                           const uint32_t* __restrict__ emit_n,
                                                           const uint64_t* __restrict__ off, uint32_t n_src,
-                                                          uint32_t dst_begin, uint64_t* pos,
-                                                          tgsim_delivery* __restrict__ out) {
+                                                          uint32_t dst_begin, const uint64_t* __restrict__ doff,
+                                                          uint64_t* pos, tgsim_delivery* __restrict__ out) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
   uint32_t n = 0, cap = 0;
   const tgsim_delivery* base = emit.base;  // the source's region: its first cap records
@@ -3145,7 +3185,7 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
   }
   auto rec = [&](uint32_t i) -> const tgsim_delivery& { return i < cap ? base[i] : over[i - cap]; };
   unsigned long long* p = reinterpret_cast<unsigned long long*>(pos);
-  if constexpr (!kAgg) {  // records to many destinations (storm shapes): one cursor atomic each
+  if constexpr (kMode != kScatterAgg) {  // one cursor atomic per record (storm shapes), or none (slots)
     for (uint32_t i = 0; __ballot(i < n); i += 4) {
       tgsim_delivery r[4];
 #pragma unroll
@@ -3154,7 +3194,7 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
       uint64_t at[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
-        if (i + u < n) at[u] = atomicAdd(&p[r[u].dst - dst_begin], 1ull);
+        if (i + u < n) at[u] = scatter_at<kMode == kScatterSlot>(r[u], dst_begin, doff, p);
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
         if (i + u < n) out[at[u]] = r[u];
@@ -3819,10 +3859,14 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
 
 constexpr uint32_t kLaneScatterMin = 65536;  // sources: below, the wavefront-per-source scatter
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
-                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st, uint64_t n_hint,
-                          bool few_dst) {
+                          uint32_t dst_begin, const uint64_t* doff, uint64_t* pos, tgsim_delivery* out,
+                          hipStream_t st, uint64_t n_hint, bool few_dst) {
+#ifdef TGSIM_DIAG_NO_SCATTER  // diagnostic build only (window time without this kernel): wrong deliveries
+  return;
+#endif
   if (!n_src) return;
   static const int mode = env_knob("TGSIM_LOCAL_SCATTER");
+  const uint32_t lwg = (n_src + 255) / 256;
   // up to tens of records per source and enough sources to fill the chip with one lane each (gossip at
   // 1M peers, even at the flood's peak): one lane per source.  With fewer sources (the sub-capacity
   // storm's 10,000: 40 workgroups) a wavefront per source spreads the records over 10,000 waves
@@ -3831,20 +3875,32 @@ void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const ui
     // few_dst (gossip: a peer forwards to its neighbours): one cursor atomic per destination of a
     // source (1M-peer gossip +1-2 %); with records to many destinations that pass over the records
     // costs more than it saves (sub-capacity storm 1.09 against 1.15-1.17 G pkt/s)
-    if (few_dst)
-      hipLaunchKernelGGL(k_local_scatter_ls<true>, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
-                         dst_begin, pos, out);
+    // (records with their destination slot need no cursor at all)
+    if (emit.slot)
+      hipLaunchKernelGGL(k_local_scatter_ls<kScatterSlot>, dim3(lwg), dim3(256), 0, st, emit, emit_n, off, n_src,
+                         dst_begin, doff, pos, out);
+    else if (few_dst)
+      hipLaunchKernelGGL(k_local_scatter_ls<kScatterAgg>, dim3(lwg), dim3(256), 0, st, emit, emit_n, off, n_src,
+                         dst_begin, doff, pos, out);
     else
-      hipLaunchKernelGGL(k_local_scatter_ls<false>, dim3((n_src + 255) / 256), dim3(256), 0, st, emit, emit_n, off, n_src,
-                         dst_begin, pos, out);
+      hipLaunchKernelGGL(k_local_scatter_ls<kScatterEach>, dim3(lwg), dim3(256), 0, st, emit, emit_n, off, n_src,
+                         dst_begin, doff, pos, out);
     return;
   }
   const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);
-  hipLaunchKernelGGL(k_local_scatter, dim3(wgs), dim3(256), 0, st, emit, emit_n, off, n_src, dst_begin, pos, out);
+  if (emit.slot)
+    hipLaunchKernelGGL(k_local_scatter<true>, dim3(wgs), dim3(256), 0, st, emit, emit_n, off, n_src, dst_begin, doff,
+                       pos, out);
+  else
+    hipLaunchKernelGGL(k_local_scatter<false>, dim3(wgs), dim3(256), 0, st, emit, emit_n, off, n_src, dst_begin, doff,
+                       pos, out);
 }
 
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                      tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin) {
+#ifdef TGSIM_DIAG_NO_SORT  // diagnostic build only (window time without this kernel): unsorted deliveries
+  return;
+#endif
   if (!n_dst) return;
   static const int sparse_sort = env_knob("TGSIM_SPARSE_SORT");
   if (!cnt && n_hint <= 48ull * n_dst && sparse_sort != 1) {

@@ -90,9 +90,11 @@ void launch_dst_scatter(const tgsim_delivery* in, uint64_t n, uint32_t dst_begin
                         tgsim_delivery* out, hipStream_t st, uint64_t slot = 0, uint32_t n_win = 1);
 void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n, uint32_t n_src, uint64_t* cnt,
                           uint64_t* off, uint32_t n_dst, uint64_t* err_host, hipStream_t st);
+// pos: the destinations' cursors (= doff, the scanned segment starts, before the scatter); records that
+// carry their destination slot (emit.slot) go to doff[d] + slot with no cursor atomic
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
-                          uint32_t dst_begin, uint64_t* pos, tgsim_delivery* out, hipStream_t st,
-                          uint64_t n_hint, bool few_dst = false);
+                          uint32_t dst_begin, const uint64_t* doff, uint64_t* pos, tgsim_delivery* out,
+                          hipStream_t st, uint64_t n_hint, bool few_dst = false);
 // Orders each destination's records (segment d: off[d] .. off[d + 1]; dst_begin: the first
 // destination's id) and resets cnt[] to zero for the next histogram, unless cnt is null (the scan
 // cleared it: then sparse windows take the flattened sort).  (in, the scatter buffer, is
