@@ -275,7 +275,6 @@ struct tgsim_engine_s {
 
   DevBuf<SrcParams> d_params;
   DevBuf<SrcState> d_state;
-  DevBuf<uint64_t> d_qhint;  // SimArgs::qhint
   DevBuf<uint8_t> d_enabled;
   DevBuf<uint32_t> d_ip;
   DevBuf<Interval> d_rules;
@@ -328,6 +327,7 @@ struct tgsim_engine_s {
   int emit_compact = 1;           // TGSIM_EMIT_COMPACT: 0 every window in the classic layout, 1 auto,
                                   // 2 every sparse window compact (tests)
   bool dst_slot = true;           // TGSIM_DST_SLOT: sparse windows place records by destination slot
+  bool dst_bkt = true;            // TGSIM_DST_BKT: ... and write them into destination buckets
   uint32_t emit_r = 64;           // TGSIM_EMIT_R: a compact region's reserve beyond 2 records per offered packet
   uint32_t emit_pool = 64;        // TGSIM_EMIT_POOL: the compact pool's records per source
   // the choice tgsim_sim_capacity made for the next window (run_sim takes it, so the exchange's
@@ -341,6 +341,7 @@ struct tgsim_engine_s {
   bool slack_forced = false;              // TGSIM_DELIVER_SLACK set: the bounded form at any size
   DevBuf<uint32_t> d_emit_n, d_emit_n_alt;
   DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (the delivery's scan clears it)
+  DevBuf<tgsim_delivery> d_dbkt, d_dbkt_alt;  // destination buckets of a sparse window (SimArgs::dst_bkt)
   hipEvent_t ev_local = nullptr, ev_local_alt = nullptr;
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
@@ -836,7 +837,6 @@ SimArgs base_sim_args(Eng* E) {
   SimArgs a{};
   a.params = E->d_params.p;
   a.state = E->d_state.p;
-  a.qhint = E->d_qhint.p;
   a.enabled = E->d_enabled.p;
   a.ip = E->d_ip.p;
   a.rules = E->d_rules.p;
@@ -863,6 +863,7 @@ void rotate_emit(Eng* E) {
   std::swap(E->d_pidx, E->d_pidx_alt);
   std::swap(E->d_emit_n, E->d_emit_n_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
+  std::swap(E->d_dbkt, E->d_dbkt_alt);
   std::swap(E->ev_local, E->ev_local_alt);
 }
 
@@ -1050,6 +1051,13 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     // takes no cursor atomic (TGSIM_DST_SLOT=0: the cursors, for A/B)
     a.dst_slot = sparse && E->dst_slot ? 1u : 0u;
     E->el.slot = a.dst_slot;
+    // and, where nothing but the local delivery reads the records (no metrics, receipts folded in at
+    // emission), straight into the destinations' buckets (TGSIM_DST_BKT=0: the emit records only)
+    if (a.dst_slot && E->dst_bkt && !E->metrics_on && (!E->gossip_on || E->fold_recv)) {
+      HIPCHK(E->d_dbkt.ensure(static_cast<size_t>(E->N) * kBktC));
+      a.dst_bkt = E->d_dbkt.p;
+      E->el.bkt = a.dst_bkt;
+    }
   }
   if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard
     a.g_first = E->d_gfirst.p;
@@ -1417,16 +1425,24 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, E->d_doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
+  // (a bucketed window: only the records past their destination's bucket are in the emit records)
   launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
-  // while this one's per-destination sort still runs (the sort reads only the scatter buffer)
-  HIPCHK(hipEventRecord(released, sq));
+  // while this one's per-destination sort still runs (the sort reads only the scatter buffer) --
+  // unless the sort reads the window's buckets (released behind it, below)
+  if (!emit.bkt) HIPCHK(hipEventRecord(released, sq));
   if (!E->gossip_on) HIPCHK(hipEventRecord(E->ev_recv, sq));
   tgsim_delivery* dst = nullptr;
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
-  launch_dst_sort(E->d_scatter.p, E->d_doff.p, nullptr, nd, dst, sq, need_n ? n : n_in);
+  if (emit.bkt) {
+    launch_dst_sort_bkt(emit.bkt, E->d_scatter.p, E->d_doff.p, nd, dst, sq);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(released, sq));
+  } else {
+    launch_dst_sort(E->d_scatter.p, E->d_doff.p, nullptr, nd, dst, sq, need_n ? n : n_in);
+  }
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
     launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
@@ -1857,6 +1873,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   }
   if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
   if (const char* ds = getenv("TGSIM_DST_SLOT")) E->dst_slot = atoi(ds) != 0;
+  if (const char* db = getenv("TGSIM_DST_BKT")) E->dst_bkt = atoi(db) != 0;
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
   if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));
   E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
@@ -1893,7 +1910,6 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   E->any_patch = false;
   if ((rc = E->hip(E->d_params.ensure(E->S), "alloc params"))) return bail(rc);
   if ((rc = E->hip(E->d_state.ensure(E->S), "alloc state"))) return bail(rc);
-  if ((rc = E->hip(E->d_qhint.ensure(E->S), "alloc queue-head hints"))) return bail(rc);
   if ((rc = E->hip(E->d_enabled.ensure(E->N), "alloc enabled"))) return bail(rc);
   if ((rc = E->hip(E->d_ip.ensure(E->N), "alloc ip"))) return bail(rc);
   if ((rc = E->hip(E->d_heap.ensure(static_cast<size_t>(E->S) * kHeapCap), "alloc heap"))) return bail(rc);
@@ -1922,7 +1938,6 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(E->d_off.ensure(E->S + 1), "alloc off"))) return bail(rc);
   if ((rc = E->hip(E->d_in.ensure(1), "alloc in"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_state.p, 0, sizeof(SrcState) * E->S), "memset"))) return bail(rc);
-  if ((rc = E->hip(hipMemset(E->d_qhint.p, 0, sizeof(uint64_t) * E->S), "memset"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_gen_seq.p, 0, sizeof(uint32_t) * E->S), "memset"))) return bail(rc);
   if ((rc = E->hip(hipMemset(E->d_stats.p, 0, sizeof(unsigned long long) * kStSlots * kStatCopies), "memset")))
     return bail(rc);
@@ -1960,10 +1975,10 @@ void tgsim_destroy(void* e) {
   if (E->sy_st) (void)hipStreamDestroy(E->sy_st);
   DevBuf<int> dummy;
   (void)dummy;
-  E->d_params.release(); E->d_state.release(); E->d_qhint.release(); E->d_enabled.release(); E->d_ip.release();
+  E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_dbkt.release(); E->d_dbkt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();

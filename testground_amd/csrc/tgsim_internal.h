@@ -133,10 +133,11 @@ struct SimArgs {
   uint64_t* g_pend;         // [s] received, not yet forwarded
   const uint64_t* g_fwd;    // [s] forwarded (stable during the step: written by k_gossip_write before it)
   uint32_t g_floods, g_degree;
-  // [s] a lower bound of the eligibility time of source s's queue head (0: unknown), kept by the
-  // sparse kernels' FIFO path so that an idle source's check needs no read of its queue head; every
-  // other writer of SrcState stores 0 (TGSIM_HEAD_HINT builds read it)
-  uint64_t* qhint;
+  // Sparse windows of a single shard with dst_slot (below): the destinations' buckets, kBktC records
+  // each.  A record whose destination slot is below kBktC is written to dst_bkt[dst * kBktC + slot]
+  // and never to its source's emit region (emit_n counts only the others); null: every record to the
+  // emit region
+  tgsim_delivery* dst_bkt;
   // dst_slot (sparse windows of a single shard): each record's arrival rank at its destination (the
   // value its dst_cnt increment returned) rides in its t_ns bits 46-63, so the local scatter places it
   // with no atomic (kSlotShift, EmitRead::slot)
@@ -186,16 +187,21 @@ struct EmitRead {
   const uint32_t* pool_idx;
   uint32_t r;
   uint32_t slot;  // the records carry their destination slot above kEMask in t_ns (SimArgs::dst_slot)
+  // SimArgs::dst_bkt of the window, or null: the records with a slot below kBktC are there, not in
+  // the emit records above (which hold only the others; the delivery reads both)
+  const tgsim_delivery* bkt;
 };
 // A record's destination slot (its arrival rank among the window's records to that destination) in
 // t_ns above the delivery time (< 2^46); kSlotNone: the rank did not fit, the scatter claims a place
 // behind the first kSlotNone with a cursor atomic.
 constexpr uint32_t kSlotShift = 46;
-#ifdef TGSIM_CHECK  // the check build sends every rank from 3 on through the cursor fallback
-constexpr uint64_t kSlotNone = 3;
+constexpr uint32_t kBktC = 16;  // records per destination bucket (SimArgs::dst_bkt)
+#ifdef TGSIM_CHECK  // the check build sends every rank from kBktC + 3 on through the cursor fallback
+constexpr uint64_t kSlotNone = kBktC + 3;
 #else
 constexpr uint64_t kSlotNone = (1ull << (64 - kSlotShift)) - 1;
 #endif
+static_assert(kSlotNone >= kBktC, "the fallback places records behind every bucket slot");
 __host__ __device__ inline uint64_t slot_bits(unsigned long long rank) {
   return (uint64_t)(rank < kSlotNone ? rank : kSlotNone) << kSlotShift;
 }

@@ -250,12 +250,6 @@ __device__ __forceinline__ RecvFold recv_fold(const SimArgs& a) {
 #define TGSIM_GOSSIP_NOFWD 0
 #endif
 constexpr bool kFwdSentinel = TGSIM_GOSSIP_NOFWD != 0;
-// kHeadHint: k_sim_sparse's idle check reads SimArgs::qhint (the queue head's eligibility time the
-// FIFO path stored) beside the state, instead of the head item itself behind it.
-#ifndef TGSIM_HEAD_HINT
-#define TGSIM_HEAD_HINT 0
-#endif
-constexpr bool kHeadHint = TGSIM_HEAD_HINT != 0;
 __device__ __forceinline__ void fold_receipt(const RecvFold& g, uint32_t dst, uint32_t seq, uint32_t flags, uint64_t d,
                                              uint64_t fw) {
   const uint32_t f = seq / g.degree, s = dst - g.shard_begin;
@@ -425,6 +419,7 @@ struct SimQueue {
   uint32_t cap;              // kOver: records that fit in the source's region
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
   bool dslot;                // kOver: the records carry their destination slot (SimArgs::dst_slot)
+  tgsim_delivery* bkt;       // kOver: the destinations' buckets (SimArgs::dst_bkt), or null
   RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
@@ -495,24 +490,28 @@ struct SimQueue {
     else commit_plain(c, n, qi, d, tat_after);
   }
   // records past the region with no pool space are dropped (kErrEmitPool)
+  // (as emit_record: the destination slot first, then the bucket or the emit records)
   __device__ __forceinline__ void commit_over(bool c, uint32_t n, const uint4& qi, uint64_t d, uint64_t tat_after) {
-    bool live = c && qi.w != kDeadDst;
-    const uint32_t ri = n_emit + (uint32_t)__popcll(__ballot(live) & ((1ull << lane) - 1));
-    live = live && (ri < cap || over != nullptr);
-    const uint64_t lm = __ballot(live);
+    const bool live = c && qi.w != kDeadDst;
+    unsigned long long rank = 0;
+    if (live && dcnt) {
+      if (dslot) rank = atomicAdd(&dcnt[qi.w], 1ull);
+      else atomicAdd(&dcnt[qi.w], 1ull);
+    }
+    const bool inb = live && bkt != nullptr && rank < kBktC;
+    bool ov = live && !inb;
+    const uint32_t ri = n_emit + (uint32_t)__popcll(__ballot(ov) & ((1ull << lane) - 1));
+    ov = ov && (ri < cap || over != nullptr);
+    const uint64_t lm = __ballot(ov);
     if (c) {
       *reinterpret_cast<uint2*>(&slot(rn + lane)) = make_uint2((uint32_t)d, (uint32_t)(d >> 32));
-      if (live) {
+      if (inb || ov) {
         const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
-        uint64_t* rw = reinterpret_cast<uint64_t*>(ri >= cap ? over + (ri - cap) : emit + ri);
-        uint64_t sl = 0;  // the record's destination slot (dst_slot), from the histogram increment
-        if (dcnt) {
-          if (dslot) sl = slot_bits(atomicAdd(&dcnt[qi.w], 1ull));
-          else atomicAdd(&dcnt[qi.w], 1ull);
-        }
+        uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? bkt + (uint64_t)qi.w * kBktC + rank
+                                                       : ri >= cap ? over + (ri - cap) : emit + ri);
         rw[1] = ((uint64_t)qi.w << 32) | src;
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
-        rw[0] = d | sl;
+        rw[0] = inb || !dslot ? d : d | slot_bits(rank);
         if (rf.first && qi.w - rf.shard_begin < rf.n_local)
           fold_receipt(rf, qi.w, qi.z, flags, d, kFwdSentinel ? 0ull : rf.fwd[qi.w - rf.shard_begin]);
         sched++;
@@ -1013,6 +1012,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
   Q.dslot = kList && a.dst_slot;
+  Q.bkt = kList ? a.dst_bkt : nullptr;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
@@ -1513,7 +1513,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
       ns.last_dup = last_dup;
       ns.last_cor = last_cor;
       ns.last_reo = last_reo;
-      if (kHeadHint) a.qhint[s] = 0ull;  // unknown: the next sparse step reads the queue head
       if constexpr (kH) {
         const auto rs = region(a.state + s, sizeof(SrcState));
         const StatePair sp = __builtin_bit_cast(StatePair, ns);
@@ -1651,6 +1650,35 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f
 
 constexpr uint32_t kSparseQ = 4;  // chunks of 64 queued items / ring entries held in registers
 constexpr uint32_t kFifoRounds = 4;  // FIFO sources: items served per step, in rounds of 64
+
+// One served item's record (lanes with live set; x the queue item, d its HTB departure): the
+// histogram increment first, whose return value is the record's destination slot (dst_slot); a slot
+// below kBktC goes to the destination's bucket (dst_bkt), any other record to the source's emit
+// records (emitted of them so far, wave-uniform; past the region and the pool: dropped,
+// kErrEmitPool), with its slot above the delivery time.  The receipt is folded in (gossip).  Returns
+// whether the lane's record was written.
+__device__ __forceinline__ bool emit_record(const SimArgs& a, const EmitOut& eo, bool live, const uint4& x, uint64_t d,
+                                            uint32_t xlen, uint32_t src, uint32_t fw, uint32_t fw_f,
+                                            uint32_t& emitted, uint64_t below) {
+  unsigned long long rank = 0;
+  if (live && a.dst_cnt) {
+    if (a.dst_slot) rank = atomicAdd(&a.dst_cnt[x.w], 1ull);
+    else atomicAdd(&a.dst_cnt[x.w], 1ull);
+  }
+  const bool inb = live && a.dst_bkt != nullptr && rank < kBktC;
+  bool ov = live && !inb;
+  const uint32_t i = emitted + (uint32_t)__popcll(__ballot(ov) & below);
+  ov = ov && eo.fits(i);
+  emitted += (uint32_t)__popcll(__ballot(ov));
+  if (!inb && !ov) return false;
+  const uint32_t flags = x.y >> 30;
+  uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? a.dst_bkt + (uint64_t)x.w * kBktC + rank : eo.at(i));
+  rw[1] = ((uint64_t)x.w << 32) | src;
+  rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
+  rw[0] = inb || !a.dst_slot ? d : d | slot_bits(rank);
+  if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
+  return true;
+}
 
 // ---------------------------------------------------------------------------------------------
 // k_sim_multi: the FIFO sources k_sim_sparse cannot take in one round of lanes -- more than 64
@@ -1825,7 +1853,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
   // ---- HTB, records, receipts and the ring, for the served items in rounds of 64 lanes: the
   // queue's due items, then the due candidates, contiguous from the head slot
   uint64_t tat_c = st.tat;
-  uint32_t emitted = 0, sk0 = 0, t_cor = 0, t_lost = 0;
+  uint32_t emitted = 0, sched_n = 0, sk0 = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
   bool releasing = T_enq && !ring_stop;
   EmitOut eo = emit_out(a, s, sbeg, send);
@@ -1851,24 +1879,9 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     tat_c = readlane64(tat_after, ns - 1);
     bool live = hs && x.w != kDeadDst;
     const bool dead = hs && !live;
-    const uint32_t i = emitted + (uint32_t)__popcll(__ballot(live) & below);
-    live = live && eo.fits(i);  // past the region with no pool space: dropped (kErrEmitPool)
-    const uint64_t lm = __ballot(live);
-    if (live) {
-      const uint32_t flags = x.y >> 30;
-      uint64_t* rw = reinterpret_cast<uint64_t*>(eo.at(i));
-      uint64_t sl = 0;  // the record's destination slot (dst_slot), from the histogram increment
-      if (a.dst_cnt) {
-        if (a.dst_slot) sl = slot_bits(atomicAdd(&a.dst_cnt[x.w], 1ull));
-        else atomicAdd(&a.dst_cnt[x.w], 1ull);
-      }
-      rw[1] = ((uint64_t)x.w << 32) | src;
-      rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-      rw[0] = d | sl;
-      if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
-      bytes += xlen;
-    }
-    emitted += (uint32_t)__popcll(lm);
+    live = emit_record(a, eo, live, x, d, xlen, src, fw, fw_f, emitted, below);
+    if (live) bytes += xlen;
+    sched_n += (uint32_t)__popcll(__ballot(live));
     t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
     t_lost += (uint32_t)__popcll(__ballot(dead));
     if (releasing) {  // a prefix of the served entries departed before the last enqueue
@@ -1895,7 +1908,6 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     ns_.last_cor = st.last_cor;
     ns_.last_reo = st.last_reo;
     a.state[s] = ns_;
-    if (kHeadHint) a.qhint[s] = 0ull;
     a.emit_n[s] = emitted;
   }
   // ---- statistics
@@ -1909,7 +1921,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     const uint64_t q_kept = qn + wpos > q_moved ? 16ull * (qn + wpos - q_moved) : 0ull;
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
-    if (emitted) atomicAdd(&sc[kStScheduled], (unsigned long long)emitted);
+    if (sched_n) atomicAdd(&sc[kStScheduled], (unsigned long long)sched_n);
     if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
     if (t_cor) atomicAdd(&sc[kStCorrupted], (unsigned long long)t_cor);
     if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
@@ -1973,10 +1985,8 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     }
   };
   unsigned long long* const sc = a.stats + (size_t)(s % kStatCopies) * kStSlots;
-  const uint64_t hint = kHeadHint ? a.qhint[s] : 0ull;  // a lower bound of the head's e (0: unknown)
-  const bool hint_idle = kHeadHint && hint >= a.horizon_ns;
-  const uint4 qh0 = sorted_st && qn && !n && !hint_idle ? gh[q_head(st)] : make_uint4(0, 0, 0, 0);
-  if (!n && (!qn || (sorted_st && (hint_idle || (w0_of(qh0) & kEMask) >= a.horizon_ns)))) {
+  const uint4 qh0 = sorted_st && qn && !n ? gh[q_head(st)] : make_uint4(0, 0, 0, 0);
+  if (!n && (!qn || (sorted_st && (w0_of(qh0) & kEMask) >= a.horizon_ns))) {
     // nothing offered and nothing eligible before the horizon: the state stays as it is (the ring
     // is released only by an enqueue); only the per-window queue model is counted.  Checked before
     // the capacity limits below: an idle source with a long ring (the end of a flood) is not deferred
@@ -2252,7 +2262,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   // ---- HTB, records, receipts and the ring, for the served items in rounds of 64 lanes (more than
   // one only on the FIFO path: the queue's due prefix, then the due candidates, in order)
   uint64_t tat_c = st.tat;
-  uint32_t emitted = 0, sk0 = 0, t_sched = 0, t_cor = 0, t_lost = 0;
+  uint32_t emitted = 0, sched_n = 0, sk0 = 0, t_sched = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
   bool releasing = T_enq && !ring_stop;  // served entries departing before the last enqueue are released
   EmitOut eo = emit_out(a, s, sbeg, send);
@@ -2280,24 +2290,9 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     // records of the served items (dead destinations leave the sender and are lost)
     bool live = hs && x.w != kDeadDst;
     const bool dead = hs && !live;
-    const uint32_t i = emitted + (uint32_t)__popcll(__ballot(live) & below);
-    live = live && eo.fits(i);  // past the region with no pool space: dropped (kErrEmitPool)
-    const uint64_t lm = __ballot(live);
-    if (live) {
-      const uint32_t flags = x.y >> 30;
-      uint64_t* rw = reinterpret_cast<uint64_t*>(eo.at(i));
-      uint64_t sl = 0;  // the record's destination slot (dst_slot), from the histogram increment
-      if (a.dst_cnt) {
-        if (a.dst_slot) sl = slot_bits(atomicAdd(&a.dst_cnt[x.w], 1ull));
-        else atomicAdd(&a.dst_cnt[x.w], 1ull);
-      }
-      rw[1] = ((uint64_t)x.w << 32) | src;
-      rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
-      rw[0] = d | sl;
-      if (a.g_first) fold_receipt(recv_fold(a), x.w, x.z, flags, d, (uint64_t)fw << (fw_f & 32u));
-      bytes += xlen;
-    }
-    emitted += (uint32_t)__popcll(lm);
+    live = emit_record(a, eo, live, x, d, xlen, src, fw, fw_f, emitted, below);
+    if (live) bytes += xlen;
+    sched_n += (uint32_t)__popcll(__ballot(live));
     t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
     t_lost += (uint32_t)__popcll(__ballot(dead));
     // the served entries join the ring, behind the old entries kept; a prefix of them departing
@@ -2321,22 +2316,9 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     ns = fifo_nq > nb ? (fifo_nq - nb < kWave ? fifo_nq - nb : kWave) : 0u;
     gather(due_f && cpos >= nb && cpos < nb + kWave, io);
   }
-  t_sched = emitted;
+  t_sched = sched_n;
   const uint32_t rn_new = old_kept + ns_all - sk0;
-  uint64_t hint_new = 0;  // the new queue head's e on the FIFO path, where it is in registers
-  if (kHeadHint && fifo && wpos) {
-    if (fifo_nq < qn) {  // an old item stays at the head
-      if (fifo_nq < kWave) hint_new = w0_of(make_uint4(readlane32(q[0].x, fifo_nq), readlane32(q[0].y, fifo_nq), 0u, 0u)) & kEMask;
-    } else {  // the first candidate not served
-      const uint64_t mnd = __ballot(cand && !due_f);
-      if (mnd) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(mnd);
-        hint_new = w0_of(make_uint4(readlane32(io.x, l), readlane32(io.y, l), 0u, 0u)) & kEMask;
-      }
-    }
-  }
   if (lane == 0) {
-    if (kHeadHint) a.qhint[s] = hint_new;
     SrcState ns_;
     ns_.tat = tat_c;
     ns_.heap_n = wpos;
@@ -3363,12 +3345,15 @@ __device__ __forceinline__ tgsim_delivery load_rec_l2(const tgsim_delivery* p) {
   return __builtin_bit_cast(tgsim_delivery, w);
 }
 
-__device__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_delivery* out, uint32_t lane) {
+// ld(j): the segment's record j as the first pass reads it (by default in[b + j]; the bucketed
+// delivery reads the first kBktC from the destination's bucket); in[b, b + n) is then the work space.
+template <typename Ld>
+__device__ void sort_segment_ld(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_delivery* out, uint32_t lane, Ld ld) {
   if (n <= kWave) {
     tgsim_delivery r;
     RecKey k{~0ull, ~0ull, 1u};
     if (lane < n) {
-      r = in[b + lane];
+      r = ld(lane);
       k = rec_key(r);
     }
     const uint32_t rank = wave_rank(k, n, lane);
@@ -3380,7 +3365,7 @@ __device__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_d
       tgsim_delivery r;
       RecKey k{~0ull, ~0ull, 1u};
       if (lane < m) {
-        r = in[b + c0 + lane];
+        r = ld(c0 + lane);
         k = rec_key(r);
       }
       const uint32_t rank = wave_rank(k, m, lane);
@@ -3423,6 +3408,10 @@ __device__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_d
       for (uint32_t i = lane; i < n; i += kWave) out[b + i] = load_rec_l2(src + i);
     }
   }
+}
+__device__ __forceinline__ void sort_segment(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_delivery* out,
+                                             uint32_t lane) {
+  sort_segment_ld(in, b, n, out, lane, [&](uint32_t j) { return in[b + j]; });
 }
 
 // One destination per wavefront (segments of tens of records and more: storm).
@@ -3516,6 +3505,60 @@ __global__ __launch_bounds__(256) void k_dst_sort_flat(tgsim_delivery* in, const
       sort_segment(in, b, (uint32_t)(readlane64(se, gl) - b), out, lane);
     }
     wave_lds_sync();  // this chunk's LDS reads are done before the next chunk's writes
+  }
+}
+
+// Per-destination order of a bucketed window (SimArgs::dst_bkt): destination d's first kBktC records
+// (in slot order) are in its bucket, any more in the scatter buffer at doff[d] + slot (the slot
+// scatter of the emit records).  kWave / kBktC destinations per wavefront, a lane per bucket entry:
+// a segment of at most kBktC records is ranked among its lanes through LDS and stored at its rank; a
+// longer one is sorted whole (sort_segment_ld, its first kBktC records read from the bucket) by the
+// wavefront.  No record pass before this kernel: the buckets are the simulate kernels' output.
+__global__ __launch_bounds__(256) void k_dst_sort_bkt(const tgsim_delivery* __restrict__ bkt, tgsim_delivery* sc,
+                                                      const uint64_t* __restrict__ doff, uint32_t n_dst,
+                                                      tgsim_delivery* __restrict__ out) {
+  constexpr uint32_t kG = kWave / kBktC;  // destinations per wavefront
+  __shared__ uint64_t kt[4][kWave], kq[4][kWave];
+  __shared__ uint32_t kc[4][kWave];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t g = lane / kBktC, k = lane % kBktC;
+  const uint32_t d0 = (blockIdx.x * 4 + wv) * kG, d = d0 + g;
+  uint64_t sb = 0, se = 0;
+  if (d < n_dst) {
+    sb = doff[d];
+    se = doff[d + 1];
+  }
+  const uint64_t cnt = se - sb;
+  const bool small = cnt <= kBktC && k < cnt;
+  tgsim_delivery r;
+  uint64_t t = ~0ull, q = ~0ull;
+  uint32_t cl = 1u;
+  if (small) {
+    r = bkt[(uint64_t)d * kBktC + k];
+    t = r.t_ns;
+    q = ((uint64_t)r.src << 32) | r.seq;
+    cl = (r.flags & TGSIM_FLAG_DUP) ? 0u : 1u;
+  }
+  kt[wv][lane] = t;
+  kq[wv][lane] = q;
+  kc[wv][lane] = cl;
+  wave_lds_sync();
+  if (small) {
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < (uint32_t)cnt; ++j) {
+      const uint32_t x = g * kBktC + j;
+      const uint64_t ot = kt[wv][x], oq = kq[wv][x];
+      const uint32_t oc = kc[wv][x];
+      rank += (rec_lt(ot, oq, oc, t, q, cl) || (!rec_lt(t, q, cl, ot, oq, oc) && j < k)) ? 1u : 0u;
+    }
+    out[sb + rank] = r;
+  }
+  for (uint64_t big = __ballot(k == 0 && cnt > kBktC); big; big &= big - 1) {
+    const uint32_t gl = (uint32_t)__builtin_ctzll(big);
+    const uint64_t b = readlane64(sb, gl);
+    const uint32_t n = (uint32_t)(readlane64(se, gl) - b);
+    const tgsim_delivery* bk = bkt + (uint64_t)(d0 + gl / kBktC) * kBktC;
+    sort_segment_ld(sc, b, n, out, lane, [&](uint32_t j) { return j < kBktC ? bk[j] : sc[b + j]; });
   }
 }
 
@@ -3914,6 +3957,12 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
     return;
   }
   hipLaunchKernelGGL(k_dst_sort_wide<4>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
+}
+
+void launch_dst_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const uint64_t* doff, uint32_t n_dst,
+                        tgsim_delivery* out, hipStream_t st) {
+  constexpr uint32_t per_wg = 4 * (kWave / kBktC);
+  if (n_dst) hipLaunchKernelGGL(k_dst_sort_bkt, dim3((n_dst + per_wg - 1) / per_wg), dim3(256), 0, st, bkt, sc, doff, n_dst, out);
 }
 
 void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
