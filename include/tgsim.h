@@ -480,6 +480,10 @@ int64_t tgsim_debug_stamps(void* engine, uint64_t* out, size_t cap);
  * queue_state_bytes models one load and one store per window; a fused group (tgsim_step_n) keeps
  * each source's queue in LDS across its windows and moves it once per group. */
 int64_t tgsim_debug_carry_bytes(void* engine);
+/* Diagnostics: records the simulate kernels wrote straight into destination buckets (sparse windows
+ * of an engine that owns every peer) since the engine was created.  The others went
+ * through the emit regions and the scatter. */
+int64_t tgsim_debug_bucket_records(void* engine);
 /* Diagnostics: windows simulated by fused launches (tgsim_step_n) since the engine was created. */
 int64_t tgsim_debug_fused_windows(void* engine);
 /* Diagnostics of a TGSIM_CHECK build of the engine (scripts/r05_check_build.sh): cross-lane reads whose

@@ -18,7 +18,7 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 root, steps = sys.argv[1], int(sys.argv[2])
 MARK = ("k_local_scatter_ls", "k_local_scatter(", "k_dst_scatter(", "k_dst_slot<true>")  # one per window
-BODY = MARK + ("k_dst_sort_flat", "k_dst_sort_wide", "k_deliver_guard", "k_dst_hist", "k_dst_slot<false>")
+BODY = MARK + ("k_dst_sort_flat", "k_dst_sort_wide", "k_dst_sort_bkt", "k_deliver_guard", "k_dst_hist", "k_dst_slot<false>")
 SCAN = ("k_scan_local", "k_scan_sums", "k_scan_add")
 avg = {}
 for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):

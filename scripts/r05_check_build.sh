@@ -5,10 +5,10 @@
 # library (product objects), so they run unchecked.  Log: gpurun_out/r05/check/pytest_gpu_check.log.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r05/check; mkdir -p $O
-TGSIM_LIB=$PWD/testground_amd/libtgsim_check.so timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s \
+TGSIM_LIB=$PWD/testground_amd/libtgsim_check.so timeout -k 10 900 python -u -m pytest tests -m gpu -v -s \
   --timeout 600 --timeout-method thread > $O/pytest_gpu_check.log 2>&1; rc=$?
 tail -4 $O/pytest_gpu_check.log
-echo "EXEC CHECK lines: $(grep -c 'EXEC CHECK' $O/pytest_gpu_check.log)"
+echo "EXEC CHECK lines (one per source line): $(grep -c "EXEC CHECK" $O/pytest_gpu_check.log)"; grep "EXEC CHECK" $O/pytest_gpu_check.log | sort | uniq | head -40
 echo "queue CHECK lines: $(grep -c '^CHECK tag' $O/pytest_gpu_check.log)"
 grep -m1 "TGSIM_CHECK exec-mask guard violations" $O/pytest_gpu_check.log
 exit $rc

@@ -2620,6 +2620,19 @@ int64_t tgsim_debug_carry_bytes(void* e) {
   return static_cast<int64_t>(q - skipped);
 }
 
+int64_t tgsim_debug_bucket_records(void* e) {
+  Eng* E = as_eng(e);
+  if (!E) return -EINVAL;
+  HIPCHK(hipSetDevice(E->dev));
+  int rc = sync_stream(E);
+  if (rc) return rc;
+  std::vector<unsigned long long> all(static_cast<size_t>(kStSlots) * kStatCopies);
+  HIPCHK(hipMemcpy(all.data(), E->d_stats.p, sizeof(unsigned long long) * all.size(), hipMemcpyDeviceToHost));
+  unsigned long long n = 0;
+  for (uint32_t c = 0; c < kStatCopies; ++c) n += all[static_cast<size_t>(c) * kStSlots + kStBktRecs];
+  return static_cast<int64_t>(n);
+}
+
 int64_t tgsim_debug_exec_faults(void) { return exec_faults(); }
 
 int64_t tgsim_debug_fused_windows(void* e) {

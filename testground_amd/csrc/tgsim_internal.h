@@ -82,6 +82,7 @@ enum StatSlot {
   kStOffered = 0, kStScheduled, kStCloned, kStCorrupted, kStVerdict0,  // 4..11 verdicts
   kStBytes = 12, kStErr = 13, kStQueue = 14, kStLost = 15, kStFlushed = 16,
   kStCarrySkip = 17,  // modeled queue state bytes a source-major fused group kept in LDS (never moved)
+  kStBktRecs = 18,    // records the simulate kernels wrote straight into destination buckets
   kStSlots = 20
 };
 // Counters are spread over kStatCopies copies (workgroup w adds into copy w % kStatCopies) so that

@@ -104,38 +104,42 @@ constexpr uint32_t kFvPass = 0xFFu;
 // printed by the first active lane of the offending wave.
 #ifdef TGSIM_CHECK
 __device__ unsigned int tg_exec_faults;
-__device__ __noinline__ void tg_exec_fault(const char* what, uint64_t exec, uint32_t l) {
+__device__ unsigned int tg_exec_lines[8192];  // violations per source line (the first one printed)
+__device__ __noinline__ void tg_exec_fault(const char* what, uint64_t exec, uint32_t l, int line) {
   const uint32_t me = __lane_id();
   if (me == (uint32_t)__builtin_ctzll(exec)) {
-    const unsigned int k = atomicAdd(&tg_exec_faults, 1u);
-    if (k < 16)
-      printf("EXEC CHECK %s: exec %016llx lane %u (block %u)\n", what, (unsigned long long)exec, l, blockIdx.x);
+    atomicAdd(&tg_exec_faults, 1u);
+    if (atomicAdd(&tg_exec_lines[(uint32_t)line & 8191u], 1u) == 0u)
+      printf("EXEC CHECK %s at line %d: exec %016llx lane %u (block %u)\n", what, line, (unsigned long long)exec, l,
+             blockIdx.x);
   }
 }
-__device__ __forceinline__ void tg_full_exec(const char* what) {
+__device__ __forceinline__ void tg_full_exec(const char* what, int line) {
   const uint64_t x = __builtin_amdgcn_read_exec();
-  if (x != ~0ull) tg_exec_fault(what, x, 64u);
+  if (x != ~0ull) tg_exec_fault(what, x, 64u, line);
 }
-__device__ __forceinline__ void tg_lane_live(const char* what, uint32_t l) {
+__device__ __forceinline__ void tg_lane_live(const char* what, uint32_t l, int line) {
   const uint64_t x = __builtin_amdgcn_read_exec();
-  if (l >= 64u || !(x >> l & 1ull)) tg_exec_fault(what, x, l);
+  if (l >= 64u || !(x >> l & 1ull)) tg_exec_fault(what, x, l, line);
 }
-#define TG_FULL_EXEC(what) tg_full_exec(what)
-#define TG_LANE_LIVE(what, l) tg_lane_live(what, l)
+#define TG_FULL_EXEC(what) tg_full_exec(what, __LINE__)
+#define TG_FULL_EXEC_AT(what, line) tg_full_exec(what, line)
+#define TG_LANE_LIVE_AT(what, l, line) tg_lane_live(what, l, line)
 #else
 #define TG_FULL_EXEC(what) ((void)0)
-#define TG_LANE_LIVE(what, l) ((void)0)
+#define TG_FULL_EXEC_AT(what, line) ((void)(line))
+#define TG_LANE_LIVE_AT(what, l, line) ((void)(line))
 #endif
-
-__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l) {
-  TG_LANE_LIVE("readlane", l);
+// (line: the caller's source line, for the check build's report)
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l, int line = __builtin_LINE()) {
+  TG_LANE_LIVE_AT("readlane", l, line);
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-  return ((uint64_t)readlane32((uint32_t)(v >> 32), l) << 32) | readlane32((uint32_t)v, l);
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l, int line = __builtin_LINE()) {
+  return ((uint64_t)readlane32((uint32_t)(v >> 32), l, line) << 32) | readlane32((uint32_t)v, l, line);
 }
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
-  TG_FULL_EXEC("shfl64");
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src, int line = __builtin_LINE()) {
+  TG_FULL_EXEC_AT("shfl64", line);
   const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
   return ((uint64_t)hi << 32) | lo;
 }
@@ -145,14 +149,14 @@ __device__ __forceinline__ uint32_t ballot_count(bool p) { return (uint32_t)__po
 // row of 16 lanes, then row_bcast:15 and row_bcast:31 carry the row totals (GFX9 wave64 pattern).
 // Lanes without a source lane read the identity.
 template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp(uint32_t id, uint32_t v) {
-  TG_FULL_EXEC("dpp scan");
+__device__ __forceinline__ uint32_t dpp(uint32_t id, uint32_t v, int line = __builtin_LINE()) {
+  TG_FULL_EXEC_AT("dpp", line);
   return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, ROWS, 0xF, false);
 }
 template <int CTRL, int ROWS>
-__device__ __forceinline__ uint64_t dpp64(uint64_t id, uint64_t v) {
-  return ((uint64_t)dpp<CTRL, ROWS>((uint32_t)(id >> 32), (uint32_t)(v >> 32)) << 32) |
-         dpp<CTRL, ROWS>((uint32_t)id, (uint32_t)v);
+__device__ __forceinline__ uint64_t dpp64(uint64_t id, uint64_t v, int line = __builtin_LINE()) {
+  return ((uint64_t)dpp<CTRL, ROWS>((uint32_t)(id >> 32), (uint32_t)(v >> 32), line) << 32) |
+         dpp<CTRL, ROWS>((uint32_t)id, (uint32_t)v, line);
 }
 #define TG_SCAN_STEPS(STEP) STEP(0x111, 0xF) STEP(0x112, 0xF) STEP(0x114, 0xF) STEP(0x118, 0xF) \
                             STEP(0x142, 0xA) STEP(0x143, 0xC)
@@ -160,56 +164,57 @@ constexpr int kDppWaveShr1 = 0x138;  // wave_shr:1 (lane i reads lane i - 1; lan
 
 // wave_shr:1 must stay a plain v_mov_b32_dpp: folded into a VOP2 ALU op (v_sub_u32_dpp ...
 // wave_shr:1) it gave wrong results on gfx950, so the asm barrier keeps the DPP combiner off it.
-__device__ __forceinline__ uint32_t shr1_u32(uint32_t v, uint32_t id) {
-  uint32_t r = dpp<kDppWaveShr1, 0xF>(id, v);
+__device__ __forceinline__ uint32_t shr1_u32(uint32_t v, uint32_t id, int line = __builtin_LINE()) {
+  uint32_t r = dpp<kDppWaveShr1, 0xF>(id, v, line);
   __asm__ volatile("" : "+v"(r));
   return r;
 }
-__device__ __forceinline__ uint64_t shr1_u64(uint64_t v, uint64_t id) {
-  return ((uint64_t)shr1_u32((uint32_t)(v >> 32), (uint32_t)(id >> 32)) << 32) | shr1_u32((uint32_t)v, (uint32_t)id);
+__device__ __forceinline__ uint64_t shr1_u64(uint64_t v, uint64_t id, int line = __builtin_LINE()) {
+  return ((uint64_t)shr1_u32((uint32_t)(v >> 32), (uint32_t)(id >> 32), line) << 32) |
+         shr1_u32((uint32_t)v, (uint32_t)id, line);
 }
 
-__device__ __forceinline__ void scan_maxplus(uint64_t& a, uint64_t& b) {
+__device__ __forceinline__ void scan_maxplus(uint64_t& a, uint64_t& b, int line = __builtin_LINE()) {
   // maps x -> max(x + a, b); earlier (pa, pb) then later (a, b) = (pa + a, max(pb + a, b))
-#define STEP(C, R) { const uint64_t pa = dpp64<C, R>(0, a), pb = dpp64<C, R>(0, b); \
+#define STEP(C, R) { const uint64_t pa = dpp64<C, R>(0, a, line), pb = dpp64<C, R>(0, b, line); \
                      const uint64_t nb = pb + a; b = nb > b ? nb : b; a = pa + a; }
   TG_SCAN_STEPS(STEP)
 #undef STEP
 }
-__device__ __forceinline__ int32_t scan_sum_i32(int32_t v) {
-#define STEP(C, R) v += (int32_t)dpp<C, R>(0u, (uint32_t)v);
+__device__ __forceinline__ int32_t scan_sum_i32(int32_t v, int line = __builtin_LINE()) {
+#define STEP(C, R) v += (int32_t)dpp<C, R>(0u, (uint32_t)v, line);
   TG_SCAN_STEPS(STEP)
 #undef STEP
   return v;
 }
-__device__ __forceinline__ int32_t scan_max_i32(int32_t v) {
-#define STEP(C, R) v = max(v, (int32_t)dpp<C, R>(0x80000000u, (uint32_t)v));
+__device__ __forceinline__ int32_t scan_max_i32(int32_t v, int line = __builtin_LINE()) {
+#define STEP(C, R) v = max(v, (int32_t)dpp<C, R>(0x80000000u, (uint32_t)v, line));
   TG_SCAN_STEPS(STEP)
 #undef STEP
   return v;
 }
-__device__ __forceinline__ uint32_t scan_max_u32(uint32_t v) {
-#define STEP(C, R) v = max(v, dpp<C, R>(0u, v));
+__device__ __forceinline__ uint32_t scan_max_u32(uint32_t v, int line = __builtin_LINE()) {
+#define STEP(C, R) v = max(v, dpp<C, R>(0u, v, line));
   TG_SCAN_STEPS(STEP)
 #undef STEP
   return v;
 }
-__device__ __forceinline__ uint64_t scan_max_u64(uint64_t v) {
-#define STEP(C, R) { const uint64_t p = dpp64<C, R>(0ull, v); v = p > v ? p : v; }
+__device__ __forceinline__ uint64_t scan_max_u64(uint64_t v, int line = __builtin_LINE()) {
+#define STEP(C, R) { const uint64_t p = dpp64<C, R>(0ull, v, line); v = p > v ? p : v; }
   TG_SCAN_STEPS(STEP)
 #undef STEP
   return v;
 }
-__device__ __forceinline__ uint64_t scan_min_u64(uint64_t v) {
-#define STEP(C, R) { const uint64_t p = dpp64<C, R>(~0ull, v); v = p < v ? p : v; }
+__device__ __forceinline__ uint64_t scan_min_u64(uint64_t v, int line = __builtin_LINE()) {
+#define STEP(C, R) { const uint64_t p = dpp64<C, R>(~0ull, v, line); v = p < v ? p : v; }
   TG_SCAN_STEPS(STEP)
 #undef STEP
   return v;
 }
 
 // Count of the 64 lane values v (sorted ascending over lanes) that are <= t, for every lane's t.
-__device__ __forceinline__ uint32_t count_le_sorted_u32(uint32_t v, uint32_t t) {
-  TG_FULL_EXEC("count_le_sorted");
+__device__ __forceinline__ uint32_t count_le_sorted_u32(uint32_t v, uint32_t t, int line = __builtin_LINE()) {
+  TG_FULL_EXEC_AT("count_le_sorted", line);
   uint32_t lo = 0;
 #pragma unroll
   for (uint32_t s = 32; s; s >>= 1)
@@ -329,8 +334,8 @@ __device__ __forceinline__ uint32_t filter(const SimArgs& a, const SrcParams& p,
   return kFvPass;
 }
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-  TG_FULL_EXEC("wave_sum");
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v, int line = __builtin_LINE()) {
+  TG_FULL_EXEC_AT("wave_sum", line);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t lo = __shfl_xor((uint32_t)v, o, 64);
@@ -372,8 +377,8 @@ template <uint32_t J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
   TG_FULL_EXEC("xor_lane");
   uint32_t r;
-  if constexpr (J == 1) r = dpp<0xB1, 0xF>(0u, v);       // quad_perm [1, 0, 3, 2]
-  else if constexpr (J == 2) r = dpp<0x4E, 0xF>(0u, v);  // quad_perm [2, 3, 0, 1]
+  if constexpr (J == 1) r = dpp<0xB1, 0xF>(0u, v, __LINE__);       // quad_perm [1, 0, 3, 2]
+  else if constexpr (J == 2) r = dpp<0x4E, 0xF>(0u, v, __LINE__);  // quad_perm [2, 3, 0, 1]
   else if constexpr (J < 32) r = (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (int)(0x1Fu | (J << 10)));
   else r = (uint32_t)__shfl_xor((int)v, 32, 64);
   __asm__ volatile("" : "+v"(r));  // keep the DPP moves plain (see shr1_u32)
@@ -1541,6 +1546,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   if (lane == 0) {
     if (send > sbeg) atomicAdd(&sc[kStOffered], (unsigned long long)(send - sbeg));
     if (sched) atomicAdd(&sc[kStScheduled], (unsigned long long)sched);
+    if (kList && a.dst_bkt && sched > Q.n_emit) atomicAdd(&sc[kStBktRecs], (unsigned long long)(sched - Q.n_emit));
     if (c_clone) atomicAdd(&sc[kStCloned], (unsigned long long)c_clone);
     if (corrupted) atomicAdd(&sc[kStCorrupted], (unsigned long long)corrupted);
     if (lost) atomicAdd(&sc[kStLost], (unsigned long long)lost);
@@ -1922,6 +1928,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (sched_n) atomicAdd(&sc[kStScheduled], (unsigned long long)sched_n);
+    if (a.dst_bkt && sched_n > emitted) atomicAdd(&sc[kStBktRecs], (unsigned long long)(sched_n - emitted));
     if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
     if (t_cor) atomicAdd(&sc[kStCorrupted], (unsigned long long)t_cor);
     if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
@@ -2353,6 +2360,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (t_sched) atomicAdd(&sc[kStScheduled], (unsigned long long)t_sched);
+    if (a.dst_bkt && t_sched > emitted) atomicAdd(&sc[kStBktRecs], (unsigned long long)(t_sched - emitted));
     if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
     if (t_cor) atomicAdd(&sc[kStCorrupted], (unsigned long long)t_cor);
     if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);

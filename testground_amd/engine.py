@@ -344,6 +344,12 @@ class CABIEngine:
             return 0
         return self._check(self._fn("debug_carry_bytes")(self._h), "debug_carry_bytes")
 
+    def bucket_records(self) -> int:
+        """Records written straight into destination buckets (tgsim_debug_bucket_records)."""
+        if not hasattr(self._lib, self._p + "debug_bucket_records"):  # an older library (A/B runs)
+            return 0
+        return self._check(self._fn("debug_bucket_records")(self._h), "debug_bucket_records")
+
     def sim_kernel_ms(self, reset: bool = False) -> Tuple[float, int]:
         n = C.c_uint64()
         ms = self._fn("sim_kernel_ms")(self._h, C.byref(n), 1 if reset else 0)

@@ -305,6 +305,10 @@ def test_gossip_gpu_equals_oracle(make_oracle):
     rg, rc = g.gossip_reached(), c.gossip_reached()
     assert (rg == rc).all() and (rg > 0.99 * n).all()
     assert total == 8 * int(rg.sum())  # every reached peer forwarded once (floods drained)
+    # the sparse windows wrote records straight into destination buckets, and the
+    # destinations that received more than a bucket holds took the rest through the slot scatter
+    b, sched = g.bucket_records(), g.stats()["scheduled"]
+    assert 0 < b < sched, (b, sched)
 
 
 def test_gossip_two_shards_equal_one():
