@@ -197,7 +197,8 @@ struct EmitRead {
 // behind the first kSlotNone with a cursor atomic.
 constexpr uint32_t kSlotShift = 46;
 constexpr uint32_t kBktC = 16;  // records per destination bucket (SimArgs::dst_bkt)
-#ifdef TGSIM_CHECK  // the check build sends every rank from kBktC + 3 on through the cursor fallback
+#if defined(TGSIM_CHECK) && !defined(TGSIM_CHECK_FULL_SLOTS)  // the check build sends every rank from
+                                                                // kBktC + 3 on through the cursor fallback
 constexpr uint64_t kSlotNone = kBktC + 3;
 #else
 constexpr uint64_t kSlotNone = (1ull << (64 - kSlotShift)) - 1;
