@@ -8,7 +8,7 @@ from pathlib import Path
 
 src = sys.argv[1] if len(sys.argv) > 1 else str(Path(__file__).resolve().parents[1] / "testground_amd/csrc/tgsim_kernels.hip")
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-mllvm",
-       "-amdgpu-use-amdgpu-trackers=1", "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", "/dev/null",
+       "-amdgpu-use-amdgpu-trackers=1", "-mllvm", "-disable-promote-alloca-to-lds", "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", "/dev/null",
        *sys.argv[2:]]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None

@@ -2435,6 +2435,8 @@ int64_t tgsim_drain(void* e, tgsim_delivery* out, size_t cap) {
   HIPCHK(hipSetDevice(E->dev));
   int rc = sync_stream(E);
   if (rc) return rc;
+  // a window whose simulation failed (sticky error bits) hands out nothing
+  if ((rc = check_sim_error(E))) return rc;
   const uint64_t n = std::min<uint64_t>(cap, E->drain_n);
   if (n) {
     HIPCHK(hipMemcpy(out, E->d_drain.p + E->drain_head, sizeof(tgsim_delivery) * n, hipMemcpyDeviceToHost));
@@ -2456,6 +2458,8 @@ int64_t tgsim_verdicts(void* e, uint8_t* out, size_t cap) {
   HIPCHK(hipSetDevice(E->dev));
   int rc = sync_stream(E);
   if (rc) return rc;
+  // a window whose simulation failed (sticky error bits) hands out nothing
+  if ((rc = check_sim_error(E))) return rc;
   if (cap >= E->n_verdict && E->n_verdict) {
     std::vector<uint8_t> tmp(E->n_verdict);
     HIPCHK(hipMemcpy(tmp.data(), E->d_verdict.p, E->n_verdict, hipMemcpyDeviceToHost));

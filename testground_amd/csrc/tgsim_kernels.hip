@@ -444,8 +444,8 @@ struct SimQueue {
   }
 
 #ifdef TGSIM_CHECK
-  // Debug: near < B <= soon < H <= far (B <= H only with soon or far items), near sorted; prints
-  // the first violation.
+  // Debug: near < B <= soon < H <= far and B <= far (B may pass H when there are no soon items), near
+  // sorted; prints the first violation.
   __device__ void check(int tag) {
     uint32_t bad = 0;
     uint64_t be = 0;
@@ -460,11 +460,11 @@ struct SimQueue {
     }
     for (uint32_t k = lane; k < fn; k += kWave) {
       const uint64_t e = w0_of(slot(rn + qn + pn + k)) & kEMask;
-      if (e < H) { bad |= 8 | (k << 8); be = e; }
+      if (e < H || e < B) { bad |= 8 | (k << 8); be = e; }
     }
-    // (near items past the horizon are fine while nothing is queued behind them: the sparse FIFO
-    // path stores a whole sorted queue as the near region, due prefix served, the rest after H)
-    if (B > H && (pn | fn)) bad |= 16;
+    // (B > H is fine without soon items: the sparse FIFO path stores a whole sorted queue as the
+    // near region, due prefix served, the rest after H, and every item behind it is >= B)
+    if (B > H && pn) bad |= 16;
     const uint64_t m = __ballot(bad != 0);
     if (m) {
       const uint32_t l = (uint32_t)__builtin_ctzll(m);
