@@ -976,6 +976,15 @@ uint64_t emit_records(Eng* E, uint64_t n_in, bool compact) {  // the emit buffer
                  : 2 * n_in + static_cast<uint64_t>(kHeapCap) * E->S;
 }
 
+// Records per destination bucket of a window (log2): room for about twice the window's offered
+// packets per destination (a gossip window's records are about its offered packets), 8 to 64.
+uint32_t bucket_log(uint64_t n_in, uint32_t n_dst) {
+  const uint64_t want = 2 * n_in / std::max<uint32_t>(1, n_dst) + 4;
+  uint32_t l = kBktLogMin;
+  while (l < kBktLogMax && (1ull << l) < want) ++l;
+  return l;
+}
+
 int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   int erc = check_sim_error(E);
   if (erc) return erc;
@@ -1054,9 +1063,11 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     // and, where nothing but the local delivery reads the records (no metrics, receipts folded in at
     // emission), straight into the destinations' buckets (TGSIM_DST_BKT=0: the emit records only)
     if (a.dst_slot && E->dst_bkt && !E->metrics_on && (!E->gossip_on || E->fold_recv)) {
-      HIPCHK(E->d_dbkt.ensure(static_cast<size_t>(E->N) * kBktC));
+      HIPCHK(E->d_dbkt.ensure(static_cast<size_t>(E->N) << kBktLogMax));
       a.dst_bkt = E->d_dbkt.p;
+      a.bkt_log = bucket_log(E->n_in, E->N);
       E->el.bkt = a.dst_bkt;
+      E->el.bkt_log = a.bkt_log;
     }
   }
   if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard
@@ -1437,7 +1448,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
   if (emit.bkt) {
-    launch_dst_sort_bkt(emit.bkt, E->d_scatter.p, E->d_doff.p, nd, dst, sq);
+    launch_dst_sort_bkt(emit.bkt, emit.bkt_log, E->d_scatter.p, E->d_doff.p, nd, dst, sq);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(released, sq));
   } else {

@@ -134,15 +134,16 @@ struct SimArgs {
   uint64_t* g_pend;         // [s] received, not yet forwarded
   const uint64_t* g_fwd;    // [s] forwarded (stable during the step: written by k_gossip_write before it)
   uint32_t g_floods, g_degree;
-  // Sparse windows of a single shard with dst_slot (below): the destinations' buckets, kBktC records
-  // each.  A record whose destination slot is below kBktC is written to dst_bkt[dst * kBktC + slot]
+  // Sparse windows of a single shard with dst_slot (below): the destinations' buckets, 2^bkt_log
+  // records each.  A record whose destination slot is below that is written to
+  // dst_bkt[(dst << bkt_log) + slot]
   // and never to its source's emit region (emit_n counts only the others); null: every record to the
   // emit region
   tgsim_delivery* dst_bkt;
   // dst_slot (sparse windows of a single shard): each record's arrival rank at its destination (the
   // value its dst_cnt increment returned) rides in its t_ns bits 46-63, so the local scatter places it
   // with no atomic (kSlotShift, EmitRead::slot)
-  uint32_t emit_r : 31, dst_slot : 1;
+  uint32_t emit_r : 24, bkt_log : 7, dst_slot : 1;  // bkt_log: log2 of a bucket's records (dst_bkt)
   uint32_t emit_pool_cap;
   // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the scheduler spilled
   // 9 more SGPRs in k_sim_fused (155 -> 164)
@@ -188,22 +189,25 @@ struct EmitRead {
   const uint32_t* pool_idx;
   uint32_t r;
   uint32_t slot;  // the records carry their destination slot above kEMask in t_ns (SimArgs::dst_slot)
-  // SimArgs::dst_bkt of the window, or null: the records with a slot below kBktC are there, not in
-  // the emit records above (which hold only the others; the delivery reads both)
+  // SimArgs::dst_bkt of the window, or null: the records with a slot below 2^bkt_log are there, not
+  // in the emit records above (which hold only the others; the delivery reads both)
   const tgsim_delivery* bkt;
+  uint32_t bkt_log, _pad;
 };
 // A record's destination slot (its arrival rank among the window's records to that destination) in
 // t_ns above the delivery time (< 2^46); kSlotNone: the rank did not fit, the scatter claims a place
 // behind the first kSlotNone with a cursor atomic.
 constexpr uint32_t kSlotShift = 46;
-constexpr uint32_t kBktC = 16;  // records per destination bucket (SimArgs::dst_bkt)
+// Records per destination bucket (SimArgs::dst_bkt): 2^3 .. 2^6, chosen per window from its offered
+// packets per destination
+constexpr uint32_t kBktLogMin = 3, kBktLogMax = 6;
 #if defined(TGSIM_CHECK) && !defined(TGSIM_CHECK_FULL_SLOTS)  // the check build sends every rank from
-                                                                // kBktC + 3 on through the cursor fallback
-constexpr uint64_t kSlotNone = kBktC + 3;
+                                                                // 67 on through the cursor fallback
+constexpr uint64_t kSlotNone = (1u << kBktLogMax) + 3;
 #else
 constexpr uint64_t kSlotNone = (1ull << (64 - kSlotShift)) - 1;
 #endif
-static_assert(kSlotNone >= kBktC, "the fallback places records behind every bucket slot");
+static_assert(kSlotNone >= (1u << kBktLogMax), "the fallback places records behind every bucket slot");
 __host__ __device__ inline uint64_t slot_bits(unsigned long long rank) {
   return (uint64_t)(rank < kSlotNone ? rank : kSlotNone) << kSlotShift;
 }

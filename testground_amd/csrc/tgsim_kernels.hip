@@ -428,6 +428,7 @@ struct SimQueue {
   unsigned long long* dcnt;  // per-destination histogram (single shard) or null
   bool dslot;                // kOver: the records carry their destination slot (SimArgs::dst_slot)
   tgsim_delivery* bkt;       // kOver: the destinations' buckets (SimArgs::dst_bkt), or null
+  uint32_t bkt_log;
   RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
@@ -509,7 +510,7 @@ struct SimQueue {
       if (dslot) rank = atomicAdd(&dcnt[qi.w], 1ull);
       else atomicAdd(&dcnt[qi.w], 1ull);
     }
-    const bool inb = live && bkt != nullptr && rank < kBktC;
+    const bool inb = live && bkt != nullptr && rank < (1ull << bkt_log);
     bool ov = live && !inb;
     const uint32_t ri = n_emit + (uint32_t)__popcll(__ballot(ov) & ((1ull << lane) - 1));
     ov = ov && (ri < cap || over != nullptr);
@@ -518,7 +519,7 @@ struct SimQueue {
       *reinterpret_cast<uint2*>(&slot(rn + lane)) = make_uint2((uint32_t)d, (uint32_t)(d >> 32));
       if (inb || ov) {
         const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
-        uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? bkt + (uint64_t)qi.w * kBktC + rank
+        uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? bkt + ((uint64_t)qi.w << bkt_log) + rank
                                                        : ri >= cap ? over + (ri - cap) : emit + ri);
         rw[1] = ((uint64_t)qi.w << 32) | src;
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
@@ -1024,6 +1025,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.dcnt = a.dst_cnt;
   Q.dslot = kList && a.dst_slot;
   Q.bkt = kList ? a.dst_bkt : nullptr;
+  Q.bkt_log = a.bkt_log;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
@@ -1666,7 +1668,7 @@ constexpr uint32_t kFifoRounds = 4;  // FIFO sources: items served per step, in 
 
 // One served item's record (lanes with live set; x the queue item, d its HTB departure): the
 // histogram increment first, whose return value is the record's destination slot (dst_slot); a slot
-// below kBktC goes to the destination's bucket (dst_bkt), any other record to the source's emit
+// below 2^bkt_log goes to the destination's bucket (dst_bkt), any other record to the source's emit
 // records (emitted of them so far, wave-uniform; past the region and the pool: dropped,
 // kErrEmitPool), with its slot above the delivery time.  The receipt is folded in (gossip).  Returns
 // whether the lane's record was written.
@@ -1678,14 +1680,14 @@ __device__ __forceinline__ bool emit_record(const SimArgs& a, const EmitOut& eo,
     if (a.dst_slot) rank = atomicAdd(&a.dst_cnt[x.w], 1ull);
     else atomicAdd(&a.dst_cnt[x.w], 1ull);
   }
-  const bool inb = live && a.dst_bkt != nullptr && rank < kBktC;
+  const bool inb = live && a.dst_bkt != nullptr && rank < (1ull << a.bkt_log);
   bool ov = live && !inb;
   const uint32_t i = emitted + (uint32_t)__popcll(__ballot(ov) & below);
   ov = ov && eo.fits(i);
   emitted += (uint32_t)__popcll(__ballot(ov));
   if (!inb && !ov) return false;
   const uint32_t flags = x.y >> 30;
-  uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? a.dst_bkt + (uint64_t)x.w * kBktC + rank : eo.at(i));
+  uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? a.dst_bkt + ((uint64_t)x.w << a.bkt_log) + rank : eo.at(i));
   rw[1] = ((uint64_t)x.w << 32) | src;
   rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
   rw[0] = inb || !a.dst_slot ? d : d | slot_bits(rank);
@@ -3369,7 +3371,7 @@ __device__ __forceinline__ tgsim_delivery load_rec_l2(const tgsim_delivery* p) {
 }
 
 // ld(j): the segment's record j as the first pass reads it (by default in[b + j]; the bucketed
-// delivery reads the first kBktC from the destination's bucket); in[b, b + n) is then the work space.
+// delivery reads the first ones from the destination's bucket); in[b, b + n) is then the work space.
 template <typename Ld>
 __device__ void sort_segment_ld(tgsim_delivery* in, uint64_t b, uint32_t n, tgsim_delivery* out, uint32_t lane, Ld ld) {
   if (n <= kWave) {
@@ -3531,33 +3533,36 @@ __global__ __launch_bounds__(256) void k_dst_sort_flat(tgsim_delivery* in, const
   }
 }
 
-// Per-destination order of a bucketed window (SimArgs::dst_bkt): destination d's first kBktC records
-// (in slot order) are in its bucket, any more in the scatter buffer at doff[d] + slot (the slot
-// scatter of the emit records).  kWave / kBktC destinations per wavefront, a lane per bucket entry:
-// a segment of at most kBktC records is ranked among its lanes through LDS and stored at its rank; a
-// longer one is sorted whole (sort_segment_ld, its first kBktC records read from the bucket) by the
-// wavefront.  No record pass before this kernel: the buckets are the simulate kernels' output.
+// Per-destination order of a bucketed window (SimArgs::dst_bkt): destination d's first kC records (in
+// slot order) are in its bucket, any more in the scatter buffer at doff[d] + slot (the slot scatter of
+// the emit records).  kWave / kC destinations per wavefront, a lane per bucket entry, every load of a
+// wavefront in flight at once (the bucket entries past a destination's count are read and ignored): a
+// segment of at most kC records is ranked among its lanes through LDS and stored at its rank; a longer
+// one is sorted whole by the wavefront (sort_segment_ld, its first kC records read from the bucket).
+// No record pass before this kernel: the buckets are the simulate kernels' output.
+template <uint32_t kC>
 __global__ __launch_bounds__(256) void k_dst_sort_bkt(const tgsim_delivery* __restrict__ bkt, tgsim_delivery* sc,
                                                       const uint64_t* __restrict__ doff, uint32_t n_dst,
                                                       tgsim_delivery* __restrict__ out) {
-  constexpr uint32_t kG = kWave / kBktC;  // destinations per wavefront
+  constexpr uint32_t kG = kWave / kC;  // destinations per wavefront
   __shared__ uint64_t kt[4][kWave], kq[4][kWave];
   __shared__ uint32_t kc[4][kWave];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t g = lane / kBktC, k = lane % kBktC;
+  const uint32_t g = lane / kC, k = lane % kC;
   const uint32_t d0 = (blockIdx.x * 4 + wv) * kG, d = d0 + g;
+  const bool in_range = d < n_dst;
   uint64_t sb = 0, se = 0;
-  if (d < n_dst) {
+  tgsim_delivery r;
+  if (in_range) {
     sb = doff[d];
     se = doff[d + 1];
+    r = bkt[((uint64_t)d * kC) + k];
   }
   const uint64_t cnt = se - sb;
-  const bool small = cnt <= kBktC && k < cnt;
-  tgsim_delivery r;
+  const bool small = cnt <= kC && k < cnt;
   uint64_t t = ~0ull, q = ~0ull;
   uint32_t cl = 1u;
   if (small) {
-    r = bkt[(uint64_t)d * kBktC + k];
     t = r.t_ns;
     q = ((uint64_t)r.src << 32) | r.seq;
     cl = (r.flags & TGSIM_FLAG_DUP) ? 0u : 1u;
@@ -3569,19 +3574,19 @@ __global__ __launch_bounds__(256) void k_dst_sort_bkt(const tgsim_delivery* __re
   if (small) {
     uint32_t rank = 0;
     for (uint32_t j = 0; j < (uint32_t)cnt; ++j) {
-      const uint32_t x = g * kBktC + j;
+      const uint32_t x = g * kC + j;
       const uint64_t ot = kt[wv][x], oq = kq[wv][x];
       const uint32_t oc = kc[wv][x];
       rank += (rec_lt(ot, oq, oc, t, q, cl) || (!rec_lt(t, q, cl, ot, oq, oc) && j < k)) ? 1u : 0u;
     }
     out[sb + rank] = r;
   }
-  for (uint64_t big = __ballot(k == 0 && cnt > kBktC); big; big &= big - 1) {
+  for (uint64_t big = __ballot(k == 0 && cnt > kC); big; big &= big - 1) {
     const uint32_t gl = (uint32_t)__builtin_ctzll(big);
     const uint64_t b = readlane64(sb, gl);
     const uint32_t n = (uint32_t)(readlane64(se, gl) - b);
-    const tgsim_delivery* bk = bkt + (uint64_t)(d0 + gl / kBktC) * kBktC;
-    sort_segment_ld(sc, b, n, out, lane, [&](uint32_t j) { return j < kBktC ? bk[j] : sc[b + j]; });
+    const tgsim_delivery* bk = bkt + (uint64_t)(d0 + gl / kC) * kC;
+    sort_segment_ld(sc, b, n, out, lane, [&](uint32_t j) { return j < kC ? bk[j] : sc[b + j]; });
   }
 }
 
@@ -3982,10 +3987,21 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
   hipLaunchKernelGGL(k_dst_sort_wide<4>, dim3((n_dst + 3) / 4), dim3(256), 0, st, in, off, cnt, n_dst, out);
 }
 
-void launch_dst_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const uint64_t* doff, uint32_t n_dst,
-                        tgsim_delivery* out, hipStream_t st) {
-  constexpr uint32_t per_wg = 4 * (kWave / kBktC);
-  if (n_dst) hipLaunchKernelGGL(k_dst_sort_bkt, dim3((n_dst + per_wg - 1) / per_wg), dim3(256), 0, st, bkt, sc, doff, n_dst, out);
+template <uint32_t kC>
+static void launch_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const uint64_t* doff, uint32_t n_dst,
+                            tgsim_delivery* out, hipStream_t st) {
+  constexpr uint32_t per_wg = 4 * (kWave / kC);
+  hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3((n_dst + per_wg - 1) / per_wg), dim3(256), 0, st, bkt, sc, doff, n_dst, out);
+}
+void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,
+                         uint32_t n_dst, tgsim_delivery* out, hipStream_t st) {
+  if (!n_dst) return;
+  switch (bkt_log) {
+    case 3: launch_sort_bkt<8>(bkt, sc, doff, n_dst, out, st); break;
+    case 4: launch_sort_bkt<16>(bkt, sc, doff, n_dst, out, st); break;
+    case 5: launch_sort_bkt<32>(bkt, sc, doff, n_dst, out, st); break;
+    default: launch_sort_bkt<64>(bkt, sc, doff, n_dst, out, st); break;
+  }
 }
 
 void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,

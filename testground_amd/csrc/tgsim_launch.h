@@ -92,10 +92,10 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
                           uint64_t* off, uint32_t n_dst, uint64_t* err_host, hipStream_t st);
 // pos: the destinations' cursors (= doff, the scanned segment starts, before the scatter); records that
 // carry their destination slot (emit.slot) go to doff[d] + slot with no cursor atomic
-// The per-destination order of a bucketed window (SimArgs::dst_bkt): the buckets and, for the
-// destinations with more than kBktC records, the scatter buffer (sc) from doff[d] + kBktC on.
-void launch_dst_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const uint64_t* doff, uint32_t n_dst,
-                        tgsim_delivery* out, hipStream_t st);
+// The per-destination order of a bucketed window (SimArgs::dst_bkt, 2^bkt_log records per bucket):
+// the buckets and, for the destinations with more records, the scatter buffer (sc) behind them.
+void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,
+                         uint32_t n_dst, tgsim_delivery* out, hipStream_t st);
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, const uint64_t* doff, uint64_t* pos, tgsim_delivery* out,
                           hipStream_t st, uint64_t n_hint, bool few_dst = false);
