@@ -1432,12 +1432,17 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     n = E->h_dtot;
   }
   HIPCHK(E->d_scatter.ensure(n ? n : 1));
-  if (!need_n && slack < kHeapCap) {
+  const bool bounded = !need_n && slack < kHeapCap;
+  EmitRead er = emit;
+  if (bounded && emit.bkt) {  // the scatter and the sort check the total themselves (one dispatch fewer)
+    er.guard_total = E->d_dtot.p;
+    er.guard_cap = n;
+  } else if (bounded) {
     launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, E->d_doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
   // (a bucketed window: only the records past their destination's bucket are in the emit records)
-  launch_local_scatter(emit, emit_n, off, E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
+  launch_local_scatter(er, emit_n, off, E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
   // while this one's per-destination sort still runs (the sort reads only the scatter buffer) --
@@ -1448,7 +1453,8 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
   if (emit.bkt) {
-    launch_dst_sort_bkt(emit.bkt, emit.bkt_log, E->d_scatter.p, E->d_doff.p, nd, dst, sq);
+    launch_dst_sort_bkt(emit.bkt, emit.bkt_log, E->d_scatter.p, E->d_doff.p, nd, dst, sq, er.guard_total, er.guard_cap,
+                        E->d_err_host);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(released, sq));
   } else {

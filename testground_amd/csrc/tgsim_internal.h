@@ -193,6 +193,10 @@ struct EmitRead {
   // in the emit records above (which hold only the others; the delivery reads both)
   const tgsim_delivery* bkt;
   uint32_t bkt_log, _pad;
+  // a bounded local delivery of a bucketed window: the readers check the window's exact total (on the
+  // device) against the buffers' bound themselves and write nothing past it (no k_deliver_guard)
+  const uint64_t* guard_total;
+  uint64_t guard_cap;
 };
 // A record's destination slot (its arrival rank among the window's records to that destination) in
 // t_ns above the delivery time (< 2^46); kSlotNone: the rank did not fit, the scatter claims a place

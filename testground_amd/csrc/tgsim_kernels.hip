@@ -3152,6 +3152,7 @@ template <bool kSlot>
 __global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint32_t* emit_n,
                                                        const uint64_t* off, uint32_t n_src, uint32_t dst_begin,
                                                        const uint64_t* doff, uint64_t* pos, tgsim_delivery* out) {
+  if (emit.guard_total && *emit.guard_total > emit.guard_cap) return;  // (EmitRead::guard_total)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nw = gridDim.x * 4;
   for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
@@ -3179,6 +3180,7 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
                                                           const uint64_t* __restrict__ off, uint32_t n_src,
                                                           uint32_t dst_begin, const uint64_t* __restrict__ doff,
                                                           uint64_t* pos, tgsim_delivery* __restrict__ out) {
+  if (emit.guard_total && *emit.guard_total > emit.guard_cap) return;  // (EmitRead::guard_total)
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
   uint32_t n = 0, cap = 0;
   const tgsim_delivery* base = emit.base;  // the source's region: its first cap records
@@ -3535,57 +3537,72 @@ __global__ __launch_bounds__(256) void k_dst_sort_flat(tgsim_delivery* in, const
 
 // Per-destination order of a bucketed window (SimArgs::dst_bkt): destination d's first kC records (in
 // slot order) are in its bucket, any more in the scatter buffer at doff[d] + slot (the slot scatter of
-// the emit records).  kWave / kC destinations per wavefront, a lane per bucket entry, every load of a
-// wavefront in flight at once (the bucket entries past a destination's count are read and ignored): a
-// segment of at most kC records is ranked among its lanes through LDS and stored at its rank; a longer
-// one is sorted whole by the wavefront (sort_segment_ld, its first kC records read from the bucket).
-// No record pass before this kernel: the buckets are the simulate kernels' output.
+// the emit records).  kL = min(kC, 16) lanes per destination, kWave / kL destinations per wavefront,
+// each lane kC / kL bucket entries, every load of a wavefront in flight at once (entries past a
+// destination's count are read and ignored): a segment of at most kC records is ranked among its
+// group's keys in LDS and each record stored at its rank; a longer one is sorted whole by the
+// wavefront (sort_segment_ld, its first kC records read from the bucket).  No record pass before
+// this kernel: the buckets are the simulate kernels' output.  A bounded delivery whose exact total
+// (total) exceeds its buffers (cap) writes nothing and raises kErrDeliverCap.
 template <uint32_t kC>
 __global__ __launch_bounds__(256) void k_dst_sort_bkt(const tgsim_delivery* __restrict__ bkt, tgsim_delivery* sc,
                                                       const uint64_t* __restrict__ doff, uint32_t n_dst,
-                                                      tgsim_delivery* __restrict__ out) {
-  constexpr uint32_t kG = kWave / kC;  // destinations per wavefront
-  __shared__ uint64_t kt[4][kWave], kq[4][kWave];
-  __shared__ uint32_t kc[4][kWave];
+                                                      tgsim_delivery* __restrict__ out, const uint64_t* total,
+                                                      uint64_t cap, uint64_t* err_host) {
+  constexpr uint32_t kL = kC < 16 ? kC : 16;  // lanes per destination
+  constexpr uint32_t kG = kWave / kL;         // destinations per wavefront
+  constexpr uint32_t kR = kC / kL;            // bucket entries per lane
+  __shared__ uint64_t kt[4][kG * kC], kq[4][kG * kC];
+  __shared__ uint32_t kc[4][kG * kC];
+  if (total && *total > cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && err_host)
+      __hip_atomic_store(err_host, (uint64_t)kErrDeliverCap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t g = lane / kC, k = lane % kC;
+  const uint32_t g = lane / kL, k = lane % kL;
   const uint32_t d0 = (blockIdx.x * 4 + wv) * kG, d = d0 + g;
   const bool in_range = d < n_dst;
   uint64_t sb = 0, se = 0;
-  tgsim_delivery r;
+  tgsim_delivery r[kR];
   if (in_range) {
     sb = doff[d];
     se = doff[d + 1];
-    r = bkt[((uint64_t)d * kC) + k];
+#pragma unroll
+    for (uint32_t u = 0; u < kR; ++u) r[u] = bkt[(uint64_t)d * kC + u * kL + k];
   }
   const uint64_t cnt = se - sb;
-  const bool small = cnt <= kC && k < cnt;
-  uint64_t t = ~0ull, q = ~0ull;
-  uint32_t cl = 1u;
-  if (small) {
-    t = r.t_ns;
-    q = ((uint64_t)r.src << 32) | r.seq;
-    cl = (r.flags & TGSIM_FLAG_DUP) ? 0u : 1u;
+  const bool small = cnt <= kC;
+#pragma unroll
+  for (uint32_t u = 0; u < kR; ++u) {
+    const uint32_t j = u * kL + k;
+    const bool v = small && j < cnt;
+    kt[wv][g * kC + j] = v ? r[u].t_ns : ~0ull;
+    kq[wv][g * kC + j] = v ? ((uint64_t)r[u].src << 32) | r[u].seq : ~0ull;
+    kc[wv][g * kC + j] = v ? ((r[u].flags & TGSIM_FLAG_DUP) ? 0u : 1u) : 1u;
   }
-  kt[wv][lane] = t;
-  kq[wv][lane] = q;
-  kc[wv][lane] = cl;
   wave_lds_sync();
-  if (small) {
-    uint32_t rank = 0;
-    for (uint32_t j = 0; j < (uint32_t)cnt; ++j) {
-      const uint32_t x = g * kC + j;
-      const uint64_t ot = kt[wv][x], oq = kq[wv][x];
-      const uint32_t oc = kc[wv][x];
-      rank += (rec_lt(ot, oq, oc, t, q, cl) || (!rec_lt(t, q, cl, ot, oq, oc) && j < k)) ? 1u : 0u;
+#pragma unroll
+  for (uint32_t u = 0; u < kR; ++u) {
+    const uint32_t j = u * kL + k;
+    if (small && j < cnt) {
+      const uint64_t t = kt[wv][g * kC + j], q = kq[wv][g * kC + j];
+      const uint32_t cl = kc[wv][g * kC + j];
+      uint32_t rank = 0;
+      for (uint32_t i = 0; i < (uint32_t)cnt; ++i) {
+        const uint32_t x = g * kC + i;
+        const uint64_t ot = kt[wv][x], oq = kq[wv][x];
+        const uint32_t oc = kc[wv][x];
+        rank += (rec_lt(ot, oq, oc, t, q, cl) || (!rec_lt(t, q, cl, ot, oq, oc) && i < j)) ? 1u : 0u;
+      }
+      out[sb + rank] = r[u];
     }
-    out[sb + rank] = r;
   }
   for (uint64_t big = __ballot(k == 0 && cnt > kC); big; big &= big - 1) {
     const uint32_t gl = (uint32_t)__builtin_ctzll(big);
     const uint64_t b = readlane64(sb, gl);
     const uint32_t n = (uint32_t)(readlane64(se, gl) - b);
-    const tgsim_delivery* bk = bkt + (uint64_t)(d0 + gl / kC) * kC;
+    const tgsim_delivery* bk = bkt + (uint64_t)(d0 + gl / kL) * kC;
     sort_segment_ld(sc, b, n, out, lane, [&](uint32_t j) { return j < kC ? bk[j] : sc[b + j]; });
   }
 }
@@ -3989,18 +4006,21 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
 
 template <uint32_t kC>
 static void launch_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const uint64_t* doff, uint32_t n_dst,
-                            tgsim_delivery* out, hipStream_t st) {
-  constexpr uint32_t per_wg = 4 * (kWave / kC);
-  hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3((n_dst + per_wg - 1) / per_wg), dim3(256), 0, st, bkt, sc, doff, n_dst, out);
+                            tgsim_delivery* out, hipStream_t st, const uint64_t* total, uint64_t cap,
+                            uint64_t* err_host) {
+  constexpr uint32_t per_wg = 4 * (kWave / (kC < 16 ? kC : 16));
+  hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3((n_dst + per_wg - 1) / per_wg), dim3(256), 0, st, bkt, sc, doff, n_dst,
+                     out, total, cap, err_host);
 }
 void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,
-                         uint32_t n_dst, tgsim_delivery* out, hipStream_t st) {
+                         uint32_t n_dst, tgsim_delivery* out, hipStream_t st, const uint64_t* total, uint64_t cap,
+                         uint64_t* err_host) {
   if (!n_dst) return;
   switch (bkt_log) {
-    case 3: launch_sort_bkt<8>(bkt, sc, doff, n_dst, out, st); break;
-    case 4: launch_sort_bkt<16>(bkt, sc, doff, n_dst, out, st); break;
-    case 5: launch_sort_bkt<32>(bkt, sc, doff, n_dst, out, st); break;
-    default: launch_sort_bkt<64>(bkt, sc, doff, n_dst, out, st); break;
+    case 3: launch_sort_bkt<8>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
+    case 4: launch_sort_bkt<16>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
+    case 5: launch_sort_bkt<32>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
+    default: launch_sort_bkt<64>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
   }
 }
 
