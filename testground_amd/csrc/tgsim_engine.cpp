@@ -207,6 +207,8 @@ struct tgsim_engine_s {
   hipEvent_t ev_dst = nullptr;   // recorded after the last delivery on dst_st
   hipEvent_t ev_recv = nullptr;  // recorded after the last delivery's scatter (and gossip receipts)
   hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
+  hipEvent_t ev_scan = nullptr;  // after a bucketed window's histogram scan on the simulate stream
+  bool scan_on_sim = true;       // TGSIM_SCAN_ON_SIM: that scan on the simulate stream (0: delivery stream)
   // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize), with
   // the number of windows the launch simulated (a fused launch counts each of its windows)
   struct PendingTiming {
@@ -1021,7 +1023,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   // the local delivery or routing two steps back read this emit pair
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
   HIPCHK(E->d_emit.ensure(emit_cap));
-  HIPCHK(E->d_emit_n.ensure(E->S));
+  if (E->d_emit_n.cap < static_cast<size_t>(E->S) + 1) {  // [S]: a bucketed window's overflow-list length
+    HIPCHK(E->d_emit_n.ensure(E->S + 1));
+    HIPCHK(hipMemsetAsync(E->d_emit_n.p, 0, sizeof(uint32_t) * E->d_emit_n.cap, E->st));
+  }
   SimArgs a = base_sim_args(E);
   a.off = E->d_off.p;
   a.in = E->d_in.p;
@@ -1066,6 +1071,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
       HIPCHK(E->d_dbkt.ensure(static_cast<size_t>(E->N) << kBktLogMax));
       a.dst_bkt = E->d_dbkt.p;
       a.bkt_log = bucket_log(E->n_in, E->N);
+      // the overflow list lives in the emit records (no region of them is written in such a window)
+      a.emit_pool_cap = static_cast<uint32_t>(std::min<uint64_t>(emit_cap, 0xFFFFFFFFull));
       E->el.bkt = a.dst_bkt;
       E->el.bkt_log = a.bkt_log;
     }
@@ -1412,8 +1419,17 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   HIPCHK(E->d_dpos.ensure(nd));
   HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
   HIPCHK(E->d_dtot.ensure(1));
-  launch_scan(lcnt, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, sq, E->d_dpos.p, lcnt);  // (clears lcnt)
+  // a bucketed window's scan runs on the simulate stream right behind the simulation (a few tens of
+  // microseconds at its priority; on the low-priority delivery stream its three dispatches waited for
+  // the next window's simulate waves, up to 1.3 ms at the 1M-peer flood's peak, while that simulate
+  // kernel's successor waited for this delivery to release the bucket set)
+  const bool scan_sim = E->scan_on_sim && emit.bkt;
+  launch_scan(lcnt, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, scan_sim ? E->st : sq, E->d_dpos.p, lcnt);  // (clears lcnt)
   HIPCHK(hipGetLastError());
+  if (scan_sim) {
+    HIPCHK(hipEventRecord(E->ev_scan, E->st));
+    HIPCHK(hipStreamWaitEvent(sq, E->ev_scan, 0));
+  }
   const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
   // without the exact count (no host round trip): what the window's sources can emit, 2 per offered
   // packet plus the full netem limit per source.  Where that bound exceeds kExactBoundBytes (24 GB
@@ -1441,8 +1457,9 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, E->d_doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
-  // (a bucketed window: only the records past their destination's bucket are in the emit records)
-  launch_local_scatter(er, emit_n, off, E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
+  // (a bucketed window: only the records past their destination's bucket, in its overflow list)
+  if (emit.bkt) launch_ovl_scatter(er, emit_n + E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq);
+  else launch_local_scatter(er, emit_n, off, E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
   // while this one's per-destination sort still runs (the sort reads only the scatter buffer) --
@@ -1454,7 +1471,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   if (rc) return rc;
   if (emit.bkt) {
     launch_dst_sort_bkt(emit.bkt, emit.bkt_log, E->d_scatter.p, E->d_doff.p, nd, dst, sq, er.guard_total, er.guard_cap,
-                        E->d_err_host);
+                        E->d_err_host, emit_n + E->S);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(released, sq));
   } else {
@@ -1833,6 +1850,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_scan, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_recv, E->dst_st), "event"))) return bail(rc);
   for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt}) {
     if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
@@ -1891,6 +1909,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
   if (const char* ds = getenv("TGSIM_DST_SLOT")) E->dst_slot = atoi(ds) != 0;
   if (const char* db = getenv("TGSIM_DST_BKT")) E->dst_bkt = atoi(db) != 0;
+  if (const char* ss = getenv("TGSIM_SCAN_ON_SIM")) E->scan_on_sim = atoi(ss) != 0;
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
   if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));
   E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
@@ -2031,6 +2050,7 @@ void tgsim_destroy(void* e) {
   if (E->ev_dst) (void)hipEventDestroy(E->ev_dst);
   if (E->ev_rt) (void)hipEventDestroy(E->ev_rt);
   if (E->ev_recv) (void)hipEventDestroy(E->ev_recv);
+  if (E->ev_scan) (void)hipEventDestroy(E->ev_scan);
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->ev_local) (void)hipEventDestroy(E->ev_local);
   if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);
