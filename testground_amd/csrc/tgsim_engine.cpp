@@ -1075,6 +1075,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
       a.emit_pool_cap = static_cast<uint32_t>(std::min<uint64_t>(emit_cap, 0xFFFFFFFFull));
       E->el.bkt = a.dst_bkt;
       E->el.bkt_log = a.bkt_log;
+      E->el.ovl_cap = a.emit_pool_cap;
     }
   }
   if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard

@@ -3221,11 +3221,13 @@ __global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint
 // A bucketed window's overflow list (EmitRead::bkt: the emit records from 0, *count of them) to
 // doff[d] + slot; a grid-stride loop over the count the simulate kernels left on the device.
 __global__ __launch_bounds__(256) void k_ovl_scatter(const tgsim_delivery* __restrict__ list, const uint32_t* count,
-                                                     uint32_t dst_begin, const uint64_t* __restrict__ doff,
-                                                     uint64_t* pos, tgsim_delivery* __restrict__ out,
-                                                     const uint64_t* total, uint64_t cap) {
+                                                     uint32_t list_cap, uint32_t dst_begin,
+                                                     const uint64_t* __restrict__ doff, uint64_t* pos,
+                                                     tgsim_delivery* __restrict__ out, const uint64_t* total,
+                                                     uint64_t cap) {
   if (total && *total > cap) return;
-  const uint32_t n = *count;
+  // (claims past the capacity were dropped, kErrEmitPool: the window fails at the next call)
+  const uint32_t n = min(*count, list_cap);
   unsigned long long* p = reinterpret_cast<unsigned long long*>(pos);
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     tgsim_delivery r = list[i];
@@ -4088,8 +4090,8 @@ void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_deli
 
 void launch_ovl_scatter(const EmitRead& emit, const uint32_t* count, uint32_t dst_begin, const uint64_t* doff,
                         uint64_t* pos, tgsim_delivery* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_ovl_scatter, dim3(1024), dim3(256), 0, st, emit.base, count, dst_begin, doff, pos, out,
-                     emit.guard_total, emit.guard_cap);
+  hipLaunchKernelGGL(k_ovl_scatter, dim3(1024), dim3(256), 0, st, emit.base, count, emit.ovl_cap, dst_begin, doff, pos,
+                     out, emit.guard_total, emit.guard_cap);
 }
 
 void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
