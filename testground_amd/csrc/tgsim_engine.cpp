@@ -348,6 +348,9 @@ struct tgsim_engine_s {
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
+  // a bucketed window's scan outputs, per emit set (its scan runs on the simulate stream while the
+  // delivery two windows back, of the other set, may still read the other set's)
+  DevBuf<uint64_t> d_sdoff, d_sdpos, d_sdblk, d_sdtot, d_sdoff_alt, d_sdpos_alt, d_sdblk_alt, d_sdtot_alt;
   uint64_t h_dtot = 0;
   DevBuf<tgsim_delivery> d_drain;
   uint64_t drain_head = 0, drain_n = 0;
@@ -866,6 +869,10 @@ void rotate_emit(Eng* E) {
   std::swap(E->d_emit_n, E->d_emit_n_alt);
   std::swap(E->d_lcnt, E->d_lcnt_alt);
   std::swap(E->d_dbkt, E->d_dbkt_alt);
+  std::swap(E->d_sdoff, E->d_sdoff_alt);
+  std::swap(E->d_sdpos, E->d_sdpos_alt);
+  std::swap(E->d_sdblk, E->d_sdblk_alt);
+  std::swap(E->d_sdtot, E->d_sdtot_alt);
   std::swap(E->ev_local, E->ev_local_alt);
 }
 
@@ -1416,16 +1423,21 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     HIPCHK(take_event(E, &dv1));
     HIPCHK(hipEventRecord(dv0, sq));
   }
-  HIPCHK(E->d_doff.ensure(nd + 1));
-  HIPCHK(E->d_dpos.ensure(nd));
-  HIPCHK(E->d_dblk.ensure((nd + 1023) / 1024 + 1));
-  HIPCHK(E->d_dtot.ensure(1));
+  // a bucketed window: the scan outputs of its emit set (see Eng::d_sdoff), else the shared ones
+  DevBuf<uint64_t>& doff = emit.bkt ? E->d_sdoff : E->d_doff;
+  DevBuf<uint64_t>& dpos = emit.bkt ? E->d_sdpos : E->d_dpos;
+  DevBuf<uint64_t>& dblk = emit.bkt ? E->d_sdblk : E->d_dblk;
+  DevBuf<uint64_t>& dtot = emit.bkt ? E->d_sdtot : E->d_dtot;
+  HIPCHK(doff.ensure(nd + 1));
+  HIPCHK(dpos.ensure(nd));
+  HIPCHK(dblk.ensure((nd + 1023) / 1024 + 1));
+  HIPCHK(dtot.ensure(1));
   // a bucketed window's scan runs on the simulate stream right behind the simulation (a few tens of
   // microseconds at its priority; on the low-priority delivery stream its three dispatches waited for
   // the next window's simulate waves, up to 1.3 ms at the 1M-peer flood's peak, while that simulate
   // kernel's successor waited for this delivery to release the bucket set)
   const bool scan_sim = E->scan_on_sim && emit.bkt;
-  launch_scan(lcnt, E->d_doff.p, nd, E->d_dblk.p, E->d_dtot.p, scan_sim ? E->st : sq, E->d_dpos.p, lcnt);  // (clears lcnt)
+  launch_scan(lcnt, doff.p, nd, dblk.p, dtot.p, scan_sim ? E->st : sq, dpos.p, lcnt);  // (clears lcnt)
   HIPCHK(hipGetLastError());
   if (scan_sim) {
     HIPCHK(hipEventRecord(E->ev_scan, E->st));
@@ -1444,7 +1456,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   if (E->wide_windows) E->wide_windows--;
   uint64_t n = 2 * n_in + slack * E->S;
   if (need_n) {
-    HIPCHK(hipMemcpyAsync(&E->h_dtot, E->d_dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
+    HIPCHK(hipMemcpyAsync(&E->h_dtot, dtot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, sq));
     HIPCHK(hipStreamSynchronize(sq));
     n = E->h_dtot;
   }
@@ -1452,15 +1464,15 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   const bool bounded = !need_n && slack < kHeapCap;
   EmitRead er = emit;
   if (bounded && emit.bkt) {  // the scatter and the sort check the total themselves (one dispatch fewer)
-    er.guard_total = E->d_dtot.p;
+    er.guard_total = dtot.p;
     er.guard_cap = n;
   } else if (bounded) {
-    launch_deliver_guard(E->d_dtot.p, n, emit_n, E->S, lcnt, E->d_doff.p, nd, E->d_err_host, sq);
+    launch_deliver_guard(dtot.p, n, emit_n, E->S, lcnt, doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
   // (a bucketed window: only the records past their destination's bucket, in its overflow list)
-  if (emit.bkt) launch_ovl_scatter(er, emit_n + E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq);
-  else launch_local_scatter(er, emit_n, off, E->S, 0, E->d_doff.p, E->d_dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
+  if (emit.bkt) launch_ovl_scatter(er, emit_n + E->S, 0, doff.p, dpos.p, E->d_scatter.p, sq);
+  else launch_local_scatter(er, emit_n, off, E->S, 0, doff.p, dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
   // while this one's per-destination sort still runs (the sort reads only the scatter buffer) --
@@ -1471,16 +1483,16 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   int rc = delivery_out(E, n, &dst, sq);
   if (rc) return rc;
   if (emit.bkt) {
-    launch_dst_sort_bkt(emit.bkt, emit.bkt_log, E->d_scatter.p, E->d_doff.p, nd, dst, sq, er.guard_total, er.guard_cap,
+    launch_dst_sort_bkt(emit.bkt, emit.bkt_log, E->d_scatter.p, doff.p, nd, dst, sq, er.guard_total, er.guard_cap,
                         E->d_err_host, emit_n + E->S);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(released, sq));
   } else {
-    launch_dst_sort(E->d_scatter.p, E->d_doff.p, nullptr, nd, dst, sq, need_n ? n : n_in);
+    launch_dst_sort(E->d_scatter.p, doff.p, nullptr, nd, dst, sq, need_n ? n : n_in);
   }
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
-    launch_metrics_dst(dst, E->d_doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
+    launch_metrics_dst(dst, doff.p, nd, E->d_mdst.p, E->d_mhist.p, sq);
     HIPCHK(hipGetLastError());
   }
   if (timed) {
@@ -2015,7 +2027,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_dbkt.release(); E->d_dbkt_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_dbkt.release(); E->d_dbkt_alt.release(); E->d_sdoff.release(); E->d_sdpos.release(); E->d_sdblk.release(); E->d_sdtot.release(); E->d_sdoff_alt.release(); E->d_sdpos_alt.release(); E->d_sdblk_alt.release(); E->d_sdtot_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
