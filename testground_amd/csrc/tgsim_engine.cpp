@@ -1030,10 +1030,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   // the local delivery or routing two steps back read this emit pair
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
   HIPCHK(E->d_emit.ensure(emit_cap));
-  if (E->d_emit_n.cap < static_cast<size_t>(E->S) + 1) {  // [S]: a bucketed window's overflow-list length
-    HIPCHK(E->d_emit_n.ensure(E->S + 1));
-    HIPCHK(hipMemsetAsync(E->d_emit_n.p, 0, sizeof(uint32_t) * E->d_emit_n.cap, E->st));
-  }
+  HIPCHK(E->d_emit_n.ensure(E->S));
   SimArgs a = base_sim_args(E);
   a.off = E->d_off.p;
   a.in = E->d_in.p;
@@ -1078,11 +1075,8 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
       HIPCHK(E->d_dbkt.ensure(static_cast<size_t>(E->N) << kBktLogMax));
       a.dst_bkt = E->d_dbkt.p;
       a.bkt_log = bucket_log(E->n_in, E->N);
-      // the overflow list lives in the emit records (no region of them is written in such a window)
-      a.emit_pool_cap = static_cast<uint32_t>(std::min<uint64_t>(emit_cap, 0xFFFFFFFFull));
       E->el.bkt = a.dst_bkt;
       E->el.bkt_log = a.bkt_log;
-      E->el.ovl_cap = a.emit_pool_cap;
     }
   }
   if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard
@@ -1470,9 +1464,8 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     launch_deliver_guard(dtot.p, n, emit_n, E->S, lcnt, doff.p, nd, E->d_err_host, sq);
     HIPCHK(hipGetLastError());
   }
-  // (a bucketed window: only the records past their destination's bucket, in its overflow list)
-  if (emit.bkt) launch_ovl_scatter(er, emit_n + E->S, 0, doff.p, dpos.p, E->d_scatter.p, sq);
-  else launch_local_scatter(er, emit_n, off, E->S, 0, doff.p, dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
+  // (a bucketed window: only the records past their destination's bucket are in the emit records)
+  launch_local_scatter(er, emit_n, off, E->S, 0, doff.p, dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
   // while this one's per-destination sort still runs (the sort reads only the scatter buffer) --
@@ -1484,7 +1477,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   if (rc) return rc;
   if (emit.bkt) {
     launch_dst_sort_bkt(emit.bkt, emit.bkt_log, E->d_scatter.p, doff.p, nd, dst, sq, er.guard_total, er.guard_cap,
-                        E->d_err_host, emit_n + E->S);
+                        E->d_err_host);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(released, sq));
   } else {

@@ -192,8 +192,7 @@ struct EmitRead {
   // SimArgs::dst_bkt of the window, or null: the records with a slot below 2^bkt_log are there, not
   // in the emit records above (which hold only the others; the delivery reads both)
   const tgsim_delivery* bkt;
-  uint32_t bkt_log;
-  uint32_t ovl_cap;  // with bkt: the overflow list's capacity (its length, emit_n[S], may count past it)
+  uint32_t bkt_log, _pad;
   // a bounded local delivery of a bucketed window: the readers check the window's exact total (on the
   // device) against the buffers' bound themselves and write nothing past it (no k_deliver_guard)
   const uint64_t* guard_total;

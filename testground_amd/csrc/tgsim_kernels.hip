@@ -296,7 +296,7 @@ __device__ __forceinline__ EmitOut emit_out(const SimArgs& a, uint32_t s, uint64
 // For up to `total` records: what exceeds the region comes from the pool, one atomic (lane 0; the
 // caller is wave-uniform).  The classic layout (emit_r = kHeapCap) never needs it.
 __device__ __forceinline__ void emit_claim(const SimArgs& a, uint32_t s, EmitOut& o, uint32_t total, uint32_t lane) {
-  if (total <= o.cap || a.dst_bkt) return;  // (a bucketed window writes no emit regions: ovl_slot)
+  if (total <= o.cap) return;
   const uint32_t need = total - o.cap;
   uint32_t at = 0;
   if (lane == 0) at = atomicAdd(a.worklist - 2, need);
@@ -308,27 +308,6 @@ __device__ __forceinline__ void emit_claim(const SimArgs& a, uint32_t s, EmitOut
     atomicOr(&a.stats[kStErr], (unsigned long long)kErrEmitPool);
     if (a.err_host) __hip_atomic_store(a.err_host, (uint64_t)kErrEmitPool, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-}
-
-// A bucketed window (SimArgs::dst_bkt): the records that do not fit their destination's bucket go to
-// the window's overflow list -- the emit records from index 0, emit_n[n_src] its length, claimed with
-// one atomic per wavefront -- not to their source's region, so the delivery's pass over them reads
-// only them.  Wave-uniform call; returns the lane's place, or null (want unset, or the list is full:
-// the record is dropped and kErrEmitPool raised, -ENOSPC at the next call).
-__device__ __forceinline__ tgsim_delivery* ovl_slot(tgsim_delivery* list, uint32_t* count, uint32_t cap, bool want,
-                                                    uint64_t below, unsigned long long* stats, uint64_t* err_host) {
-  const uint64_t m = __ballot(want);
-  if (!m) return nullptr;
-  const uint32_t first = (uint32_t)__builtin_ctzll(m);
-  uint32_t base = 0;
-  if (__lane_id() == first) base = atomicAdd(count, (uint32_t)__popcll(m));
-  base = readlane32(base, first);
-  const uint32_t i = base + (uint32_t)__popcll(m & below);
-  if (!want) return nullptr;
-  if (i < cap) return list + i;
-  atomicOr(&stats[kStErr], (unsigned long long)kErrEmitPool);
-  if (err_host) __hip_atomic_store(err_host, (uint64_t)kErrEmitPool, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return nullptr;
 }
 
 __device__ __forceinline__ uint32_t fib_lookup(const Interval* iv, uint32_t n, uint32_t ip) {
@@ -450,11 +429,6 @@ struct SimQueue {
   bool dslot;                // kOver: the records carry their destination slot (SimArgs::dst_slot)
   tgsim_delivery* bkt;       // kOver: the destinations' buckets (SimArgs::dst_bkt), or null
   uint32_t bkt_log;
-  tgsim_delivery* ovl;       // kOver with bkt: the window's overflow list (ovl_slot) and its length
-  uint32_t* ovl_n;
-  uint32_t ovl_cap, n_bkt;    // n_bkt: records written into buckets so far (wave-uniform)
-  unsigned long long* stats;
-  uint64_t* err_host;
   RecvFold rf;               // gossip receipts folded in at emission (rf.first null: none)
   uint32_t n_emit, src;
   // per-lane accumulators (summed over the wave at the end)
@@ -537,23 +511,16 @@ struct SimQueue {
       else atomicAdd(&dcnt[qi.w], 1ull);
     }
     const bool inb = live && bkt != nullptr && rank < (1ull << bkt_log);
-    const uint64_t below = (1ull << lane) - 1;
-    n_bkt += (uint32_t)__popcll(__ballot(inb));
-    tgsim_delivery* dst = nullptr;
-    uint64_t lm = 0;
-    if (bkt) {
-      dst = inb ? bkt + ((uint64_t)qi.w << bkt_log) + rank : ovl_slot(ovl, ovl_n, ovl_cap, live, below, stats, err_host);
-    } else {
-      const uint32_t ri = n_emit + (uint32_t)__popcll(__ballot(live) & below);
-      const bool ov = live && (ri < cap || over != nullptr);
-      lm = __ballot(ov);
-      if (ov) dst = ri >= cap ? over + (ri - cap) : emit + ri;
-    }
+    bool ov = live && !inb;
+    const uint32_t ri = n_emit + (uint32_t)__popcll(__ballot(ov) & ((1ull << lane) - 1));
+    ov = ov && (ri < cap || over != nullptr);
+    const uint64_t lm = __ballot(ov);
     if (c) {
       *reinterpret_cast<uint2*>(&slot(rn + lane)) = make_uint2((uint32_t)d, (uint32_t)(d >> 32));
-      if (dst) {
+      if (inb || ov) {
         const uint32_t len = qi.y >> 14 & 0xFFFFu, flags = qi.y >> 30;
-        uint64_t* rw = reinterpret_cast<uint64_t*>(dst);
+        uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? bkt + ((uint64_t)qi.w << bkt_log) + rank
+                                                       : ri >= cap ? over + (ri - cap) : emit + ri);
         rw[1] = ((uint64_t)qi.w << 32) | src;
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
         rw[0] = inb || !dslot ? d : d | slot_bits(rank);
@@ -1059,12 +1026,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.dslot = kList && a.dst_slot;
   Q.bkt = kList ? a.dst_bkt : nullptr;
   Q.bkt_log = a.bkt_log;
-  Q.ovl = a.emit;
-  Q.ovl_n = a.emit_n + a.n_src;
-  Q.ovl_cap = a.emit_pool_cap;
-  Q.n_bkt = 0;
-  Q.stats = a.stats;
-  Q.err_host = a.err_host;
   Q.rf = kRecv ? recv_fold(a) : RecvFold{};
   Q.sched = Q.corrupted = Q.lost = 0;
   Q.bytes = 0;
@@ -1594,7 +1555,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   if (lane == 0) {
     if (send > sbeg) atomicAdd(&sc[kStOffered], (unsigned long long)(send - sbeg));
     if (sched) atomicAdd(&sc[kStScheduled], (unsigned long long)sched);
-    if (kList && Q.n_bkt) atomicAdd(&sc[kStBktRecs], (unsigned long long)Q.n_bkt);
+    if (kList && a.dst_bkt && sched > Q.n_emit) atomicAdd(&sc[kStBktRecs], (unsigned long long)(sched - Q.n_emit));
     if (c_clone) atomicAdd(&sc[kStCloned], (unsigned long long)c_clone);
     if (corrupted) atomicAdd(&sc[kStCorrupted], (unsigned long long)corrupted);
     if (lost) atomicAdd(&sc[kStLost], (unsigned long long)lost);
@@ -1713,28 +1674,20 @@ constexpr uint32_t kFifoRounds = 4;  // FIFO sources: items served per step, in 
 // whether the lane's record was written.
 __device__ __forceinline__ bool emit_record(const SimArgs& a, const EmitOut& eo, bool live, const uint4& x, uint64_t d,
                                             uint32_t xlen, uint32_t src, uint32_t fw, uint32_t fw_f,
-                                            uint32_t& emitted, uint32_t& bkt_n, uint64_t below) {
+                                            uint32_t& emitted, uint64_t below) {
   unsigned long long rank = 0;
   if (live && a.dst_cnt) {
     if (a.dst_slot) rank = atomicAdd(&a.dst_cnt[x.w], 1ull);
     else atomicAdd(&a.dst_cnt[x.w], 1ull);
   }
   const bool inb = live && a.dst_bkt != nullptr && rank < (1ull << a.bkt_log);
-  tgsim_delivery* dst = nullptr;
-  bkt_n += (uint32_t)__popcll(__ballot(inb));
-  if (a.dst_bkt) {
-    dst = inb ? a.dst_bkt + ((uint64_t)x.w << a.bkt_log) + rank
-              : ovl_slot(a.emit, a.emit_n + a.n_src, a.emit_pool_cap, live, below, a.stats, a.err_host);
-  } else {
-    bool ov = live;
-    const uint32_t i = emitted + (uint32_t)__popcll(__ballot(ov) & below);
-    ov = ov && eo.fits(i);
-    emitted += (uint32_t)__popcll(__ballot(ov));
-    if (ov) dst = eo.at(i);
-  }
-  if (!dst) return false;
+  bool ov = live && !inb;
+  const uint32_t i = emitted + (uint32_t)__popcll(__ballot(ov) & below);
+  ov = ov && eo.fits(i);
+  emitted += (uint32_t)__popcll(__ballot(ov));
+  if (!inb && !ov) return false;
   const uint32_t flags = x.y >> 30;
-  uint64_t* rw = reinterpret_cast<uint64_t*>(dst);
+  uint64_t* rw = reinterpret_cast<uint64_t*>(inb ? a.dst_bkt + ((uint64_t)x.w << a.bkt_log) + rank : eo.at(i));
   rw[1] = ((uint64_t)x.w << 32) | src;
   rw[2] = ((uint64_t)flags << 48) | ((uint64_t)xlen << 32) | x.z;
   rw[0] = inb || !a.dst_slot ? d : d | slot_bits(rank);
@@ -1915,7 +1868,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
   // ---- HTB, records, receipts and the ring, for the served items in rounds of 64 lanes: the
   // queue's due items, then the due candidates, contiguous from the head slot
   uint64_t tat_c = st.tat;
-  uint32_t emitted = 0, sched_n = 0, bkt_n = 0, sk0 = 0, t_cor = 0, t_lost = 0;
+  uint32_t emitted = 0, sched_n = 0, sk0 = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
   bool releasing = T_enq && !ring_stop;
   EmitOut eo = emit_out(a, s, sbeg, send);
@@ -1941,7 +1894,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     tat_c = readlane64(tat_after, ns - 1);
     bool live = hs && x.w != kDeadDst;
     const bool dead = hs && !live;
-    live = emit_record(a, eo, live, x, d, xlen, src, fw, fw_f, emitted, bkt_n, below);
+    live = emit_record(a, eo, live, x, d, xlen, src, fw, fw_f, emitted, below);
     if (live) bytes += xlen;
     sched_n += (uint32_t)__popcll(__ballot(live));
     t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
@@ -1984,7 +1937,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (sched_n) atomicAdd(&sc[kStScheduled], (unsigned long long)sched_n);
-    if (bkt_n) atomicAdd(&sc[kStBktRecs], (unsigned long long)bkt_n);
+    if (a.dst_bkt && sched_n > emitted) atomicAdd(&sc[kStBktRecs], (unsigned long long)(sched_n - emitted));
     if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
     if (t_cor) atomicAdd(&sc[kStCorrupted], (unsigned long long)t_cor);
     if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
@@ -2325,7 +2278,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   // ---- HTB, records, receipts and the ring, for the served items in rounds of 64 lanes (more than
   // one only on the FIFO path: the queue's due prefix, then the due candidates, in order)
   uint64_t tat_c = st.tat;
-  uint32_t emitted = 0, sched_n = 0, bkt_n = 0, sk0 = 0, t_sched = 0, t_cor = 0, t_lost = 0;
+  uint32_t emitted = 0, sched_n = 0, sk0 = 0, t_sched = 0, t_cor = 0, t_lost = 0;
   uint64_t bytes = 0;
   bool releasing = T_enq && !ring_stop;  // served entries departing before the last enqueue are released
   EmitOut eo = emit_out(a, s, sbeg, send);
@@ -2353,7 +2306,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     // records of the served items (dead destinations leave the sender and are lost)
     bool live = hs && x.w != kDeadDst;
     const bool dead = hs && !live;
-    live = emit_record(a, eo, live, x, d, xlen, src, fw, fw_f, emitted, bkt_n, below);
+    live = emit_record(a, eo, live, x, d, xlen, src, fw, fw_f, emitted, below);
     if (live) bytes += xlen;
     sched_n += (uint32_t)__popcll(__ballot(live));
     t_cor += (uint32_t)__popcll(__ballot(live && (x.y >> 31)));
@@ -2416,7 +2369,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (t_sched) atomicAdd(&sc[kStScheduled], (unsigned long long)t_sched);
-    if (bkt_n) atomicAdd(&sc[kStBktRecs], (unsigned long long)bkt_n);
+    if (a.dst_bkt && t_sched > emitted) atomicAdd(&sc[kStBktRecs], (unsigned long long)(t_sched - emitted));
     if (t_clone) atomicAdd(&sc[kStCloned], (unsigned long long)t_clone);
     if (t_cor) atomicAdd(&sc[kStCorrupted], (unsigned long long)t_cor);
     if (t_lost) atomicAdd(&sc[kStLost], (unsigned long long)t_lost);
@@ -3218,23 +3171,6 @@ __global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint
 // cursor atomic and store of a round independent of the others; a pass over the records'
 // destinations first, so that a destination's records share one cursor atomic.  The wave per source above walks
 // its sources one after another, each behind four dependent round trips with 57 of 64 lanes idle.
-// A bucketed window's overflow list (EmitRead::bkt: the emit records from 0, *count of them) to
-// doff[d] + slot; a grid-stride loop over the count the simulate kernels left on the device.
-__global__ __launch_bounds__(256) void k_ovl_scatter(const tgsim_delivery* __restrict__ list, const uint32_t* count,
-                                                     uint32_t list_cap, uint32_t dst_begin,
-                                                     const uint64_t* __restrict__ doff, uint64_t* pos,
-                                                     tgsim_delivery* __restrict__ out, const uint64_t* total,
-                                                     uint64_t cap) {
-  if (total && *total > cap) return;
-  // (claims past the capacity were dropped, kErrEmitPool: the window fails at the next call)
-  const uint32_t n = min(*count, list_cap);
-  unsigned long long* p = reinterpret_cast<unsigned long long*>(pos);
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    tgsim_delivery r = list[i];
-    out[scatter_at<true>(r, dst_begin, doff, p)] = r;
-  }
-}
-
 // kMode: kScatterEach one cursor atomic per record; kScatterAgg one per destination of a source (below);
 // kScatterSlot records that carry their destination slot, no atomic.
 constexpr int kScatterEach = 0, kScatterAgg = 1, kScatterSlot = 2;
@@ -3612,9 +3548,8 @@ template <uint32_t kC>
 __global__ __launch_bounds__(256) void k_dst_sort_bkt(const tgsim_delivery* __restrict__ bkt, tgsim_delivery* sc,
                                                       const uint64_t* __restrict__ doff, uint32_t n_dst,
                                                       tgsim_delivery* __restrict__ out, const uint64_t* total,
-                                                      uint64_t cap, uint64_t* err_host, uint32_t* ovl_n) {
+                                                      uint64_t cap, uint64_t* err_host) {
   constexpr uint32_t kL = kC < 16 ? kC : 16;  // lanes per destination
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ovl_n = 0u;  // the list is read (k_ovl_scatter ran before)
   constexpr uint32_t kG = kWave / kL;         // destinations per wavefront
   constexpr uint32_t kR = kC / kL;            // bucket entries per lane
   __shared__ uint64_t kt[4][kG * kC], kq[4][kG * kC];
@@ -4072,26 +4007,21 @@ void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uin
 template <uint32_t kC>
 static void launch_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const uint64_t* doff, uint32_t n_dst,
                             tgsim_delivery* out, hipStream_t st, const uint64_t* total, uint64_t cap,
-                            uint64_t* err_host, uint32_t* ovl_n) {
+                            uint64_t* err_host) {
   constexpr uint32_t per_wg = 4 * (kWave / (kC < 16 ? kC : 16));
   hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3((n_dst + per_wg - 1) / per_wg), dim3(256), 0, st, bkt, sc, doff, n_dst,
-                     out, total, cap, err_host, ovl_n);
+                     out, total, cap, err_host);
 }
 void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,
                          uint32_t n_dst, tgsim_delivery* out, hipStream_t st, const uint64_t* total, uint64_t cap,
-                         uint64_t* err_host, uint32_t* ovl_n) {
+                         uint64_t* err_host) {
+  if (!n_dst) return;
   switch (bkt_log) {
-    case 3: launch_sort_bkt<8>(bkt, sc, doff, n_dst, out, st, total, cap, err_host, ovl_n); break;
-    case 4: launch_sort_bkt<16>(bkt, sc, doff, n_dst, out, st, total, cap, err_host, ovl_n); break;
-    case 5: launch_sort_bkt<32>(bkt, sc, doff, n_dst, out, st, total, cap, err_host, ovl_n); break;
-    default: launch_sort_bkt<64>(bkt, sc, doff, n_dst, out, st, total, cap, err_host, ovl_n); break;
+    case 3: launch_sort_bkt<8>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
+    case 4: launch_sort_bkt<16>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
+    case 5: launch_sort_bkt<32>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
+    default: launch_sort_bkt<64>(bkt, sc, doff, n_dst, out, st, total, cap, err_host); break;
   }
-}
-
-void launch_ovl_scatter(const EmitRead& emit, const uint32_t* count, uint32_t dst_begin, const uint64_t* doff,
-                        uint64_t* pos, tgsim_delivery* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_ovl_scatter, dim3(1024), dim3(256), 0, st, emit.base, count, emit.ovl_cap, dst_begin, doff, pos,
-                     out, emit.guard_total, emit.guard_cap);
 }
 
 void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,

@@ -95,14 +95,9 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
 // The per-destination order of a bucketed window (SimArgs::dst_bkt, 2^bkt_log records per bucket):
 // the buckets and, for the destinations with more records, the scatter buffer (sc) behind them.
 // total/cap/err_host: a bounded delivery's exact total against its buffers (null total: exact buffers).
-// ovl_n: the window's overflow-list length, zeroed here for the set's next window.
 void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,
                          uint32_t n_dst, tgsim_delivery* out, hipStream_t st, const uint64_t* total, uint64_t cap,
-                         uint64_t* err_host, uint32_t* ovl_n);
-// A bucketed window's overflow list (emit.base, *count records) to doff[d] + slot (emit.guard_*: a
-// bounded delivery's check).
-void launch_ovl_scatter(const EmitRead& emit, const uint32_t* count, uint32_t dst_begin, const uint64_t* doff,
-                        uint64_t* pos, tgsim_delivery* out, hipStream_t st);
+                         uint64_t* err_host);
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, const uint64_t* doff, uint64_t* pos, tgsim_delivery* out,
                           hipStream_t st, uint64_t n_hint, bool few_dst = false);
