@@ -208,7 +208,7 @@ struct tgsim_engine_s {
   hipEvent_t ev_recv = nullptr;  // recorded after the last delivery's scatter (and gossip receipts)
   hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
   hipEvent_t ev_scan = nullptr;  // after a bucketed window's histogram scan on the simulate stream
-  bool scan_on_sim = true;       // TGSIM_SCAN_ON_SIM: that scan on the simulate stream (0: delivery stream)
+  bool scan_on_sim = false;      // TGSIM_SCAN_ON_SIM=1: that scan on the simulate stream (A/B: 0.6 % slower)
   // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize), with
   // the number of windows the launch simulated (a fused launch counts each of its windows)
   struct PendingTiming {
@@ -317,15 +317,19 @@ struct tgsim_engine_s {
   // emit regions and per-destination histogram written by k_sim; a single-shard step reads them
   // on the delivery stream while the next k_sim writes the other pair (swapped by deliver_local;
   // ev_local: the delivery that last read the pair)
-  // Emit sets: window k's k_sim writes set k % 2 (d_emit, ...) while the delivery of the window
-  // before it reads the other (the *_alt set, swapped after every window); k_sim waits only for the
-  // delivery of window k - 2 (a third set, so that a delivery could lag two windows at the gossip
-  // flood's peak, was tried: at 1M peers a set is ~38 GB and the third one thrashed)
-  DevBuf<tgsim_delivery> d_emit, d_emit_alt;
+  // Emit sets: window k's k_sim writes set k % 3 (d_emit, ...) while the deliveries of the windows
+  // before it read the others (*_alt: window k - 1's, *_alt2: k - 2's; rotate_emit after every window);
+  // k_sim waits only for the delivery of window k - 3.  (A third set was first tried in round 3, when
+  // a classic set was ~38 GB at 1M peers and it thrashed; compact sets and buckets
+  // are a few GB.)
+  DevBuf<tgsim_delivery> d_emit, d_emit_alt, d_emit_alt2;
+  // TGSIM_EMIT_SETS: 3 (default) lets the delivery of window k lag until window k + 3 starts (alt2: the
+  // set of window k - 2); the sets are allocated as they are first used
+  uint32_t emit_sets = 3;
   // where each emit set's records are (classic regions, or compact regions and a pool: DESIGN §4),
   // and the per-source pool indices of each set
-  EmitRead el{}, el_alt{};
-  DevBuf<uint32_t> d_pidx, d_pidx_alt;
+  EmitRead el{}, el_alt{}, el_alt2{};
+  DevBuf<uint32_t> d_pidx, d_pidx_alt, d_pidx_alt2;
   int emit_compact = 1;           // TGSIM_EMIT_COMPACT: 0 every window in the classic layout, 1 auto,
                                   // 2 every sparse window compact (tests)
   bool dst_slot = true;           // TGSIM_DST_SLOT: sparse windows place records by destination slot
@@ -341,16 +345,17 @@ struct tgsim_engine_s {
   uint64_t deliver_slack = 128;           // TGSIM_DELIVER_SLACK: queued items per source a bounded local
                                           // delivery allows for (besides 2 per offered packet)
   bool slack_forced = false;              // TGSIM_DELIVER_SLACK set: the bounded form at any size
-  DevBuf<uint32_t> d_emit_n, d_emit_n_alt;
-  DevBuf<uint64_t> d_lcnt, d_lcnt_alt;  // stays zero between steps (the delivery's scan clears it)
-  DevBuf<tgsim_delivery> d_dbkt, d_dbkt_alt;  // destination buckets of a sparse window (SimArgs::dst_bkt)
-  hipEvent_t ev_local = nullptr, ev_local_alt = nullptr;
+  DevBuf<uint32_t> d_emit_n, d_emit_n_alt, d_emit_n_alt2;
+  DevBuf<uint64_t> d_lcnt, d_lcnt_alt, d_lcnt_alt2;  // stays zero between steps (the delivery's scan clears it)
+  DevBuf<tgsim_delivery> d_dbkt, d_dbkt_alt, d_dbkt_alt2;  // destination buckets of a sparse window (SimArgs::dst_bkt)
+  hipEvent_t ev_local = nullptr, ev_local_alt = nullptr, ev_local_alt2 = nullptr;
   DevBuf<uint64_t> d_rcnt, d_rpos, d_rblk, d_rtot;  // routing: [rank][source] counts, scan
   DevBuf<tgsim_delivery> d_bucket, d_scatter, d_sorted;
   DevBuf<uint64_t> d_dcnt, d_doff, d_dpos, d_dblk, d_dtot;  // d_dcnt stays zero between steps
   // a bucketed window's scan outputs, per emit set (its scan runs on the simulate stream while the
   // delivery two windows back, of the other set, may still read the other set's)
   DevBuf<uint64_t> d_sdoff, d_sdpos, d_sdblk, d_sdtot, d_sdoff_alt, d_sdpos_alt, d_sdblk_alt, d_sdtot_alt;
+  DevBuf<uint64_t> d_sdoff_alt2, d_sdpos_alt2, d_sdblk_alt2, d_sdtot_alt2;
   uint64_t h_dtot = 0;
   DevBuf<tgsim_delivery> d_drain;
   uint64_t drain_head = 0, drain_n = 0;
@@ -863,17 +868,27 @@ SimArgs base_sim_args(Eng* E) {
 
 // The next window's emit set: the current one becomes the newest being delivered.
 void rotate_emit(Eng* E) {
-  std::swap(E->d_emit, E->d_emit_alt);
-  std::swap(E->el, E->el_alt);
-  std::swap(E->d_pidx, E->d_pidx_alt);
-  std::swap(E->d_emit_n, E->d_emit_n_alt);
-  std::swap(E->d_lcnt, E->d_lcnt_alt);
-  std::swap(E->d_dbkt, E->d_dbkt_alt);
-  std::swap(E->d_sdoff, E->d_sdoff_alt);
-  std::swap(E->d_sdpos, E->d_sdpos_alt);
-  std::swap(E->d_sdblk, E->d_sdblk_alt);
-  std::swap(E->d_sdtot, E->d_sdtot_alt);
-  std::swap(E->ev_local, E->ev_local_alt);
+  // (current, newest delivered, older) <- (older, current, newest delivered): window k + 1 writes the
+  // set of window k - 2 (three sets) or k - 1 (two), whose delivery it waits for (ev_local)
+  auto rot = [E](auto& cur, auto& alt, auto& alt2) {
+    if (E->emit_sets == 3) {
+      std::swap(cur, alt2);  // (alt2, alt, cur)
+      std::swap(alt, alt2);  // (alt2, cur, alt)
+    } else {
+      std::swap(cur, alt);
+    }
+  };
+  rot(E->d_emit, E->d_emit_alt, E->d_emit_alt2);
+  rot(E->el, E->el_alt, E->el_alt2);
+  rot(E->d_pidx, E->d_pidx_alt, E->d_pidx_alt2);
+  rot(E->d_emit_n, E->d_emit_n_alt, E->d_emit_n_alt2);
+  rot(E->d_lcnt, E->d_lcnt_alt, E->d_lcnt_alt2);
+  rot(E->d_dbkt, E->d_dbkt_alt, E->d_dbkt_alt2);
+  rot(E->d_sdoff, E->d_sdoff_alt, E->d_sdoff_alt2);
+  rot(E->d_sdpos, E->d_sdpos_alt, E->d_sdpos_alt2);
+  rot(E->d_sdblk, E->d_sdblk_alt, E->d_sdblk_alt2);
+  rot(E->d_sdtot, E->d_sdtot_alt, E->d_sdtot_alt2);
+  rot(E->ev_local, E->ev_local_alt, E->ev_local_alt2);
 }
 
 // The size of a gossip window generated ahead of it (tgsim_gen_gossip): waits for the published
@@ -1858,7 +1873,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_scan, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_recv, E->dst_st), "event"))) return bail(rc);
-  for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt}) {
+  for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt, &E->ev_local_alt2}) {
     if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
     if ((rc = E->hip(hipEventRecord(*ev, E->dst_st), "event"))) return bail(rc);
   }
@@ -1916,6 +1931,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (const char* ds = getenv("TGSIM_DST_SLOT")) E->dst_slot = atoi(ds) != 0;
   if (const char* db = getenv("TGSIM_DST_BKT")) E->dst_bkt = atoi(db) != 0;
   if (const char* ss = getenv("TGSIM_SCAN_ON_SIM")) E->scan_on_sim = atoi(ss) != 0;
+  if (const char* es = getenv("TGSIM_EMIT_SETS")) E->emit_sets = atoi(es) == 2 ? 2u : 3u;
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
   if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));
   E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
@@ -2020,7 +2036,7 @@ void tgsim_destroy(void* e) {
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
   E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
-  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_dbkt.release(); E->d_dbkt_alt.release(); E->d_sdoff.release(); E->d_sdpos.release(); E->d_sdblk.release(); E->d_sdtot.release(); E->d_sdoff_alt.release(); E->d_sdpos_alt.release(); E->d_sdblk_alt.release(); E->d_sdtot_alt.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
+  E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_dbkt.release(); E->d_dbkt_alt.release(); E->d_sdoff.release(); E->d_sdpos.release(); E->d_sdblk.release(); E->d_sdtot.release(); E->d_sdoff_alt.release(); E->d_sdpos_alt.release(); E->d_sdblk_alt.release(); E->d_sdtot_alt.release(); E->d_sdoff_alt2.release(); E->d_sdpos_alt2.release(); E->d_sdblk_alt2.release(); E->d_sdtot_alt2.release(); E->d_emit_alt2.release(); E->d_emit_n_alt2.release(); E->d_lcnt_alt2.release(); E->d_dbkt_alt2.release(); E->d_pidx.release(); E->d_pidx_alt.release(); E->d_pidx_alt2.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();
   E->d_doff.release(); E->d_dpos.release(); E->d_dblk.release(); E->d_dtot.release();
   E->d_drain.release(); E->d_gfirst.release(); E->d_gfwd.release(); E->d_gpend.release(); E->d_gnbr.release(); E->d_gerr.release(); E->d_stats.release(); E->d_stamps.release(); E->d_order.release();
@@ -2060,6 +2076,7 @@ void tgsim_destroy(void* e) {
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->ev_local) (void)hipEventDestroy(E->ev_local);
   if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);
+  if (E->ev_local_alt2) (void)hipEventDestroy(E->ev_local_alt2);
   if (E->dst_st) (void)hipStreamDestroy(E->dst_st);
   if (E->rt_st) (void)hipStreamDestroy(E->rt_st);
   if (E->st) (void)hipStreamDestroy(E->st);
@@ -2198,7 +2215,7 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   HIPCHK(E->d_verdict.ensure(reserve));
   // the emit regions of both parities, for the same reserve (a hipFree + hipMalloc of several GB inside the flood stalls the loop)
   const uint64_t emit_cap = emit_records(E, reserve, compact_layout(E, reserve, true));
-  for (auto* b : {&E->d_emit, &E->d_emit_alt}) HIPCHK(b->ensure(emit_cap));
+  for (auto* b : {&E->d_emit, &E->d_emit_alt, &E->d_emit_alt2}) HIPCHK(b->ensure(emit_cap));
   E->gossip_on = true;
   return 0;
 }
