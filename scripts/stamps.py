@@ -74,7 +74,17 @@ print("  cycles per batch (mean over wgs): " + ", ".join(f"{v} {np.mean(pf[:, k]
 print(f"  per batch: {np.mean(pf[:, 3] / nb):.2f} windows, {np.mean(pf[:, 2] / nb):.2f} full-queue runs, "
       f"{np.mean(pf[:, 5] / nb):.2f} inserted items, {np.mean(pf[:, 6] / nb):.2f} shift chunks, "
       f"{np.mean(pf[:, 17] / nb):.2f} refill rounds, {np.mean(pf[:, 18] / nb):.2f} refilled items, "
-      f"{np.mean(pf[:, 19] / nb):.2f} pool appends")
+      f"{np.mean(pf[:, 19] / nb):.2f} pool appends, {np.mean(pf[:, 23] / nb):.2f} windows ended by an admission")
+# the heavy-source chain's limit.  A sub-window ends early when an item admitted in
+# it becomes eligible before a later packet of it (reorder, or a delay <= 0 with J > L); absorbing
+# those into the sub-window's departure scan would leave windows - admission-ended sub-windows.
+top = np.argsort(-tot)[:512]
+w_top, a_top = pf[top, 3].sum(), pf[top, 23].sum()
+print(f"  512 slowest sources: {np.mean(pf[top, 3] / nb[top]):.2f} sub-windows per batch, "
+      f"{np.mean(tot[top] / np.maximum(pf[top, 3], 1)):.2f} us per sub-window, {a_top / max(w_top, 1) * 100:.1f} % of "
+      f"their sub-windows ended by an admission; the slowest source {tot[top[0]]:.1f} us with {pf[top[0], 3]} "
+      f"sub-windows, {pf[top[0], 23]} of them admission-ended (absorbing them: >= "
+      f"{tot[top[0]] * (1 - pf[top[0], 23] / max(pf[top[0], 3], 1)):.1f} us if time scales with sub-windows)")
 shapes = workloads.storm_shapes(a.peers) if a.workload == "storm" else None
 print("  slowest workgroups (= sources):")
 for i in np.argsort(-tot)[:a.top]:

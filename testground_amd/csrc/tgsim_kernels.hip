@@ -1353,6 +1353,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
           const uint64_t Bex = shr1_u64(scan_min_u64(beta), ~0ull);
           const uint64_t mv = __ballot(inw && Bex < T);
           if (mv) wend = (uint32_t)__builtin_ctzll(mv);
+          PROF_CNT(23, mv ? 1u : 0u);  // a sub-window ended by an admission eligible inside it
         }
         const bool inwin = inw && lane < wend;
         const uint64_t mwin = __ballot(inwin);
