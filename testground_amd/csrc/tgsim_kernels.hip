@@ -1487,7 +1487,10 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.serve_until(a.horizon_ns);
   QCHECK(4);
   PROF_ADD(13, e);
-  if (lane == 0) a.emit_n[s] = Q.n_emit;
+  if (lane == 0) {
+    a.emit_n[s] = Q.n_emit;
+    if (kList && a.dst_bkt && Q.n_emit) a.emit_n[a.n_src + (s >> 8)] = 1u;  // (bkt_block_flag)
+  }
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   uint32_t next_ticket = 0;
   if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
@@ -1925,6 +1928,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     ns_.last_reo = st.last_reo;
     a.state[s] = ns_;
     a.emit_n[s] = emitted;
+    if (a.dst_bkt && emitted) a.emit_n[a.n_src + (s >> 8)] = 1u;  // (bkt_block_flag)
   }
   // ---- statistics
   const uint64_t t_bytes = wave_sum(bytes);
@@ -2346,6 +2350,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     ns_.last_reo = st.last_reo;
     a.state[s] = ns_;
     a.emit_n[s] = emitted;
+    if (a.dst_bkt && emitted) a.emit_n[a.n_src + (s >> 8)] = 1u;  // (bkt_block_flag)
   }
   if (staged) a.verdict[sbeg + lane] = (uint8_t)vout;
   stamp(a, s, lane, 4, __builtin_amdgcn_s_memrealtime());
@@ -3182,6 +3187,10 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
                                                           uint32_t dst_begin, const uint64_t* __restrict__ doff,
                                                           uint64_t* pos, tgsim_delivery* __restrict__ out) {
   if (emit.guard_total && *emit.guard_total > emit.guard_cap) return;  // (EmitRead::guard_total)
+  // a bucketed window: the simulate kernels flagged the blocks of 256 sources that wrote emit records
+  // (the records past their destination's bucket); the others hold none (emit_n[n_src + block])
+  uint32_t* const bflag = kMode == kScatterSlot && emit.bflag ? emit.bflag + blockIdx.x : nullptr;
+  if (bflag && *bflag == 0u) return;
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
   uint32_t n = 0, cap = 0;
   const tgsim_delivery* base = emit.base;  // the source's region: its first cap records
@@ -3208,6 +3217,10 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
         if (i + u < n) out[at[u]] = r[u];
+    }
+    if (bflag) {  // every lane has read the flag: clear it for the set's next window
+      __syncthreads();
+      if (threadIdx.x == 0) *bflag = 0u;
     }
     return;
   }
@@ -3562,49 +3575,55 @@ __global__ __launch_bounds__(256) void k_dst_sort_bkt(const tgsim_delivery* __re
   }
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t g = lane / kL, k = lane % kL;
-  const uint32_t d0 = (blockIdx.x * 4 + wv) * kG, d = d0 + g;
-  const bool in_range = d < n_dst;
-  uint64_t sb = 0, se = 0;
-  tgsim_delivery r[kR];
-  if (in_range) {
-    sb = doff[d];
-    se = doff[d + 1];
+  // a grid of resident workgroups walks the destination groups (launch_sort_bkt): workgroup slots are
+  // taken once, not once per four wavefronts' worth of destinations, beside the simulate waves
+  const uint32_t n_grp = (n_dst + 4 * kG - 1) / (4 * kG);
+  for (uint32_t grp = blockIdx.x; grp < n_grp; grp += gridDim.x) {
+    const uint32_t d0 = (grp * 4 + wv) * kG, d = d0 + g;
+    const bool in_range = d < n_dst;
+    uint64_t sb = 0, se = 0;
+    tgsim_delivery r[kR];
+    if (in_range) {
+      sb = doff[d];
+      se = doff[d + 1];
 #pragma unroll
-    for (uint32_t u = 0; u < kR; ++u) r[u] = bkt[(uint64_t)d * kC + u * kL + k];
-  }
-  const uint64_t cnt = se - sb;
-  const bool small = cnt <= kC;
-#pragma unroll
-  for (uint32_t u = 0; u < kR; ++u) {
-    const uint32_t j = u * kL + k;
-    const bool v = small && j < cnt;
-    kt[wv][g * kC + j] = v ? r[u].t_ns : ~0ull;
-    kq[wv][g * kC + j] = v ? ((uint64_t)r[u].src << 32) | r[u].seq : ~0ull;
-    kc[wv][g * kC + j] = v ? ((r[u].flags & TGSIM_FLAG_DUP) ? 0u : 1u) : 1u;
-  }
-  wave_lds_sync();
-#pragma unroll
-  for (uint32_t u = 0; u < kR; ++u) {
-    const uint32_t j = u * kL + k;
-    if (small && j < cnt) {
-      const uint64_t t = kt[wv][g * kC + j], q = kq[wv][g * kC + j];
-      const uint32_t cl = kc[wv][g * kC + j];
-      uint32_t rank = 0;
-      for (uint32_t i = 0; i < (uint32_t)cnt; ++i) {
-        const uint32_t x = g * kC + i;
-        const uint64_t ot = kt[wv][x], oq = kq[wv][x];
-        const uint32_t oc = kc[wv][x];
-        rank += (rec_lt(ot, oq, oc, t, q, cl) || (!rec_lt(t, q, cl, ot, oq, oc) && i < j)) ? 1u : 0u;
-      }
-      out[sb + rank] = r[u];
+      for (uint32_t u = 0; u < kR; ++u) r[u] = bkt[(uint64_t)d * kC + u * kL + k];
     }
-  }
-  for (uint64_t big = __ballot(k == 0 && cnt > kC); big; big &= big - 1) {
-    const uint32_t gl = (uint32_t)__builtin_ctzll(big);
-    const uint64_t b = readlane64(sb, gl);
-    const uint32_t n = (uint32_t)(readlane64(se, gl) - b);
-    const tgsim_delivery* bk = bkt + (uint64_t)(d0 + gl / kL) * kC;
-    sort_segment_ld(sc, b, n, out, lane, [&](uint32_t j) { return j < kC ? bk[j] : sc[b + j]; });
+    const uint64_t cnt = se - sb;
+    const bool small = cnt <= kC;
+#pragma unroll
+    for (uint32_t u = 0; u < kR; ++u) {
+      const uint32_t j = u * kL + k;
+      const bool v = small && j < cnt;
+      kt[wv][g * kC + j] = v ? r[u].t_ns : ~0ull;
+      kq[wv][g * kC + j] = v ? ((uint64_t)r[u].src << 32) | r[u].seq : ~0ull;
+      kc[wv][g * kC + j] = v ? ((r[u].flags & TGSIM_FLAG_DUP) ? 0u : 1u) : 1u;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t u = 0; u < kR; ++u) {
+      const uint32_t j = u * kL + k;
+      if (small && j < cnt) {
+        const uint64_t t = kt[wv][g * kC + j], q = kq[wv][g * kC + j];
+        const uint32_t cl = kc[wv][g * kC + j];
+        uint32_t rank = 0;
+        for (uint32_t i = 0; i < (uint32_t)cnt; ++i) {
+          const uint32_t x = g * kC + i;
+          const uint64_t ot = kt[wv][x], oq = kq[wv][x];
+          const uint32_t oc = kc[wv][x];
+          rank += (rec_lt(ot, oq, oc, t, q, cl) || (!rec_lt(t, q, cl, ot, oq, oc) && i < j)) ? 1u : 0u;
+        }
+        out[sb + rank] = r[u];
+      }
+    }
+    for (uint64_t big = __ballot(k == 0 && cnt > kC); big; big &= big - 1) {
+      const uint32_t gl = (uint32_t)__builtin_ctzll(big);
+      const uint64_t b = readlane64(sb, gl);
+      const uint32_t n = (uint32_t)(readlane64(se, gl) - b);
+      const tgsim_delivery* bk = bkt + (uint64_t)(d0 + gl / kL) * kC;
+      sort_segment_ld(sc, b, n, out, lane, [&](uint32_t j) { return j < kC ? bk[j] : sc[b + j]; });
+    }
+    wave_lds_sync();  // this group's LDS reads are done before the next group's writes
   }
 }
 
@@ -4010,8 +4029,10 @@ static void launch_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const
                             tgsim_delivery* out, hipStream_t st, const uint64_t* total, uint64_t cap,
                             uint64_t* err_host) {
   constexpr uint32_t per_wg = 4 * (kWave / (kC < 16 ? kC : 16));
-  hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3((n_dst + per_wg - 1) / per_wg), dim3(256), 0, st, bkt, sc, doff, n_dst,
-                     out, total, cap, err_host);
+  const uint32_t groups = (n_dst + per_wg - 1) / per_wg;
+  static const int cap_wg = env_knob("TGSIM_SORT_GRID");  // A/B: 0 the default cap, < 0 one per group
+  const uint32_t grid = cap_wg < 0 ? groups : std::min<uint32_t>(groups, cap_wg > 0 ? (uint32_t)cap_wg : 4096u);
+  hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3(grid), dim3(256), 0, st, bkt, sc, doff, n_dst, out, total, cap, err_host);
 }
 void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,
                          uint32_t n_dst, tgsim_delivery* out, hipStream_t st, const uint64_t* total, uint64_t cap,
