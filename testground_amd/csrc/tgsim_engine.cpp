@@ -929,16 +929,17 @@ int retire_gen(Eng* E, Eng::GenWindow&& w, bool by_group = false) {
 
 // A free window for the next generation (the OLDEST retired one).  Its offsets were last read by the
 // delivery and routing of the window they belonged to; those are waited for by the simulation of
-// the window two later (through its emit pair or fused buffer set), which the simulate stream runs
-// before this generation once two more simulate calls were made.  Otherwise (a short rotation) the
-// generation waits for the latest delivery and routing.  With the gossip driver's three windows in
-// rotation that never happens, so the generation never waits for a lagging delivery (an event per
-// window instead cost ~20 us of host time per step).
+// the window emit_sets later (through its emit set or, two later, its fused buffer set), which the
+// simulate stream runs before this generation once emit_sets more simulate calls were made.
+// Otherwise (a short rotation) the generation waits for the latest delivery and routing.  With the
+// gossip driver's emit_sets + 1 windows in rotation (tgsim_gossip_init) that never happens, so the
+// generation never waits for a lagging delivery (an event per window instead cost ~20 us of host
+// time per step).
 int take_gen(Eng* E, Eng::GenWindow* w) {
   if (E->gen_free.empty()) return 0;
   *w = std::move(E->gen_free.front());
   E->gen_free.erase(E->gen_free.begin());
-  if (w->retired_call && E->sim_calls < w->retired_call + 2) {
+  if (w->retired_call && E->sim_calls < w->retired_call + E->emit_sets) {
     HIPCHK(hipStreamWaitEvent(E->st, E->ev_dst, 0));
     HIPCHK(hipStreamWaitEvent(E->st, E->ev_rt, 0));
   }
@@ -2216,7 +2217,7 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   // out-neighbour (the 1M-peer flood's peak windows offer ~30 packets per peer), so no window of the
   // flood reallocates (each hipFree + hipMalloc stalls the closed loop for 0.3-0.5 ms)
   const size_t reserve = static_cast<size_t>(E->S) * g->degree * 4;  // the flood's peak: ~30 per peer
-  while (E->gen_free.size() < 3) E->gen_free.emplace_back();  // three in rotation (take_gen)
+  while (E->gen_free.size() < E->emit_sets + 1) E->gen_free.emplace_back();  // in rotation (take_gen)
   for (auto& w : E->gen_free) {
     HIPCHK(w.off.ensure(E->S + 1));
     HIPCHK(w.in.ensure(reserve));
