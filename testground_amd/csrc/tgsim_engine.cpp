@@ -1046,13 +1046,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   // the local delivery or routing two steps back read this emit pair
   HIPCHK(hipStreamWaitEvent(E->st, E->ev_local, 0));
   HIPCHK(E->d_emit.ensure(emit_cap));
-  // [S, S + S/256]: a bucketed window's per-block flags (sources that wrote emit records), cleared by
-  // the delivery's scatter as it reads them; zero when allocated
-  const size_t n_emit_n = static_cast<size_t>(E->S) + E->S / 256 + 1;
-  if (E->d_emit_n.cap < n_emit_n) {
-    HIPCHK(E->d_emit_n.ensure(n_emit_n));
-    HIPCHK(hipMemsetAsync(E->d_emit_n.p, 0, sizeof(uint32_t) * E->d_emit_n.cap, E->st));
-  }
+  HIPCHK(E->d_emit_n.ensure(E->S));
   SimArgs a = base_sim_args(E);
   a.off = E->d_off.p;
   a.in = E->d_in.p;
@@ -1099,7 +1093,6 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
       a.bkt_log = bucket_log(E->n_in, E->N);
       E->el.bkt = a.dst_bkt;
       E->el.bkt_log = a.bkt_log;
-      E->el.bflag = E->d_emit_n.p + E->S;
     }
   }
   if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard

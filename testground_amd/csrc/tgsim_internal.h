@@ -193,9 +193,6 @@ struct EmitRead {
   // in the emit records above (which hold only the others; the delivery reads both)
   const tgsim_delivery* bkt;
   uint32_t bkt_log, _pad;
-  // with bkt: one word per 256 sources, set by the simulate kernels when one of them wrote emit
-  // records, cleared by the scatter that reads them (emit_n + n_src)
-  uint32_t* bflag;
   // a bounded local delivery of a bucketed window: the readers check the window's exact total (on the
   // device) against the buffers' bound themselves and write nothing past it (no k_deliver_guard)
   const uint64_t* guard_total;

@@ -1487,10 +1487,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.serve_until(a.horizon_ns);
   QCHECK(4);
   PROF_ADD(13, e);
-  if (lane == 0) {
-    a.emit_n[s] = Q.n_emit;
-    if (kList && a.dst_bkt && Q.n_emit) a.emit_n[a.n_src + (s >> 8)] = 1u;  // (bkt_block_flag)
-  }
+  if (lane == 0) a.emit_n[s] = Q.n_emit;
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   uint32_t next_ticket = 0;
   if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
@@ -1928,7 +1925,6 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     ns_.last_reo = st.last_reo;
     a.state[s] = ns_;
     a.emit_n[s] = emitted;
-    if (a.dst_bkt && emitted) a.emit_n[a.n_src + (s >> 8)] = 1u;  // (bkt_block_flag)
   }
   // ---- statistics
   const uint64_t t_bytes = wave_sum(bytes);
@@ -2350,7 +2346,6 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     ns_.last_reo = st.last_reo;
     a.state[s] = ns_;
     a.emit_n[s] = emitted;
-    if (a.dst_bkt && emitted) a.emit_n[a.n_src + (s >> 8)] = 1u;  // (bkt_block_flag)
   }
   if (staged) a.verdict[sbeg + lane] = (uint8_t)vout;
   stamp(a, s, lane, 4, __builtin_amdgcn_s_memrealtime());
@@ -3187,10 +3182,6 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
                                                           uint32_t dst_begin, const uint64_t* __restrict__ doff,
                                                           uint64_t* pos, tgsim_delivery* __restrict__ out) {
   if (emit.guard_total && *emit.guard_total > emit.guard_cap) return;  // (EmitRead::guard_total)
-  // a bucketed window: the simulate kernels flagged the blocks of 256 sources that wrote emit records
-  // (the records past their destination's bucket); the others hold none (emit_n[n_src + block])
-  uint32_t* const bflag = kMode == kScatterSlot && emit.bflag ? emit.bflag + blockIdx.x : nullptr;
-  if (bflag && *bflag == 0u) return;
   const uint32_t s = blockIdx.x * 256 + threadIdx.x;
   uint32_t n = 0, cap = 0;
   const tgsim_delivery* base = emit.base;  // the source's region: its first cap records
@@ -3217,10 +3208,6 @@ __global__ __launch_bounds__(256) void k_local_scatter_ls(EmitRead emit,
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u)
         if (i + u < n) out[at[u]] = r[u];
-    }
-    if (bflag) {  // every lane has read the flag: clear it for the set's next window
-      __syncthreads();
-      if (threadIdx.x == 0) *bflag = 0u;
     }
     return;
   }
