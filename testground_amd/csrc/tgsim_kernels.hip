@@ -4017,8 +4017,11 @@ static void launch_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const
                             uint64_t* err_host) {
   constexpr uint32_t per_wg = 4 * (kWave / (kC < 16 ? kC : 16));
   const uint32_t groups = (n_dst + per_wg - 1) / per_wg;
+  // 1,024 resident workgroups (four waves per SIMD): at the 1M-peer flood the sort then leaves the
+  // simulate kernels room beside it (A/B, 1M-peer gossip G pkt/s: 256 3.3, 512 5.16, 768 5.61,
+  // 1,024 5.60-5.64, 1,536 5.46, 2,048 5.46, 4,096 5.48, 8,192 5.32, one per group 5.30)
   static const int cap_wg = env_knob("TGSIM_SORT_GRID");  // A/B: 0 the default cap, < 0 one per group
-  const uint32_t grid = cap_wg < 0 ? groups : std::min<uint32_t>(groups, cap_wg > 0 ? (uint32_t)cap_wg : 4096u);
+  const uint32_t grid = cap_wg < 0 ? groups : std::min<uint32_t>(groups, cap_wg > 0 ? (uint32_t)cap_wg : 1024u);
   hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3(grid), dim3(256), 0, st, bkt, sc, doff, n_dst, out, total, cap, err_host);
 }
 void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,
