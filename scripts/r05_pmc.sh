@@ -23,7 +23,7 @@ for v in ${VARIANTS:-cur}; do
     TGSIM_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $O/p$i -o run -- python3 bench.py $B > $O/p$i.log 2>&1 || { echo "$v pass $i failed"; tail -5 $O/p$i.log; exit 1; }
   done
   python scripts/pmc_summary.py $O $STEPS $PEERS $LAM $WIN $SH > $O/pmc_k_sim.json
-  python scripts/pmc_delivery.py $O $STEPS $PEERS $LAM $WIN $SH > $O/pmc_delivery.json
+  python scripts/pmc_delivery.py $O $STEPS $PEERS $LAM $WIN $SH $([ $WL = storm ] && echo 8) > $O/pmc_delivery.json
   python - $O <<'PY'
 import json, sys
 o = sys.argv[1]
