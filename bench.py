@@ -203,8 +203,9 @@ def cpu_baseline(a, workload, peers_total, lam, window, cpu_seconds, shapes=None
         busy, steps = 0.0, 0
         while busy < seconds:
             if workload == "epochs" and steps:
+                plan = workloads.epoch_plan(peers_total, steps)  # (ahead of the timing, as on the GPU leg)
                 r0 = time.perf_counter()
-                workloads.epoch_reshape(e, peers_total, steps)
+                workloads.epoch_reshape(e, peers_total, steps, plan=plan)
                 busy += time.perf_counter() - r0
             e.gen_storm(lam, window)
             t0 = time.perf_counter()
@@ -486,6 +487,10 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         stepper = CommStepper(eng, bounds, device="cpu")  # the id crosses the gloo host group
     step = eng.step if stepper is None else stepper.step
     epoch = [0]
+    plans = {}  # epochs: each epoch's reshape as its plan asks for it, computed before the timed loop
+
+    def reshape(k):
+        workloads.epoch_reshape(eng, peers_total, k, plan=plans.pop(k, None))
 
     def one_step():
         if workload == "gossip":
@@ -498,12 +503,12 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
                 # host while epoch k simulates (the step is asynchronous) and take effect at the
                 # next step; epoch 0 runs on the initial configs
                 step(window)
-                workloads.epoch_reshape(eng, peers_total, k + 1)
+                reshape(k + 1)
             else:
                 # the sharded step waits for its records, so epoch k+1's ConfigureNetwork calls
                 # are staged on the host while epoch k simulates (epoch k's were staged during
                 # epoch k-1); staged configs take effect at the next launch, after the barrier below
-                stepper.step(window, between=lambda: workloads.epoch_reshape(eng, peers_total, k + 1))
+                stepper.step(window, between=lambda: reshape(k + 1))
             state, rnd = workloads.epoch_state(k)
             eng.signal_async(state, peers)  # K7: the count stays on the device
             ok = stepper.barrier(state, rnd * peers_total) if stepper else eng.barrier_poll(state, rnd * peers_total)
@@ -522,6 +527,8 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
         settle = 0  # a flood is a transient by nature: the timed windows cover it from the start
     else:
         settle = int(a.settle_ms * 1000 / window + 0.999)
+        if workload == "epochs":  # the plan's reshape requests of the warm-up and timed epochs, ahead
+            plans.update({k: workloads.epoch_plan(peers_total, k) for k in range(settle + 1, settle + warmup + steps + 2)})
         for _ in range(settle):  # untimed: bring every netem queue to its sustained state
             eng.gen_storm(lam, window)
             one_step()

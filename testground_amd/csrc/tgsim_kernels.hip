@@ -2396,8 +2396,8 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
 #ifndef TGSIM_SPARSE_WPG
 #define TGSIM_SPARSE_WPG 1
 #endif
-#ifndef TGSIM_SPARSE_XCD
-#define TGSIM_SPARSE_XCD 0
+#ifndef TGSIM_SPARSE_XCD  // on: the 1M-peer window's simulate bytes -11 % at equal time
+#define TGSIM_SPARSE_XCD 1
 #endif
 constexpr uint32_t kSparseWpg = TGSIM_SPARSE_WPG;
 constexpr bool kSparseXcd = TGSIM_SPARSE_XCD != 0;

@@ -244,10 +244,18 @@ def epoch_selection(n_peers: int, epoch: int, frac: float = EPOCH_RESHAPE_FRAC, 
     return np.nonzero((x >> np.uint64(32)) < np.uint64(int(frac * 2**32)))[0].astype(np.uint32)
 
 
-def epoch_reshape(eng, n_peers: int, epoch: int, seed: int = SEED) -> int:
-    """Fresh C3-style shapes for the epoch's selected peers; every shard receives every call."""
+def epoch_plan(n_peers: int, epoch: int, seed: int = SEED) -> Tuple[np.ndarray, np.ndarray]:
+    """What epoch `epoch`'s plan asks for: the reshaped peers and their fresh C3-style configs."""
     sel = epoch_selection(n_peers, epoch, seed=seed)
-    eng.configure_batch(sel, storm_configs(len(sel), (seed + 0x1000 * (epoch + 1)) & 0xFFFFFFFF))
+    return sel, storm_configs(len(sel), (seed + 0x1000 * (epoch + 1)) & 0xFFFFFFFF)
+
+
+def epoch_reshape(eng, n_peers: int, epoch: int, seed: int = SEED, plan=None) -> int:
+    """Fresh C3-style shapes for the epoch's selected peers; every shard receives every call.
+    plan: epoch_plan's output computed ahead (the bench keeps the plan's own work out of the timed
+    loop, as it does the traffic; the ConfigureNetwork calls stay in it)."""
+    sel, cfg = plan if plan is not None else epoch_plan(n_peers, epoch, seed)
+    eng.configure_batch(sel, cfg)
     return len(sel)
 
 
