@@ -311,6 +311,32 @@ def test_gossip_gpu_equals_oracle(make_oracle):
     assert 0 < b < sched, (b, sched)
 
 
+@pytest.mark.parametrize("knobs", [{"TGSIM_DST_BKT": "0"}, {"TGSIM_DST_SLOT": "0"}, {"TGSIM_EMIT_SETS": "2"},
+                                   {"TGSIM_SCAN_ON_SIM": "1"}],
+                         ids=["slot-scatter", "cursor-scatter", "two-sets", "scan-on-sim"])
+def test_gossip_delivery_layouts_equal_oracle(make_oracle, monkeypatch, knobs):
+    """The delivery layouts the engine can be switched to for A/B runs (read at
+    tgsim_create) give the default's results: every window bit-exact with the oracle, at a size
+    where destinations overflow their buckets."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    n, floods = 2000, 16
+    g, c = both(make_oracle, n, lookahead_ns=wl.GOSSIP_MIN_LAT)
+    for e in (g, c):
+        wl.configure_gossip(e, n)
+        e.gossip_init(n_floods=floods, degree=8, msg_len=1024, start_gap_ticks=500, start_tick=0)
+    w = wl.gossip_window_ticks(g)
+    for k in range(30):
+        g.gen_gossip(w)
+        c.gen_gossip(w)
+        g.step(w)
+        c.step(w)
+        assert_same(g, c, f"gossip window {k} ({knobs})")
+    assert (g.gossip_reached() == c.gossip_reached()).all()
+    if "TGSIM_DST_BKT" in knobs or "TGSIM_DST_SLOT" in knobs:
+        assert g.bucket_records() == 0
+
+
 def test_gossip_two_shards_equal_one():
     """C4 sharded: receipts are folded on the destination's shard and forwarded from there."""
     n, floods, half = 2000, 8, 1000
