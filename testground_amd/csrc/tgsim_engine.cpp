@@ -2224,6 +2224,11 @@ int tgsim_gossip_init(void* e, const tgsim_gossip* g) {
   const uint64_t emit_cap = emit_records(E, reserve, compact_layout(E, reserve, true));
   for (auto* b : {&E->d_emit, &E->d_emit_alt, &E->d_emit_alt2})
     if (b != &E->d_emit_alt2 || E->emit_sets == 3) HIPCHK(b->ensure(emit_cap));
+  // and the delivery's scatter buffer and (discarded deliveries) its output, which a window sizes by
+  // its records' bound: grown inside the flood, each growth was a hipFree + hipMalloc on the host
+  // with the device idle (0.3-0.7 ms gaps in the routed step's trace, profiles/r05/routed_trace/)
+  HIPCHK(E->d_scatter.ensure(emit_cap));
+  if (E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES) HIPCHK(E->d_sorted.ensure(emit_cap));
   E->gossip_on = true;
   return 0;
 }
