@@ -55,7 +55,7 @@ REC = 24  # sizeof(tgsim_delivery), the record an exchange moves
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=None, help="timed steps (default: storm 30, epochs 10, gossip 70 windows)")
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default: storm 30, epochs 30, gossip 70 windows)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; gossip: 0)")
     p.add_argument("--workload", default="storm", choices=["storm", "gossip", "epochs", "bridge"])
     p.add_argument("--peers", type=int, default=0,
@@ -102,7 +102,7 @@ def parse(argv=None):
     if a.workload == "gossip":
         a.window = 5000
     if a.steps is None:
-        a.steps = {"gossip": 70, "epochs": 10, "bridge": 200}.get(a.workload, 30)  # storm: amortizes the pipeline fill and drain
+        a.steps = {"gossip": 70, "epochs": 30, "bridge": 200}.get(a.workload, 30)  # storm: amortizes the pipeline fill and drain
     if a.warmup is None:
         a.warmup = 0 if a.workload == "gossip" else 3
     return a
@@ -764,7 +764,9 @@ def main(argv=None):
                 "setup_s", "roofline", "cpu_baseline")
         sub = run_workload(a, "storm", a.peers, 30, 3, 2000, STORM_OPEN_LAMBDA, world, rank, local, dist,
                            want_cpu=not a.no_cpu, split=True, shapes="open")
-        ep = run_workload(a, "epochs", 100_000, 10, 3, 1000, 0.2, world, rank, local, dist,
+        # 30 timed epochs, not 10: ten ~1.1-ms epochs made a 12-ms timed region that one host stall
+        # halved (9.7 against 17.3 G pkt/s, profiles/r05/epochs_steps/)
+        ep = run_workload(a, "epochs", 100_000, 30, 3, 1000, 0.2, world, rank, local, dist,
                           want_cpu=not a.no_cpu, split=True)
         if res is not None:
             res["at_subcapacity"] = dict({k: sub[k] for k in keys},
