@@ -55,6 +55,17 @@ static_assert(sizeof(SrcState) == 32, "SrcState must stay 32 B");
 // before a fused launch, whose bounded loads assume slot 0).
 __host__ __device__ inline uint32_t q_near(const SrcState& s) { return s.near_n & 0xFFFFu; }
 __host__ __device__ inline uint32_t q_head(const SrcState& s) { return (s.near_n >> 16) & (kHeapCap - 1); }
+// heap_n packs the items held in the source's heap array (bits 0..15) and the far items parked in
+// its timing wheel (bits 16..31, DESIGN.md §4 "Timing wheel"); both count towards the netem limit.
+__host__ __device__ inline uint32_t q_len(const SrcState& s) { return s.heap_n & 0xFFFFu; }
+__host__ __device__ inline uint32_t q_parked(const SrcState& s) { return s.heap_n >> 16; }
+__host__ __device__ inline uint32_t q_pack(uint32_t len, uint32_t parked) { return len | parked << 16; }
+// ring_n packs the departure ring's length (bits 0..15) and the slot of its head in the source's
+// kHeapCap-entry HBM ring (bits 16..25): the ring is circular in HBM, so a window reads only the head
+// entries it may release and writes only the entries it appends (DESIGN.md §4 "Departure ring").
+__host__ __device__ inline uint32_t r_len(const SrcState& s) { return s.ring_n & 0xFFFFu; }
+__host__ __device__ inline uint32_t r_head(const SrcState& s) { return (s.ring_n >> 16) & (kHeapCap - 1); }
+__host__ __device__ inline uint32_t r_pack(uint32_t len, uint32_t head) { return len | (head & (kHeapCap - 1)) << 16; }
 
 // Offered packet as staged on the device (16 B, CSR by source, ordered by (tick, seq)).
 struct alignas(16) InRec {

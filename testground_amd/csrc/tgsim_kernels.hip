@@ -419,6 +419,7 @@ struct SimQueue {
   uint32_t lane;
   uint32_t rh, rn, qn, pn;  // ring head slot, ring length, near-region length, soon-pool length
   uint32_t fn;              // far-pool length (behind the soon pool)
+  uint32_t rpush;           // entries appended to the ring this window (the ones written back)
   uint64_t B;               // near/pool boundary: near items have e < B, pool items e >= B
   uint64_t H;               // the step's horizon: every serve is before it; soon items e < H <= far
   uint64_t tat;             // HTB theoretical arrival time
@@ -535,6 +536,7 @@ struct SimQueue {
     }
     tat = readlane64(tat_after, n - 1);
     rn += n;
+    rpush += n;
     qn -= n;
     n_emit += (uint32_t)__popcll(lm);
     wave_lds_sync();
@@ -562,6 +564,7 @@ struct SimQueue {
     }
     tat = readlane64(tat_after, n - 1);
     rn += n;
+    rpush += n;
     qn -= n;
     n_emit += (uint32_t)__popcll(lm);
     wave_lds_sync();
@@ -959,6 +962,7 @@ __device__ __forceinline__ uint4 make_item(uint64_t e, uint32_t len, uint32_t fl
 // source's completion word; the consumer polls that word and reads every handed-off byte with
 // L1-bypassing sc1 buffer loads (MI355X_MICROARCH.md, "Valid forms", first row of the hand-off table).
 using v4u = unsigned int __attribute__((ext_vector_type(4)));
+using v2u = unsigned int __attribute__((ext_vector_type(2)));
 constexpr int kSc1 = 16;  // buffer cache-policy bit SC1 (gfx940+)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t region(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -974,6 +978,10 @@ __device__ __forceinline__ uint64_t ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 template <int kPol>
 __device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)off, 0, kPol);
+}
+template <int kPol>
+__device__ __forceinline__ void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, (int)off, 0, kPol);
 }
 struct StatePair {
   uint4 lo, hi;
@@ -1006,9 +1014,10 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   }
   SimQueue<kCap, kList> Q{lds, pp, lane};
   Q.rh = 0;
-  Q.rn = st.ring_n;
+  Q.rn = r_len(st);
+  Q.rpush = 0;
   Q.qn = q_near(st);
-  Q.pn = st.heap_n - q_near(st);  // the whole pool until it is split
+  Q.pn = q_len(st) - q_near(st);  // the whole pool until it is split
   Q.fn = 0;
   Q.H = a.horizon_ns;
   Q.tat = st.tat;
@@ -1017,7 +1026,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.emit = a.emit + 2 * a.off[s] + (uint64_t)(kList ? a.emit_r : kHeapCap) * s;
   if constexpr (kList) {  // at most the queue at the start plus two items per offered packet are served
     EmitOut eo = emit_out(a, s, a.off[s], a.off[s + 1]);
-    emit_claim(a, s, eo, st.heap_n + (uint32_t)(2 * (a.off[s + 1] - a.off[s])), lane);
+    emit_claim(a, s, eo, q_len(st) + q_parked(st) + (uint32_t)(2 * (a.off[s + 1] - a.off[s])), lane);
     Q.over = eo.over;
     Q.cap = eo.cap;
   }
@@ -1033,37 +1042,56 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   for (int k = 0; k < 24; ++k) Q.pf[k] = 0;
   uint64_t* pf = Q.pf;
 #endif
-  // ---- load the departure ring (compacted) and the sorted eligibility queue into LDS
+  // ---- load the head of the departure ring and the eligibility queue into LDS
+  // The ring is circular in HBM (r_head): entry k of the ring is at slot (rh0 + k) of the source's
+  // array.  Only a prefix is loaded, up to (and including) the first entry departing at or after the
+  // horizon: every release this window stops at an entry >= an offer time < horizon, so the entries
+  // behind it are never read; their LDS slots keep whatever they held (moved, never read) and they
+  // stay in HBM untouched.  The ring moves in LDS only as a whole (release, append, the two-sided
+  // merge), so the loaded entries stay the prefix.
+  const uint32_t rh0 = r_head(st), rn0 = Q.rn;
+  uint32_t rl = 0;  // ring entries loaded (a prefix)
+  uint64_t moved = 0;  // queue-state bytes this source actually moves through HBM (carry accounting)
   {
     const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     const uint4* gh = a.heap + (size_t)s * kHeapCap;
     const uint32_t rn = Q.rn, qn = Q.qn + Q.pn;
-    // every load of the ring and the queue in flight before the first LDS write (one HBM
-    // latency instead of one per 256 slots); regions of exactly rn / qn entries, so the loads
-    // past them return 0 with no memory access (branch-free: a conditional load made the compiler
+    // every load of the ring's first chunk and the queue in flight before the first LDS write (one
+    // HBM latency instead of one per 256 slots); a queue region of exactly qn entries, so the loads
+    // past it return 0 with no memory access (branch-free: a conditional load made the compiler
     // wait for each chunk inside its branch)
-    uint64_t rv[kCap / kWave];
+    uint64_t rv0;
     uint4 qv[kCap / kWave];
     if constexpr (kBounded) {
-      const auto rr = region(gr, 8u * rn), rq = region(gh, 16u * qn);
+      const auto rr = region(gr, 8u * kHeapCap), rq = region(gh, 16u * qn);
+      rv0 = ld8<kPol>(rr, 8u * ((rh0 + (lane < rn ? lane : 0u)) & (kHeapCap - 1)));
 #pragma unroll
-      for (uint32_t u = 0; u < kCap / kWave; ++u) {
-        const uint32_t k = u * kWave + lane;
-        rv[u] = ld8<kPol>(rr, 8u * k);
-        qv[u] = ld16<kPol>(rq, 16u * k);
-      }
+      for (uint32_t u = 0; u < kCap / kWave; ++u) qv[u] = ld16<kPol>(rq, 16u * (u * kWave + lane));
     } else {  // a lane past the end re-reads the last entry (the same line as its neighbours)
-      const uint32_t rl = rn ? rn - 1 : 0, ql = qn ? qn - 1 : 0, qh = q_head(st);
+      const uint32_t ql = qn ? qn - 1 : 0, qh = q_head(st);
+      rv0 = gr[(rh0 + (lane < rn ? lane : 0u)) & (kHeapCap - 1)];
 #pragma unroll
       for (uint32_t u = 0; u < kCap / kWave; ++u) {
         const uint32_t k = u * kWave + lane;
-        rv[u] = gr[k < rn ? k : rl];
         qv[u] = gh[(qh + (k < qn ? k : ql)) & (kHeapCap - 1)];
       }
     }
     // every load issued before the partition's ballots, which the scheduler would otherwise
     // interleave with them (one HBM round trip per chunk)
     __builtin_amdgcn_sched_barrier(0);
+    rl = rn < kWave ? rn : kWave;
+    if (lane < rl) *reinterpret_cast<uint2*>(&lds.slot[lane]) = make_uint2((uint32_t)rv0, (uint32_t)(rv0 >> 32));
+    // more of the ring only while no loaded entry departs at or after the horizon (rare: a fast link
+    // releasing more than 64 entries in one window)
+    for (bool stop = __ballot(lane < rl && rv0 >= Q.H) != 0; !stop && rl < rn; rl = rl + kWave < rn ? rl + kWave : rn) {
+      const uint32_t k = rl + lane;
+      uint64_t v = ~0ull;
+      if constexpr (kBounded) v = ld8<kPol>(region(gr, 8u * kHeapCap), 8u * ((rh0 + k) & (kHeapCap - 1)));
+      else if (k < rn) v = gr[(rh0 + k) & (kHeapCap - 1)];
+      if (k < rn) *reinterpret_cast<uint2*>(&lds.slot[k]) = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+      stop = __ballot(k < rn && v >= Q.H) != 0;
+    }
+    moved = 8ull * rl + 16ull * qn;
     // the pool (queue items near_n .. qn) splits into the soon part (e < H), placed from the pool's
     // front, and the far part, placed from its back (no order in either): one pass
     const uint32_t nq = Q.qn;
@@ -1072,7 +1100,6 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
 #pragma unroll
     for (uint32_t u = 0; u < kCap / kWave; ++u) {
       const uint32_t k = u * kWave + lane;
-      if (k < rn) *reinterpret_cast<uint2*>(&lds.slot[k]) = make_uint2((uint32_t)rv[u], (uint32_t)(rv[u] >> 32));
       const bool pool = k >= nq && k < qn;
       const bool soon = pool && (w0_of(qv[u]) & kEMask) < Q.H;
       const uint64_t msn = __ballot(soon), mfr = __ballot(pool && !soon);
@@ -1100,10 +1127,10 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   // into the statistics every 2^14 batches (at most 2 counts per lane and batch), before a field
   // can overflow
   unsigned long long* const sc = a.stats + (size_t)(wg % kStatCopies) * kStSlots;
-  if (lane == 0 && (Q.qn | Q.pn | Q.fn | Q.rn)) {  // the queue state at the start (the end's is added there)
-    const unsigned long long b0 = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
-    atomicAdd(&sc[kStQueue], b0);  // the per-window model (bit-exact with the oracle)
-  }
+  // the per-window model of the queue state (a load of all of it here and a store at the end;
+  // bit-exact with the oracle): the carry accounting subtracts what the window really moved
+  const uint64_t b0 = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
+  if (lane == 0 && b0) atomicAdd(&sc[kStQueue], (unsigned long long)b0);
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
   auto flush_verdicts = [&]() {
@@ -1492,19 +1519,20 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   uint32_t next_ticket = 0;
   if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
   {
-    // ---- write back the compacted ring (16-B stores, two entries each), the queue (near, then
-    // pool) and the state
+    // ---- write back the ring entries appended this window (the others are in HBM already: the
+    // head moves past the released ones), the queue (near, then pool) and the state
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     uint4* gh = a.heap + (size_t)s * kHeapCap;
-    if constexpr (kH) {  // 16-B write-through stores (two ring entries per store)
+    const uint32_t r_new = Q.rpush < Q.rn ? Q.rpush : Q.rn;             // the ring's last r_new entries
+    const uint32_t rh1 = (rh0 + rn0 + Q.rpush - Q.rn) & (kHeapCap - 1);  // head after the releases
+    moved += 8ull * r_new + 16ull * (Q.qn + Q.pn + Q.fn);
+    if constexpr (kH) {  // write-through stores
       const auto rr = region(gr, kHeapCap * 8u), rq = region(gh, kHeapCap * 16u);
-      for (uint32_t k = lane; 2 * k < Q.rn; k += kWave) {
-        const uint64_t d0 = Q.ring_d(2 * k), d1 = Q.ring_d(2 * k + 1);
-        st16<kSc1>(rr, 16u * k, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)));
-      }
+      for (uint32_t k = Q.rn - r_new + lane; k < Q.rn; k += kWave)
+        st8<kSc1>(rr, 8u * ((rh1 + k) & (kHeapCap - 1)), Q.ring_d(k));
       for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) st16<kSc1>(rq, 16u * k, Q.slot(Q.rn + k));
     } else {
-      for (uint32_t k = lane; k < Q.rn; k += kWave) gr[k] = Q.ring_d(k);
+      for (uint32_t k = Q.rn - r_new + lane; k < Q.rn; k += kWave) gr[(rh1 + k) & (kHeapCap - 1)] = Q.ring_d(k);
       for (uint32_t k = lane; k < Q.qn + Q.pn + Q.fn; k += kWave) gh[k] = Q.slot(Q.rn + k);  // near, then pool
     }
     uint32_t near_out = Q.qn;
@@ -1522,9 +1550,9 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     if (lane == 0) {
       SrcState ns;
       ns.tat = Q.tat;
-      ns.heap_n = Q.qn + Q.pn + Q.fn;
+      ns.heap_n = q_pack(Q.qn + Q.pn + Q.fn, 0);
       ns.near_n = near_out;
-      ns.ring_n = Q.rn;
+      ns.ring_n = r_pack(Q.rn, rh1);
       ns.last_dup = last_dup;
       ns.last_cor = last_cor;
       ns.last_reo = last_reo;
@@ -1562,6 +1590,9 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     if (lost) atomicAdd(&sc[kStLost], (unsigned long long)lost);
     if (bytes) atomicAdd(&sc[kStBytes], (unsigned long long)bytes);
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
+    // what the model charged and the window did not move (wraps below zero when it moved more: the
+    // readers sum modulo 2^64)
+    if (b0 + qbytes != moved) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(b0 + qbytes - moved));
     if (err) {
       atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
       if (a.err_host)  // the host's pinned copy (sticky; read at its sync points)
@@ -1717,7 +1748,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
   const SrcParams pp = a.params[s];
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const uint32_t n = (uint32_t)(send - sbeg);
-  const uint32_t rn = st.ring_n, qn = st.heap_n;
+  const uint32_t rn = r_len(st), qn = q_len(st), rh0 = r_head(st);
   auto defer = [&]() {
     if (lane == 0) a.worklist[atomicAdd(a.worklist - 4, 1u)] = s;
   };
@@ -1736,7 +1767,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
 #pragma unroll
   for (uint32_t u = 0; u < kSparseQ; ++u) {
     const uint32_t k = u * kWave + lane;
-    rg[u] = k < rn ? gr[k] : ~0ull;
+    rg[u] = k < rn ? gr[(rh0 + k) & (kHeapCap - 1)] : ~0ull;
   }
   const uint4 qt = qn ? gh[(qh + qn - 1) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
   const bool src_on = a.enabled[src] != 0;
@@ -1855,12 +1886,8 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
       }
     }
   }
-#pragma unroll
-  for (uint32_t u = 0; u < kSparseQ; ++u) {
-    const uint32_t k = u * kWave + lane;
-    if (k < rn && k >= k0) wr[k - k0] = rg[u];
-  }
-  const uint32_t old_kept = rn - k0;
+  // the kept old entries stay where they are in HBM: the head moves past the released ones
+  const uint32_t old_kept = rn - k0, rh1 = (rh0 + k0) & (kHeapCap - 1);
   // ---- in place: the served prefix (a due candidate means the whole queue is due) leaves by moving
   // the head slot; the candidates not served are already behind the tail
   const uint32_t new_head = (qh + nq + n_due) & (kHeapCap - 1);
@@ -1911,15 +1938,15 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
         releasing = n1 == kWave;
       }
     }
-    if (hs && k >= sk0) wr[old_kept + k - sk0] = d;
+    if (hs && k >= sk0) wr[(rh1 + old_kept + k - sk0) & (kHeapCap - 1)] = d;
   }
   const uint32_t rn_new = old_kept + ns_all - sk0;
   if (lane == 0) {
     SrcState ns_;
     ns_.tat = tat_c;
-    ns_.heap_n = wpos;
+    ns_.heap_n = q_pack(wpos, 0);
     ns_.near_n = wpos | new_head << 16;  // sorted in place
-    ns_.ring_n = rn_new;
+    ns_.ring_n = r_pack(rn_new, rh1);
     ns_.last_dup = st.last_dup;
     ns_.last_cor = st.last_cor;
     ns_.last_reo = st.last_reo;
@@ -1934,7 +1961,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     const uint64_t qb = 16ull * qn + 8ull * rn + 16ull * wpos + 8ull * rn_new;
     // HBM items of the queue this step touched: the due prefix read, the tail item, the appended ones
     const uint32_t q_moved = nq + (qn ? 1u : 0u) + nc - n_due;
-    const uint64_t q_kept = qn + wpos > q_moved ? 16ull * (qn + wpos - q_moved) : 0ull;
+    const uint64_t q_kept = (qn + wpos > q_moved ? 16ull * (qn + wpos - q_moved) : 0ull) + 8ull * old_kept;
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (sched_n) atomicAdd(&sc[kStScheduled], (unsigned long long)sched_n);
@@ -1984,7 +2011,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const SrcState st = a.state[s];
   const uint64_t sbeg = a.off[s], send = a.off[s + 1];
   const uint32_t n = (uint32_t)(send - sbeg);
-  const uint32_t rn = st.ring_n, qn = st.heap_n;
+  const uint32_t rn = r_len(st), qn = q_len(st), rh0 = r_head(st);
   auto defer = [&](uint32_t why) {
     if (lane == 0) a.worklist[atomicAdd(a.worklist - 4, 1u)] = s;
 #ifdef TGSIM_DEFER_STATS  // diagnostic build: deferrals by reason, behind the list
@@ -2035,7 +2062,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   uint4 q[kSparseQ];
   uint64_t rg[kSparseQ];
   q[0] = lane < qn ? gh[(qh + lane) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
-  rg[0] = lane < rn ? gr[lane] : ~0ull;
+  rg[0] = lane < rn ? gr[(rh0 + lane) & (kHeapCap - 1)] : ~0ull;
   auto load_rest = [&]() {
 #pragma unroll
     for (uint32_t u = 1; u < kSparseQ; ++u) {
@@ -2054,7 +2081,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
 #pragma unroll
   for (uint32_t u = 1; u < kSparseQ; ++u) {
     const uint32_t k = u * kWave + lane;
-    rg[u] = k < rn ? gr[k] : ~0ull;
+    rg[u] = k < rn ? gr[(rh0 + k) & (kHeapCap - 1)] : ~0ull;
   }
   InRec r = {};
   const bool staged = lane < n;
@@ -2140,8 +2167,9 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   // soon as the source is known not to defer.
   uint64_t* wr = a.ring + (size_t)s * kHeapCap;
   uint32_t old_kept = rn;     // old entries still in the ring
+  uint32_t rh1 = rh0;         // the ring's head slot after the release
   bool ring_stop = T_enq == 0;  // the release stopped inside the old ring (or nothing was released)
-  auto write_old_ring = [&]() {
+  auto write_old_ring = [&]() {  // (the kept old entries stay in place in HBM: only the head moves)
     uint32_t k0 = 0;
     if (T_enq) {
 #pragma unroll
@@ -2158,12 +2186,8 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
         }
       }
     }
-#pragma unroll
-    for (uint32_t u = 0; u < kSparseQ; ++u) {
-      const uint32_t k = u * kWave + lane;
-      if (k < rn && k >= k0) wr[k - k0] = rg[u];
-    }
     old_kept = rn - k0;
+    rh1 = (rh0 + k0) & (kHeapCap - 1);
   };
   // ---- FIFO sources (no jitter, no reordering, no duplicates: gossip): the stored queue is sorted
   // (a whole near region) and the new items, in offer order, are sorted and not before its last
@@ -2325,7 +2349,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
         releasing = n1 == kWave;
       }
     }
-    if (hs && base + lane >= sk0) wr[old_kept + base + lane - sk0] = d;
+    if (hs && base + lane >= sk0) wr[(rh1 + old_kept + base + lane - sk0) & (kHeapCap - 1)] = d;
     if (base + kWave >= ns_all) break;
     // the next round (FIFO): the queue's due items from HBM, then the due candidates
     const uint32_t nb = base + kWave, k = nb + lane;
@@ -2338,9 +2362,9 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   if (lane == 0) {
     SrcState ns_;
     ns_.tat = tat_c;
-    ns_.heap_n = wpos;
+    ns_.heap_n = q_pack(wpos, 0);
     ns_.near_n = fifo ? wpos | new_head << 16 : 0;  // sorted in place (FIFO), or all of it pool, compacted
-    ns_.ring_n = rn_new;
+    ns_.ring_n = r_pack(rn_new, rh1);
     ns_.last_dup = st.last_dup;
     ns_.last_cor = st.last_cor;
     ns_.last_reo = st.last_reo;
@@ -2366,7 +2390,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   if (lane == 0) {
     const uint64_t qb = 16ull * qn + 8ull * rn + 16ull * wpos + 8ull * rn_new;
     // the per-window model counts the whole queue loaded and stored; the FIFO path left most of it
-    const uint64_t q_kept = fifo && qn + wpos > q_moved ? 16ull * (qn + wpos - q_moved) : 0ull;
+    const uint64_t q_kept = (fifo && qn + wpos > q_moved ? 16ull * (qn + wpos - q_moved) : 0ull) + 8ull * old_kept;
     if (q_kept) atomicAdd(&sc[kStCarrySkip], (unsigned long long)q_kept);
     if (n) atomicAdd(&sc[kStOffered], (unsigned long long)n);
     if (t_sched) atomicAdd(&sc[kStScheduled], (unsigned long long)t_sched);
@@ -2480,7 +2504,7 @@ __global__ void k_apply_cfg(const CfgPatch* __restrict__ patches, uint32_t n, Sr
   if (c.mask & 4u) st.last_reo = c.last_reo;
   if (c.mask & 8u) st.tat = 0;
   if (c.mask & 16u) {
-    const uint32_t k = st.heap_n + st.ring_n;
+    const uint32_t k = q_len(st) + q_parked(st) + r_len(st);
     if (k) atomicAdd(&stats[(size_t)(i % kStatCopies) * kStSlots + kStFlushed], (unsigned long long)k);
     st.heap_n = st.ring_n = st.near_n = 0;
   }
@@ -2497,7 +2521,7 @@ __global__ __launch_bounds__(256) void k_unrotate(uint4* heap, SrcState* state, 
   const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (s >= n_src) return;
   SrcState st = state[s];
-  const uint32_t qh = q_head(st), qn = st.heap_n;
+  const uint32_t qh = q_head(st), qn = q_len(st);
   if (!qh) return;
   uint4* q = heap + (size_t)s * kHeapCap;
   uint4 v[kHeapCap / kWave];
@@ -2520,7 +2544,7 @@ __global__ __launch_bounds__(256) void k_purge(uint4* heap, const SrcState* stat
   const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (s >= n_src) return;
   const SrcState st = state[s];
-  const uint32_t qn = st.heap_n, qh = q_head(st);
+  const uint32_t qn = q_len(st), qh = q_head(st);
   uint4* q = heap + (size_t)s * kHeapCap;
   for (uint32_t k = lane; k < qn; k += kWave) {
     const uint32_t j = (qh + k) & (kHeapCap - 1);
@@ -3657,7 +3681,7 @@ __global__ __launch_bounds__(256) void k_metrics_src(MetricsArgs m) {
     row[10] += n_emit;
     row[11] += ts;
     const SrcState st = m.state[s];
-    atomicAdd(&m.hist[log2_bin((uint64_t)st.heap_n + st.ring_n)], 1ull);
+    atomicAdd(&m.hist[log2_bin((uint64_t)q_len(st) + q_parked(st) + r_len(st))], 1ull);
   }
 }
 
