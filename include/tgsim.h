@@ -338,7 +338,9 @@ int tgsim_comm_barrier(void* engine, uint32_t state, uint64_t target);
 /* Every host wait of tgsim_comm_{step,finish,run,barrier} on a peer rank is bounded by
  * TGSIM_COMM_TIMEOUT_MS (read at tgsim_comm_init; default 300000): a rank whose peer stopped gets
  * -ETIMEDOUT naming the window, and every later tgsim_comm_* call on that engine fails the same way;
- * tgsim_destroy then aborts the communicator (ncclCommAbort) instead of waiting on it. */
+ * tgsim_destroy then aborts the communicator (ncclCommAbort) instead of waiting on it; with an RCCL
+ * that has no ncclCommAbort it leaves the communicator, its stream and buffers allocated (a message on
+ * stderr) rather than wait forever. */
 typedef struct {
     int32_t rank, nranks;
     uint64_t exchanged_records; /* records (slotted: record slots) this rank has sent, self included */

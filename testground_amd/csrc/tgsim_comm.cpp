@@ -232,6 +232,13 @@ void comm_free(void* p) {
     (void)C->R->CommAbort(C->nc);
     C->nc = nullptr;
   }
+  if (C->timed_out && C->nc) {
+    // no ncclCommAbort in this RCCL: the stream would never drain and a destroy would wait for it, so
+    // the communicator, its stream and the buffers its kernels may still touch are left behind
+    fprintf(stderr, "tgsim: communicator of rank %d leaked after a timed-out exchange (no ncclCommAbort)\n", C->rank);
+    delete C;
+    return;
+  }
   if (C->xs) (void)hipStreamSynchronize(C->xs);
   if (C->nc) (void)C->R->CommDestroy(C->nc);
   for (auto& b : C->out) b.release();

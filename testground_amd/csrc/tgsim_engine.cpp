@@ -171,6 +171,13 @@ struct DevBuf {
     if (e == hipSuccess) cap = c;
     return e;
   }
+  hipError_t ensure_exact(size_t n) {  // no growth headroom (buffers sized once)
+    if (n <= cap) return hipSuccess;
+    release();
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -282,6 +289,9 @@ struct tgsim_engine_s {
   DevBuf<Interval> d_rules;
   DevBuf<uint4> d_heap;
   DevBuf<uint64_t> d_ring;
+  DevBuf<uint4> d_wheel;       // timing wheel: [s][kWheelB][kWheelCB] parked far items
+  DevBuf<WheelMeta> d_wmeta;   // [s] bucket counts, base id, width (read only while items are parked)
+  bool wheel_failed = false;   // no memory for the wheel: dense windows run without parking
   DevBuf<CfgPatch> d_patch;
   DevBuf<uint32_t> d_gen_seq;
 
@@ -631,7 +641,7 @@ int flush_config(Eng* E) {
   if (E->any_gone) {  // packets queued towards a removed link: marked dead in every sender's queue
     HIPCHK(E->d_gone.ensure(E->N));
     HIPCHK(hipMemcpyAsync(E->d_gone.p, E->gone.data(), E->N, hipMemcpyHostToDevice, E->st));
-    launch_purge(E->d_heap.p, E->d_state.p, E->S, E->d_gone.p, E->st);
+    launch_purge(E->d_heap.p, E->d_wheel.p, E->d_wmeta.p, E->d_state.p, E->S, E->d_gone.p, E->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(E->st));
     std::fill(E->gone.begin(), E->gone.end(), 0);
@@ -842,6 +852,22 @@ int sync_stream(Eng* E) {
   return harvest_timing(E, true);
 }
 
+// The timing wheel, allocated at the first dense window: sparse windows never park
+// items (k_sim_sparse defers a source with parked items to k_sim_list, which takes them all back), so
+// an engine that only runs sparse windows never pays its 64 KiB per source; a gossip flood never parks
+// (its dense windows would send their sources through k_sim_list afterwards).  No memory for it: the
+// dense windows run without parking (every far item stays in the heap array).
+void ensure_wheel(Eng* E) {
+  if (E->d_wheel.p || E->wheel_failed || E->gossip_on) return;
+  if (E->d_wheel.ensure_exact(static_cast<size_t>(E->S) * kWheelB * kWheelCB) != hipSuccess ||
+      E->d_wmeta.ensure_exact(E->S) != hipSuccess) {
+    (void)hipGetLastError();
+    E->d_wheel.release();
+    E->d_wmeta.release();
+    E->wheel_failed = true;
+  }
+}
+
 // The step-independent part of k_sim's arguments (tables, state, statistics, keys).
 SimArgs base_sim_args(Eng* E) {
   SimArgs a{};
@@ -852,6 +878,8 @@ SimArgs base_sim_args(Eng* E) {
   a.rules = E->d_rules.p;
   a.heap = E->d_heap.p;
   a.ring = E->d_ring.p;
+  a.wheel = E->d_wheel.p;
+  a.wmeta = E->d_wmeta.p;
   a.stats = E->d_stats.p;
   a.key0 = E->key0;
   a.key1 = E->key1;
@@ -972,7 +1000,10 @@ bool sparse_choice(Eng* E, uint64_t n_in, bool commit) {
   // behind it, read without waiting) decides; every 64th such step runs sparse again to re-measure
   if (E->next_sparse >= 0 && E->next_sparse_n == n_in) {
     const bool sp = E->next_sparse == 1;
-    if (commit) E->next_sparse = -1;
+    if (commit) {  // the choice made ahead (tgsim_sim_capacity) commits like a fresh one
+      E->next_sparse = -1;
+      E->dense_streak = sp ? 0 : E->dense_streak + 1;
+    }
     return sp;
   }
   const uint32_t deferred = __atomic_load_n(E->h_work, __ATOMIC_RELAXED);
@@ -1040,6 +1071,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   int rc = flush_config(E);
   if (rc) return rc;
   const bool sparse = sparse_choice(E, E->n_in, true);
+  if (!sparse) ensure_wheel(E);
   const bool compact = compact_layout(E, E->n_in, sparse);
   const uint64_t emit_cap = emit_records(E, E->n_in, compact);
   HIPCHK(E->d_verdict.ensure(E->n_in ? E->n_in : 1));
@@ -1585,6 +1617,7 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
     HIPCHK(hipMemsetAsync(E->d_ticket.p, 0, sizeof(uint32_t), E->st));
     E->step_no = E->ticket_no = 0;
   }
+  ensure_wheel(E);
   SimArgs a = base_sim_args(E);
   const bool ordered = E->S <= kOrderMaxSources;
   a.order = ordered && E->order_valid ? E->d_order.p : nullptr;
@@ -2041,7 +2074,7 @@ void tgsim_destroy(void* e) {
   DevBuf<int> dummy;
   (void)dummy;
   E->d_params.release(); E->d_state.release(); E->d_enabled.release(); E->d_ip.release();
-  E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_patch.release();
+  E->d_rules.release(); E->d_heap.release(); E->d_ring.release(); E->d_wheel.release(); E->d_wmeta.release(); E->d_patch.release();
   E->d_gen_seq.release(); E->d_off.release(); E->d_cnt.release(); E->d_blk.release(); E->d_tot.release();
   E->d_in.release(); E->d_verdict.release(); E->d_emit.release(); E->d_emit_n.release(); E->d_emit_alt.release(); E->d_emit_n_alt.release(); E->d_lcnt.release(); E->d_lcnt_alt.release(); E->d_dbkt.release(); E->d_dbkt_alt.release(); E->d_sdoff.release(); E->d_sdpos.release(); E->d_sdblk.release(); E->d_sdtot.release(); E->d_sdoff_alt.release(); E->d_sdpos_alt.release(); E->d_sdblk_alt.release(); E->d_sdtot_alt.release(); E->d_sdoff_alt2.release(); E->d_sdpos_alt2.release(); E->d_sdblk_alt2.release(); E->d_sdtot_alt2.release(); E->d_emit_alt2.release(); E->d_emit_n_alt2.release(); E->d_lcnt_alt2.release(); E->d_dbkt_alt2.release(); E->d_pidx.release(); E->d_pidx_alt.release(); E->d_pidx_alt2.release(); E->d_rcnt.release(); E->d_rpos.release(); E->d_rblk.release(); E->d_rtot.release();
   E->d_bucket.release(); E->d_scatter.release(); E->d_sorted.release(); E->d_dcnt.release();

@@ -67,6 +67,24 @@ __host__ __device__ inline uint32_t r_len(const SrcState& s) { return s.ring_n &
 __host__ __device__ inline uint32_t r_head(const SrcState& s) { return (s.ring_n >> 16) & (kHeapCap - 1); }
 __host__ __device__ inline uint32_t r_pack(uint32_t len, uint32_t head) { return len | (head & (kHeapCap - 1)) << 16; }
 
+// Timing wheel: a source's far netem items (eligible at or after the window's
+// horizon) parked in HBM by eligibility time, so that a window reads only the buckets coming due
+// and writes only the items it parks, instead of carrying the whole queue through LDS.  Bucket j of
+// source s covers eligibility times [id << g, (id + 1) << g) for the one id = base + ((j - base) mod
+// kWheelB) in [base, base + kWheelB); it holds up to kWheelCB items, unordered.  Parked items are
+// queued items like any other (netem limit, flush, purge); they are only kept out of LDS.
+constexpr uint32_t kWheelB = 64;   // buckets per source (one per lane)
+constexpr uint32_t kWheelCB = 64;  // items per bucket (one per lane)
+constexpr uint32_t kWheelGMin = 14, kWheelGMax = 40;  // bucket width 2^g ns (g >= 14: ids fit 32 bits)
+struct alignas(16) WheelMeta {
+  uint16_t cnt[kWheelB];  // items in each bucket (valid only while the state's q_parked() > 0)
+  uint32_t base;          // lowest bucket id that may hold items
+  uint32_t ctl;           // bits 0..7 g; bit 8 rebuild (the next window loads every bucket);
+                          // bits 16..31 windows before another rebuild may be asked for
+  uint32_t _pad[2];
+};
+static_assert(sizeof(WheelMeta) == 144, "WheelMeta");
+
 // Offered packet as staged on the device (16 B, CSR by source, ordered by (tick, seq)).
 struct alignas(16) InRec {
   uint32_t dst;
@@ -156,10 +174,12 @@ struct SimArgs {
   // with no atomic (kSlotShift, EmitRead::slot)
   uint32_t emit_r : 24, bkt_log : 7, dst_slot : 1;  // bkt_log: log2 of a bucket's records (dst_bkt)
   uint32_t emit_pool_cap;
-  // sizeof(SimArgs) 264, not 256: at exactly 256 B (kernarg windows k * 256) the scheduler spilled
-  // 9 more SGPRs in k_sim_fused (155 -> 164)
+  // the timing wheel (WheelMeta): [s][kWheelB][kWheelCB] parked items and [s] bucket counts
+  uint4* wheel;
+  WheelMeta* wmeta;
+  // (at exactly 256 B, kernarg windows k * 256, the scheduler had spilled 9 more SGPRs in k_sim_fused)
 };
-static_assert(sizeof(SimArgs) == 264, "SimArgs must stay 264 B");
+static_assert(sizeof(SimArgs) == 280, "SimArgs layout");
 constexpr uint32_t kStampSlots = 32;  // 8 phase stamps + 24 profile counters (TGSIM_PROFILE)
 
 // Fused launch of up to kFuseMax consecutive windows (k_sim_fused).  Window-major:

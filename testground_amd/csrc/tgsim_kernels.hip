@@ -92,6 +92,9 @@ __device__ __forceinline__ bool item_lt(const uint4& a, const uint4& b) {
 template <uint32_t kCap>
 struct SimLdsT {
   uint4 slot[kCap];         // circular: departure ring, then the eligibility queue (near, pool)
+  uint32_t wcnt[kWheelB];   // the timing wheel's bucket counts while far items are parked
+  uint32_t whdr[4];         // and its base id, control word, due items loaded (kept here, not in
+                            // registers, from the window's start to its end)
 };
 static_assert(sizeof(SimLdsT<kHeapCap>) <= 65536, "simulate workgroup LDS");
 
@@ -419,6 +422,7 @@ struct SimQueue {
   uint32_t lane;
   uint32_t rh, rn, qn, pn;  // ring head slot, ring length, near-region length, soon-pool length
   uint32_t fn;              // far-pool length (behind the soon pool)
+  uint32_t pk;              // far items parked in the timing wheel (not in LDS; all >= H)
   uint32_t rpush;           // entries appended to the ring this window (the ones written back)
   uint64_t B;               // near/pool boundary: near items have e < B, pool items e >= B
   uint64_t H;               // the step's horizon: every serve is before it; soon items e < H <= far
@@ -606,6 +610,11 @@ struct SimQueue {
     const uint64_t e = w0_of(it) & kEMask;
     const bool pool = has && e >= B;
     insert_near(has && !pool, it, true);
+    append_pool(pool, it);
+  }
+  // Pool items of the lanes (pool: every one >= B) appended to the soon or the far part.
+  __device__ __forceinline__ void append_pool(bool pool, const uint4& it) {
+    const uint64_t e = w0_of(it) & kEMask;
     const bool vfar = pool && e >= H;
     const uint64_t ms = __ballot(pool && !vfar), mf = __ballot(vfar);
     if (!(ms | mf)) return;
@@ -980,12 +989,34 @@ __device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, con
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)off, 0, kPol);
 }
 template <int kPol>
+__device__ __forceinline__ uint32_t ld2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, __builtin_amdgcn_raw_buffer_load_b16(r, (int)off, 0, kPol));
+}
+template <int kPol>
+__device__ __forceinline__ void st2(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (uint16_t)v), r, (int)off, 0, kPol);
+}
+template <int kPol>
 __device__ __forceinline__ void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, (int)off, 0, kPol);
 }
 struct StatePair {
   uint4 lo, hi;
 };
+
+// Bucket width of an empty timing wheel (2^g ns): the narrowest for which the source's whole delay
+// range (latency + jitter: every far item is eligible less than that past the horizon) spans at most
+// kWheelB - 2 buckets, so the wheel holds every far item as its base slides up.  At the netem limit
+// that is 16-32 items a bucket when they are spread evenly; bursts of admissions crowd some buckets,
+// hence room for kWheelCB = 64.  Only the cost depends on it: a far item that does not fit (a full
+// bucket, or a reshaped link's longer delay) stays in the heap array.
+__device__ __forceinline__ uint32_t wheel_width(uint64_t span) {
+  uint32_t g = kWheelGMin;
+  while (g < kWheelGMax && (span >> g) > kWheelB - 2) ++g;
+  return g;
+}
+constexpr uint32_t kWheelRebuildKeep = 32;  // far items left out of the wheel that ask for a rebuild
+constexpr uint32_t kWheelCooldown = 16;     // windows before the next rebuild may be asked for
 static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
 
 // One source's step (K1-K4), run by one wavefront.  kOpen: the caller has checked that the step
@@ -1012,6 +1043,18 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   } else {
     st = a.state[s];
   }
+  // the timing wheel's counts (lane j: bucket j) and header, loaded beside the state (used only when
+  // the state says items are parked; an engine without a wheel reads nothing: offsets past a buffer
+  // resource return 0 without a memory access)
+  const auto rm = region(a.wmeta + s, sizeof(WheelMeta));
+  const auto rw = region(a.wheel + (size_t)s * kWheelB * kWheelCB, kWheelB * kWheelCB * 16u);
+  constexpr uint32_t kOff = 0xFFFFFFF0u;
+  uint32_t wcnt = ld2<kPol>(rm, a.wmeta ? 2u * lane : kOff);
+  const uint4 whd = ld16<kPol>(rm, a.wmeta ? 2u * kWheelB : kOff);
+  // the offered packets' range and the source's link state with them (the records themselves are
+  // loaded with the queue: one HBM round trip less before the first batch)
+  const uint64_t sbeg = a.off[s], send = a.off[s + 1];
+  const bool src_on = a.enabled[a.shard_begin + s] != 0;
   SimQueue<kCap, kList> Q{lds, pp, lane};
   Q.rh = 0;
   Q.rn = r_len(st);
@@ -1023,13 +1066,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   Q.tat = st.tat;
   Q.src = a.shard_begin + s;
   // dense steps and fused windows: the classic layout; k_sim_list: the window's (EmitRead, emit_claim below)
-  Q.emit = a.emit + 2 * a.off[s] + (uint64_t)(kList ? a.emit_r : kHeapCap) * s;
-  if constexpr (kList) {  // at most the queue at the start plus two items per offered packet are served
-    EmitOut eo = emit_out(a, s, a.off[s], a.off[s + 1]);
-    emit_claim(a, s, eo, q_len(st) + q_parked(st) + (uint32_t)(2 * (a.off[s + 1] - a.off[s])), lane);
-    Q.over = eo.over;
-    Q.cap = eo.cap;
-  }
+  Q.emit = a.emit + 2 * sbeg + (uint64_t)(kList ? a.emit_r : kHeapCap) * s;
   Q.n_emit = 0;
   Q.dcnt = a.dst_cnt;
   Q.dslot = kList && a.dst_slot;
@@ -1051,6 +1088,27 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   // merge), so the loaded entries stay the prefix.
   const uint32_t rh0 = r_head(st), rn0 = Q.rn;
   uint32_t rl = 0;  // ring entries loaded (a prefix)
+  uint64_t idx = sbeg + lane;  // the lane's next offered record
+  const uint64_t last_in = send > sbeg ? send - 1 : sbeg;
+  InRec rec = {}, rec2 = {};   // records of batches b and b + 1
+  uint32_t wbase = 0, wctl = 0, wdue = 0, nd = 0;  // wheel: base id, control word, lane j: bucket j's due count
+  uint64_t wlast = 0;                              // the last bucket id due before H
+  // due item c + lane: its bucket (from the base) is the first whose running sum exceeds it (the
+  // running sums are re-derived at each call: nothing but wdue stays live across the queue's loads)
+  auto wheel_item = [&](uint32_t c, bool& in) -> uint4 {
+    TG_FULL_EXEC("ds_bpermute");
+    const uint32_t rot = (uint32_t)__shfl((int)wdue, (int)((wbase + lane) & (kWheelB - 1)), 64);
+    const uint32_t wincl = (uint32_t)scan_sum_i32((int32_t)rot), wexcl = wincl - rot;
+    const uint32_t k = c + lane;
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t sb = kWave / 2; sb; sb >>= 1)
+      if ((uint32_t)__shfl((int)wincl, (int)(lo + sb - 1), 64) <= k) lo += sb;
+    const uint32_t j = lo & (kWheelB - 1);
+    const uint32_t idx = k - (uint32_t)__shfl((int)wexcl, (int)j, 64);
+    in = k < nd;
+    return ld16<kPol>(rw, in ? 16u * (((wbase + j) & (kWheelB - 1)) * kWheelCB + idx) : kOff);
+  };
   uint64_t moved = 0;  // queue-state bytes this source actually moves through HBM (carry accounting)
   {
     const uint64_t* gr = a.ring + (size_t)s * kHeapCap;
@@ -1076,6 +1134,30 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
         qv[u] = gh[(qh + (k < qn ? k : ql)) & (kHeapCap - 1)];
       }
     }
+    // the records of the first two batches (two batches in flight from here on); branch-free loads, a
+    // lane past the end re-reads the last record (never used): a conditional load left a wait inside
+    // its branch
+    if (send > sbeg) {
+      rec = a.in[idx < send ? idx : last_in];
+      rec2 = a.in[idx + kWave < send ? idx + kWave : last_in];
+    }
+    // the timing wheel's due buckets (every bucket for k_sim_list or a rebuild): lane j holds the
+    // running sum of the due counts of the buckets from the base up to the j-th; their items are
+    // loaded with the queue (the first 64 here, the rest after the partition)
+    if (q_parked(st)) {
+      wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)whd.x);
+      wctl = (uint32_t)__builtin_amdgcn_readfirstlane((int)whd.y);
+      const bool all = kList || (wctl >> 8 & 1u);
+      wlast = (Q.H - 1) >> (wctl & 0xFFu);
+      const bool due = all || (uint64_t)wbase + ((lane - wbase) & (kWheelB - 1)) <= wlast;
+      wdue = due ? wcnt : 0u;
+      nd = readlane32((uint32_t)scan_sum_i32((int32_t)wdue), kWave - 1);
+      wcnt = due ? 0u : wcnt;
+    } else {
+      wcnt = 0;
+    }
+    bool win0;
+    const uint4 wv0 = wheel_item(0, win0);
     // every load issued before the partition's ballots, which the scheduler would otherwise
     // interleave with them (one HBM round trip per chunk)
     __builtin_amdgcn_sched_barrier(0);
@@ -1112,9 +1194,40 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     }
     Q.pn = cs;
     Q.fn = cf;
+    // ---- the timing wheel: the due buckets' items join the pool (every parked item is >= the B of
+    // any window since it was parked); the other buckets stay parked, only counted (Q.pk)
+    Q.append_pool(win0, wv0);
   }
-  const uint64_t sbeg = a.off[s], send = a.off[s + 1];
-  const bool src_on = a.enabled[Q.src] != 0;
+  for (uint32_t c = kWave; c < nd; c += kWave) {
+    bool in;
+    const uint4 v = wheel_item(c, in);
+    Q.append_pool(in, v);
+  }
+  Q.pk = readlane32((uint32_t)scan_sum_i32((int32_t)wcnt), kWave - 1);
+  if (Q.pk && wlast > wbase) wbase = (uint32_t)wlast;  // its items >= H are parked again
+  if constexpr (kList) {
+    // records past the source's region come from the emit pool: at most the queued items eligible
+    // before the horizon (the near region and the soon pool; far items are >= H and cannot be
+    // served) plus two per offered packet
+    EmitOut eo = emit_out(a, s, sbeg, send);
+    emit_claim(a, s, eo, Q.qn + Q.pn + (uint32_t)(2 * (send - sbeg)), lane);
+    Q.over = eo.over;
+    Q.cap = eo.cap;
+  }
+  if (q_parked(st)) moved += sizeof(WheelMeta) + 16ull * nd;
+  lds.wcnt[lane] = wcnt;
+  if (lane == 0) {
+    lds.whdr[0] = wbase;
+    lds.whdr[1] = wctl;
+    lds.whdr[2] = nd;
+    lds.whdr[3] = rh0 + rn0;  // the ring's head slot after the window = this - its length + appends
+  }
+#ifndef TGSIM_PROFILE
+  stamp(a, wg, lane, 11, rl | (uint64_t)rn0 << 16);
+#endif
+#ifndef TGSIM_PROFILE
+  stamp(a, wg, lane, 10, __builtin_amdgcn_s_memrealtime());  // (diagnostics: the wheel's phase)
+#endif
   // no rules and every peer connected (the storm and gossip runs): the filter reduces to the
   // external-destination check, and the FIB/peer tables stay out of the loop's registers
   const bool plain = src_on && !a.any_disabled && pp.rule_n == 0;
@@ -1129,8 +1242,12 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   unsigned long long* const sc = a.stats + (size_t)(wg % kStatCopies) * kStSlots;
   // the per-window model of the queue state (a load of all of it here and a store at the end;
   // bit-exact with the oracle): the carry accounting subtracts what the window really moved
-  const uint64_t b0 = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
-  if (lane == 0 && b0) atomicAdd(&sc[kStQueue], (unsigned long long)b0);
+  // (the start's part of both here, the end's at the end: nothing of it held through the window)
+  {
+    const uint64_t b0 = 16ull * (Q.qn + Q.pn + Q.fn + Q.pk) + 8ull * Q.rn;
+    if (lane == 0 && b0) atomicAdd(&sc[kStQueue], (unsigned long long)b0);
+    if (lane == 0 && b0 != moved) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(b0 - moved));
+  }
   uint64_t vc_lo = 0, vc_hi = 0;
   uint32_t n_clone = 0;
   auto flush_verdicts = [&]() {
@@ -1153,17 +1270,8 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   const uint32_t n_batches = (uint32_t)((send - sbeg + kWave - 1) / kWave);
   // open queue: even if every offered packet and its clone were admitted the queue would stay
   // below the netem limit (sparse sources: gossip, ping-pong, splitbrain)
-  const bool open_q = kOpen || (!corr && (uint64_t)Q.rn + Q.qn + Q.pn + Q.fn + 2 * (send - sbeg) < lim);
+  const bool open_q = kOpen || (!corr && (uint64_t)Q.rn + Q.qn + Q.pn + Q.fn + Q.pk + 2 * (send - sbeg) < lim);
   uint64_t T_enq = 0;  // open queue: offer time of the last packet that reached the netem enqueue
-  uint64_t idx = sbeg + lane;
-  // records of batches b and b + 1 (two batches in flight); branch-free loads, a lane past the end
-  // re-reads the last record (never used): a conditional load left a wait inside its branch
-  const uint64_t last_in = send > sbeg ? send - 1 : sbeg;
-  InRec rec = {}, rec2 = {};
-  if (send > sbeg) {
-    rec = a.in[idx < send ? idx : last_in];
-    rec2 = a.in[idx + kWave < send ? idx + kWave : last_in];
-  }
   // the verdict bytes of batch b are stored during batch b + 1: stored last in their own batch,
   // their write latency sat in front of the loop's back edge (vmcnt counts stores)
   uint64_t v_idx = 0;
@@ -1244,11 +1352,11 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
       uint64_t pend = (kOpen || open_q) ? 0ull : __ballot(cand);
       if constexpr (!kOpen) while (pend) {
         PROF_CNT(3, 1);
-        if (Q.rn + Q.qn + Q.pn + Q.fn >= lim) {
+        if (Q.rn + Q.qn + Q.pn + Q.fn + Q.pk >= lim) {
           // full queue: nothing changes before the next eligibility or departure time, so every
           // packet offered up to then is a QUEUE_FULL drop (B bounds the soon pool's earliest e,
-          // H the far pool's)
-          const uint64_t qh = Q.qn ? (w0_of(Q.slot(Q.rn)) & kEMask) : Q.pn ? Q.B : Q.fn ? Q.H : ~0ull;
+          // H the far pool's and the parked items')
+          const uint64_t qh = Q.qn ? (w0_of(Q.slot(Q.rn)) & kEMask) : Q.pn ? Q.B : (Q.fn | Q.pk) ? Q.H : ~0ull;
           const uint64_t dh = Q.rn ? Q.ring_d(0) : ~0ull;
           const uint64_t t_ev = qh < dh ? qh : dh;
           const uint64_t mf = __ballot(((pend >> lane) & 1ull) && T <= t_ev);
@@ -1336,7 +1444,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
         const int32_t cnt = inw ? 1 + (cst == 2) : 0;
         const int32_t P = scan_sum_i32(cnt - delta);
         const int32_t M = scan_max_i32(P);
-        const int32_t x0 = (int32_t)(Q.rn + Q.qn + Q.pn + Q.fn), ilim = (int32_t)lim;
+        const int32_t x0 = (int32_t)(Q.rn + Q.qn + Q.pn + Q.fn + Q.pk), ilim = (int32_t)lim;
         const int32_t Pex = (int32_t)shr1_u32((uint32_t)P, 0u);
         const int32_t Mex = (int32_t)shr1_u32((uint32_t)M, 0u);  // lane 0: 0 = identity here
         const int32_t xb = Pex + min(x0, ilim - Mex);
@@ -1462,7 +1570,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
           auto enq = [&](uint32_t reo_raw, uint32_t delay_raw, uint32_t fl) -> uint32_t {
             Q.serve_until(Tj);
             Q.depart_before(Tj);
-            if (Q.rn + Q.qn + Q.pn + Q.fn >= lim) return TGSIM_V_QUEUE_FULL;
+            if (Q.rn + Q.qn + Q.pn + Q.fn + Q.pk >= lim) return TGSIM_V_QUEUE_FULL;
             bool reordered = false;
             if (pp.thr_reo) reordered = !(pp.thr_reo < crand(reo_raw, pp.rho_reo, last_reo));
             uint64_t e = reordered ? Tj : delayed(pp, Tj, delay_raw);
@@ -1518,14 +1626,91 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   stamp(a, wg, lane, 3, __builtin_amdgcn_s_memrealtime());
   uint32_t next_ticket = 0;
   if (claim && lane == 0) next_ticket = atomicAdd(claim, 1u) - claim_base;
+  // ---- park the far items in the timing wheel (k_sim_list keeps every item in the heap array: the
+  // sparse kernels that run the next windows read only that)
+  uint32_t pk_end = Q.pk;
+  uint64_t moved_end = 0;  // queue-state bytes the end of the window moves through HBM
+  if constexpr (!kList) {
+    const uint32_t fn0 = a.wheel ? Q.fn : 0u;  // (no wheel: the engine had no memory for it)
+    const auto rm = region(a.wmeta + s, sizeof(WheelMeta));
+    const auto rw = region(a.wheel + (size_t)s * kWheelB * kWheelCB, kWheelB * kWheelCB * 16u);
+    wbase = lds.whdr[0];
+    wctl = lds.whdr[1];
+    nd = lds.whdr[2];
+    wcnt = lds.wcnt[lane];
+    if (fn0) {
+      const uint32_t f0 = Q.rn + Q.qn + Q.pn;
+      if (!Q.pk) {  // an empty wheel: buckets wide enough for the source's delay range to fit
+        wctl = (wctl & 0xFFFF0000u) | wheel_width(pp.lat_ns + (uint64_t)(pp.sigma > 0 ? pp.sigma : 0));
+        lds.wcnt[lane] = 0;
+        wave_lds_sync();
+      }
+      const uint32_t g0 = wctl & 0xFFu;
+      // the base slides up to the lowest bucket in use (every bucket below it is empty): the far items
+      // about to be parked and the buckets still parked
+      uint64_t mn = ~0ull;
+      for (uint32_t k = lane; k < fn0; k += kWave) {
+        const uint64_t e = w0_of(Q.slot(f0 + k)) & kEMask;
+        mn = e < mn ? e : mn;
+      }
+      mn >>= g0;
+      if (Q.pk && wcnt) {
+        const uint64_t id = (uint64_t)wbase + ((lane - wbase) & (kWheelB - 1));
+        mn = id < mn ? id : mn;
+      }
+      wbase = (uint32_t)readlane64(scan_min_u64(mn), kWave - 1);
+      const uint32_t g = g0;
+      const uint64_t below = (1ull << lane) - 1;
+      uint32_t kept = 0;
+      for (uint32_t c = 0; c < fn0; c += kWave) {
+        const uint32_t k = c + lane;
+        const bool in = k < fn0;
+        const uint4 it = in ? Q.slot(f0 + k) : make_uint4(0, 0, 0, 0);
+        const uint64_t id = (w0_of(it) & kEMask) >> g;  // >= base: every far item is >= H
+        bool ok = in && id - wbase < kWheelB;
+        uint32_t pos = kWheelCB;
+        if (ok) pos = atomicAdd(&lds.wcnt[(uint32_t)id & (kWheelB - 1)], 1u);
+        ok = ok && pos < kWheelCB;
+        if (ok) st16<kPol>(rw, 16u * (((uint32_t)id & (kWheelB - 1)) * kWheelCB + pos), it);
+        // the others stay in the heap array, compacted behind the near region and the soon pool
+        // (every lane has read its item before any lane writes; writes land at or below k)
+        const bool kp = in && !ok;
+        const uint64_t mk = __ballot(kp);
+        if (kp) Q.slot(f0 + kept + (uint32_t)__popcll(mk & below)) = it;
+        kept += (uint32_t)__popcll(mk);
+      }
+      wave_lds_sync();
+      wcnt = lds.wcnt[lane];
+      wcnt = wcnt < kWheelCB ? wcnt : kWheelCB;
+      pk_end = readlane32((uint32_t)scan_sum_i32((int32_t)wcnt), kWave - 1);
+      moved_end += 16ull * (fn0 - kept);
+      Q.fn = kept;
+#ifndef TGSIM_PROFILE
+      stamp(a, wg, lane, 8, nd | (uint64_t)Q.pk << 16 | (uint64_t)fn0 << 32 | (uint64_t)kept << 48);
+      stamp(a, wg, lane, 9, (uint64_t)g << 32 | (uint64_t)(wctl >> 8 & 1u) << 40);
+#endif
+    }
+    if (pk_end && (nd || fn0 || (wctl >> 16))) {  // the wheel's counts and control word, when they changed
+      // a reshaped link whose delay range no longer fits the buckets: every bucket comes back at the
+      // next window and the wheel takes the new width
+      const uint32_t cool = wctl >> 16;
+      if (Q.fn > kWheelRebuildKeep && !cool &&
+          wheel_width(pp.lat_ns + (uint64_t)(pp.sigma > 0 ? pp.sigma : 0)) != (wctl & 0xFFu))
+        wctl = (wctl & 0xFFu) | 0x100u | kWheelCooldown << 16;
+      else wctl = (wctl & 0xFFu) | (cool ? cool - 1 : 0u) << 16;
+      st2<kPol>(rm, 2u * lane, wcnt);
+      if (lane == 0) st16<kPol>(rm, 2u * kWheelB, make_uint4(wbase, wctl, 0u, 0u));
+      moved_end += sizeof(WheelMeta);
+    }
+  }
   {
     // ---- write back the ring entries appended this window (the others are in HBM already: the
     // head moves past the released ones), the queue (near, then pool) and the state
     uint64_t* gr = a.ring + (size_t)s * kHeapCap;
     uint4* gh = a.heap + (size_t)s * kHeapCap;
     const uint32_t r_new = Q.rpush < Q.rn ? Q.rpush : Q.rn;             // the ring's last r_new entries
-    const uint32_t rh1 = (rh0 + rn0 + Q.rpush - Q.rn) & (kHeapCap - 1);  // head after the releases
-    moved += 8ull * r_new + 16ull * (Q.qn + Q.pn + Q.fn);
+    const uint32_t rh1 = (lds.whdr[3] + Q.rpush - Q.rn) & (kHeapCap - 1);  // head after the releases
+    moved_end += 8ull * r_new + 16ull * (Q.qn + Q.pn + Q.fn);
     if constexpr (kH) {  // write-through stores
       const auto rr = region(gr, kHeapCap * 8u), rq = region(gh, kHeapCap * 16u);
       for (uint32_t k = Q.rn - r_new + lane; k < Q.rn; k += kWave)
@@ -1550,7 +1735,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     if (lane == 0) {
       SrcState ns;
       ns.tat = Q.tat;
-      ns.heap_n = q_pack(Q.qn + Q.pn + Q.fn, 0);
+      ns.heap_n = q_pack(Q.qn + Q.pn + Q.fn, pk_end);
       ns.near_n = near_out;
       ns.ring_n = r_pack(Q.rn, rh1);
       ns.last_dup = last_dup;
@@ -1577,7 +1762,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   const uint32_t corrupted = readlane32((uint32_t)scan_sum_i32((int32_t)Q.corrupted), kWave - 1);
   const uint32_t lost = readlane32((uint32_t)scan_sum_i32((int32_t)Q.lost), kWave - 1);
   const uint64_t bytes = wave_sum(Q.bytes);
-  const uint64_t qbytes = 16ull * (Q.qn + Q.pn + Q.fn) + 8ull * Q.rn;
+  const uint64_t qbytes = 16ull * (Q.qn + Q.pn + Q.fn + pk_end) + 8ull * Q.rn;
   const bool err = __ballot(perr != 0) != 0;
   const uint32_t c_clone = readlane32((uint32_t)scan_sum_i32((int32_t)n_clone), kWave - 1);
   flush_verdicts();
@@ -1592,7 +1777,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     if (qbytes) atomicAdd(&sc[kStQueue], (unsigned long long)qbytes);
     // what the model charged and the window did not move (wraps below zero when it moved more: the
     // readers sum modulo 2^64)
-    if (b0 + qbytes != moved) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(b0 + qbytes - moved));
+    if (qbytes != moved_end) atomicAdd(&sc[kStCarrySkip], (unsigned long long)(qbytes - moved_end));
     if (err) {
       atomicOr(&a.stats[kStErr], (unsigned long long)kErrTimeOverflow);
       if (a.err_host)  // the host's pinned copy (sticky; read at its sync points)
@@ -1602,7 +1787,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)next_ticket);
 }
 
-__global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
+__global__ __launch_bounds__(kWave, 3) void k_sim(SimArgs a) {
   __shared__ SimLdsT<kHeapCap> lds;
   // heavy-first dispatch order (previous step's HTB work per source), identity when absent
   const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
@@ -1615,7 +1800,7 @@ __global__ __launch_bounds__(kWave) void k_sim(SimArgs a) {
 }
 
 // k_sim with the gossip receipts folded in (a dense window of the single-shard gossip loop).
-__global__ __launch_bounds__(kWave) void k_sim_recv(SimArgs a) {
+__global__ __launch_bounds__(kWave, 3) void k_sim_recv(SimArgs a) {
   __shared__ SimLdsT<kHeapCap> lds;
   const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
   if (s >= a.n_src) return;
@@ -2020,6 +2205,10 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     (void)why;
 #endif
   };
+  if (q_parked(st)) {  // far items parked in the timing wheel: the general path reads them
+    defer(5u);
+    return;
+  }
   const bool sorted_st = q_near(st) == qn;  // the whole queue is one sorted region
   // FIFO candidates beyond one round of lanes go to k_sim_multi (multi-round, candidates written behind
   // the queue tail in HBM)
@@ -2540,7 +2729,8 @@ __global__ __launch_bounds__(256) void k_unrotate(uint4* heap, SrcState* state, 
   if (lane == 0) state[s].near_n = q_near(st);
 }
 
-__global__ __launch_bounds__(256) void k_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone) {
+__global__ __launch_bounds__(256) void k_purge(uint4* heap, uint4* wheel, const WheelMeta* wmeta, const SrcState* state,
+                                               uint32_t n_src, const uint8_t* gone) {
   const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (s >= n_src) return;
   const SrcState st = state[s];
@@ -2550,6 +2740,17 @@ __global__ __launch_bounds__(256) void k_purge(uint4* heap, const SrcState* stat
     const uint32_t j = (qh + k) & (kHeapCap - 1);
     const uint32_t d = q[j].w;
     if (d != kDeadDst && gone[d]) q[j].w = kDeadDst;
+  }
+  if (q_parked(st)) {  // and the items parked in the timing wheel, bucket by bucket
+    const uint32_t cnt = wmeta[s].cnt[lane];
+    uint4* w = wheel + (size_t)s * kWheelB * kWheelCB;
+    for (uint32_t b = 0; b < kWheelB; ++b) {
+      const uint32_t c = (uint32_t)__shfl((int)cnt, (int)b, 64);
+      if (lane < c) {
+        const uint32_t d = w[b * kWheelCB + lane].w;
+        if (d != kDeadDst && gone[d]) w[b * kWheelCB + lane].w = kDeadDst;
+      }
+    }
   }
 }
 
@@ -3786,8 +3987,9 @@ void launch_unrotate(uint4* heap, SrcState* state, uint32_t n_src, hipStream_t s
   if (n_src) hipLaunchKernelGGL(k_unrotate, dim3((n_src + 3) / 4), dim3(256), 0, st, heap, state, n_src);
 }
 
-void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone, hipStream_t st) {
-  if (n_src) hipLaunchKernelGGL(k_purge, dim3((n_src + 3) / 4), dim3(256), 0, st, heap, state, n_src, gone);
+void launch_purge(uint4* heap, uint4* wheel, const WheelMeta* wmeta, const SrcState* state, uint32_t n_src,
+                  const uint8_t* gone, hipStream_t st) {
+  if (n_src) hipLaunchKernelGGL(k_purge, dim3((n_src + 3) / 4), dim3(256), 0, st, heap, wheel, wmeta, state, n_src, gone);
 }
 
 // Publishes *v0 (and *v1 when given) into pinned host words, then the sequence number (release):

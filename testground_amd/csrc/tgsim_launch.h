@@ -39,7 +39,8 @@ void launch_order(const uint32_t* weight, uint32_t n, uint32_t* order, hipStream
 void launch_apply_cfg(const CfgPatch* p, uint32_t n, SrcParams* params, SrcState* state,
                       unsigned long long* stats, hipStream_t st);
 // marks queued items towards gone[dst] != 0 dead (kDeadDst)
-void launch_purge(uint4* heap, const SrcState* state, uint32_t n_src, const uint8_t* gone, hipStream_t st);
+void launch_purge(uint4* heap, uint4* wheel, const WheelMeta* wmeta, const SrcState* state, uint32_t n_src,
+                  const uint8_t* gone, hipStream_t st);
 void launch_unrotate(uint4* heap, SrcState* state, uint32_t n_src, hipStream_t st);
 // *v0 (and *v1) into pinned slot[0], slot[1], then seq into slot[2] (system-scope release)
 void launch_publish(const uint64_t* v0, const uint32_t* v1, uint64_t* slot, uint64_t seq, hipStream_t st);
