@@ -488,6 +488,13 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     step = eng.step if stepper is None else stepper.step
     epoch = [0]
     plans = {}  # epochs: each epoch's reshape as its plan asks for it, computed before the timed loop
+    host_s = {"step": 0.0, "reshape": 0.0, "signal": 0.0, "barrier": 0.0}  # epochs: host time per call
+
+    def timed(name, fn, *args):
+        t = time.perf_counter()
+        r = fn(*args)
+        host_s[name] += time.perf_counter() - t
+        return r
 
     def reshape(k):
         workloads.epoch_reshape(eng, peers_total, k, plan=plans.pop(k, None))
@@ -502,16 +509,16 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
                 # as the sharded step below: epoch k+1's ConfigureNetwork calls are staged on the
                 # host while epoch k simulates (the step is asynchronous) and take effect at the
                 # next step; epoch 0 runs on the initial configs
-                step(window)
-                reshape(k + 1)
+                timed("step", step, window)
+                timed("reshape", reshape, k + 1)
             else:
                 # the sharded step waits for its records, so epoch k+1's ConfigureNetwork calls
                 # are staged on the host while epoch k simulates (epoch k's were staged during
                 # epoch k-1); staged configs take effect at the next launch, after the barrier below
                 stepper.step(window, between=lambda: reshape(k + 1))
             state, rnd = workloads.epoch_state(k)
-            eng.signal_async(state, peers)  # K7: the count stays on the device
-            ok = stepper.barrier(state, rnd * peers_total) if stepper else eng.barrier_poll(state, rnd * peers_total)
+            timed("signal", eng.signal_async, state, peers)  # K7: the count stays on the device
+            ok = timed("barrier", stepper.barrier if stepper else eng.barrier_poll, state, rnd * peers_total)
             if not ok:
                 raise RuntimeError(f"barrier epoch-{k} did not release")
             epoch[0] += 1
@@ -555,6 +562,8 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     run_steps(warmup)
     eng.drain()
     setup_s = time.perf_counter() - t_setup
+    for k in host_s:
+        host_s[k] = 0.0
     s0 = eng.stats()
     x0 = stepper.exchanged_records if stepper is not None else 0
     eng.sim_kernel_ms(reset=True)
@@ -591,6 +600,8 @@ def run_workload(a, workload, peers, steps, warmup, window, lam, world, rank, lo
     else:
         offered_all, scheduled_all, exch_all, verd_all = float(offered), float(scheduled), 0.0, verd
     extra = {}
+    if workload == "epochs":  # where the host's time per epoch goes
+        extra["host_us_per_epoch"] = {k: v * 1e6 / max(1, steps) for k, v in host_s.items()}
     if workload == "gossip":
         reached = eng.gossip_reached()
         if dist:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B builds: testground_amd/libtgsim_<name>.so from the current sources with extra compiler flags
-# (e.g. -DTGSIM_X), for scripts/r04_gossip_ab.sh; PROMOTE_ALLOCA=1 lets LLVM promote private arrays to LDS.  usage: build_variant.sh NAME [FLAGS...]
+# (e.g. -DTGSIM_X), for scripts/ab.sh; PROMOTE_ALLOCA=1 lets LLVM promote private arrays to LDS.  usage: build_variant.sh NAME [FLAGS...]
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift

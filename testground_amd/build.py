@@ -37,7 +37,7 @@ def build_engine(force: bool = False, verbose: bool = False, profile: bool = Fal
     """Compiles the HIP engine (kernels + host runtime) into libtgsim.so.  profile=True builds the
     diagnostic variant libtgsim_prof.so (k_sim cycle counters in the stamp slots; scripts only);
     check=True the invariant-checking variant libtgsim_check.so (-DTGSIM_CHECK: queue invariants and
-    the cross-lane exec-mask guards; loaded by TGSIM_LIB=... for scripts/r05_check_build.sh only)."""
+    the cross-lane exec-mask guards; loaded by TGSIM_LIB=... for scripts/check_build.sh only)."""
     lib = PROF_LIB if profile else CHECK_LIB if check else LIB
     if not force and not _stale(lib, SOURCES + HEADERS):
         return lib

@@ -293,6 +293,13 @@ struct tgsim_engine_s {
   DevBuf<WheelMeta> d_wmeta;   // [s] bucket counts, base id, width (read only while items are parked)
   bool wheel_failed = false;   // no memory for the wheel: dense windows run without parking
   DevBuf<CfgPatch> d_patch;
+  // pinned staging of the configuration patches, two sets in turn: a set is refilled once the copy
+  // that last read it has run (its event), so a reshape never waits for the simulation in flight
+  CfgPatch* h_patch[2] = {nullptr, nullptr};
+  size_t h_patch_cap[2] = {0, 0};
+  hipEvent_t ev_patch[2] = {nullptr, nullptr};
+  uint32_t patch_turn = 0;
+  std::vector<uint32_t> dirty_src;  // sources with a pending patch (HostSrc::dirty), in marking order
   DevBuf<uint32_t> d_gen_seq;
 
   // step input
@@ -444,6 +451,14 @@ using Eng = tgsim_engine_s;
 
 namespace {
 
+// Source s has a configuration patch pending (flushed at the next step, k_apply_cfg).
+void mark_dirty(Eng* E, uint32_t s) {
+  HostSrc& h = E->src[s];
+  if (!h.dirty) E->dirty_src.push_back(s);
+  h.dirty = true;
+  E->any_patch = true;
+}
+
 void reset_source(Eng* E, uint32_t s) {
   HostSrc& h = E->src[s];
   tgsim_shape zero;
@@ -457,8 +472,7 @@ void reset_source(Eng* E, uint32_t s) {
   h.p.rho_dup = h.p.rho_cor = h.p.rho_reo = 0;
   h.patch_mask |= 1u | 2u | 4u | 8u | 16u;
   h.last[0] = h.last[1] = h.last[2] = 0;
-  h.dirty = true;
-  E->any_patch = true;
+  mark_dirty(E, s);
 }
 
 bool owns(const Eng* E, uint32_t peer) { return peer >= E->o.shard_begin && peer < E->o.shard_end; }
@@ -477,10 +491,8 @@ void link_down(Eng* E, uint32_t peer) {
   E->any_gone = true;
   E->link_gen[peer]++;
   if (owns(E, peer)) {
-    HostSrc& h = E->src[peer - E->o.shard_begin];
-    h.patch_mask |= 16u;
-    h.dirty = true;
-    E->any_patch = true;
+    E->src[peer - E->o.shard_begin].patch_mask |= 16u;
+    mark_dirty(E, peer - E->o.shard_begin);
   }
 }
 
@@ -532,8 +544,7 @@ void apply_shape(Eng* E, uint32_t peer, const tgsim_shape& shape) {
     h.last[2] = rnd[2];
     h.patch_mask |= 4u;
   }
-  h.dirty = true;
-  E->any_patch = true;
+  mark_dirty(E, peer - E->o.shard_begin);
 }
 
 // link.AddRules (link.go:187-217): cumulative; Accept deletes; host bits -> EINVAL.
@@ -569,8 +580,7 @@ void apply_policy(Eng* E, uint32_t peer, uint8_t policy) {
   const bool allow = policy == TGSIM_ALLOW_ALL;
   if (allow != h.allow_ext) {
     h.allow_ext = allow;
-    h.dirty = true;
-    E->any_patch = true;
+    mark_dirty(E, peer - E->o.shard_begin);
   }
 }
 
@@ -679,11 +689,28 @@ int flush_config(Eng* E) {
     if (E->now_tick) E->wide_windows = kWideAfterReshape;
   }
   if (E->any_patch) {
-    std::vector<CfgPatch> patches;
-    for (uint32_t s = 0; s < E->S; ++s) {
+    // The patches go through pinned memory, asynchronously: the copy and k_apply_cfg queue behind the
+    // window in flight on the simulate stream, and the host goes on (a stream synchronize here held
+    // every reshaping step until the previous window had finished: the C5 epochs' host gap)
+    const size_t n = E->dirty_src.size();
+    const uint32_t t = E->patch_turn;
+    if (E->ev_patch[t]) HIPCHK(hipEventSynchronize(E->ev_patch[t]));  // its last copy has run
+    else HIPCHK(hipEventCreateWithFlags(&E->ev_patch[t], hipEventDisableTiming));
+    if (n > E->h_patch_cap[t]) {
+      if (E->h_patch[t]) HIPCHK(hipHostFree(E->h_patch[t]));
+      E->h_patch[t] = nullptr;
+      E->h_patch_cap[t] = 0;
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&E->h_patch[t]), sizeof(CfgPatch) * (n + n / 2),
+                           hipHostMallocDefault));
+      E->h_patch_cap[t] = n + n / 2;
+    }
+    CfgPatch* patches = E->h_patch[t];
+    size_t k = 0;
+    // in source order, as the full scan gave them (a source patched twice is applied once)
+    std::sort(E->dirty_src.begin(), E->dirty_src.end());
+    for (const uint32_t s : E->dirty_src) {
       HostSrc& h = E->src[s];
-      if (!h.dirty) continue;
-      CfgPatch c;
+      CfgPatch& c = patches[k++];
       memset(&c, 0, sizeof c);
       c.s = s;
       c.mask = h.patch_mask;
@@ -692,18 +719,20 @@ int flush_config(Eng* E) {
       c.last_reo = h.last[2];
       c.p = h.p;
       c.p.shift_ext = (c.p.shift_ext & 0xFFu) | (h.allow_ext ? 0x100u : 0u);
-      patches.push_back(c);
       h.dirty = false;
       h.patch_mask = 0;
     }
-    if (!patches.empty()) {
-      HIPCHK(E->d_patch.ensure(patches.size()));
-      HIPCHK(hipMemcpyAsync(E->d_patch.p, patches.data(), sizeof(CfgPatch) * patches.size(),
-                            hipMemcpyHostToDevice, E->st));
-      launch_apply_cfg(E->d_patch.p, static_cast<uint32_t>(patches.size()), E->d_params.p, E->d_state.p,
-                       E->d_stats.p, E->st);
+    E->dirty_src.clear();
+    if (k) {
+      if (E->d_patch.cap < k) {  // (a grown buffer: the old one may still be read by an apply in flight)
+        HIPCHK(hipStreamSynchronize(E->st));
+        HIPCHK(E->d_patch.ensure(k));
+      }
+      HIPCHK(hipMemcpyAsync(E->d_patch.p, patches, sizeof(CfgPatch) * k, hipMemcpyHostToDevice, E->st));
+      launch_apply_cfg(E->d_patch.p, static_cast<uint32_t>(k), E->d_params.p, E->d_state.p, E->d_stats.p, E->st);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipStreamSynchronize(E->st));
+      HIPCHK(hipEventRecord(E->ev_patch[t], E->st));
+      E->patch_turn = t ^ 1u;
       if (E->now_tick) E->wide_windows = kWideAfterReshape;
     }
     E->any_patch = false;
@@ -2005,6 +2034,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
     E->src[s].patch_mask = 0;
     E->src[s].dirty = false;
   }
+  E->dirty_src.clear();
   E->any_patch = false;
   if ((rc = E->hip(E->d_params.ensure(E->S), "alloc params"))) return bail(rc);
   if ((rc = E->hip(E->d_state.ensure(E->S), "alloc state"))) return bail(rc);
@@ -2068,6 +2098,10 @@ void tgsim_destroy(void* e) {
   if (E->comm.free_fn) E->comm.free_fn(E->comm.state);
   E->d_sync.release(); E->d_gone.release();
   if (E->h_mirror) (void)hipHostFree(E->h_mirror);
+  for (int t = 0; t < 2; ++t) {
+    if (E->h_patch[t]) (void)hipHostFree(E->h_patch[t]);
+    if (E->ev_patch[t]) (void)hipEventDestroy(E->ev_patch[t]);
+  }
   if (E->h_sig) (void)hipHostFree(E->h_sig);
   if (E->ev_sig) (void)hipEventDestroy(E->ev_sig);
   if (E->sy_st) (void)hipStreamDestroy(E->sy_st);

@@ -48,7 +48,7 @@ def make_oracle(oracle_lib):
 
 
 def pytest_sessionfinish(session, exitstatus):
-    """With TGSIM_LIB naming a TGSIM_CHECK build (scripts/r05_check_build.sh), report the cross-lane
+    """With TGSIM_LIB naming a TGSIM_CHECK build (scripts/check_build.sh), report the cross-lane
     exec-mask guard violations the run's kernels counted."""
     import os
 
