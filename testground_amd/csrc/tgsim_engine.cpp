@@ -50,17 +50,21 @@ uint32_t duration_us(int64_t ns) {  // link.go:143-151
 
 uint32_t us_to_ticks(uint32_t us) { return go_float_to_u32(static_cast<double>(us) * 15.625); }
 
+// psched_ratecfg_precompute: the smallest shift whose mult = (NSEC_PER_SEC << shift) / rate has bit 31
+// set (or whose factor reaches bit 63).  floor(f / rate) >= 2^31 exactly when f >= 2^31 * rate (rate is
+// a u32: no overflow), so the shift is found with shifts alone and one division (the kernel's loop
+// divides at every step: ~30 divisions a configure call).
 void psched_precompute(uint64_t rate, uint32_t* mult, uint32_t* shift) {
   *mult = 1;
   *shift = 0;
   if (!rate) return;
+  const uint64_t need = rate << 31;
   uint64_t factor = 1000000000ull;
-  for (;;) {
-    *mult = static_cast<uint32_t>(factor / rate);
-    if ((*mult & 0x80000000u) || (factor & 0x8000000000000000ull)) return;
+  while (factor < need && !(factor & 0x8000000000000000ull)) {
     factor <<= 1;
     ++*shift;
   }
+  *mult = static_cast<uint32_t>(factor / rate);
 }
 
 struct Compiled {
