@@ -17,7 +17,7 @@ from testground_amd import abi, workloads  # noqa: E402
 from testground_amd.engine import Engine  # noqa: E402
 
 n, window, lam = 100_000, 1000, 0.2
-e = Engine(n)
+e = Engine(n, flags=abi.OPT_DISCARD_DELIVERIES)
 workloads.configure_storm(e, n)
 for _ in range(20):
     e.gen_storm(lam, window)
