@@ -47,7 +47,7 @@ namespace {
 constexpr size_t kRec = sizeof(tgsim_delivery);
 // Grid of the sharded fused groups at N > 1: the exchange's kernels (RCCL) and the group delivery need
 // CU slots while the next group simulates, so the persistent grid holds 90 % of the resident
-// workgroups (the rest stay free for them).  Timed at one rank (TGSIM_COMM_ROUTE1, TGSIM_FUSED_PERSIST,
+// workgroups (the rest stay free for them).  Timed at one rank (TGSIM_COMM_ROUTE1, grid fractions A/B'd,
 // profiles/r04/grids): turnover (one workgroup per ticket) 31.2-31.3 G pkt/s, 80 % 31.8-32.1, 90 %
 // 34.0-34.4, the whole grid 34.0-34.2.
 constexpr uint32_t kRoutedGridPct = 90;

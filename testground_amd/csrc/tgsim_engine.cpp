@@ -219,8 +219,6 @@ struct tgsim_engine_s {
   hipEvent_t ev_dst = nullptr;   // recorded after the last delivery on dst_st
   hipEvent_t ev_recv = nullptr;  // recorded after the last delivery's scatter (and gossip receipts)
   hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
-  hipEvent_t ev_scan = nullptr;  // after a bucketed window's histogram scan on the simulate stream
-  bool scan_on_sim = false;      // TGSIM_SCAN_ON_SIM=1: that scan on the simulate stream (A/B: 0.6 % slower)
   // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize), with
   // the number of windows the launch simulated (a fused launch counts each of its windows)
   struct PendingTiming {
@@ -391,12 +389,10 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_order;  // dispatch order of the next k_sim, computed behind this one
   DevBuf<uint32_t> d_work;   // sparse steps: k_sim_sparse's deferred sources, [0] = count, then ids
   int sparse_mode = -1;      // TGSIM_SPARSE: -1 auto, 0 never, 1 always
-  bool fold_recv = true;     // TGSIM_FOLD_RECV: single-shard gossip receipts folded into k_sim
   bool rotated = false;      // a sparse step may have left queues in place (head slot != 0)
   bool sparse_seen = false;  // h_work holds a measured worklist size
   uint32_t dense_streak = 0; // dense steps chosen because the last sparse step deferred too much
-  uint32_t dense_div = 4;    // TGSIM_DENSE_DIV: dense when the last sparse step deferred > S / dense_div
-  bool trace_list = false;   // TGSIM_TRACE_LIST: print each sparse decision's deferred count
+  static constexpr uint32_t dense_div = 4;  // dense when the last sparse step deferred > S / dense_div
   bool order_valid = false;
   // fused windows (tgsim_step_n): per group parity p and window i the emit regions, their counts
   // and the per-destination histogram; ev_fgrp[p]: after the deliveries that last read set p
@@ -415,9 +411,8 @@ struct tgsim_engine_s {
   uint32_t fused_wgs = 0;
   uint32_t routed_pct = 0;      // sharded (routed) groups: 0 = one workgroup per ticket (the grid turns
                                 // over), else a persistent grid of this % of the resident workgroups
-  bool persist_env = false;     // TGSIM_FUSED_PERSIST was set (the comm layer keeps its choice)
   CommSlot comm{};              // tgsim_comm_init's exchange state (tgsim_comm.cpp)
-  uint32_t prio_heavy = 512;  // TGSIM_PRIO_HEAVY: heaviest sources of a fused launch at wave priority 3 (A/B: 128 +1 %, 512 +7.5 %, 2048 +7 %, 4096 +5 %)  // k_sim_fused's persistent grid (resident workgroups), at the first launch
+  static constexpr uint32_t prio_heavy = 512;  // heaviest sources of a fused launch at wave priority 3 (A/B: 128 +1 %, 512 +7.5 %, 2048 +7 %, 4096 +5 %)  // k_sim_fused's persistent grid (resident workgroups), at the first launch
   int fuse_max = 8;  // TGSIM_FUSE: windows per fused launch, up to kFuseMax (1: never fuse; A/B at 30 windows: 4 34.8, 8 36.3, 16 36.3 G pkt/s)
   DevBuf<uint64_t> d_stamps;
   uint64_t n_stamp_wg = 0;
@@ -1174,7 +1169,7 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     E->el.slot = a.dst_slot;
     // and, where nothing but the local delivery reads the records (no metrics, receipts folded in at
     // emission), straight into the destinations' buckets (TGSIM_DST_BKT=0: the emit records only)
-    if (a.dst_slot && E->dst_bkt && !E->metrics_on && (!E->gossip_on || E->fold_recv)) {
+    if (a.dst_slot && E->dst_bkt && !E->metrics_on) {
       HIPCHK(E->d_dbkt.ensure(static_cast<size_t>(E->N) << kBktLogMax));
       a.dst_bkt = E->d_dbkt.p;
       a.bkt_log = bucket_log(E->n_in, E->N);
@@ -1182,23 +1177,12 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
       E->el.bkt_log = a.bkt_log;
     }
   }
-  if (E->gossip_on && E->fold_recv) {  // receipts at emission for the destinations of this shard
+  if (E->gossip_on) {  // receipts at emission for the destinations of this shard
     a.g_first = E->d_gfirst.p;
     a.g_pend = E->d_gpend.p;
     a.g_fwd = E->d_gfwd.p;
     a.g_floods = E->gossip.n_floods;
     a.g_degree = E->gossip.degree;
-  }
-  if (E->trace_list && E->sparse_mode < 0 && E->n_in < 64ull * E->S) {
-    fprintf(stderr, "tgsim: last sparse step deferred %u of %u sources (multi-round %u)%s",
-            __atomic_load_n(E->h_work, __ATOMIC_RELAXED), E->S, __atomic_load_n(E->h_work + 1, __ATOMIC_RELAXED),
-            compact ? " compact emit" : "");
-#ifdef TGSIM_DEFER_STATS  // by reason (corr, limit, n>64, queue, ring, fifo-due, sorted-queue, rest), cumulative
-    uint32_t why[8] = {};
-    if (E->d_work.p && hipMemcpy(why, E->d_work.p + 4 + E->S, sizeof why, hipMemcpyDeviceToHost) == hipSuccess)
-      for (uint32_t w : why) fprintf(stderr, " %u", w);
-#endif
-    fprintf(stderr, "\n");
   }
   a.worklist = nullptr;
   if (sparse) {
@@ -1446,9 +1430,9 @@ int deliver(Eng* E, const tgsim_delivery* in, uint64_t n, hipEvent_t wait, bool 
                        // from the inbound records on the simulate stream, where the next window's
                        // generation runs: it waits for the records' arrival, not for any sort; records
                        // of this shard's own sources were folded in at emission
-    if (!(E->fold_recv && E->S == E->N)) {
+    if (E->S != E->N) {
       if (wait) HIPCHK(hipStreamWaitEvent(E->st, wait, 0));
-      launch_gossip_recv_in(gossip_args(E, 0, 0), in, n, slot, E->fold_recv, E->st);
+      launch_gossip_recv_in(gossip_args(E, 0, 0), in, n, slot, true, E->st);
       HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
@@ -1532,17 +1516,8 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   HIPCHK(dpos.ensure(nd));
   HIPCHK(dblk.ensure((nd + 1023) / 1024 + 1));
   HIPCHK(dtot.ensure(1));
-  // a bucketed window's scan runs on the simulate stream right behind the simulation (a few tens of
-  // microseconds at its priority; on the low-priority delivery stream its three dispatches waited for
-  // the next window's simulate waves, up to 1.3 ms at the 1M-peer flood's peak, while that simulate
-  // kernel's successor waited for this delivery to release the bucket set)
-  const bool scan_sim = E->scan_on_sim && emit.bkt;
-  launch_scan(lcnt, doff.p, nd, dblk.p, dtot.p, scan_sim ? E->st : sq, dpos.p, lcnt);  // (clears lcnt)
+  launch_scan(lcnt, doff.p, nd, dblk.p, dtot.p, sq, dpos.p, lcnt);  // (clears lcnt)
   HIPCHK(hipGetLastError());
-  if (scan_sim) {
-    HIPCHK(hipEventRecord(E->ev_scan, E->st));
-    HIPCHK(hipStreamWaitEvent(sq, E->ev_scan, 0));
-  }
   const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
   // without the exact count (no host round trip): what the window's sources can emit, 2 per offered
   // packet plus the full netem limit per source.  Where that bound exceeds kExactBoundBytes (24 GB
@@ -1609,15 +1584,9 @@ int deliver_local(Eng* E) {
   hipStream_t sq = E->dst_st;
   HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
   HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
-  if (E->gossip_on) {  // receipts of the gossip workload: folded into k_sim at emission, or read
-                       // from the emit regions on the simulate stream (TGSIM_FOLD_RECV=0); the next
-                       // window's generation waits for nothing on the delivery side
-    if (!E->fold_recv) {
-      launch_gossip_recv_emit(gossip_args(E, 0, 0), E->el, E->d_emit_n.p, E->d_off.p, E->S, E->st);
-      HIPCHK(hipGetLastError());
-    }
+  if (E->gossip_on)  // receipts of the gossip workload: folded into k_sim at emission; the next
+                     // window's generation waits for nothing on the delivery side
     HIPCHK(hipEventRecord(E->ev_recv, E->st));
-  }
 
   int rc = deliver_local_from(E, E->el, E->d_emit_n.p, E->d_lcnt.p, E->d_off.p, E->n_in, E->ev_local);
   if (rc) return rc;
@@ -1733,10 +1702,9 @@ int step_fused(Eng* E, uint32_t n_ticks, uint32_t g, const GroupRoute* gr = null
   HIPCHK(hipEventRecord(ev0, E->st));
   if (!E->fused_wgs) {
     E->fused_wgs = sim_fused_resident();
-    if (const char* w = getenv("TGSIM_FUSED_WGS")) E->fused_wgs = static_cast<uint32_t>(std::max(1, atoi(w)));
   }
   // a sharded group's exchange (RCCL) and deliveries need CU slots while the next group simulates:
-  // there the workgroups turn over (TGSIM_FUSED_PERSIST=1 forces the persistent grid)
+  // there a persistent grid holds kRoutedGridPct of the resident workgroups (engine_persist_routed)
   f.persistent = gr ? (E->routed_pct ? 1u : 0u) : 1u;
   const uint32_t wgs = gr && E->routed_pct ? std::max(1u, E->fused_wgs * std::min(E->routed_pct, 100u) / 100u)
                                            : E->fused_wgs;
@@ -1872,9 +1840,7 @@ void engine_shard(void* e, uint32_t* begin, uint32_t* end) {
   *end = as_eng(e)->o.shard_end;
 }
 int engine_fail(void* e, int code, const char* msg) { return as_eng(e)->fail(code, "%s", msg); }
-void engine_persist_routed(void* e, uint32_t pct) {
-  if (!as_eng(e)->persist_env) as_eng(e)->routed_pct = pct;
-}
+void engine_persist_routed(void* e, uint32_t pct) { as_eng(e)->routed_pct = pct; }
 const uint64_t* engine_route_counts_dev(void* e) {
   Eng* E = as_eng(e);
   return E->route_n && E->d_rsend.p ? E->d_rsend.p + 16 * E->route_head : nullptr;
@@ -1948,12 +1914,10 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   // own, and the delivery of one step runs beside the next k_sim instead of behind it in one
   // queue): the lowest, since the delivery is off the critical path (next k_sim; the gossip loop's
   // generation) and at high priority its waves were dispatched first (A/B: storm +1.2 %, 1M-peer
-  // gossip +3 % at low priority; TGSIM_DST_PRIO=0 restores high)
+  // gossip +3 % at low priority)
   int prio_lo = 0, prio_hi = 0;
   if ((rc = E->hip(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), "stream"))) return bail(rc);
-  const char* dp = getenv("TGSIM_DST_PRIO");
-  if ((rc = E->hip(hipStreamCreateWithPriority(&E->dst_st, hipStreamNonBlocking, dp && atoi(dp) == 0 ? prio_hi : prio_lo),
-                   "stream")))
+  if ((rc = E->hip(hipStreamCreateWithPriority(&E->dst_st, hipStreamNonBlocking, prio_lo), "stream")))
     return bail(rc);
   if ((rc = E->hip(hipStreamCreateWithPriority(&E->rt_st, hipStreamNonBlocking, prio_hi), "stream")))
     return bail(rc);
@@ -1963,7 +1927,6 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, hipEventDisableTiming), "event"))) return bail(rc);
-  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_scan, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_recv, E->dst_st), "event"))) return bail(rc);
   for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt, &E->ev_local_alt2}) {
     if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
@@ -2008,7 +1971,6 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   *E->h_err = 0;
   E->stamps_on = getenv("TGSIM_STAMPS") != nullptr;
   if (const char* sp = getenv("TGSIM_SPARSE")) E->sparse_mode = atoi(sp) ? 1 : 0;
-  if (const char* dd = getenv("TGSIM_DENSE_DIV")) E->dense_div = static_cast<uint32_t>(std::max(1, atoi(dd)));
   if (const char* st = getenv("TGSIM_SIM_TIMING")) E->sim_every = static_cast<uint32_t>(std::max(0, atoi(st)));
   if (const char* dv = getenv("TGSIM_DV_TIMING")) E->dv_every = static_cast<uint32_t>(std::max(0, atoi(dv)));
   if (E->sim_every || E->dv_every) {  // the timing events, created here rather than in the step path
@@ -2022,25 +1984,16 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (const char* ec = getenv("TGSIM_EMIT_COMPACT")) E->emit_compact = std::min(std::max(atoi(ec), 0), 2);
   if (const char* ds = getenv("TGSIM_DST_SLOT")) E->dst_slot = atoi(ds) != 0;
   if (const char* db = getenv("TGSIM_DST_BKT")) E->dst_bkt = atoi(db) != 0;
-  if (const char* ss = getenv("TGSIM_SCAN_ON_SIM")) E->scan_on_sim = atoi(ss) != 0;
   // (a shard of a multi-GPU run keeps two: its deliveries are not bucketed, and the 8-rank C4 test's
   // memory budget, VERDICT r04 item 7, has no room for a third)
   E->emit_sets = E->S == E->N ? 3u : 2u;
   if (const char* es = getenv("TGSIM_EMIT_SETS")) E->emit_sets = atoi(es) == 2 ? 2u : 3u;
   if (const char* er = getenv("TGSIM_EMIT_R")) E->emit_r = static_cast<uint32_t>(std::min(std::max(1, atoi(er)), 1024));
   if (const char* ep = getenv("TGSIM_EMIT_POOL")) E->emit_pool = static_cast<uint32_t>(std::min(std::max(0, atoi(ep)), 4096));
-  E->trace_list = getenv("TGSIM_TRACE_LIST") != nullptr;
-  if (const char* fr = getenv("TGSIM_FOLD_RECV")) E->fold_recv = atoi(fr) != 0;
   if (const char* ds = getenv("TGSIM_DELIVER_SLACK")) {
     E->deliver_slack = strtoull(ds, nullptr, 10);
     E->slack_forced = true;
   }
-  if (const char* fp = getenv("TGSIM_FUSED_PERSIST")) {  // 0: turnover; 1: persistent, all resident
-    const int v = atoi(fp);                               // workgroups; 2..100: that % of them
-    E->routed_pct = v <= 0 ? 0u : v == 1 ? 100u : static_cast<uint32_t>(std::min(v, 100));
-    E->persist_env = true;
-  }
-  if (const char* ph = getenv("TGSIM_PRIO_HEAVY")) E->prio_heavy = static_cast<uint32_t>(atoi(ph));
   if (const char* fz = getenv("TGSIM_FUSE")) E->fuse_max = std::max(1, std::min(atoi(fz), static_cast<int>(kFuseMax)));
   for (hipEvent_t& ev : E->ev_fgrp) {
     if ((rc = E->hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return bail(rc);
@@ -2173,7 +2126,6 @@ void tgsim_destroy(void* e) {
   if (E->ev_dst) (void)hipEventDestroy(E->ev_dst);
   if (E->ev_rt) (void)hipEventDestroy(E->ev_rt);
   if (E->ev_recv) (void)hipEventDestroy(E->ev_recv);
-  if (E->ev_scan) (void)hipEventDestroy(E->ev_scan);
   if (E->ev_sim) (void)hipEventDestroy(E->ev_sim);
   if (E->ev_local) (void)hipEventDestroy(E->ev_local);
   if (E->ev_local_alt) (void)hipEventDestroy(E->ev_local_alt);

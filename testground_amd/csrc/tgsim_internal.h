@@ -301,7 +301,7 @@ int engine_device(void* engine);
 uint32_t engine_peers(void* engine);
 void engine_shard(void* engine, uint32_t* begin, uint32_t* end);
 int engine_fail(void* engine, int code, const char* msg);
-// Grid of a sharded fused group (unless TGSIM_FUSED_PERSIST was set): 0 = one workgroup per ticket,
+// Grid of a sharded fused group: 0 = one workgroup per ticket,
 // else a persistent grid of pct % of the resident workgroups.
 void engine_persist_routed(void* engine, uint32_t pct);
 // Records `ev` on the routing stream after every routing enqueued so far (the exchange of a launched

@@ -254,17 +254,10 @@ __device__ __forceinline__ RecvFold recv_fold(const SimArgs& a) {
   return RecvFold{a.g_first, a.g_pend,  a.g_fwd,   a.g_floods,
                   a.g_degree, a.shard_begin, a.n_src, a.tick_ns, 1.0 / (double)a.tick_ns};
 }
-// kFwdSentinel: a peer's forwarded floods also read as receipt tick 0 in its own row (the forward
-// kernels store it), so a receipt of a forwarded flood is a no-op atomicMin and the fold needs no
-// read of the destination's forwarded mask (a scattered 4-B read, i.e. a 128-B line, per record).
-#ifndef TGSIM_GOSSIP_NOFWD
-#define TGSIM_GOSSIP_NOFWD 0
-#endif
-constexpr bool kFwdSentinel = TGSIM_GOSSIP_NOFWD != 0;
 __device__ __forceinline__ void fold_receipt(const RecvFold& g, uint32_t dst, uint32_t seq, uint32_t flags, uint64_t d,
                                              uint64_t fw) {
   const uint32_t f = seq / g.degree, s = dst - g.shard_begin;
-  if (s >= g.n_local || f >= g.floods || (flags & TGSIM_FLAG_CORRUPT) || (!kFwdSentinel && (fw >> f & 1ull))) return;
+  if (s >= g.n_local || f >= g.floods || (flags & TGSIM_FLAG_CORRUPT) || (fw >> f & 1ull)) return;
   // t = d / tick + 1 without a 64-bit division: d < 2^46 is exact in a double, and the estimate is
   // off by at most one
   uint64_t q = (uint64_t)((double)d * g.inv_tick);
@@ -530,7 +523,7 @@ struct SimQueue {
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
         rw[0] = inb || !dslot ? d : d | slot_bits(rank);
         if (rf.first && qi.w - rf.shard_begin < rf.n_local)
-          fold_receipt(rf, qi.w, qi.z, flags, d, kFwdSentinel ? 0ull : rf.fwd[qi.w - rf.shard_begin]);
+          fold_receipt(rf, qi.w, qi.z, flags, d, rf.fwd[qi.w - rf.shard_begin]);
         sched++;
         bytes += len;
         corrupted += (flags >> 1) & 1u;
@@ -558,7 +551,7 @@ struct SimQueue {
         rw[2] = ((uint64_t)flags << 48) | ((uint64_t)len << 32) | qi.z;
         if (dcnt) atomicAdd(&dcnt[qi.w], 1ull);
         if (rf.first && qi.w - rf.shard_begin < rf.n_local)
-          fold_receipt(rf, qi.w, qi.z, flags, d, kFwdSentinel ? 0ull : rf.fwd[qi.w - rf.shard_begin]);
+          fold_receipt(rf, qi.w, qi.z, flags, d, rf.fwd[qi.w - rf.shard_begin]);
         sched++;
         bytes += len;
         corrupted += (flags >> 1) & 1u;
@@ -1792,10 +1785,6 @@ __global__ __launch_bounds__(kWave, 3) void k_sim(SimArgs a) {
   // heavy-first dispatch order (previous step's HTB work per source), identity when absent
   const uint32_t s = a.order ? a.order[blockIdx.x] : blockIdx.x;
   if (s >= a.n_src) return;
-#ifndef TGSIM_PRIO
-#define TGSIM_PRIO 0
-#endif
-  if (TGSIM_PRIO && a.order && blockIdx.x < TGSIM_PRIO) __builtin_amdgcn_s_setprio(3);
   sim_source<false, kHeapCap>(a, s, blockIdx.x, lds);
 }
 
@@ -1834,12 +1823,9 @@ __device__ __forceinline__ const SimArgs& kernarg_window(uint32_t k) {
 // Tickets interleave the windows of all sources at a granularity of one source-window, which keeps
 // the launch's tail short (a source-major form, each source's windows back to back with its queue
 // resident in LDS, was bit-exact but slower: DESIGN.md §5.2).
-#ifndef TGSIM_FUSED_CAP
-#define TGSIM_FUSED_CAP kHeapCap
-#endif
 __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f) {
   const SimArgs& a0 = fs.w[0];
-  __shared__ SimLdsT<TGSIM_FUSED_CAP> lds;
+  __shared__ SimLdsT<kHeapCap> lds;
   const uint32_t total = f.n_win * a0.n_src;
   uint32_t t = 0;
   if (threadIdx.x == 0) t = atomicAdd(f.ticket, 1u) - f.ticket_base;
@@ -1870,7 +1856,7 @@ __global__ __launch_bounds__(kWave, 3) void k_sim_fused(FusedSim fs, FusedArgs f
           __hip_atomic_store(a0.err_host, (uint64_t)kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    const uint32_t next = sim_source<false, TGSIM_FUSED_CAP, kModeHandoff>(kernarg_window(k), s, t, lds,
+    const uint32_t next = sim_source<false, kHeapCap, kModeHandoff>(kernarg_window(k), s, t, lds,
                                                             f.persistent ? f.ticket : nullptr, f.ticket_base);
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every hand-off store written through
     if (threadIdx.x == 0)
@@ -2092,7 +2078,7 @@ __device__ __forceinline__ void multi_source(const SimArgs& a, const uint32_t s)
     const bool hs = lane < ns;
     const uint4 x = hs ? gh[(qh + k) & (kHeapCap - 1)] : make_uint4(0, 0, 0, 0);
     const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
-    const uint32_t fw = !kFwdSentinel && a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
+    const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
                             ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
                             : 0u;
     const uint64_t e = w0_of(x) & kEMask;
@@ -2199,11 +2185,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
   const uint32_t rn = r_len(st), qn = q_len(st), rh0 = r_head(st);
   auto defer = [&](uint32_t why) {
     if (lane == 0) a.worklist[atomicAdd(a.worklist - 4, 1u)] = s;
-#ifdef TGSIM_DEFER_STATS  // diagnostic build: deferrals by reason, behind the list
-    if (lane == 0) atomicAdd(a.worklist + a.n_src + why, 1u);
-#else
     (void)why;
-#endif
   };
   if (q_parked(st)) {  // far items parked in the timing wheel: the general path reads them
     defer(5u);
@@ -2502,7 +2484,7 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
     // the destinations' forwarded masks, for the receipts folded in below (in flight during the scan)
     // (the 32-bit half of the mask that holds the record's flood bit: one register across the scan)
     const uint32_t fw_f = a.g_first ? x.z / a.g_degree : 0u;
-    const uint32_t fw = !kFwdSentinel && a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
+    const uint32_t fw = a.g_first && hs && x.w - a.shard_begin < a.n_src && fw_f < 64u
                             ? reinterpret_cast<const uint32_t*>(a.g_fwd)[2ull * (x.w - a.shard_begin) + (fw_f >> 5)]
                             : 0u;
     // HTB: d = max(e, TAT before), TAT' = max(TAT, e - burst) + cost, one max-plus scan
@@ -2606,22 +2588,13 @@ __device__ __forceinline__ void sparse_source(const SimArgs& a, const uint32_t s
 // parameters, 8-B offsets, offered records and emit counts share 128-B lines -- on eight different
 // L2s, each fetching the whole line.  With kSparseXcd the blocks of one XCD take one contiguous
 // eighth of the sources, so a line is fetched by one L2.
-#ifndef TGSIM_SPARSE_WPG
-#define TGSIM_SPARSE_WPG 1
-#endif
-#ifndef TGSIM_SPARSE_XCD  // on: the 1M-peer window's simulate bytes -11 % at equal time
-#define TGSIM_SPARSE_XCD 1
-#endif
-constexpr uint32_t kSparseWpg = TGSIM_SPARSE_WPG;
-constexpr bool kSparseXcd = TGSIM_SPARSE_XCD != 0;
+constexpr uint32_t kSparseWpg = 1;
+constexpr bool kSparseXcd = true;  // the 1M-peer window's simulate bytes -11 % at equal time
 __host__ __device__ inline uint32_t sparse_blocks(uint32_t n_src) {
   const uint32_t nb = (n_src + kSparseWpg - 1) / kSparseWpg;
   return kSparseXcd ? (nb + 7) / 8 * 8 : nb;
 }
-#ifndef TGSIM_SPARSE_OCC
-#define TGSIM_SPARSE_OCC 7
-#endif
-__global__ __launch_bounds__(kWave * kSparseWpg, TGSIM_SPARSE_OCC) void k_sim_sparse(SimArgs a) {
+__global__ __launch_bounds__(kWave * kSparseWpg, 7) void k_sim_sparse(SimArgs a) {
   // the source index must stay wave-uniform for the compiler (a VGPR index turns every per-source
   // load into a vector load: 126 VGPR spills at 7 waves per SIMD), hence readfirstlane
   const uint32_t b = blockIdx.x;
@@ -2896,25 +2869,6 @@ __global__ __launch_bounds__(256) void k_gossip_nbr(GossipArgs g, uint32_t* nbr)
   nbr[i] = gossip_neighbour(g, g.shard_begin + s, k);
 }
 
-// Receipts straight from the step's emit regions (single shard), before any delivery ordering:
-// the gossip loop's next window then waits for k_sim and this kernel only, while the scatter and
-// the per-destination sort run beside it at low priority.  Receipts are order-free (earliest tick
-// wins), and a delivery of an already forwarded flood costs one read of its peer's mask.
-__global__ __launch_bounds__(256) void k_gossip_recv_emit(GossipArgs g, EmitRead emit, const uint32_t* emit_n,
-                                                          const uint64_t* off, uint32_t n_src) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nw = gridDim.x * 4;
-  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
-    const uint32_t n = emit_n[s];
-    const uint64_t o0 = off[s], o1 = off[s + 1];
-    const uint32_t pidx = n > 2 * (o1 - o0) + emit.r ? emit.pool_idx[s] : 0u;
-    for (uint32_t i = lane; i < n; i += kWave) {
-      tgsim_delivery r = *emit_rec(emit, s, o0, o1, i, pidx);
-      r.t_ns &= kEMask;  // (a destination slot above it, EmitRead::slot)
-      gossip_recv_one(g, r);
-    }
-  }
-}
 
 // Floods due in [win0, win0 + n_ticks) for local peer s: lane f holds flood f's earliest receipt
 // tick (a coalesced 256-B row); late receipts are flagged.  One wavefront handles kGossipPeers
@@ -3000,7 +2954,6 @@ __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint6
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) nb[k] = k < deg ? readlane32(nbr_l, i * deg + k) : 0u;
     if (!me) continue;
-    if (kFwdSentinel) g.first[(uint64_t)(s0 + i) * 64 + lane] = 0u;  // forwarded: later receipts fold to nothing
     const uint64_t o = o0 + (uint64_t)rank * deg;
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
@@ -3046,7 +2999,6 @@ __global__ __launch_bounds__(256) void k_gossip_write(GossipArgs g, const uint64
       rank += (tj < t[i] || (tj == t[i] && j < lane)) ? 1u : 0u;
     }
     if (!me) continue;
-    if (kFwdSentinel) g.first[(uint64_t)s * 64 + lane] = 0u;  // forwarded: later receipts fold to nothing
     const uint32_t src = g.shard_begin + s;
     const uint64_t o = off[s] + (uint64_t)rank * g.degree;
     for (uint32_t k = 0; k < g.degree; ++k) {
@@ -3905,13 +3857,6 @@ __global__ __launch_bounds__(256) void k_metrics_dst(const tgsim_delivery* recs,
 
 // ---------------------------------------------------------------------------------------------
 // Host-side launchers.
-// Diagnostic knobs of the delivery kernels' choice (A/B of the sub-capacity storm):
-// TGSIM_SPARSE_SORT=1 sorts sparse windows one wavefront per destination instead of flattened;
-// TGSIM_LOCAL_SCATTER=1 lane per source always, 2 wavefront per source always.
-static int env_knob(const char* name) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : 0;
-}
 
 void launch_sim(const SimArgs& a, uint32_t n_wg, hipStream_t st) {
   if (a.g_first) hipLaunchKernelGGL(k_sim_recv, dim3(n_wg), dim3(kWave), 0, st, a);
@@ -3965,8 +3910,7 @@ void launch_sim_sparse(const SimArgs& a, hipStream_t st, uint32_t* work_host, ui
   // grid-stride loop covers any count): each of its workgroups needs 16 KiB of LDS, and at the
   // 1M-peer flood's peak, with the delivery kernels holding the LDS, 16,384 workgroups that found an
   // empty list still waited 1.1 ms for it (the simulate stream's critical path)
-  static const int fixed = env_knob("TGSIM_LIST_GRID");  // A/B: a fixed grid instead of the hint
-  const uint32_t want = fixed > 0 ? static_cast<uint32_t>(fixed) : std::max<uint32_t>(64u, 2u * list_hint);
+  const uint32_t want = std::max<uint32_t>(64u, 2u * list_hint);
   const uint32_t lg = std::min<uint32_t>(std::min<uint32_t>(a.n_src, 16384u), want);
   hipLaunchKernelGGL(k_sim_list, dim3(lg), dim3(kWave), 0, st, a);
   hipLaunchKernelGGL(k_work_done, dim3(1), dim3(64), 0, st, a.worklist - 4, work_host);
@@ -4047,13 +3991,6 @@ void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_
 void launch_gossip_nbr(const GossipArgs& g, uint32_t* nbr, hipStream_t st) {
   const uint64_t n = (uint64_t)g.n_src * g.degree;
   if (n) hipLaunchKernelGGL(k_gossip_nbr, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, g, nbr);
-}
-
-void launch_gossip_recv_emit(const GossipArgs& g, const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off,
-                             uint32_t n_src, hipStream_t st) {
-  if (!n_src) return;
-  const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);
-  hipLaunchKernelGGL(k_gossip_recv_emit, dim3(wgs), dim3(256), 0, st, g, emit, emit_n, off, n_src);
 }
 
 void launch_gossip_recv_in(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t slot, bool skip_own,
@@ -4182,17 +4119,13 @@ constexpr uint32_t kLaneScatterMin = 65536;  // sources: below, the wavefront-pe
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, const uint64_t* doff, uint64_t* pos, tgsim_delivery* out,
                           hipStream_t st, uint64_t n_hint, bool few_dst) {
-#ifdef TGSIM_DIAG_NO_SCATTER  // diagnostic build only (window time without this kernel): wrong deliveries
-  return;
-#endif
   if (!n_src) return;
-  static const int mode = env_knob("TGSIM_LOCAL_SCATTER");
   const uint32_t lwg = (n_src + 255) / 256;
   // up to tens of records per source and enough sources to fill the chip with one lane each (gossip at
   // 1M peers, even at the flood's peak): one lane per source.  With fewer sources (the sub-capacity
   // storm's 10,000: 40 workgroups) a wavefront per source spreads the records over 10,000 waves
   // (A/B: 1.17-1.19 against 1.09-1.12 G pkt/s)
-  if ((n_hint <= 64ull * n_src && n_src >= kLaneScatterMin && mode != 2) || mode == 1) {
+  if (n_hint <= 64ull * n_src && n_src >= kLaneScatterMin) {
     // few_dst (gossip: a peer forwards to its neighbours): one cursor atomic per destination of a
     // source (1M-peer gossip +1-2 %); with records to many destinations that pass over the records
     // costs more than it saves (sub-capacity storm 1.09 against 1.15-1.17 G pkt/s)
@@ -4219,12 +4152,8 @@ void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const ui
 
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
                      tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin) {
-#ifdef TGSIM_DIAG_NO_SORT  // diagnostic build only (window time without this kernel): unsorted deliveries
-  return;
-#endif
   if (!n_dst) return;
-  static const int sparse_sort = env_knob("TGSIM_SPARSE_SORT");
-  if (!cnt && n_hint <= 48ull * n_dst && sparse_sort != 1) {
+  if (!cnt && n_hint <= 48ull * n_dst) {
     // up to tens of records per destination (gossip, sparse windows): 64 records per wave-iteration
     // over the records, on a grid of at most 8,192 workgroups of 4 waves.  At the 1M-peer flood's
     // peak it replaced a wavefront per destination (or lane groups of 8-32 for short segments):
@@ -4246,8 +4175,7 @@ static void launch_sort_bkt(const tgsim_delivery* bkt, tgsim_delivery* sc, const
   // 1,024 resident workgroups (four waves per SIMD): at the 1M-peer flood the sort then leaves the
   // simulate kernels room beside it (A/B, 1M-peer gossip G pkt/s: 256 3.3, 512 5.16, 768 5.61,
   // 1,024 5.60-5.64, 1,536 5.46, 2,048 5.46, 4,096 5.48, 8,192 5.32, one per group 5.30)
-  static const int cap_wg = env_knob("TGSIM_SORT_GRID");  // A/B: 0 the default cap, < 0 one per group
-  const uint32_t grid = cap_wg < 0 ? groups : std::min<uint32_t>(groups, cap_wg > 0 ? (uint32_t)cap_wg : 1024u);
+  const uint32_t grid = std::min<uint32_t>(groups, 1024u);
   hipLaunchKernelGGL(k_dst_sort_bkt<kC>, dim3(grid), dim3(256), 0, st, bkt, sc, doff, n_dst, out, total, cap, err_host);
 }
 void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_delivery* sc, const uint64_t* doff,

@@ -59,8 +59,6 @@ void launch_metrics_dst(const tgsim_delivery* recs, const uint64_t* off, uint32_
                         unsigned long long* hist, hipStream_t st);
 // Receipts of n_dev[0] records (count read on the device).
 void launch_gossip_nbr(const GossipArgs& g, uint32_t* nbr, hipStream_t st);
-void launch_gossip_recv_emit(const GossipArgs& g, const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off,
-                             uint32_t n_src, hipStream_t st);
 void launch_gossip_recv_dev(const GossipArgs& g, const tgsim_delivery* recs, const uint64_t* n_dev, hipStream_t st);
 void launch_gossip_recv_in(const GossipArgs& g, const tgsim_delivery* recs, uint64_t n, uint64_t slot, bool skip_own,
                            hipStream_t st);

@@ -312,8 +312,8 @@ def test_gossip_gpu_equals_oracle(make_oracle):
 
 
 @pytest.mark.parametrize("knobs", [{"TGSIM_DST_BKT": "0"}, {"TGSIM_DST_SLOT": "0"}, {"TGSIM_EMIT_SETS": "2"},
-                                   {"TGSIM_SCAN_ON_SIM": "1"}],
-                         ids=["slot-scatter", "cursor-scatter", "two-sets", "scan-on-sim"])
+                                   {"TGSIM_STAMPS": "1", "TGSIM_SIM_TIMING": "1", "TGSIM_DV_TIMING": "1"}],
+                         ids=["slot-scatter", "cursor-scatter", "two-sets", "diagnostics-on"])
 def test_gossip_delivery_layouts_equal_oracle(make_oracle, monkeypatch, knobs):
     """The delivery layouts the engine can be switched to for A/B runs (read at
     tgsim_create) give the default's results: every window bit-exact with the oracle, at a size

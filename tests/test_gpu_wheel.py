@@ -82,10 +82,15 @@ def test_wheel_dense_then_sparse_windows(make_oracle):
         assert_same(g, c, f"window {k}")
 
 
-def test_wheel_fused_groups(make_oracle):
+@pytest.mark.parametrize("diag", [False, True], ids=["plain", "stamps-and-timing"])
+def test_wheel_fused_groups(make_oracle, monkeypatch, diag):
     """Generated windows fused eight per launch (k_sim_fused: the wheel's counts, header and items
     cross between windows of one launch by the write-through hand-off) after a settle in single
-    windows; two groups, equal to the oracle's eight-window steps."""
+    windows; two groups, equal to the oracle's eight-window steps.  With the diagnostics on (in-kernel
+    stamps, timing events around every launch) the results are the same."""
+    if diag:
+        for k in ("TGSIM_STAMPS", "TGSIM_SIM_TIMING", "TGSIM_DV_TIMING"):
+            monkeypatch.setenv(k, "1")
     n, window = 1000, 2000
     g, c = both(make_oracle, n)
     wl.configure_storm(g, n)
@@ -118,12 +123,12 @@ def test_compact_emit_long_jittered_queues_default_knobs(make_oracle):
                            loss=0.5, duplicate=0.5)
     g.configure_batch(np.arange(n), cfg)
     c.configure_batch(np.arange(n), cfg)
-    for k in range(36):
-        g.gen_storm(0.006, window)  # 12 packets per source and window: sparse
-        c.gen_storm(0.006, window)
+    for k in range(28):
+        g.gen_storm(0.008, window)  # 16 packets per source and window: sparse
+        c.gen_storm(0.008, window)
         g.step(window)
         c.step(window)
-        if k >= 32:
+        if k >= 26:
             assert_same(g, c, f"window {k}")
         else:
             g.drain(), c.drain()
