@@ -41,6 +41,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 from .bridge import NativeBridge, PacketBridge
 from .engine import LIB_PATH, EngineError
 from .sidecar import Context, NetClient, SimReactor, SyncClient, handler
+from .sync_service import SyncService
 
 OUTCOME_UNKNOWN = "unknown"     # pkg/task/task.go:25-28
 OUTCOME_SUCCESS = "success"
@@ -123,6 +124,11 @@ class RunParams:
     TestSidecar: bool = True
     TestSubnet: str = "16.0.0.0/8"
     TestStartTime: float = 0.0
+    # the run's sync endpoint (sdk-go runenv SYNC_SERVICE_HOST/PORT, set by local_common.go:77-82's
+    # sync-service container in the reference): out-of-process plan code reaches the run's sync
+    # counters through it (sync_service.SyncServiceClient)
+    SyncServiceHost: str = ""
+    SyncServicePort: int = 0
 
 
 @dataclasses.dataclass
@@ -138,6 +144,7 @@ class LocalSimRunnerCfg:
     max_sim_ns: int = 3600 * 10**9
     # engine_factory(n_peers, **engine kwargs) -> engine; default: the HIP engine (engine.Engine)
     engine_factory: Optional[Callable] = None
+    sync_service: bool = True  # serve the run's sync counters on a loopback port (sync_service.py)
 
 
 def _make_bridge(engine, n: int, cfg):
@@ -416,6 +423,8 @@ class LocalSimRunner:
         result = Result(Outcomes={g.ID: GroupOutcome(0, g.Instances) for g in job.Groups})
         reactor = SimReactor(engine, n)
         sync_client = reactor.Client
+        service = SyncService(sync_client) if cfg.sync_service else None
+        svc_host, svc_port = service.address if service else ("", 0)
         bridge = _make_bridge(engine, n, cfg)
         reactor.on_link_removed(bridge.link_removed)
         clock = _Clock(bridge, reactor.lock, n, run_ctx, cfg.max_sim_ns)
@@ -432,7 +441,8 @@ class LocalSimRunner:
                     odir = os.path.join(run_dir, g.ID, str(gseq))
                     os.makedirs(odir, exist_ok=True)
                     rp = RunParams(job.TestPlan, job.TestCase, job.RunID, n, g.ID, g.Instances,
-                                   dict(g.Parameters), odir, TestStartTime=time.time())
+                                   dict(g.Parameters), odir, TestStartTime=time.time(),
+                                   SyncServiceHost=svc_host, SyncServicePort=svc_port)
                     env = PlanEnv(rp, peer, gseq, reactor.hostname(peer), run_ctx,
                                   ClockedSync(sync_client, clock, peer), reactor.net_client(peer),
                                   DataPlane(clock, peer))
@@ -464,6 +474,8 @@ class LocalSimRunner:
             clock_t.join(timeout=5)
         finally:
             run_ctx.cancel()
+            if service is not None:
+                service.close()
             reactor.Close()
             with self._lk:
                 if run_ctx in self._active:

@@ -287,3 +287,25 @@ def test_runner_clock_readiness_error_fails_fast(tmp_path, make_oracle):
     assert out.Result.Outcome != rn.OUTCOME_SUCCESS
     assert time.monotonic() - t0 < 20
     assert any("exploded" in e for e in out.Result.Errors.values()), out.Result.Errors
+
+
+def endpoint_plan(env: rn.PlanEnv) -> None:
+    """Plan code that reaches the run's sync counters through the run's sync endpoint (as code in
+    another process would, sync_service.SyncServiceClient over RunParams.SyncServiceHost/Port) and
+    meets the other instance there; the in-process view of the same state agrees."""
+    from testground_amd.sync_service import SyncServiceClient
+
+    rp = env.runenv
+    assert rp.SyncServiceHost and rp.SyncServicePort
+    c = SyncServiceClient((rp.SyncServiceHost, rp.SyncServicePort), timeout_s=20)
+    try:
+        seq = c.SignalEntry("via-endpoint")
+        assert 1 <= seq <= rp.TestInstanceCount
+        c.Barrier("via-endpoint", rp.TestInstanceCount)
+    finally:
+        c.Close()
+
+
+def test_runner_serves_sync_endpoint(tmp_path, make_oracle):
+    out = rn.LocalSimRunner().Run(Context(), _job("ep", [rn.RunGroup("g", 2, endpoint_plan)], _cfg(tmp_path, make_oracle)))
+    assert out.Result.Outcome == rn.OUTCOME_SUCCESS, out.Result.Errors
