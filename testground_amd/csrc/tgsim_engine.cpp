@@ -219,6 +219,8 @@ struct tgsim_engine_s {
   hipEvent_t ev_dst = nullptr;   // recorded after the last delivery on dst_st
   hipEvent_t ev_recv = nullptr;  // recorded after the last delivery's scatter (and gossip receipts)
   hipEvent_t ev_sim = nullptr;   // sim-stream point a delivery waits for
+  hipEvent_t ev_sim_t = nullptr; // the last window's timing event right behind its k_sim, or null:
+                                 // a delivery or routing waits for it instead of a marker of its own
   // k_sim duration per launch: event pairs harvested lazily (the step does not synchronize), with
   // the number of windows the launch simulated (a fused launch counts each of its windows)
   struct PendingTiming {
@@ -1213,9 +1215,11 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
   else launch_sim(a, n_wg, E->st);
   HIPCHK(hipGetLastError());
   E->sim_calls++;  // behind the wait for this emit pair's last reader (ev_local): take_gen's count
+  E->ev_sim_t = nullptr;
   if (timed) {
     HIPCHK(hipEventRecord(ev1, E->st));
     E->ev_pending.push_back({ev0, ev1, 1u});
+    if (!E->metrics_on) E->ev_sim_t = ev1;  // (k_metrics_src follows k_sim on the stream)
   }
   if (sparse) E->sparse_seen = true;
   if (E->metrics_on) {
@@ -1232,14 +1236,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     launch_metrics_src(m, E->st);
     HIPCHK(hipGetLastError());
   }
-  // heavy-first dispatch order for the next step: it shortens the tail when only a few rounds of
-  // workgroups fit; with many more sources than resident workgroups the dispatcher balances alone
-  if (ordered && !sparse) {
-    HIPCHK(E->d_order.ensure(E->S));
-    launch_order(E->d_emit_n.p, E->S, E->d_order.p, E->st);
-    HIPCHK(hipGetLastError());
-    E->order_valid = true;
-  }
+  // (no heavy-first order kernel behind a single window: on the simulate stream it delayed the next
+  // window by its launch and ~9 us, more than the order saved -- sub-capacity storm 1.38 against
+  // 1.51 G pkt/s, profiles/r06/ab_order/; the fused groups of tgsim_step_n keep theirs, once per group)
+  (void)ordered;
   E->n_verdict = E->n_in;
   E->last_perm.swap(E->perm);
   E->perm.clear();
@@ -1253,6 +1253,14 @@ int finish_sim_timing(Eng* E) {
   return check_sim_error(E);
 }
 
+// The point on the simulate stream right behind the last window's k_sim: its timing event when it has
+// one (each marker on the stream delays the next window's launch), else a marker of its own.
+hipEvent_t sim_done_event(Eng* E) {
+  if (E->ev_sim_t) return E->ev_sim_t;
+  (void)hipEventRecord(E->ev_sim, E->st);
+  return E->ev_sim;
+}
+
 // Groups the step's scheduled records by destination shard into `out` on the routing stream, after
 // the step's k_sim and beside the next one (which writes the other emit pair): per-(rank, source)
 // counts -> scan -> ordered scatter; the per-rank edges go to pinned host memory behind ev_route, so
@@ -1260,8 +1268,7 @@ int finish_sim_timing(Eng* E) {
 int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_delivery* out, size_t out_cap,
                  uint64_t slot_cap = 0, hipEvent_t routed = nullptr) {
   hipStream_t rs = E->rt_st;
-  HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
-  HIPCHK(hipStreamWaitEvent(rs, E->ev_sim, 0));
+  HIPCHK(hipStreamWaitEvent(rs, sim_done_event(E), 0));  // this step's k_sim
   RouteArgsHost h;
   memset(&h, 0, sizeof h);
   h.emit = E->el;
@@ -1516,7 +1523,13 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
   HIPCHK(dpos.ensure(nd));
   HIPCHK(dblk.ensure((nd + 1023) / 1024 + 1));
   HIPCHK(dtot.ensure(1));
-  launch_scan(lcnt, doff.p, nd, dblk.p, dtot.p, sq, dpos.p, lcnt);  // (clears lcnt)
+  // single-wave workgroups for a dense window's delivery: it runs beside the next window's k_sim, whose
+  // waves fill every CU's LDS and leave no room for a 4- or 16-wave block, so a 1,024-thread scan
+  // waited for that k_sim to drain and the next k_sim for it (ev_local): 118 against ~97 us per
+  // sub-capacity window (profiles/r06/open/).  Sparse (bucketed, lane-per-source) windows keep theirs.
+  const bool single_wave = !emit.bkt && E->S < 65536;  // (C5's 100,000: the 4-wave forms, A/B'd there)
+  if (single_wave) launch_scan_w(lcnt, doff.p, nd, dblk.p, dtot.p, sq, dpos.p, true);  // (clears lcnt)
+  else launch_scan(lcnt, doff.p, nd, dblk.p, dtot.p, sq, dpos.p, lcnt);
   HIPCHK(hipGetLastError());
   const bool need_n = !(E->o.flags & TGSIM_OPT_DISCARD_DELIVERIES);
   // without the exact count (no host round trip): what the window's sources can emit, 2 per offered
@@ -1546,7 +1559,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     HIPCHK(hipGetLastError());
   }
   // (a bucketed window: only the records past their destination's bucket are in the emit records)
-  launch_local_scatter(er, emit_n, off, E->S, 0, doff.p, dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on);
+  launch_local_scatter(er, emit_n, off, E->S, 0, doff.p, dpos.p, E->d_scatter.p, sq, n_in, E->gossip_on, single_wave);
   HIPCHK(hipGetLastError());
   // the emit set and its histogram are free once scattered: the window two later may write them
   // while this one's per-destination sort still runs (the sort reads only the scatter buffer) --
@@ -1562,7 +1575,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(released, sq));
   } else {
-    launch_dst_sort(E->d_scatter.p, doff.p, nullptr, nd, dst, sq, need_n ? n : n_in);
+    launch_dst_sort(E->d_scatter.p, doff.p, nullptr, nd, dst, sq, need_n ? n : n_in, 0, single_wave);
   }
   HIPCHK(hipGetLastError());
   if (E->metrics_on) {
@@ -1582,8 +1595,7 @@ int deliver_local_from(Eng* E, const EmitRead& emit, uint32_t* emit_n, uint64_t*
 // bookkeeping needs the record count on the host.
 int deliver_local(Eng* E) {
   hipStream_t sq = E->dst_st;
-  HIPCHK(hipEventRecord(E->ev_sim, E->st));  // this step's k_sim
-  HIPCHK(hipStreamWaitEvent(sq, E->ev_sim, 0));
+  HIPCHK(hipStreamWaitEvent(sq, sim_done_event(E), 0));  // this step's k_sim
   if (E->gossip_on)  // receipts of the gossip workload: folded into k_sim at emission; the next
                      // window's generation waits for nothing on the delivery side
     HIPCHK(hipEventRecord(E->ev_recv, E->st));

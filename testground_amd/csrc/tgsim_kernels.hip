@@ -2909,13 +2909,17 @@ __global__ __launch_bounds__(256) void k_gossip_count(GossipArgs g, uint64_t* co
 
 // Degree <= 8: every load is issued up front, in two dependent levels (the masks, offsets and the
 // 8 peers' neighbour lists, one per lane; then the pending receipt ticks), and nothing is read
-// after the first store.  The general kernel below re-read fwd[s], off[s] and the neighbours
-// between the record stores of one peer and the next (its loads could not pass stores that might
-// alias them): a chain of dependent round trips per peer.
+// after the first store.  The 8 peers' records are contiguous in the CSR (off[s0] on), so they are
+// written one record per lane, 64 consecutive records (1 KiB) per store: each due flood leaves its
+// (flood, tick) in an LDS table at its rank, and lane L of round u writes record 64u + L.  (Written
+// flood by flood -- 8 stores of 16 B per due flood at a 128-B stride, 64 store instructions per wave
+// -- the kernel took 0.6 ms in the flood's peak windows, profiles/r06/gossip/.)
 __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint64_t* __restrict__ off,
                                                        InRec* __restrict__ out, uint64_t out_cap,
                                                        const uint64_t* total) {
-  const uint32_t s0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kGossipPeers, lane = threadIdx.x & 63u;
+  __shared__ uint32_t tab[4][kGossipPeers * kWave];  // per wave: [peer][rank] = flood | tick << 8
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t s0 = (blockIdx.x * 4 + wv) * kGossipPeers, lane = threadIdx.x & 63u;
   if (s0 >= g.n_src) return;
   if (total && *total > out_cap) return;  // written again into a larger buffer (resolve_gen)
   if (*g.err) return;  // a late receipt (k_gossip_count): the window is dropped, fwd/pend stay as they are
@@ -2923,7 +2927,7 @@ __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint6
   const bool pl = lane < kGossipPeers && s0 + lane < g.n_src;  // lane i < 8: peer s0 + i's words
   const uint64_t pend_l = pl ? g.pend[s0 + lane] : 0ull;
   const uint64_t fwd_l = pl ? g.fwd[s0 + lane] : 0ull;
-  const uint64_t off_l = pl ? off[s0 + lane] : 0ull;
+  const uint64_t o_base = off[s0];
   // lane i * deg + k: neighbour k of peer s0 + i
   const uint32_t nbr_l = lane < kGossipPeers * deg && s0 + lane / deg < g.n_src ? g.nbr[(uint64_t)s0 * deg + lane] : 0u;
   uint64_t pend[kGossipPeers];
@@ -2934,11 +2938,14 @@ __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint6
     t[i] = (pend[i] >> lane & 1ull) ? g.first[(uint64_t)(s0 + i) * 64 + lane] : 0xFFFFFFFFu;
   }
   uint64_t due_l = 0;  // lane i: the floods peer s0 + i forwards in this window
+  uint32_t pre[kGossipPeers + 1];  // records of the peers before peer i (wave-uniform)
+  pre[0] = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kGossipPeers; ++i) {
     const bool me = gossip_due(g, pend[i], t[i], lane);
     const uint64_t due = __ballot(me);
     if (lane == i) due_l = due;
+    pre[i + 1] = pre[i] + (uint32_t)__popcll(due) * deg;
     if (!due) continue;
     // earliest receipt first, ties by flood id (seq order within a tick)
     uint32_t rank = 0;
@@ -2947,23 +2954,29 @@ __global__ __launch_bounds__(256) void k_gossip_write8(GossipArgs g, const uint6
       const uint32_t tj = readlane32(t[i], j);
       rank += (tj < t[i] || (tj == t[i] && j < lane)) ? 1u : 0u;
     }
-    // peer s0 + i's offset and neighbours, read while every lane is active (below only the lanes
-    // of its due floods are)
-    const uint64_t o0 = readlane64(off_l, i);
-    uint32_t nb[8];
+    if (me) tab[wv][i * kWave + rank] = lane | (uint32_t)(t[i] - g.win0) << 8;
+  }
+  wave_lds_sync();
+  const uint32_t n_rec = pre[kGossipPeers];
+  for (uint32_t base = 0; base < n_rec; base += kWave) {
+    const uint32_t r = base + lane;
+    uint32_t i = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) nb[k] = k < deg ? readlane32(nbr_l, i * deg + k) : 0u;
-    if (!me) continue;
-    const uint64_t o = o0 + (uint64_t)rank * deg;
+    for (uint32_t p = 1; p < kGossipPeers; ++p) i += r >= pre[p] ? 1u : 0u;
+    uint32_t pi = pre[0];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-      if (k >= deg) break;
+    for (uint32_t p = 1; p < kGossipPeers; ++p) pi = i == p ? pre[p] : pi;
+    const uint32_t q = r - pi, j = q / deg, k = q - j * deg;
+    const uint32_t e = r < n_rec ? tab[wv][i * kWave + j] : 0u;
+    TG_FULL_EXEC("ds_bpermute");
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((i * deg + k) << 2), (int)nbr_l);
+    if (r < n_rec) {
       InRec rec;
-      rec.dst = nb[k];
-      rec.seq = lane * deg + k;
-      rec.tick = (uint32_t)(t[i] - g.win0);
+      rec.dst = nb;
+      rec.seq = (e & 63u) * deg + k;
+      rec.tick = e >> 8;
       rec.len = g.msg_len;
-      out[o + k] = rec;
+      out[o_base + r] = rec;
     }
   }
   if (pl && due_l) {
@@ -3331,9 +3344,9 @@ __global__ __launch_bounds__(256) void k_local_scatter(EmitRead emit, const uint
                                                        const uint64_t* off, uint32_t n_src, uint32_t dst_begin,
                                                        const uint64_t* doff, uint64_t* pos, tgsim_delivery* out) {
   if (emit.guard_total && *emit.guard_total > emit.guard_cap) return;  // (EmitRead::guard_total)
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nw = gridDim.x * 4;
-  for (uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6); s < n_src; s += nw) {
+  const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x >> 6;  // (4 waves, or 1: see k_dst_sort_flat)
+  const uint32_t nw = gridDim.x * wpb;
+  for (uint32_t s = blockIdx.x * wpb + (threadIdx.x >> 6); s < n_src; s += nw) {
     const uint32_t n = emit_n[s];
     const uint64_t o0 = off[s], o1 = off[s + 1];
     const uint32_t pidx = n > 2 * (o1 - o0) + emit.r ? emit.pool_idx[s] : 0u;
@@ -3473,8 +3486,8 @@ __global__ __launch_bounds__(64) void k_scan_w1(const uint64_t* in, uint64_t n, 
   s = wave_sum(s);
   if (threadIdx.x == 0) blk[blockIdx.x] = s;
 }
-__global__ __launch_bounds__(64) void k_scan_w2(const uint64_t* in, uint64_t n, const uint64_t* blk, uint64_t* out,
-                                                uint64_t* pos, uint64_t* total_out) {
+__global__ __launch_bounds__(64) void k_scan_w2(uint64_t* in, uint64_t n, const uint64_t* blk, uint64_t* out,
+                                                uint64_t* pos, uint64_t* total_out, uint32_t clear) {
   const uint32_t lane = threadIdx.x;
   uint64_t pre = 0;
   for (uint32_t j = lane; j < blockIdx.x; j += kWave) pre += blk[j];
@@ -3485,6 +3498,13 @@ __global__ __launch_bounds__(64) void k_scan_w2(const uint64_t* in, uint64_t n, 
   for (uint32_t u = 0; u < 16; ++u) {
     const uint64_t e = base + u * kWave + lane;
     x[u] = e < n ? in[e] : 0ull;
+  }
+  if (clear) {  // the histogram free for its next window (k_scan_w1 of this scan has read it)
+#pragma unroll
+    for (uint32_t u = 0; u < 16; ++u) {
+      const uint64_t e = base + u * kWave + lane;
+      if (e < n) in[e] = 0;
+    }
   }
 #pragma unroll
   for (uint32_t u = 0; u < 16; ++u) {
@@ -3656,14 +3676,17 @@ __global__ __launch_bounds__(1024) void k_deliver_guard(const uint64_t* total, u
 // segment's keys before its own (ties, which the key order never has, by position).  A longer
 // segment is sorted whole (sort_segment) by the wavefront holding its first record.  A persistent
 // grid walks the chunks up to the device's total (off[n_dst]); the destination counts are not read.
-__global__ __launch_bounds__(256) void k_dst_sort_flat(tgsim_delivery* in, const uint64_t* off, uint32_t n_dst,
-                                                       uint32_t dst_begin, tgsim_delivery* out) {
-  __shared__ uint64_t kt[4][3 * kWave], kq[4][3 * kWave];
-  __shared__ uint32_t kc[4][3 * kWave];
+// kW waves per workgroup (1: beside a running k_sim, whose waves leave no CU room for a 4-wave block
+// with 15 KiB of LDS)
+template <uint32_t kW>
+__global__ __launch_bounds__(64 * kW) void k_dst_sort_flat(tgsim_delivery* in, const uint64_t* off, uint32_t n_dst,
+                                                           uint32_t dst_begin, tgsim_delivery* out) {
+  __shared__ uint64_t kt[kW][3 * kWave], kq[kW][3 * kWave];
+  __shared__ uint32_t kc[kW][3 * kWave];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t total = off[n_dst];
   const uint64_t n_chunks = (total + kWave - 1) / kWave;
-  for (uint64_t c = (uint64_t)blockIdx.x * 4 + wv; c < n_chunks; c += (uint64_t)gridDim.x * 4) {
+  for (uint64_t c = (uint64_t)blockIdx.x * kW + wv; c < n_chunks; c += (uint64_t)gridDim.x * kW) {
     const uint64_t w0 = c * kWave;  // the staged window is [w0 - 64, w0 + 128)
     tgsim_delivery r;
 #pragma unroll
@@ -4118,7 +4141,7 @@ void launch_deliver_guard(const uint64_t* total, uint64_t cap, uint32_t* emit_n,
 constexpr uint32_t kLaneScatterMin = 65536;  // sources: below, the wavefront-per-source scatter
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, const uint64_t* doff, uint64_t* pos, tgsim_delivery* out,
-                          hipStream_t st, uint64_t n_hint, bool few_dst) {
+                          hipStream_t st, uint64_t n_hint, bool few_dst, bool single_wave) {
   if (!n_src) return;
   const uint32_t lwg = (n_src + 255) / 256;
   // up to tens of records per source and enough sources to fill the chip with one lane each (gossip at
@@ -4141,25 +4164,31 @@ void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const ui
                          dst_begin, doff, pos, out);
     return;
   }
-  const uint32_t wgs = std::min<uint32_t>((n_src + 3) / 4, 4096);
+  const uint32_t wpb = single_wave ? 1u : 4u, wgs = std::min<uint32_t>((n_src + wpb - 1) / wpb, 16384 / wpb);
   if (emit.slot)
-    hipLaunchKernelGGL(k_local_scatter<true>, dim3(wgs), dim3(256), 0, st, emit, emit_n, off, n_src, dst_begin, doff,
-                       pos, out);
+    hipLaunchKernelGGL(k_local_scatter<true>, dim3(wgs), dim3(64 * wpb), 0, st, emit, emit_n, off, n_src, dst_begin,
+                       doff, pos, out);
   else
-    hipLaunchKernelGGL(k_local_scatter<false>, dim3(wgs), dim3(256), 0, st, emit, emit_n, off, n_src, dst_begin, doff,
-                       pos, out);
+    hipLaunchKernelGGL(k_local_scatter<false>, dim3(wgs), dim3(64 * wpb), 0, st, emit, emit_n, off, n_src, dst_begin,
+                       doff, pos, out);
 }
 
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin) {
+                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin, bool single_wave) {
   if (!n_dst) return;
+  if (!cnt && single_wave) {
+    const uint64_t chunks = (n_hint + kWave - 1) / kWave;
+    hipLaunchKernelGGL(k_dst_sort_flat<1>, dim3((uint32_t)(chunks < 32768 ? (chunks ? chunks : 1) : 32768)), dim3(64), 0,
+                       st, in, off, n_dst, dst_begin, out);
+    return;
+  }
   if (!cnt && n_hint <= 48ull * n_dst) {
     // up to tens of records per destination (gossip, sparse windows): 64 records per wave-iteration
     // over the records, on a grid of at most 8,192 workgroups of 4 waves.  At the 1M-peer flood's
     // peak it replaced a wavefront per destination (or lane groups of 8-32 for short segments):
     // 4.66-4.70 against 4.57-4.60 G pkt/s
     const uint64_t chunks = (n_hint + kWave - 1) / kWave, wgs = (chunks + 3) / 4;
-    hipLaunchKernelGGL(k_dst_sort_flat, dim3((uint32_t)(wgs < 8192 ? (wgs ? wgs : 1) : 8192)), dim3(256), 0, st, in, off,
+    hipLaunchKernelGGL(k_dst_sort_flat<4>, dim3((uint32_t)(wgs < 8192 ? (wgs ? wgs : 1) : 8192)), dim3(256), 0, st, in, off,
                        n_dst, dst_begin, out);
     return;
   }
@@ -4195,15 +4224,16 @@ void launch_dst_sort_w1(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, 
   if (n_dst) hipLaunchKernelGGL(k_dst_sort_wide<1>, dim3(n_dst), dim3(64), 0, st, in, off, cnt, n_dst, out);
 }
 
-void launch_scan_w(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
-                   hipStream_t st, uint64_t* pos) {
+void launch_scan_w(uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
+                   hipStream_t st, uint64_t* pos, bool clear) {
   const uint32_t nb = (uint32_t)((n + 1023) / 1024);
   if (!nb) {
     launch_scan(in, out, n, block_sums, total, st, pos);
     return;
   }
   hipLaunchKernelGGL(k_scan_w1, dim3(nb), dim3(64), 0, st, in, n, block_sums);
-  hipLaunchKernelGGL(k_scan_w2, dim3(nb), dim3(64), 0, st, in, n, (const uint64_t*)block_sums, out, pos, total);
+  hipLaunchKernelGGL(k_scan_w2, dim3(nb), dim3(64), 0, st, in, n, (const uint64_t*)block_sums, out, pos, total,
+                     clear ? 1u : 0u);
 }
 
 void launch_local_scatter_group(const GroupDeliver& g, uint32_t n_win, hipStream_t st) {

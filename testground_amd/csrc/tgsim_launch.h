@@ -99,17 +99,19 @@ void launch_dst_sort_bkt(const tgsim_delivery* bkt, uint32_t bkt_log, tgsim_deli
                          uint64_t* err_host);
 void launch_local_scatter(const EmitRead& emit, const uint32_t* emit_n, const uint64_t* off, uint32_t n_src,
                           uint32_t dst_begin, const uint64_t* doff, uint64_t* pos, tgsim_delivery* out,
-                          hipStream_t st, uint64_t n_hint, bool few_dst = false);
+                          hipStream_t st, uint64_t n_hint, bool few_dst = false, bool single_wave = false);
 // Orders each destination's records (segment d: off[d] .. off[d + 1]; dst_begin: the first
 // destination's id) and resets cnt[] to zero for the next histogram, unless cnt is null (the scan
 // cleared it: then sparse windows take the flattened sort).  (in, the scatter buffer, is
 // overwritten for segments longer than 64.)  n_hint: about how many records.
 void launch_dst_sort(tgsim_delivery* in, const uint64_t* off, uint64_t* cnt, uint32_t n_dst,
-                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin = 0);
-// The fused group's K5 (single-wave workgroups, see k_scan_w1): scan of n counts, scatter of the
-// n_win windows' emit regions, one wavefront per (window, destination) segment.
-void launch_scan_w(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
-                   hipStream_t st, uint64_t* pos);
+                     tgsim_delivery* out, hipStream_t st, uint64_t n_hint, uint32_t dst_begin = 0,
+                     bool single_wave = false);
+// The fused group's K5 (single-wave workgroups, see k_scan_w1): scan of n counts (clear: zeroed as
+// read), scatter of the n_win windows' emit regions, one wavefront per (window, destination) segment.
+// single_wave (above): the same single-wave form of a window's scatter and sort beside a running k_sim.
+void launch_scan_w(uint64_t* in, uint64_t* out, uint64_t n, uint64_t* block_sums, uint64_t* total,
+                   hipStream_t st, uint64_t* pos, bool clear = false);
 void launch_local_scatter_group(const GroupDeliver& g, uint32_t n_win, hipStream_t st);
 // TGSIM_CHECK builds: cross-lane helper calls whose source lanes were inactive (-ENOSYS otherwise)
 int64_t exec_faults();
