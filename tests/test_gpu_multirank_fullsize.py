@@ -196,8 +196,10 @@ def _c5(r, e, chk, n):
 def test_c4_gossip_1m_at_8_ranks_equals_oracle(lib):
     chk = _run(lib, "c4", _c4)
     # the compact emit layout (and the exchange buffers sized from it) keeps the
-    # 8 shards of 125,000 peers within 80 GB (about 160 GB with regions for the netem limit)
-    assert chk.mem_peak == 0 or chk.mem_peak <= 80e9, f"{chk.mem_peak / 1e9:.1f} GB in use"
+    # 8 shards of 125,000 peers far below the ~160 GB of regions for the netem limit: measured 74.1 GB
+    # before tgsim_gossip_init reserved each shard's scatter and sorted-output buffers for the
+    # flood's peak (grown inside the flood, each growth stalled the device 0.3-0.7 ms), 80.4 GB since
+    assert chk.mem_peak == 0 or chk.mem_peak <= 88e9, f"{chk.mem_peak / 1e9:.1f} GB in use"
 
 
 @pytest.mark.timeout(900)
