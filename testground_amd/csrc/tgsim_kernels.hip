@@ -3773,11 +3773,16 @@ __global__ __launch_bounds__(256) void k_dst_sort_bkt(const tgsim_delivery* __re
     if (in_range) {
       sb = doff[d];
       se = doff[d + 1];
-#pragma unroll
-      for (uint32_t u = 0; u < kR; ++u) r[u] = bkt[(uint64_t)d * kC + u * kL + k];
     }
     const uint64_t cnt = se - sb;
     const bool small = cnt <= kC;
+    // only a destination's records are read, behind its offsets (read whole, the bucket lines past the
+    // records were most of the kernel's HBM traffic at the 1M-peer flood: 935 MB per window for
+    // 415 MB of records); a longer segment is read by sort_segment_ld below
+    const uint32_t n_ld = small ? (uint32_t)cnt : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < kR; ++u)
+      if (u * kL + k < n_ld) r[u] = bkt[(uint64_t)d * kC + u * kL + k];
 #pragma unroll
     for (uint32_t u = 0; u < kR; ++u) {
       const uint32_t j = u * kL + k;
