@@ -488,6 +488,9 @@ int64_t tgsim_debug_carry_bytes(void* engine);
 int64_t tgsim_debug_bucket_records(void* engine);
 /* Diagnostics: windows simulated by fused launches (tgsim_step_n) since the engine was created. */
 int64_t tgsim_debug_fused_windows(void* engine);
+/* Diagnostics: windows simulated by the sparse kernels (k_sim_sparse + k_sim_multi + k_sim_list) since
+ * the engine was created; the others ran the dense k_sim (or were fused). */
+int64_t tgsim_debug_sparse_windows(void* engine);
 /* Diagnostics of a TGSIM_CHECK build of the engine (scripts/r05_check_build.sh): cross-lane reads whose
  * source lanes were inactive so far, process-wide.  -ENOSYS in the product build. */
 int64_t tgsim_debug_exec_faults(void);

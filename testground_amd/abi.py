@@ -136,7 +136,7 @@ EXPORTS = [
     "tgsim_deliver_slotted_async", "tgsim_step_sim_launch_slotted_n", "tgsim_deliver_slotted_n_async",
     "tgsim_sim_capacity", "tgsim_drain", "tgsim_pending_deliveries", "tgsim_verdicts", "tgsim_stats",
     "tgsim_signal", "tgsim_signal_async", "tgsim_barrier_poll", "tgsim_sync_counters", "tgsim_sim_kernel_ms", "tgsim_delivery_kernel_ms", "tgsim_stream", "tgsim_debug_stamps",
-    "tgsim_debug_fused_windows", "tgsim_debug_carry_bytes", "tgsim_debug_bucket_records", "tgsim_debug_exec_faults", "tgsim_step_n",
+    "tgsim_debug_fused_windows", "tgsim_debug_sparse_windows", "tgsim_debug_carry_bytes", "tgsim_debug_bucket_records", "tgsim_debug_exec_faults", "tgsim_step_n",
     "tgsim_gossip_init", "tgsim_gen_gossip", "tgsim_gossip_reached", "tgsim_metrics",
     "tgsim_comm_id", "tgsim_comm_init", "tgsim_comm_step", "tgsim_comm_launch", "tgsim_comm_finish", "tgsim_comm_run", "tgsim_comm_barrier", "tgsim_comm_info",
     "tgsim_bridge_create", "tgsim_bridge_destroy", "tgsim_bridge_send", "tgsim_bridge_step",
@@ -198,6 +198,7 @@ def declare(lib: C.CDLL, prefix: str) -> None:
     f("stream", vp, vp)
     f("debug_stamps", C.c_int64, vp, C.c_void_p, C.c_size_t)
     f("debug_fused_windows", C.c_int64, vp)
+    f("debug_sparse_windows", C.c_int64, vp)
     f("debug_exec_faults", C.c_int64)
     f("debug_carry_bytes", C.c_int64, vp)
     f("debug_bucket_records", C.c_int64, vp)

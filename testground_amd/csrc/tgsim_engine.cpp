@@ -410,6 +410,7 @@ struct tgsim_engine_s {
   DevBuf<uint32_t> d_done, d_ticket;    // per-source completion words (window-major), ticket counter
   uint32_t step_no = 0, ticket_no = 0;  // windows and tickets issued by fused launches so far
   uint64_t fused_windows = 0;
+  uint64_t sparse_windows = 0;  // windows run by the sparse kernels (tgsim_debug_sparse_windows)
   uint32_t fused_wgs = 0;
   uint32_t routed_pct = 0;      // sharded (routed) groups: 0 = one workgroup per ticket (the grid turns
                                 // over), else a persistent grid of this % of the resident workgroups
@@ -1221,7 +1222,10 @@ int run_sim(Eng* E, uint32_t n_ticks, bool local_hist = false) {
     E->ev_pending.push_back({ev0, ev1, 1u});
     if (!E->metrics_on) E->ev_sim_t = ev1;  // (k_metrics_src follows k_sim on the stream)
   }
-  if (sparse) E->sparse_seen = true;
+  if (sparse) {
+    E->sparse_seen = true;
+    E->sparse_windows++;
+  }
   if (E->metrics_on) {
     MetricsArgs m;
     m.off = E->d_off.p;
@@ -2792,6 +2796,11 @@ int64_t tgsim_debug_bucket_records(void* e) {
 }
 
 int64_t tgsim_debug_exec_faults(void) { return exec_faults(); }
+
+int64_t tgsim_debug_sparse_windows(void* e) {
+  Eng* E = as_eng(e);
+  return E ? static_cast<int64_t>(E->sparse_windows) : -EINVAL;
+}
 
 int64_t tgsim_debug_fused_windows(void* e) {
   Eng* E = as_eng(e);
