@@ -1020,6 +1020,10 @@ static_assert(sizeof(StatePair) == sizeof(SrcState), "SrcState hand-off");
 // the stores; returned minus claim_base.  kMode: 0 plain loads and stores (k_sim, k_sim_list); 1 the
 // HBM state is handed off inside a fused launch (bounded sc1 loads and stores).
 constexpr int kModePlain = 0, kModeHandoff = 1;
+// Departure-ring entries read with the queue (more, 64 at a time, only while none of them departs at
+// or after the horizon): a window releases at most the entries before the first one >= an offer
+// time < H, about a dozen per source in the C3 storm and three in C5
+constexpr uint32_t kRingFirst = 16;
 template <bool kOpen, uint32_t kCap, int kMode = kModePlain, bool kRecv = false, bool kList = false>
 __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t s, const uint32_t wg, SimLdsT<kCap>& lds,
                                                uint32_t* claim = nullptr, uint32_t claim_base = 0) {
@@ -1115,12 +1119,12 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     uint4 qv[kCap / kWave];
     if constexpr (kBounded) {
       const auto rr = region(gr, 8u * kHeapCap), rq = region(gh, 16u * qn);
-      rv0 = ld8<kPol>(rr, 8u * ((rh0 + (lane < rn ? lane : 0u)) & (kHeapCap - 1)));
+      rv0 = ld8<kPol>(rr, lane < kRingFirst ? 8u * ((rh0 + (lane < rn ? lane : 0u)) & (kHeapCap - 1)) : kOff);
 #pragma unroll
       for (uint32_t u = 0; u < kCap / kWave; ++u) qv[u] = ld16<kPol>(rq, 16u * (u * kWave + lane));
     } else {  // a lane past the end re-reads the last entry (the same line as its neighbours)
       const uint32_t ql = qn ? qn - 1 : 0, qh = q_head(st);
-      rv0 = gr[(rh0 + (lane < rn ? lane : 0u)) & (kHeapCap - 1)];
+      rv0 = gr[(rh0 + (lane < rn && lane < kRingFirst ? lane : 0u)) & (kHeapCap - 1)];
 #pragma unroll
       for (uint32_t u = 0; u < kCap / kWave; ++u) {
         const uint32_t k = u * kWave + lane;
@@ -1154,7 +1158,7 @@ __device__ __forceinline__ uint32_t sim_source(const SimArgs& a, const uint32_t 
     // every load issued before the partition's ballots, which the scheduler would otherwise
     // interleave with them (one HBM round trip per chunk)
     __builtin_amdgcn_sched_barrier(0);
-    rl = rn < kWave ? rn : kWave;
+    rl = rn < kRingFirst ? rn : kRingFirst;
     if (lane < rl) *reinterpret_cast<uint2*>(&lds.slot[lane]) = make_uint2((uint32_t)rv0, (uint32_t)(rv0 >> 32));
     // more of the ring only while no loaded entry departs at or after the horizon (rare: a fast link
     // releasing more than 64 entries in one window)
