@@ -301,6 +301,9 @@ int wait_word(Comm* C, const uint64_t* w, uint64_t want, hipEvent_t ev, const ch
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 1;; ++it) {
     if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == want) return 0;
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
     if ((it & 255) == 0) {
       const hipError_t q = hipEventQuery(ev);
       if (q == hipSuccess) {
@@ -316,7 +319,7 @@ int wait_word(Comm* C, const uint64_t* w, uint64_t want, hipEvent_t ev, const ch
                     "stopped?); the communicator is aborted at tgsim_destroy", C->rank, C->nranks,
                     static_cast<unsigned long long>(ms), what, static_cast<unsigned long long>(C->k));
       }
-      sched_yield();
+      if (it > (1u << 16)) sched_yield();  // (a yield on a loaded host costs a scheduler slice per wait)
     }
   }
 }

@@ -25,6 +25,22 @@
 
 using namespace tgsim;
 
+// Host spin-waits on words the device publishes to pinned memory: a pause per poll, and no yield of
+// the core before about this many polls (a few ms).
+inline void spin_pause() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#endif
+}
+constexpr uint32_t kSpinBeforeYield = 1u << 16;
+
+// Events that order work between this engine's own streams (and its timing events) skip the
+// system-scope fence a recorded event otherwise makes (a writeback of the device caches that the
+// next command on the stream waits for; A/B, profiles/r06/ab_nofence/: C5 +1.6 %, sub-capacity +3 %,
+// C3 +0.6 %).  Events the host relies on to see device writes in host memory keep it.
+constexpr unsigned kEvSync = hipEventDisableTiming | hipEventDisableSystemFence;
+constexpr unsigned kEvTiming = hipEventDefault | hipEventDisableSystemFence;
+
 namespace {
 
 // ------------------------------------------------------------------------------------------------
@@ -745,14 +761,14 @@ int flush_config(Eng* E) {
       // it sat between two windows: ~45 us of a 1 ms C5 epoch); the apply waits for it
       HIPCHK(E->d_patch_t[t].ensure(E->S));  // (sized once: never reallocated under a copy or apply)
       HIPCHK(sync_stream_ready(E));
-      if (!E->ev_pcopy) HIPCHK(hipEventCreateWithFlags(&E->ev_pcopy, hipEventDisableTiming));
+      if (!E->ev_pcopy) HIPCHK(hipEventCreateWithFlags(&E->ev_pcopy, kEvSync));
       if (E->ev_patch[t]) HIPCHK(hipStreamWaitEvent(E->sy_st, E->ev_patch[t], 0));
       HIPCHK(hipMemcpyAsync(E->d_patch_t[t].p, E->h_patch[t], sizeof(CfgPatch) * k, hipMemcpyHostToDevice, E->sy_st));
       HIPCHK(hipEventRecord(E->ev_pcopy, E->sy_st));
       HIPCHK(hipStreamWaitEvent(E->st, E->ev_pcopy, 0));
       launch_apply_cfg(E->d_patch_t[t].p, static_cast<uint32_t>(k), E->d_params.p, E->d_state.p, E->d_stats.p, E->st);
       HIPCHK(hipGetLastError());
-      if (!E->ev_patch[t]) HIPCHK(hipEventCreateWithFlags(&E->ev_patch[t], hipEventDisableTiming));
+      if (!E->ev_patch[t]) HIPCHK(hipEventCreateWithFlags(&E->ev_patch[t], kEvSync));
       HIPCHK(hipEventRecord(E->ev_patch[t], E->st));
       E->patch_turn = t ^ 1u;
       if (E->now_tick) E->wide_windows = kWideAfterReshape;
@@ -837,7 +853,7 @@ hipError_t take_event(Eng* E, hipEvent_t* ev) {
     E->ev_pool.pop_back();
     return hipSuccess;
   }
-  return hipEventCreate(ev);
+  return hipEventCreateWithFlags(ev, kEvTiming);
 }
 
 // Folds finished k_sim event pairs into the running average (wait: block until all are done).
@@ -1320,9 +1336,13 @@ int route_launch(Eng* E, uint32_t n_ranks, const uint32_t* bounds, tgsim_deliver
 
 // Spins until the device publishes `want` into the pinned word (kernels release it at system
 // scope); `ev`, recorded after the publishing kernel, tells a fault from a slow step.
+// The spin gives its core up only after a long wait (~ms): a yield on a loaded host handed the core
+// away for a scheduler slice, ~0.9 ms added to every window of the closed gossip loop (1M peers:
+// 3.3 against 5.6 G pkt/s in two runs of profiles/r06/ab_nofence/).
 int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev, const char* what) {
   for (uint32_t it = 1;; ++it) {
     if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == want) return 0;
+    spin_pause();
     if ((it & 255) == 0) {
       const hipError_t q = hipEventQuery(ev);
       if (q == hipSuccess) {
@@ -1330,7 +1350,7 @@ int wait_published(Eng* E, const uint64_t* word, uint64_t want, hipEvent_t ev, c
         return E->fail(-EIO, "%s: the device finished without publishing its result", what);
       }
       if (q != hipErrorNotReady) HIPCHK(q);
-      std::this_thread::yield();
+      if (it > kSpinBeforeYield) std::this_thread::yield();
     }
   }
 }
@@ -1940,12 +1960,12 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_rt, hipEventDisableTiming), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_rt, E->rt_st), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_dst, hipEventDisableTiming), "event"))) return bail(rc);
-  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_sim, kEvSync), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_dst, E->dst_st), "event"))) return bail(rc);
-  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, hipEventDisableTiming), "event"))) return bail(rc);
+  if ((rc = E->hip(hipEventCreateWithFlags(&E->ev_recv, kEvSync), "event"))) return bail(rc);
   if ((rc = E->hip(hipEventRecord(E->ev_recv, E->dst_st), "event"))) return bail(rc);
   for (hipEvent_t* ev : {&E->ev_local, &E->ev_local_alt, &E->ev_local_alt2}) {
-    if ((rc = E->hip(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event"))) return bail(rc);
+    if ((rc = E->hip(hipEventCreateWithFlags(ev, kEvSync), "event"))) return bail(rc);
     if ((rc = E->hip(hipEventRecord(*ev, E->dst_st), "event"))) return bail(rc);
   }
   if ((rc = E->hip(hipHostMalloc(reinterpret_cast<void**>(&E->h_err), sizeof(uint64_t),
@@ -1992,7 +2012,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   if (E->sim_every || E->dv_every) {  // the timing events, created here rather than in the step path
     E->ev_pool.resize(kEventPool);
     for (hipEvent_t& ev : E->ev_pool)
-      if ((rc = E->hip(hipEventCreate(&ev), "event"))) {
+      if ((rc = E->hip(hipEventCreateWithFlags(&ev, kEvTiming), "event"))) {
         ev = nullptr;
         return bail(rc);
       }
@@ -2012,7 +2032,7 @@ int tgsim_create(const tgsim_opts* opts, void** out) {
   }
   if (const char* fz = getenv("TGSIM_FUSE")) E->fuse_max = std::max(1, std::min(atoi(fz), static_cast<int>(kFuseMax)));
   for (hipEvent_t& ev : E->ev_fgrp) {
-    if ((rc = E->hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return bail(rc);
+    if ((rc = E->hip(hipEventCreateWithFlags(&ev, kEvSync), "event"))) return bail(rc);
     if ((rc = E->hip(hipEventRecord(ev, E->dst_st), "event"))) return bail(rc);
   }
   E->enabled.assign(E->N, 1);  // containers start attached to the data network (local_docker.go:459)
